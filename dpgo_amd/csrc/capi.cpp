@@ -1,0 +1,882 @@
+// C-ABI implementation of libdpgo_hip.so (see include/dpgo_hip.h).
+//
+// Host side of the on-device RTR / tCG state machine.  All vector arithmetic and all scalar
+// recurrences run on the GPU (kernels.hip); the host only sequences launches and, once per RTR
+// Run, reads the per-agent "still running" flags to drive QuadraticOptimizer::trustRegion's
+// radius-shrink retry loop (src/QuadraticOptimizer.cpp:92-110).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/dpgo_hip.h"
+#include "kernels.h"
+
+using dpgo::AgentState;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess)                                                                    \
+      return fail(DPGO_HIP_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));      \
+  } while (0)
+
+#define DPGO_TRY(expr)          \
+  do {                          \
+    int _rc = (expr);           \
+    if (_rc != DPGO_HIP_OK) return _rc; \
+  } while (0)
+
+int g_devices = -1;
+
+int usable_devices() {
+  if (g_devices >= 0) return g_devices;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  int ok = 0;
+  for (int i = 0; i < n; ++i) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, i) == hipSuccess && std::strstr(p.gcnArchName, "gfx950")) ++ok;
+  }
+  g_devices = ok;
+  return ok;
+}
+
+struct HostBSR {
+  std::vector<int> rowptr, col;
+  std::vector<double> blocks;
+};
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  hipError_t ensure(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    release();
+    n = std::max<size_t>(count, 1);
+    return hipMalloc(reinterpret_cast<void**>(&p), n * sizeof(T));
+  }
+};
+
+}  // namespace
+
+struct dpgo_hip_problem_s {
+  int K = 0, d = 0, r = 0, b = 0;
+  long N = 0;  // total poses
+  std::vector<int> n_agent;
+  std::vector<long> pose_off;
+  hipStream_t stream = nullptr;
+  hipStream_t own_stream = nullptr;
+
+  // tiles
+  std::vector<int> h_tile_agent, h_tile_start, h_tile_count, h_agent_tile_off;
+  int num_tiles = 0;
+  DevBuf<int> tile_agent, tile_start, tile_count, agent_tile_off, agent_np, enabled, use_a;
+
+  // Q (per-agent host copies, concatenated on upload)
+  std::vector<HostBSR> q_agent;
+  bool q_dirty = true;
+  DevBuf<int> rowptr, col;
+  DevBuf<double> blocks, minv;
+  long nnzb = 0;
+
+  // G (sparse pose blocks per agent)
+  std::vector<std::map<int, std::vector<double>>> g_agent;
+  bool g_dirty = true;
+  DevBuf<int> gidx;
+  DevBuf<double> gblk;
+  int num_gslots = 0;
+
+  int precon = DPGO_PRECON_BLOCK_JACOBI;
+
+  // work
+  DevBuf<double> x1, x2, g, g2, S, S2, eta, Heta, rv, z, delta, Hdelta, tA, tB;
+  DevBuf<double> pa, pb, sums, coef_a, coef_b;
+  DevBuf<AgentState> state;
+  std::vector<AgentState> h_state;
+  std::vector<double> h_sums;
+
+  size_t vec_len() const { return static_cast<size_t>(N) * r * b; }
+  size_t vec_bytes() const { return vec_len() * sizeof(double); }
+  size_t s_len() const { return static_cast<size_t>(N) * (b - 1) * (b - 1); }
+};
+
+namespace {
+
+dpgo::LaunchCtx make_ctx(dpgo_hip_problem h, int flag_kind, double* partials) {
+  dpgo::LaunchCtx c;
+  c.tile_agent = h->tile_agent.p;
+  c.tile_start = h->tile_start.p;
+  c.tile_count = h->tile_count.p;
+  c.num_tiles = h->num_tiles;
+  c.flag_kind = flag_kind;
+  c.state = h->state.p;
+  c.partials = partials;
+  c.stream = h->stream;
+  return c;
+}
+
+dpgo::QView qview(dpgo_hip_problem h) { return dpgo::QView{h->rowptr.p, h->col.p, h->blocks.p}; }
+
+int check_handle(dpgo_hip_problem h) {
+  if (!h) return fail(DPGO_HIP_EINVAL, "null problem handle");
+  return DPGO_HIP_OK;
+}
+
+// Concatenate the per-agent BSR blocks into one block-diagonal device BSR and rebuild the
+// block-Jacobi inverses (QuadraticProblem::setQ, src/QuadraticProblem.cpp:31-42).
+int sync_q(dpgo_hip_problem h) {
+  if (!h->q_dirty) return DPGO_HIP_OK;
+  const int b = h->b;
+  long nnz = 0;
+  for (int a = 0; a < h->K; ++a) nnz += static_cast<long>(h->q_agent[a].col.size());
+  std::vector<int> rowptr(h->N + 1, 0), col(std::max<long>(nnz, 1));
+  std::vector<double> blocks(std::max<long>(nnz, 1) * b * b);
+  long pos = 0;
+  for (int a = 0; a < h->K; ++a) {
+    const HostBSR& q = h->q_agent[a];
+    const long off = h->pose_off[a];
+    const int na = h->n_agent[a];
+    for (int j = 0; j < na; ++j) {
+      const int beg = q.rowptr.empty() ? 0 : q.rowptr[j];
+      const int end = q.rowptr.empty() ? 0 : q.rowptr[j + 1];
+      for (int k = beg; k < end; ++k) {
+        col[pos] = static_cast<int>(off + q.col[k]);
+        std::memcpy(&blocks[pos * b * b], &q.blocks[static_cast<size_t>(k) * b * b], sizeof(double) * b * b);
+        ++pos;
+      }
+      rowptr[off + j + 1] = static_cast<int>(pos);
+    }
+  }
+  h->nnzb = nnz;
+  HIP_TRY(h->rowptr.ensure(h->N + 1));
+  HIP_TRY(h->col.ensure(col.size()));
+  HIP_TRY(h->blocks.ensure(blocks.size()));
+  HIP_TRY(h->minv.ensure(static_cast<size_t>(h->N) * b * b));
+  HIP_TRY(hipMemcpyAsync(h->rowptr.p, rowptr.data(), sizeof(int) * rowptr.size(), hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(h->col.p, col.data(), sizeof(int) * col.size(), hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(h->blocks.p, blocks.data(), sizeof(double) * blocks.size(), hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(dpgo::launch_bj_inverse(b, static_cast<int>(h->N), qview(h), 0.1, h->minv.p, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  h->q_dirty = false;
+  return DPGO_HIP_OK;
+}
+
+int sync_g(dpgo_hip_problem h) {
+  if (!h->g_dirty) return DPGO_HIP_OK;
+  const int rb = h->r * h->b;
+  std::vector<int> gidx(h->N, -1);
+  std::vector<double> gblk;
+  int slot = 0;
+  for (int a = 0; a < h->K; ++a) {
+    for (const auto& kv : h->g_agent[a]) {
+      gidx[h->pose_off[a] + kv.first] = slot++;
+      gblk.insert(gblk.end(), kv.second.begin(), kv.second.end());
+    }
+  }
+  h->num_gslots = slot;
+  HIP_TRY(h->gidx.ensure(h->N));
+  HIP_TRY(h->gblk.ensure(std::max<size_t>(gblk.size(), static_cast<size_t>(rb))));
+  HIP_TRY(hipMemcpyAsync(h->gidx.p, gidx.data(), sizeof(int) * h->N, hipMemcpyHostToDevice, h->stream));
+  if (!gblk.empty())
+    HIP_TRY(hipMemcpyAsync(h->gblk.p, gblk.data(), sizeof(double) * gblk.size(), hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  h->g_dirty = false;
+  return DPGO_HIP_OK;
+}
+
+int ensure_work(dpgo_hip_problem h) {
+  const size_t L = h->vec_len(), SL = h->s_len();
+  DevBuf<double>* vecs[] = {&h->x1, &h->x2, &h->g, &h->g2, &h->eta, &h->Heta, &h->rv,
+                            &h->z,  &h->delta, &h->Hdelta, &h->tA, &h->tB};
+  for (auto* v : vecs) HIP_TRY(v->ensure(L));
+  HIP_TRY(h->S.ensure(SL));
+  HIP_TRY(h->S2.ensure(SL));
+  return DPGO_HIP_OK;
+}
+
+int ready(dpgo_hip_problem h) {
+  DPGO_TRY(check_handle(h));
+  if (usable_devices() == 0) return fail(DPGO_HIP_ENODEV, "no gfx950 device available (no CPU fallback)");
+  DPGO_TRY(sync_q(h));
+  DPGO_TRY(sync_g(h));
+  return DPGO_HIP_OK;
+}
+
+int finalize(dpgo_hip_problem h, int op, const double* pa, int nqa, const double* pb, int nqb,
+             const dpgo::OptScalars* opt = nullptr, const int* enabled = nullptr) {
+  dpgo::FinalizeArgs f;
+  std::memset(&f, 0, sizeof(f));
+  f.op = op;
+  f.nq_a = nqa;
+  f.nq_b = nqb;
+  f.agent_tile_off = h->agent_tile_off.p;
+  f.agent_num_poses = h->agent_np.p;
+  f.agent_enabled = enabled;
+  f.pa = pa;
+  f.pb = pb;
+  f.state = h->state.p;
+  f.out_sums = h->sums.p;
+  if (opt) f.opt = *opt;
+  HIP_TRY(dpgo::launch_finalize(f, h->K, h->stream));
+  return DPGO_HIP_OK;
+}
+
+int download_sums(dpgo_hip_problem h) {
+  h->h_sums.resize(static_cast<size_t>(h->K) * 4);
+  HIP_TRY(hipMemcpyAsync(h->h_sums.data(), h->sums.p, sizeof(double) * h->h_sums.size(), hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return DPGO_HIP_OK;
+}
+
+int download_state(dpgo_hip_problem h) {
+  h->h_state.resize(h->K);
+  HIP_TRY(hipMemcpyAsync(h->h_state.data(), h->state.p, sizeof(AgentState) * h->K, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return DPGO_HIP_OK;
+}
+
+// EVAL sweep at X: g = P_X(XQ+G), S, per-agent f and |g|^2 partials into pa
+int eval_at(dpgo_hip_problem h, const double* X, double* gout, double* Sout, double* part, int flag) {
+  auto c = make_ctx(h, flag, part);
+  HIP_TRY(dpgo::launch_spmm(h->r, h->b, dpgo::MODE_EVAL, c, qview(h), X, h->gidx.p, h->gblk.p, X, nullptr,
+                            gout, Sout));
+  return DPGO_HIP_OK;
+}
+
+struct DevScratch {
+  DevBuf<double> a, b, c;
+};
+
+int upload(double* dst, const double* src, size_t n, hipStream_t s) {
+  HIP_TRY(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyHostToDevice, s));
+  return DPGO_HIP_OK;
+}
+int download(double* dst, const double* src, size_t n, hipStream_t s) {
+  HIP_TRY(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return DPGO_HIP_OK;
+}
+
+void fill_result(const AgentState& s, bool single, bool enabled, dpgo_opt_result* out) {
+  std::memset(out, 0, sizeof(*out));
+  out->success = enabled ? 1 : 0;
+  out->fInit = s.f_init;
+  out->gradNormInit = s.ngf_init;
+  if (single) {
+    const bool moved = s.runs > 0 && s.accepted && !s.gave_up;
+    out->fOpt = moved ? s.f2 : s.f_init;
+    out->gradNormOpt = moved ? s.ngf2 : s.ngf_init;
+  } else {
+    out->fOpt = s.f1;
+    out->gradNormOpt = s.ngf;
+  }
+  out->relativeChange = s.rel_change;
+  out->tCGStatus = s.tcg_status;
+  out->runs = s.runs;
+  out->outer_iters = s.outer_iters;
+  out->inner_iters = s.tcg_iters;
+  out->gave_up = s.gave_up;
+}
+
+}  // namespace
+
+// =========================================================================================
+extern "C" {
+
+const char* dpgo_hip_version(void) { return "dpgo_hip 0.1.0 (gfx950, fp64)"; }
+const char* dpgo_hip_last_error(void) { return g_last_error.c_str(); }
+int dpgo_hip_device_count(void) { return usable_devices(); }
+
+void dpgo_hip_default_params(dpgo_opt_params* p) {
+  if (!p) return;
+  p->algorithm = DPGO_ALG_RTR;
+  p->rgd_stepsize = 1e-3;
+  p->tr_iterations = 1;
+  p->tr_tolerance = 1e-2;
+  p->tr_initial_radius = 1e1;
+  p->tr_max_inner = 50;
+  p->verbose = 0;
+  p->precon = DPGO_PRECON_BLOCK_JACOBI;
+}
+
+int dpgo_hip_problem_create_batch(int num_agents, const int* poses_per_agent, int d, int r,
+                                  dpgo_hip_problem* out) {
+  if (!out) return fail(DPGO_HIP_EINVAL, "null output handle");
+  *out = nullptr;
+  if (num_agents <= 0 || !poses_per_agent) return fail(DPGO_HIP_EINVAL, "need >= 1 agent");
+  if (d != 2 && d != 3) return fail(DPGO_HIP_EINVAL, "d must be 2 or 3");
+  if (r < d || !dpgo::supported_rb(r, d + 1)) return fail(DPGO_HIP_EINVAL, "unsupported relaxation rank r");
+  for (int a = 0; a < num_agents; ++a)
+    if (poses_per_agent[a] <= 0) return fail(DPGO_HIP_EINVAL, "every agent needs >= 1 pose");
+  if (usable_devices() == 0) return fail(DPGO_HIP_ENODEV, "no gfx950 device available (no CPU fallback)");
+  auto* h = new dpgo_hip_problem_s();
+  h->K = num_agents;
+  h->d = d;
+  h->r = r;
+  h->b = d + 1;
+  h->n_agent.assign(poses_per_agent, poses_per_agent + num_agents);
+  h->pose_off.assign(num_agents + 1, 0);
+  for (int a = 0; a < num_agents; ++a) h->pose_off[a + 1] = h->pose_off[a] + poses_per_agent[a];
+  h->N = h->pose_off[num_agents];
+  if (h->N >= (1L << 31) / 16) {
+    delete h;
+    return fail(DPGO_HIP_EINVAL, "too many poses for int32 block indices");
+  }
+  // tiles of <= 64 poses that never straddle agents
+  h->h_agent_tile_off.push_back(0);
+  for (int a = 0; a < num_agents; ++a) {
+    for (int s = 0; s < poses_per_agent[a]; s += dpgo::kTilePoses) {
+      h->h_tile_agent.push_back(a);
+      h->h_tile_start.push_back(static_cast<int>(h->pose_off[a] + s));
+      h->h_tile_count.push_back(std::min(dpgo::kTilePoses, poses_per_agent[a] - s));
+    }
+    h->h_agent_tile_off.push_back(static_cast<int>(h->h_tile_agent.size()));
+  }
+  h->num_tiles = static_cast<int>(h->h_tile_agent.size());
+  h->q_agent.resize(num_agents);
+  h->g_agent.resize(num_agents);
+  auto cleanup = [&](int rc) {
+    delete h;
+    return rc;
+  };
+  if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(fail(DPGO_HIP_EDEVICE, "hipStreamCreate failed"));
+  h->stream = h->own_stream;
+  const int T = h->num_tiles;
+  if (h->tile_agent.ensure(T) || h->tile_start.ensure(T) || h->tile_count.ensure(T) ||
+      h->agent_tile_off.ensure(num_agents + 1) || h->agent_np.ensure(num_agents) ||
+      h->enabled.ensure(num_agents) || h->use_a.ensure(num_agents) || h->pa.ensure(static_cast<size_t>(T) * dpgo::kPartialStride) ||
+      h->pb.ensure(static_cast<size_t>(T) * dpgo::kPartialStride) || h->sums.ensure(static_cast<size_t>(num_agents) * 4) ||
+      h->state.ensure(num_agents) || h->coef_a.ensure(num_agents) || h->coef_b.ensure(num_agents))
+    return cleanup(fail(DPGO_HIP_ENOMEM, "device allocation failed"));
+  if (hipMemcpy(h->tile_agent.p, h->h_tile_agent.data(), sizeof(int) * T, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(h->tile_start.p, h->h_tile_start.data(), sizeof(int) * T, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(h->tile_count.p, h->h_tile_count.data(), sizeof(int) * T, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(h->agent_tile_off.p, h->h_agent_tile_off.data(), sizeof(int) * (num_agents + 1), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(h->agent_np.p, poses_per_agent, sizeof(int) * num_agents, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(h->state.p, 0, sizeof(AgentState) * num_agents) != hipSuccess)
+    return cleanup(fail(DPGO_HIP_EDEVICE, "device upload failed"));
+  // empty Q (setQ of a zero matrix, as in the reference ctor :23-24)
+  for (int a = 0; a < num_agents; ++a) h->q_agent[a].rowptr.assign(poses_per_agent[a] + 1, 0);
+  *out = h;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_problem_create(int n, int d, int r, dpgo_hip_problem* out) {
+  return dpgo_hip_problem_create_batch(1, &n, d, r, out);
+}
+
+int dpgo_hip_problem_destroy(dpgo_hip_problem h) {
+  if (!h) return DPGO_HIP_OK;
+  if (h->own_stream) {
+    (void)hipStreamSynchronize(h->own_stream);
+    (void)hipStreamDestroy(h->own_stream);
+  }
+  delete h;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_problem_set_stream(dpgo_hip_problem h, void* stream) {
+  DPGO_TRY(check_handle(h));
+  h->stream = stream ? static_cast<hipStream_t>(stream) : h->own_stream;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_problem_info(dpgo_hip_problem h, int* num_agents, int* total_poses, int* d, int* r) {
+  DPGO_TRY(check_handle(h));
+  if (num_agents) *num_agents = h->K;
+  if (total_poses) *total_poses = static_cast<int>(h->N);
+  if (d) *d = h->d;
+  if (r) *r = h->r;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_set_precon(dpgo_hip_problem h, int mode) {
+  DPGO_TRY(check_handle(h));
+  if (mode == DPGO_PRECON_EXACT)
+    return fail(DPGO_HIP_EINVAL, "exact sparse-Cholesky preconditioner not implemented yet (SURVEY 8f-1); use BLOCK_JACOBI");
+  if (mode != DPGO_PRECON_BLOCK_JACOBI && mode != DPGO_PRECON_NONE) return fail(DPGO_HIP_EINVAL, "bad preconditioner mode");
+  h->precon = mode;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_set_Q_bsr(dpgo_hip_problem h, int agent, int nbrows, const int* browptr,
+                       const int* bcolidx, const double* blocks) {
+  DPGO_TRY(check_handle(h));
+  if (agent < 0 || agent >= h->K) return fail(DPGO_HIP_EINVAL, "agent out of range");
+  if (nbrows != h->n_agent[agent]) return fail(DPGO_HIP_EINVAL, "Q block rows != poses of agent");
+  if (!browptr || browptr[0] != 0) return fail(DPGO_HIP_EINVAL, "bad block row pointer");
+  const int nnz = browptr[nbrows];
+  HostBSR q;
+  q.rowptr.assign(browptr, browptr + nbrows + 1);
+  q.col.assign(bcolidx, bcolidx + nnz);
+  for (int j = 0; j < nbrows; ++j) {
+    if (browptr[j + 1] < browptr[j]) return fail(DPGO_HIP_EINVAL, "block row pointer not monotone");
+  }
+  for (int k = 0; k < nnz; ++k)
+    if (q.col[k] < 0 || q.col[k] >= nbrows) return fail(DPGO_HIP_EINVAL, "block column out of range");
+  q.blocks.assign(blocks, blocks + static_cast<size_t>(nnz) * h->b * h->b);
+  h->q_agent[agent] = std::move(q);
+  h->q_dirty = true;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_set_Q_csr(dpgo_hip_problem h, int agent, int nrows, const int* rowptr,
+                       const int* colidx, const double* vals) {
+  DPGO_TRY(check_handle(h));
+  if (agent < 0 || agent >= h->K) return fail(DPGO_HIP_EINVAL, "agent out of range");
+  const int b = h->b, na = h->n_agent[agent];
+  if (nrows != b * na) return fail(DPGO_HIP_EINVAL, "Q rows != (d+1) n");
+  std::vector<int> browptr(na + 1, 0), bcol;
+  std::vector<double> blocks;
+  std::map<int, int> slot;
+  for (int j = 0; j < na; ++j) {
+    slot.clear();
+    for (int u = 0; u < b; ++u) {
+      const int row = j * b + u;
+      for (int k = rowptr[row]; k < rowptr[row + 1]; ++k) {
+        const int c = colidx[k];
+        if (c < 0 || c >= nrows) return fail(DPGO_HIP_EINVAL, "CSR column out of range");
+        slot.emplace(c / b, 0);
+      }
+    }
+    int base = static_cast<int>(bcol.size());
+    int idx = 0;
+    for (auto& kv : slot) {
+      kv.second = base + idx++;
+      bcol.push_back(kv.first);
+    }
+    blocks.resize(bcol.size() * b * b, 0.0);
+    for (int u = 0; u < b; ++u) {
+      const int row = j * b + u;
+      for (int k = rowptr[row]; k < rowptr[row + 1]; ++k) {
+        const int c = colidx[k];
+        const int s = slot[c / b];
+        const int w = c % b;
+        blocks[static_cast<size_t>(s) * b * b + w * b + u] += vals[k];  // column-major block
+      }
+    }
+    browptr[j + 1] = static_cast<int>(bcol.size());
+  }
+  return dpgo_hip_set_Q_bsr(h, agent, na, browptr.data(), bcol.data(), blocks.data());
+}
+
+int dpgo_hip_set_G(dpgo_hip_problem h, int agent, int count, const int* pose_idx, const double* blocks) {
+  DPGO_TRY(check_handle(h));
+  if (agent < 0 || agent >= h->K) return fail(DPGO_HIP_EINVAL, "agent out of range");
+  const int rb = h->r * h->b;
+  h->g_agent[agent].clear();
+  for (int k = 0; k < count; ++k) {
+    const int j = pose_idx[k];
+    if (j < 0 || j >= h->n_agent[agent]) return fail(DPGO_HIP_EINVAL, "G pose index out of range");
+    auto& blk = h->g_agent[agent][j];
+    if (blk.empty()) blk.assign(rb, 0.0);
+    for (int e = 0; e < rb; ++e) blk[e] += blocks[static_cast<size_t>(k) * rb + e];
+  }
+  h->g_dirty = true;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_set_G_dense(dpgo_hip_problem h, int agent, const double* G) {
+  DPGO_TRY(check_handle(h));
+  if (agent < 0 || agent >= h->K) return fail(DPGO_HIP_EINVAL, "agent out of range");
+  const int rb = h->r * h->b, na = h->n_agent[agent];
+  std::vector<int> idx;
+  std::vector<double> blk;
+  for (int j = 0; j < na; ++j) {
+    bool nz = false;
+    for (int e = 0; e < rb; ++e) nz |= G[static_cast<size_t>(j) * rb + e] != 0.0;
+    if (nz) {
+      idx.push_back(j);
+      blk.insert(blk.end(), G + static_cast<size_t>(j) * rb, G + static_cast<size_t>(j + 1) * rb);
+    }
+  }
+  return dpgo_hip_set_G(h, agent, static_cast<int>(idx.size()), idx.data(), blk.data());
+}
+
+// ---------------------------------------------------------------- device-pointer evaluations
+int dpgo_hip_egrad_dev(dpgo_hip_problem h, const double* X, double* EG) {
+  DPGO_TRY(ready(h));
+  auto c = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
+  HIP_TRY(dpgo::launch_spmm(h->r, h->b, dpgo::MODE_XQ_G, c, qview(h), X, h->gidx.p, h->gblk.p, nullptr, nullptr, EG, nullptr));
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_ehvp_dev(dpgo_hip_problem h, const double* V, double* HV) {
+  DPGO_TRY(ready(h));
+  auto c = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
+  HIP_TRY(dpgo::launch_spmm(h->r, h->b, dpgo::MODE_XQ, c, qview(h), V, nullptr, nullptr, nullptr, nullptr, HV, nullptr));
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_riegrad_dev(dpgo_hip_problem h, const double* X, double* RG) {
+  DPGO_TRY(ready(h));
+  DPGO_TRY(ensure_work(h));
+  DPGO_TRY(eval_at(h, X, RG, h->S.p, h->pa.p, dpgo::FLAG_NONE));
+  DPGO_TRY(finalize(h, dpgo::OP_SUM, h->pa.p, 2, nullptr, 0));
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_f_dev(dpgo_hip_problem h, const double* X, double* f_out_host) {
+  DPGO_TRY(ready(h));
+  DPGO_TRY(ensure_work(h));
+  DPGO_TRY(eval_at(h, X, h->tA.p, h->S.p, h->pa.p, dpgo::FLAG_NONE));
+  DPGO_TRY(finalize(h, dpgo::OP_SUM, h->pa.p, 2, nullptr, 0));
+  if (f_out_host) {
+    DPGO_TRY(download_sums(h));
+    for (int a = 0; a < h->K; ++a) f_out_host[a] = h->h_sums[a * 4 + 0];
+  }
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_rhvp_dev(dpgo_hip_problem h, const double* X, const double* V, double* HV) {
+  DPGO_TRY(ready(h));
+  DPGO_TRY(ensure_work(h));
+  DPGO_TRY(eval_at(h, X, h->tA.p, h->S.p, h->pa.p, dpgo::FLAG_NONE));
+  auto c = make_ctx(h, dpgo::FLAG_NONE, h->pb.p);
+  HIP_TRY(dpgo::launch_spmm(h->r, h->b, dpgo::MODE_HESS, c, qview(h), V, nullptr, nullptr, X, h->S.p, HV, nullptr));
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_project_polar_dev(dpgo_hip_problem h, const double* in, double* out) {
+  DPGO_TRY(check_handle(h));
+  if (usable_devices() == 0) return fail(DPGO_HIP_ENODEV, "no gfx950 device available (no CPU fallback)");
+  auto c = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
+  HIP_TRY(dpgo::launch_polar_comb(h->r, h->b, c, in, nullptr, nullptr, nullptr, out));
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_polar_combine_dev(dpgo_hip_problem h, const double* A, const double* B, const double* ca,
+                               const double* cb, double* out) {
+  DPGO_TRY(check_handle(h));
+  if (usable_devices() == 0) return fail(DPGO_HIP_ENODEV, "no gfx950 device available (no CPU fallback)");
+  HIP_TRY(hipMemcpyAsync(h->coef_a.p, ca, sizeof(double) * h->K, hipMemcpyHostToDevice, h->stream));
+  if (B) HIP_TRY(hipMemcpyAsync(h->coef_b.p, cb, sizeof(double) * h->K, hipMemcpyHostToDevice, h->stream));
+  auto c = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
+  HIP_TRY(dpgo::launch_polar_comb(h->r, h->b, c, A, B, h->coef_a.p, B ? h->coef_b.p : nullptr, out));
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_synchronize(dpgo_hip_problem h) {
+  DPGO_TRY(check_handle(h));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return DPGO_HIP_OK;
+}
+
+// --------------------------------------------------------------------------- optimisation
+int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, const double* X_in,
+                          double* X_out, const int* agent_enabled_host, dpgo_opt_result* results) {
+  DPGO_TRY(ready(h));
+  dpgo_opt_params P;
+  if (params)
+    P = *params;
+  else
+    dpgo_hip_default_params(&P);
+  if (P.precon == DPGO_PRECON_EXACT)
+    return fail(DPGO_HIP_EINVAL, "exact sparse-Cholesky preconditioner not implemented yet (SURVEY 8f-1); use BLOCK_JACOBI");
+  if (P.tr_iterations < 1 || P.tr_max_inner < 0) return fail(DPGO_HIP_EINVAL, "bad optimizer parameters");
+  DPGO_TRY(ensure_work(h));
+  const auto t0 = std::chrono::high_resolution_clock::now();
+  const int r = h->r, b = h->b, K = h->K;
+  const int pmode = P.precon == DPGO_PRECON_NONE ? dpgo::PRECON_NONE : dpgo::PRECON_BLOCK_JACOBI;
+  std::vector<int> en(K, 1);
+  if (agent_enabled_host)
+    for (int a = 0; a < K; ++a) en[a] = agent_enabled_host[a] != 0;
+  HIP_TRY(hipMemcpyAsync(h->enabled.p, en.data(), sizeof(int) * K, hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(h->x1.p, X_in, h->vec_bytes(), hipMemcpyDeviceToDevice, h->stream));
+
+  const bool single = P.algorithm == DPGO_ALG_RTR && P.tr_iterations == 1;
+  dpgo::OptScalars o;
+  std::memset(&o, 0, sizeof(o));
+  o.tol = P.tr_tolerance;
+  o.Delta0 = P.tr_initial_radius;
+  o.Delta_max = single ? P.tr_initial_radius : 5.0 * P.tr_initial_radius;
+  o.theta = 1.0;
+  o.kappa = 0.1;
+  o.min_inner = 0;
+  o.max_iter = P.tr_iterations;
+  o.single_run = single ? 1 : 0;
+
+  // f(x1), grad(x1), S(x1)  (QuadraticOptimizer::optimize :36-37, SolversTR start)
+  DPGO_TRY(eval_at(h, h->x1.p, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_NONE));
+  DPGO_TRY(finalize(h, dpgo::OP_EVAL_INIT, h->pa.p, 2, nullptr, 0, &o, h->enabled.p));
+
+  if (P.algorithm == DPGO_ALG_RGD) {
+    // one fixed-step Riemannian gradient step (QuadraticOptimizer::gradientDescent :124-149)
+    auto cr = make_ctx(h, dpgo::FLAG_NONE, h->pb.p);
+    HIP_TRY(dpgo::launch_retract(r, b, cr, h->x1.p, h->g.p, -P.rgd_stepsize, h->x2.p, nullptr, nullptr));
+    DPGO_TRY(eval_at(h, h->x2.p, h->g2.p, h->S2.p, h->pb.p, dpgo::FLAG_NONE));
+    DPGO_TRY(finalize(h, dpgo::OP_SUM, h->pb.p, 2, nullptr, 0));
+    DPGO_TRY(download_sums(h));
+    HIP_TRY(hipMemcpyAsync(h->use_a.p, en.data(), sizeof(int) * K, hipMemcpyHostToDevice, h->stream));
+    auto cs = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
+    HIP_TRY(dpgo::launch_select(r, b, cs, h->x2.p, h->x1.p, h->use_a.p, h->x1.p, X_out));
+    DPGO_TRY(finalize(h, dpgo::OP_REL_CHANGE, h->pa.p, 1, nullptr, 0));
+    DPGO_TRY(download_state(h));
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - t0).count();
+    if (results) {
+      for (int a = 0; a < K; ++a) {
+        const AgentState& s = h->h_state[a];
+        dpgo_opt_result* out = &results[a];
+        std::memset(out, 0, sizeof(*out));
+        out->success = en[a];
+        out->fInit = s.f_init;
+        out->gradNormInit = s.ngf_init;
+        out->fOpt = en[a] ? h->h_sums[a * 4] : s.f_init;
+        out->gradNormOpt = en[a] ? std::sqrt(h->h_sums[a * 4 + 1]) : s.ngf_init;
+        out->relativeChange = s.rel_change;
+        out->elapsedMs = std::floor(ms);
+        out->tCGStatus = -1;
+      }
+    }
+    return DPGO_HIP_OK;
+  }
+
+  const int max_rounds = single ? 12 : P.tr_iterations;
+  for (int round = 0; round < max_rounds; ++round) {
+    DPGO_TRY(download_state(h));
+    bool any = false;
+    for (int a = 0; a < K; ++a) any |= h->h_state[a].run_active != 0;
+    if (!any) break;
+    // ---- truncated CG (A.4)
+    auto ci = make_ctx(h, dpgo::FLAG_RUN, h->pa.p);
+    HIP_TRY(dpgo::launch_tcg_init(r, b, ci, h->x1.p, h->minv.p, pmode, h->g.p, h->eta.p, h->Heta.p, h->rv.p,
+                                  h->z.p, h->delta.p));
+    DPGO_TRY(finalize(h, dpgo::OP_TCG_INIT, h->pa.p, 2, nullptr, 0, &o));
+    for (int j = 0; j < P.tr_max_inner; ++j) {
+      auto ch = make_ctx(h, dpgo::FLAG_TCG, h->pa.p);
+      HIP_TRY(dpgo::launch_spmm(r, b, dpgo::MODE_HESS, ch, qview(h), h->delta.p, nullptr, nullptr, h->x1.p, h->S.p,
+                                h->Hdelta.p, nullptr));
+      DPGO_TRY(finalize(h, dpgo::OP_TCG_STEP, h->pa.p, 1, nullptr, 0, &o));
+      auto cu = make_ctx(h, dpgo::FLAG_TCG_MODE, h->pb.p);
+      HIP_TRY(dpgo::launch_tcg_update(r, b, cu, h->x1.p, h->minv.p, pmode, h->delta.p, h->Hdelta.p, h->eta.p,
+                                      h->Heta.p, h->rv.p, h->z.p));
+      DPGO_TRY(finalize(h, dpgo::OP_TCG_CHECK, h->pb.p, 2, nullptr, 0, &o));
+      auto cd = make_ctx(h, dpgo::FLAG_TCG, nullptr);
+      HIP_TRY(dpgo::launch_tcg_dir(r, b, cd, h->z.p, h->delta.p));
+      if (P.tr_max_inner > 10 && (j % 8) == 7) {
+        DPGO_TRY(download_state(h));
+        bool act = false;
+        for (int a = 0; a < K; ++a) act |= h->h_state[a].tcg_active != 0;
+        if (!act) break;
+      }
+    }
+    // ---- candidate x2 = R_x1(eta), rho test, radius update
+    auto cr = make_ctx(h, dpgo::FLAG_RUN, h->pa.p);
+    HIP_TRY(dpgo::launch_retract(r, b, cr, h->x1.p, h->eta.p, 1.0, h->x2.p, h->g.p, h->Heta.p));
+    DPGO_TRY(eval_at(h, h->x2.p, h->g2.p, h->S2.p, h->pb.p, dpgo::FLAG_RUN));
+    DPGO_TRY(finalize(h, dpgo::OP_RHO, h->pa.p, 2, h->pb.p, 2, &o));
+    if (!single) {
+      auto ca = make_ctx(h, dpgo::FLAG_NONE, nullptr);
+      HIP_TRY(dpgo::launch_accept(r, b, ca, h->x2.p, h->g2.p, h->S2.p, h->x1.p, h->g.p, h->S.p));
+    }
+  }
+  DPGO_TRY(download_state(h));
+  std::vector<int> use(K, 0);
+  for (int a = 0; a < K; ++a) {
+    const AgentState& s = h->h_state[a];
+    use[a] = single ? (s.runs > 0 && s.accepted && !s.gave_up) : 1;
+  }
+  HIP_TRY(hipMemcpyAsync(h->use_a.p, use.data(), sizeof(int) * K, hipMemcpyHostToDevice, h->stream));
+  auto cs = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
+  HIP_TRY(dpgo::launch_select(r, b, cs, single ? h->x2.p : h->x1.p, X_in, h->use_a.p, X_in, X_out));
+  DPGO_TRY(finalize(h, dpgo::OP_REL_CHANGE, h->pa.p, 1, nullptr, 0));
+  DPGO_TRY(download_state(h));
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - t0).count();
+  if (results) {
+    for (int a = 0; a < K; ++a) {
+      fill_result(h->h_state[a], single, en[a] != 0, &results[a]);
+      results[a].elapsedMs = std::floor(ms);
+    }
+  }
+  if (P.verbose) {
+    for (int a = 0; a < K; ++a) {
+      const AgentState& s = h->h_state[a];
+      std::printf("[dpgo_hip] agent %d: f %.6g -> %.6g, |g| %.6g -> %.6g, runs %d, tCG %d (%d its)\n", a, s.f_init,
+                  single ? s.f2 : s.f1, s.ngf_init, single ? s.ngf2 : s.ngf, s.runs, s.tcg_status, s.tcg_iters);
+    }
+  }
+  return DPGO_HIP_OK;
+}
+
+// ------------------------------------------------------------------ host-pointer variants
+namespace {
+struct HostIO {
+  dpgo_hip_problem h;
+  DevBuf<double> a, b, c;
+  int init(dpgo_hip_problem hh) {
+    h = hh;
+    HIP_TRY(a.ensure(h->vec_len()));
+    HIP_TRY(b.ensure(h->vec_len()));
+    HIP_TRY(c.ensure(h->vec_len()));
+    return DPGO_HIP_OK;
+  }
+};
+}  // namespace
+
+int dpgo_hip_f(dpgo_hip_problem h, const double* X, double* f_out) {
+  DPGO_TRY(ready(h));
+  HostIO io;
+  DPGO_TRY(io.init(h));
+  DPGO_TRY(upload(io.a.p, X, h->vec_len(), h->stream));
+  return dpgo_hip_f_dev(h, io.a.p, f_out);
+}
+
+int dpgo_hip_egrad(dpgo_hip_problem h, const double* X, double* EG) {
+  DPGO_TRY(ready(h));
+  HostIO io;
+  DPGO_TRY(io.init(h));
+  DPGO_TRY(upload(io.a.p, X, h->vec_len(), h->stream));
+  DPGO_TRY(dpgo_hip_egrad_dev(h, io.a.p, io.b.p));
+  return download(EG, io.b.p, h->vec_len(), h->stream);
+}
+
+int dpgo_hip_ehvp(dpgo_hip_problem h, const double* V, double* HV) {
+  DPGO_TRY(ready(h));
+  HostIO io;
+  DPGO_TRY(io.init(h));
+  DPGO_TRY(upload(io.a.p, V, h->vec_len(), h->stream));
+  DPGO_TRY(dpgo_hip_ehvp_dev(h, io.a.p, io.b.p));
+  return download(HV, io.b.p, h->vec_len(), h->stream);
+}
+
+int dpgo_hip_riegrad(dpgo_hip_problem h, const double* X, double* RG, double* norms, double* f_out) {
+  DPGO_TRY(ready(h));
+  HostIO io;
+  DPGO_TRY(io.init(h));
+  DPGO_TRY(upload(io.a.p, X, h->vec_len(), h->stream));
+  DPGO_TRY(dpgo_hip_riegrad_dev(h, io.a.p, io.b.p));
+  DPGO_TRY(download_sums(h));
+  for (int a = 0; a < h->K; ++a) {
+    if (norms) norms[a] = std::sqrt(h->h_sums[a * 4 + 1]);
+    if (f_out) f_out[a] = h->h_sums[a * 4 + 0];
+  }
+  if (RG) return download(RG, io.b.p, h->vec_len(), h->stream);
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_rhvp(dpgo_hip_problem h, const double* X, const double* V, double* HV) {
+  DPGO_TRY(ready(h));
+  HostIO io;
+  DPGO_TRY(io.init(h));
+  DPGO_TRY(upload(io.a.p, X, h->vec_len(), h->stream));
+  DPGO_TRY(upload(io.b.p, V, h->vec_len(), h->stream));
+  DPGO_TRY(dpgo_hip_rhvp_dev(h, io.a.p, io.b.p, io.c.p));
+  return download(HV, io.c.p, h->vec_len(), h->stream);
+}
+
+int dpgo_hip_precondition(dpgo_hip_problem h, const double* X, const double* V, double* out) {
+  DPGO_TRY(ready(h));
+  HostIO io;
+  DPGO_TRY(io.init(h));
+  DPGO_TRY(upload(io.a.p, X, h->vec_len(), h->stream));
+  DPGO_TRY(upload(io.b.p, V, h->vec_len(), h->stream));
+  auto c = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
+  const int pmode = h->precon == DPGO_PRECON_NONE ? dpgo::PRECON_NONE : dpgo::PRECON_BLOCK_JACOBI;
+  HIP_TRY(dpgo::launch_precond(h->r, h->b, c, io.a.p, h->minv.p, pmode, io.b.p, io.c.p));
+  return download(out, io.c.p, h->vec_len(), h->stream);
+}
+
+int dpgo_hip_optimize(dpgo_hip_problem h, const dpgo_opt_params* params, const double* X_in, double* X_out,
+                      dpgo_opt_result* results) {
+  DPGO_TRY(ready(h));
+  HostIO io;
+  DPGO_TRY(io.init(h));
+  DPGO_TRY(upload(io.a.p, X_in, h->vec_len(), h->stream));
+  DPGO_TRY(dpgo_hip_optimize_dev(h, params, io.a.p, io.b.p, nullptr, results));
+  return download(X_out, io.b.p, h->vec_len(), h->stream);
+}
+
+// ----------------------------------------------------------------------- stateless manifold
+namespace {
+int stateless(int r, int d, int n, const double* X, const double* V, double scale, double* out, int which) {
+  dpgo_hip_problem h = nullptr;
+  DPGO_TRY(dpgo_hip_problem_create(n, d, r, &h));
+  int rc = DPGO_HIP_OK;
+  {
+    HostIO io;
+    rc = io.init(h);
+    if (rc == DPGO_HIP_OK) rc = upload(io.a.p, X, h->vec_len(), h->stream);
+    if (rc == DPGO_HIP_OK && V) rc = upload(io.b.p, V, h->vec_len(), h->stream);
+    if (rc == DPGO_HIP_OK) {
+      auto c = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
+      hipError_t e = hipSuccess;
+      if (which == 0) e = dpgo::launch_tangent(r, d + 1, c, io.a.p, io.b.p, io.c.p);
+      if (which == 1) e = dpgo::launch_retract(r, d + 1, c, io.a.p, io.b.p, scale, io.c.p, nullptr, nullptr);
+      if (which == 2) e = dpgo::launch_polar_comb(r, d + 1, c, io.a.p, nullptr, nullptr, nullptr, io.c.p);
+      if (e != hipSuccess) rc = fail(DPGO_HIP_EDEVICE, hipGetErrorString(e));
+    }
+    if (rc == DPGO_HIP_OK) rc = download(out, io.c.p, h->vec_len(), h->stream);
+  }
+  dpgo_hip_problem_destroy(h);
+  return rc;
+}
+}  // namespace
+
+int dpgo_hip_tangent_project(int r, int d, int n, const double* X, const double* V, double* out) {
+  return stateless(r, d, n, X, V, 1.0, out, 0);
+}
+int dpgo_hip_retract_qf(int r, int d, int n, const double* X, const double* V, double scale, double* out) {
+  return stateless(r, d, n, X, V, scale, out, 1);
+}
+int dpgo_hip_project_polar(int r, int d, int n, const double* in, double* out) {
+  return stateless(r, d, n, in, nullptr, 1.0, out, 2);
+}
+
+// ----------------------------------------------------------------------- measurement
+double dpgo_hip_spmm_bytes(dpgo_hip_problem h) {
+  if (!h) return 0.0;
+  const double b = h->b;
+  long nnz = 0;
+  for (int a = 0; a < h->K; ++a) nnz += static_cast<long>(h->q_agent[a].col.size());
+  return static_cast<double>(nnz) * (b * b * 8.0 + 4.0) + static_cast<double>(h->N + 1) * 4.0 +
+         2.0 * static_cast<double>(h->r) * b * static_cast<double>(h->N) * 8.0;
+}
+
+int dpgo_hip_bench_spmm(dpgo_hip_problem h, const double* X_dev, double* Y_dev, int reps, double* ms) {
+  DPGO_TRY(ready(h));
+  if (reps <= 0 || !ms) return fail(DPGO_HIP_EINVAL, "reps must be > 0");
+  hipEvent_t e0, e1;
+  HIP_TRY(hipEventCreate(&e0));
+  HIP_TRY(hipEventCreate(&e1));
+  auto c = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
+  HIP_TRY(hipEventRecord(e0, h->stream));
+  for (int i = 0; i < reps; ++i)
+    HIP_TRY(dpgo::launch_spmm(h->r, h->b, dpgo::MODE_XQ, c, qview(h), X_dev, nullptr, nullptr, nullptr, nullptr, Y_dev, nullptr));
+  HIP_TRY(hipEventRecord(e1, h->stream));
+  HIP_TRY(hipEventSynchronize(e1));
+  float t = 0.f;
+  HIP_TRY(hipEventElapsedTime(&t, e0, e1));
+  *ms = static_cast<double>(t) / reps;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return DPGO_HIP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,268 @@
+// Device-side building blocks shared by the DPGO HIP kernels (gfx950 / CDNA4, fp64).
+//
+// Lane mapping used by every per-pose kernel ("pose quad"):
+//   a 64-lane wavefront handles 16 poses; the 4 lanes of a DPP quad belong to one pose and
+//   lane k = lane & 3 owns column k of the r x (d+1) pose block X_j = [Y_j | p_j]
+//   (column-major, so column k is r contiguous doubles).  For d = 2 (b = 3) lane 3 of each
+//   quad is idle.  A workgroup of 256 threads (4 waves) covers one tile of 64 poses.
+// Cross-lane traffic inside a quad uses DPP quad_perm moves (no LDS).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dpgo {
+
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kThreads = 256;
+constexpr int kPosesPerWave = 16;
+constexpr int kTilePoses = 64;
+
+// ---- per-agent scalar state of the on-device RTR / tCG state machine -------------------
+struct AgentState {
+  double f1, ngf, f2, ngf2;       // cost / Riemannian-gradient norm at x1 and at x2
+  double f_init, ngf_init;        // statistics before optimisation
+  double Delta, Delta_max;        // trust-region radius
+  double e_Pe, e_Pd, d_Pd, z_r;   // tCG recurrences
+  double norm_r0, alpha, tau, beta, step;
+  double g_eta, eta_Heta, rho, rel_change;
+  int tcg_active;   // tCG still iterating
+  int tcg_mode;     // update kernel: 0 CG step (alpha), 1 boundary step (tau) + stop, 2 idle
+  int tcg_status;   // 0 NEGCURVTURE 1 EXCREGION 2 LCON 3 SCON 4 MAXITER, -1 none
+  int tcg_iters;    // inner iterations of the last tCG
+  int run_active;   // participates in the current RTR Run
+  int accepted;     // last step accepted (rho > 0.1)
+  int runs;         // number of Run() calls (rejection retries)
+  int outer_iters;  // accepted + rejected outer iterations
+  int gave_up;      // too many rejections -> returns the input
+  int copy_pending;  // multi-iteration Run: accepted step still to be copied into x1
+  int pad1, pad2;
+};
+
+// ---- DPP quad helpers -------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long l = __double_as_longlong(v);
+  int lo = static_cast<int>(l);
+  int hi = static_cast<int>(l >> 32);
+  lo = __builtin_amdgcn_mov_dpp(lo, CTRL, 0xF, 0xF, false);
+  hi = __builtin_amdgcn_mov_dpp(hi, CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) |
+                              static_cast<unsigned int>(lo));
+}
+
+// broadcast lane K of the quad to all 4 lanes
+template <int K>
+__device__ __forceinline__ double qbcast(double v) {
+  return dpp_f64<K | (K << 2) | (K << 4) | (K << 6)>(v);
+}
+
+// sum over the 4 lanes of the quad; every lane gets the bitwise-identical result
+__device__ __forceinline__ double qsum(double v) {
+  v += dpp_f64<0xB1>(v);  // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);  // quad_perm [2,3,0,1]
+  return v;
+}
+
+// deterministic full-wave sum (butterfly); every lane gets the total
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Gather a full pose from per-lane columns: full[a][c] = column c held by lane c.
+template <int R, int B>
+__device__ __forceinline__ void quad_gather(const double (&col)[R], double (&full)[R][B]) {
+#pragma unroll
+  for (int a = 0; a < R; ++a) {
+    full[a][0] = qbcast<0>(col[a]);
+    full[a][1] = qbcast<1>(col[a]);
+    full[a][2] = qbcast<2>(col[a]);
+    if constexpr (B > 3) full[a][3] = qbcast<3>(col[a]);
+  }
+}
+
+// Load column k (R doubles) of pose j from a column-major r x (b n) array.
+template <int R, int B>
+__device__ __forceinline__ void load_col(const double* __restrict__ P, long j, int k, bool ok,
+                                         double (&col)[R]) {
+  if (ok && k < B) {
+    const double* p = P + j * (R * B) + k * R;
+#pragma unroll
+    for (int a = 0; a < R; ++a) col[a] = p[a];
+  } else {
+#pragma unroll
+    for (int a = 0; a < R; ++a) col[a] = 0.0;
+  }
+}
+
+template <int R, int B>
+__device__ __forceinline__ void store_col(double* __restrict__ P, long j, int k, bool ok,
+                                          const double (&full)[R][B]) {
+  if (ok && k < B) {
+    double* p = P + j * (R * B) + k * R;
+#pragma unroll
+    for (int a = 0; a < R; ++a) {
+      double v = full[a][0];
+      if (k == 1) v = full[a][1];
+      if (k == 2) v = full[a][2];
+      if constexpr (B > 3) {
+        if (k == 3) v = full[a][3];
+      }
+      p[a] = v;
+    }
+  }
+}
+
+template <int R, int B>
+__device__ __forceinline__ double col_dot(const double (&A)[R][B], const double (&C)[R][B], int k) {
+  double s = 0.0;
+#pragma unroll
+  for (int c = 0; c < B; ++c) {
+    if (c == k) {
+#pragma unroll
+      for (int a = 0; a < R; ++a) s = fma(A[a][c], C[a][c], s);
+    }
+  }
+  return s;
+}
+
+// S = sym(Y^T M_Y), Y = first D = B-1 columns
+template <int R, int B>
+__device__ __forceinline__ void sym_ytm(const double (&X)[R][B], const double (&M)[R][B],
+                                        double (&S)[B - 1][B - 1]) {
+  constexpr int D = B - 1;
+  double T[D][D];
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      double s = 0.0;
+#pragma unroll
+      for (int a = 0; a < R; ++a) s = fma(X[a][p], M[a][q], s);
+      T[p][q] = s;
+    }
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int q = 0; q < D; ++q) S[p][q] = 0.5 * (T[p][q] + T[q][p]);
+}
+
+// M_Y <- M_Y - Y S   (tangent projection given S = sym(Y^T M_Y), or Hessian correction)
+template <int R, int B>
+__device__ __forceinline__ void sub_y_times(const double (&X)[R][B], const double (&S)[B - 1][B - 1],
+                                            double (&M)[R][B]) {
+  constexpr int D = B - 1;
+#pragma unroll
+  for (int a = 0; a < R; ++a)
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      double s = M[a][q];
+#pragma unroll
+      for (int p = 0; p < D; ++p) s = fma(-X[a][p], S[p][q], s);
+      M[a][q] = s;
+    }
+}
+
+template <int R, int B>
+__device__ __forceinline__ void tangent_project_pose(const double (&X)[R][B], double (&V)[R][B]) {
+  double S[B - 1][B - 1];
+  sym_ytm<R, B>(X, V, S);
+  sub_y_times<R, B>(X, S, V);
+}
+
+// Q factor (positive diagonal R) of the R x D matrix M (in place), classical Gram-Schmidt
+// applied twice ("twice is enough") -- unique Q for full-rank M, matches Householder + sign fix.
+template <int R, int D>
+__device__ __forceinline__ void qf_inplace(double (&M)[R][D + 1]) {
+#pragma unroll
+  for (int q = 0; q < D; ++q) {
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int p = 0; p < q; ++p) {
+        double s = 0.0;
+#pragma unroll
+        for (int a = 0; a < R; ++a) s = fma(M[a][p], M[a][q], s);
+#pragma unroll
+        for (int a = 0; a < R; ++a) M[a][q] = fma(-s, M[a][p], M[a][q]);
+      }
+    }
+    double nn = 0.0;
+#pragma unroll
+    for (int a = 0; a < R; ++a) nn = fma(M[a][q], M[a][q], nn);
+    const double inv = 1.0 / sqrt(nn);
+#pragma unroll
+    for (int a = 0; a < R; ++a) M[a][q] *= inv;
+  }
+}
+
+// Polar factor U V^T of the R x D matrix held in the first D columns of M (in place), via
+// one-sided Jacobi SVD (columns rotated pairwise until orthogonal; V accumulated).
+template <int R, int D>
+__device__ __forceinline__ void polar_inplace(double (&M)[R][D + 1]) {
+  double V[D][D];
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int q = 0; q < D; ++q) V[p][q] = (p == q) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 30; ++sweep) {
+    bool rotated = false;
+#pragma unroll
+    for (int p = 0; p < D - 1; ++p) {
+#pragma unroll
+      for (int q = p + 1; q < D; ++q) {
+        double alpha = 0.0, beta = 0.0, gamma = 0.0;
+#pragma unroll
+        for (int a = 0; a < R; ++a) {
+          alpha = fma(M[a][p], M[a][p], alpha);
+          beta = fma(M[a][q], M[a][q], beta);
+          gamma = fma(M[a][p], M[a][q], gamma);
+        }
+        if (fabs(gamma) > 1e-17 * sqrt(alpha * beta) && gamma != 0.0) {
+          rotated = true;
+          const double zeta = (beta - alpha) / (2.0 * gamma);
+          const double t = copysign(1.0, zeta) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+          const double c = 1.0 / sqrt(1.0 + t * t);
+          const double s = c * t;
+#pragma unroll
+          for (int a = 0; a < R; ++a) {
+            const double mp = M[a][p], mq = M[a][q];
+            M[a][p] = c * mp - s * mq;
+            M[a][q] = s * mp + c * mq;
+          }
+#pragma unroll
+          for (int a = 0; a < D; ++a) {
+            const double vp = V[a][p], vq = V[a][q];
+            V[a][p] = c * vp - s * vq;
+            V[a][q] = s * vp + c * vq;
+          }
+        }
+      }
+    }
+    if (!rotated) break;
+  }
+  // U = M diag(1/sigma); polar = U V^T
+  double U[R][D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) {
+    double nn = 0.0;
+#pragma unroll
+    for (int a = 0; a < R; ++a) nn = fma(M[a][q], M[a][q], nn);
+    const double inv = nn > 0.0 ? 1.0 / sqrt(nn) : 0.0;
+#pragma unroll
+    for (int a = 0; a < R; ++a) U[a][q] = M[a][q] * inv;
+  }
+#pragma unroll
+  for (int a = 0; a < R; ++a)
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      double s = 0.0;
+#pragma unroll
+      for (int p = 0; p < D; ++p) s = fma(U[a][p], V[q][p], s);
+      M[a][q] = s;
+    }
+}
+
+}  // namespace dpgo

@@ -1,0 +1,901 @@
+// fp64 HIP kernels for the DPGO RBCD hot path on gfx950 (MI355X).
+//
+// Reference semantics (file:line relative to the reference root):
+//   QuadraticProblem f / EucGrad / EucHessianEta / PreConditioner / RieGrad
+//                                   src/QuadraticProblem.cpp:50-101
+//   LiftedSEManifold projection / QF retraction / polar project
+//                                   src/manifold/LiftedSEManifold.cpp:16-45, src/DPGO_utils.cpp:494-500
+//   ROPTLIB RTRNewton / tCG          SURVEY.md Appendix A.4 (restated; un-vendored dependency)
+//
+// Every kernel works on a *tile set*: tile t covers up to 64 consecutive poses of one agent
+// (agents = independent RBCD blocks batched into one launch).  See dpgo_device.h for the
+// pose-quad lane mapping.
+#include "dpgo_device.h"
+#include "kernels.h"
+
+namespace dpgo {
+
+__device__ __forceinline__ bool tile_skipped(const LaunchCtx& c, int agent) {
+  if (c.flag_kind == FLAG_NONE || c.state == nullptr) return false;
+  const AgentState& s = c.state[agent];
+  if (c.flag_kind == FLAG_RUN) return s.run_active == 0;
+  if (c.flag_kind == FLAG_TCG) return s.tcg_active == 0;
+  if (c.flag_kind == FLAG_TCG_MODE) return s.tcg_mode == 2;
+  return false;
+}
+
+template <int R, int B>
+__device__ __forceinline__ void select_col(const double (&F)[R][B], int k, double (&c)[R]) {
+  // Per-lane column pick.  The empty asm pins the candidates as SSA registers so the compiler
+  // cannot fold the selects into a dynamically indexed (scratch) load of the array.
+#pragma unroll
+  for (int a = 0; a < R; ++a) {
+    double v0 = F[a][0], v1 = F[a][1], v2 = F[a][2];
+    double v3 = B > 3 ? F[a][B > 3 ? 3 : 0] : v0;
+    asm("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));
+    c[a] = (k & 2) ? ((k & 1) ? v3 : v2) : ((k & 1) ? v1 : v0);
+  }
+}
+
+template <int R>
+__device__ __forceinline__ void store_vec(double* __restrict__ P, long off, bool ok,
+                                          const double (&c)[R]) {
+  if (ok) {
+#pragma unroll
+    for (int a = 0; a < R; ++a) P[off + a] = c[a];
+  }
+}
+
+template <int NQ>
+__device__ __forceinline__ void block_partials(double (&v)[NQ], double* __restrict__ partials,
+                                               int tile) {
+  __shared__ double red[4][NQ > 0 ? NQ : 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) v[q] = wave_sum(v[q]);
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) red[wave][q] = v[q];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      partials[tile * kPartialStride + q] = ((red[0][q] + red[1][q]) + red[2][q]) + red[3][q];
+  }
+}
+
+struct PoseLane {
+  int lane, wave, k, tile, agent, pslot;
+  long j;
+  bool ok;
+  int kk;  // column this lane owns (k < B) else -1
+};
+
+template <int B>
+__device__ __forceinline__ PoseLane pose_lane(const LaunchCtx& c) {
+  PoseLane p;
+  p.lane = threadIdx.x & 63;
+  p.wave = threadIdx.x >> 6;
+  p.k = p.lane & 3;
+  p.tile = blockIdx.x;
+  p.agent = c.tile_agent[p.tile];
+  p.pslot = p.wave * kPosesPerWave + (p.lane >> 2);
+  p.ok = p.pslot < c.tile_count[p.tile];
+  p.j = static_cast<long>(c.tile_start[p.tile]) + p.pslot;
+  p.kk = p.k < B ? p.k : -1;
+  return p;
+}
+
+// ------------------------------------------------------------------------------------------
+// X.Q SpMM over the symmetric block-sparse connection Laplacian with fused epilogues.
+//   MODE_XQ    out = in Q                                   (EucHessianEta, :68-73)
+//   MODE_XQ_G  out = in Q + G                               (EucGrad, :62-66)
+//   MODE_EVAL  g = P_X(in Q + G), S = sym(Y^T (XQ+G)_Y), f and |g|^2 partials
+//                                                           (f :50-60, RieGrad :89-97)
+//   MODE_HESS  out = P_X(in Q - [in_Y S | 0]), <in, out> partial (Riemannian Hessian, A.3)
+// BSR storage: block-row j lists neighbours i with block (j,i) of Q column-major, which is
+// block (i,j) row-major (Q symmetric), so lane k streams row k of Q_ij: Y_j += X_i[:,k] Q_ij[k,:].
+// ------------------------------------------------------------------------------------------
+template <int R, int B, int MODE>
+__global__ __launch_bounds__(kThreads) void k_spmm(LaunchCtx c, QView q, const double* __restrict__ in,
+                                                   const int* __restrict__ gidx,
+                                                   const double* __restrict__ gblk,
+                                                   const double* __restrict__ X,
+                                                   const double* __restrict__ S_in,
+                                                   double* __restrict__ out,
+                                                   double* __restrict__ S_out) {
+  constexpr int D = B - 1;
+  const PoseLane p = pose_lane<B>(c);
+  if (tile_skipped(c, p.agent)) return;
+
+  double acc[R][B];
+#pragma unroll
+  for (int a = 0; a < R; ++a)
+#pragma unroll
+    for (int cc = 0; cc < B; ++cc) acc[a][cc] = 0.0;
+
+  if (p.ok && p.k < B) {
+    const int beg = q.rowptr[p.j], end = q.rowptr[p.j + 1];
+    for (int nz = beg; nz < end; ++nz) {
+      const long i = q.col[nz];
+      const double* brow = q.blocks + static_cast<long>(nz) * (B * B) + p.k * B;
+      const double* xk = in + i * (R * B) + p.k * R;
+      double bb[B], xx[R];
+      if constexpr (B == 4) {
+        const f64x2 b0 = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(brow));
+        const f64x2 b1 = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(brow) + 1);
+        bb[0] = b0.x; bb[1] = b0.y; bb[2] = b1.x; bb[3] = b1.y;
+      } else {
+#pragma unroll
+        for (int cc = 0; cc < B; ++cc) bb[cc] = __builtin_nontemporal_load(brow + cc);
+      }
+#pragma unroll
+      for (int a = 0; a < R; ++a) xx[a] = xk[a];
+#pragma unroll
+      for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int cc = 0; cc < B; ++cc) acc[a][cc] = fma(xx[a], bb[cc], acc[a][cc]);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < R; ++a)
+#pragma unroll
+    for (int cc = 0; cc < B; ++cc) acc[a][cc] = qsum(acc[a][cc]);
+
+  const long off = p.j * (R * B) + p.k * R;
+  const bool own = p.ok && p.k < B;
+
+  if constexpr (MODE == MODE_XQ) {
+    double col[R];
+    select_col<R, B>(acc, p.k, col);
+    store_vec<R>(out, off, own, col);
+  } else if constexpr (MODE == MODE_XQ_G) {
+    double col[R];
+    select_col<R, B>(acc, p.k, col);
+    if (own && gidx != nullptr) {
+      const int slot = gidx[p.j];
+      if (slot >= 0) {
+#pragma unroll
+        for (int a = 0; a < R; ++a) col[a] += gblk[static_cast<long>(slot) * (R * B) + p.k * R + a];
+      }
+    }
+    store_vec<R>(out, off, own, col);
+  } else if constexpr (MODE == MODE_EVAL) {
+    double xcol[R], gcol[R], qcol[R];
+    load_col<R, B>(X, p.j, p.k, p.ok, xcol);
+#pragma unroll
+    for (int a = 0; a < R; ++a) gcol[a] = 0.0;
+    if (own && gidx != nullptr) {
+      const int slot = gidx[p.j];
+      if (slot >= 0) {
+#pragma unroll
+        for (int a = 0; a < R; ++a) gcol[a] = gblk[static_cast<long>(slot) * (R * B) + p.k * R + a];
+      }
+    }
+    select_col<R, B>(acc, p.k, qcol);
+    double fpart = 0.0;
+#pragma unroll
+    for (int a = 0; a < R; ++a) fpart = fma(fma(0.5, qcol[a], gcol[a]), xcol[a], fpart);
+    double Xf[R][B], Gf[R][B];
+    quad_gather<R, B>(xcol, Xf);
+    quad_gather<R, B>(gcol, Gf);
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int cc = 0; cc < B; ++cc) acc[a][cc] += Gf[a][cc];
+    double S[D][D];
+    sym_ytm<R, B>(Xf, acc, S);
+    sub_y_times<R, B>(Xf, S, acc);
+    double gc[R];
+    select_col<R, B>(acc, p.k, gc);
+    double gpart = 0.0;
+#pragma unroll
+    for (int a = 0; a < R; ++a) gpart = fma(gc[a], gc[a], gpart);
+    store_vec<R>(out, off, own, gc);
+    if (p.ok && p.k == 0 && S_out != nullptr) {
+#pragma unroll
+      for (int u = 0; u < D; ++u)
+#pragma unroll
+        for (int v = 0; v < D; ++v) S_out[p.j * (D * D) + u * D + v] = S[u][v];
+    }
+    double parts[2] = {own ? fpart : 0.0, own ? gpart : 0.0};
+    block_partials<2>(parts, c.partials, p.tile);
+  } else if constexpr (MODE == MODE_HESS) {
+    double vcol[R], xcol[R];
+    load_col<R, B>(in, p.j, p.k, p.ok, vcol);
+    load_col<R, B>(X, p.j, p.k, p.ok, xcol);
+    double S[D][D];
+#pragma unroll
+    for (int u = 0; u < D; ++u)
+#pragma unroll
+      for (int v = 0; v < D; ++v) S[u][v] = p.ok ? S_in[p.j * (D * D) + u * D + v] : 0.0;
+    double Vf[R][B], Xf[R][B];
+    quad_gather<R, B>(vcol, Vf);
+    quad_gather<R, B>(xcol, Xf);
+    sub_y_times<R, B>(Vf, S, acc);  // VQ - V_Y S
+    tangent_project_pose<R, B>(Xf, acc);
+    double hc[R];
+    select_col<R, B>(acc, p.k, hc);
+    double dpart = 0.0;
+#pragma unroll
+    for (int a = 0; a < R; ++a) dpart = fma(vcol[a], hc[a], dpart);
+    store_vec<R>(out, off, own, hc);
+    double parts[1] = {own ? dpart : 0.0};
+    block_partials<1>(parts, c.partials, p.tile);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Block-Jacobi preconditioner applied to a full pose: z = P_X(v (Q_jj + 0.1 I)^-1)
+// (block-diagonal stand-in for src/QuadraticProblem.cpp:75-87).
+// Minv stored row-major per pose.
+// ------------------------------------------------------------------------------------------
+template <int R, int B>
+__device__ __forceinline__ void precond_pose(const double (&Xf)[R][B], const double* __restrict__ Minv,
+                                             long j, bool ok, int mode, const double (&v)[R][B],
+                                             double (&z)[R][B]) {
+  if (mode == PRECON_NONE) {
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int cc = 0; cc < B; ++cc) z[a][cc] = v[a][cc];
+    return;
+  }
+  double M[B][B];
+#pragma unroll
+  for (int u = 0; u < B; ++u)
+#pragma unroll
+    for (int w = 0; w < B; ++w) M[u][w] = ok ? Minv[j * (B * B) + u * B + w] : 0.0;
+#pragma unroll
+  for (int a = 0; a < R; ++a)
+#pragma unroll
+    for (int cc = 0; cc < B; ++cc) {
+      double s = 0.0;
+#pragma unroll
+      for (int u = 0; u < B; ++u) s = fma(v[a][u], M[u][cc], s);
+      z[a][cc] = s;
+    }
+  tangent_project_pose<R, B>(Xf, z);
+}
+
+// tCG start (A.4): eta = 0, Heta = 0, r = grad, z = Prec(r), delta = -z; partials <z,r>, |r|^2
+template <int R, int B>
+__global__ __launch_bounds__(kThreads) void k_tcg_init(LaunchCtx c, const double* __restrict__ X,
+                                                       const double* __restrict__ Minv, int pmode,
+                                                       const double* __restrict__ g,
+                                                       double* __restrict__ eta, double* __restrict__ Heta,
+                                                       double* __restrict__ r, double* __restrict__ z,
+                                                       double* __restrict__ delta) {
+  const PoseLane p = pose_lane<B>(c);
+  if (tile_skipped(c, p.agent)) return;
+  const bool own = p.ok && p.k < B;
+  const long off = p.j * (R * B) + p.k * R;
+  double gcol[R], xcol[R], zero[R];
+  load_col<R, B>(g, p.j, p.k, p.ok, gcol);
+  load_col<R, B>(X, p.j, p.k, p.ok, xcol);
+#pragma unroll
+  for (int a = 0; a < R; ++a) zero[a] = 0.0;
+  double Gf[R][B], Xf[R][B], Zf[R][B];
+  quad_gather<R, B>(gcol, Gf);
+  quad_gather<R, B>(xcol, Xf);
+  precond_pose<R, B>(Xf, Minv, p.j, p.ok, pmode, Gf, Zf);
+  double zc[R], dc[R];
+  select_col<R, B>(Zf, p.k, zc);
+  double zr = 0.0, rr = 0.0;
+#pragma unroll
+  for (int a = 0; a < R; ++a) {
+    zr = fma(zc[a], gcol[a], zr);
+    rr = fma(gcol[a], gcol[a], rr);
+    dc[a] = -zc[a];
+  }
+  store_vec<R>(eta, off, own, zero);
+  store_vec<R>(Heta, off, own, zero);
+  store_vec<R>(r, off, own, gcol);
+  store_vec<R>(z, off, own, zc);
+  store_vec<R>(delta, off, own, dc);
+  double parts[2] = {own ? zr : 0.0, own ? rr : 0.0};
+  block_partials<2>(parts, c.partials, p.tile);
+}
+
+// tCG step (A.4 steps 1-3, 5 first half): eta += s delta; Heta += s Hdelta; for a CG step
+// (mode 0) also r += alpha Hdelta and z = Prec(r) with partials <z,r>, |r|^2.
+template <int R, int B>
+__global__ __launch_bounds__(kThreads) void k_tcg_update(LaunchCtx c, const double* __restrict__ X,
+                                                         const double* __restrict__ Minv, int pmode,
+                                                         const double* __restrict__ delta,
+                                                         const double* __restrict__ Hdelta,
+                                                         double* __restrict__ eta, double* __restrict__ Heta,
+                                                         double* __restrict__ r, double* __restrict__ z) {
+  const PoseLane p = pose_lane<B>(c);
+  if (tile_skipped(c, p.agent)) return;  // FLAG_TCG_MODE: skips mode 2
+  const AgentState& st = c.state[p.agent];
+  const int mode = st.tcg_mode;
+  const double step = st.step;
+  const bool own = p.ok && p.k < B;
+  const long off = p.j * (R * B) + p.k * R;
+  double dcol[R], hcol[R], ecol[R], hecol[R];
+  load_col<R, B>(delta, p.j, p.k, p.ok, dcol);
+  load_col<R, B>(Hdelta, p.j, p.k, p.ok, hcol);
+  load_col<R, B>(eta, p.j, p.k, p.ok, ecol);
+  load_col<R, B>(Heta, p.j, p.k, p.ok, hecol);
+#pragma unroll
+  for (int a = 0; a < R; ++a) {
+    ecol[a] = fma(step, dcol[a], ecol[a]);
+    hecol[a] = fma(step, hcol[a], hecol[a]);
+  }
+  store_vec<R>(eta, off, own, ecol);
+  store_vec<R>(Heta, off, own, hecol);
+  if (mode != 0) return;  // boundary step: tCG stops, r/z untouched (uniform per agent)
+  double rcol[R], xcol[R];
+  load_col<R, B>(r, p.j, p.k, p.ok, rcol);
+  load_col<R, B>(X, p.j, p.k, p.ok, xcol);
+#pragma unroll
+  for (int a = 0; a < R; ++a) rcol[a] = fma(step, hcol[a], rcol[a]);
+  double Rf[R][B], Xf[R][B], Zf[R][B];
+  quad_gather<R, B>(rcol, Rf);
+  quad_gather<R, B>(xcol, Xf);
+  precond_pose<R, B>(Xf, Minv, p.j, p.ok, pmode, Rf, Zf);
+  double zc[R];
+  select_col<R, B>(Zf, p.k, zc);
+  double zr = 0.0, rr = 0.0;
+#pragma unroll
+  for (int a = 0; a < R; ++a) {
+    zr = fma(zc[a], rcol[a], zr);
+    rr = fma(rcol[a], rcol[a], rr);
+  }
+  store_vec<R>(r, off, own, rcol);
+  store_vec<R>(z, off, own, zc);
+  double parts[2] = {own ? zr : 0.0, own ? rr : 0.0};
+  block_partials<2>(parts, c.partials, p.tile);
+}
+
+// delta = -z + beta delta for agents whose tCG continues (A.4 step 5)
+template <int R, int B>
+__global__ __launch_bounds__(kThreads) void k_tcg_dir(LaunchCtx c, const double* __restrict__ z,
+                                                      double* __restrict__ delta) {
+  const PoseLane p = pose_lane<B>(c);
+  if (tile_skipped(c, p.agent)) return;  // FLAG_TCG
+  const double beta = c.state[p.agent].beta;
+  const bool own = p.ok && p.k < B;
+  if (!own) return;
+  const long off = p.j * (R * B) + p.k * R;
+#pragma unroll
+  for (int a = 0; a < R; ++a) delta[off + a] = fma(beta, delta[off + a], -z[off + a]);
+}
+
+// x2 = R_x1(scale * eta) (QF retraction, A.2) with partials <g,eta>, <eta,Heta>
+template <int R, int B>
+__global__ __launch_bounds__(kThreads) void k_retract(LaunchCtx c, const double* __restrict__ X,
+                                                      const double* __restrict__ V, double scale,
+                                                      double* __restrict__ out,
+                                                      const double* __restrict__ g,
+                                                      const double* __restrict__ HV) {
+  constexpr int D = B - 1;
+  const PoseLane p = pose_lane<B>(c);
+  if (tile_skipped(c, p.agent)) return;
+  const bool own = p.ok && p.k < B;
+  const long off = p.j * (R * B) + p.k * R;
+  double xcol[R], vcol[R];
+  load_col<R, B>(X, p.j, p.k, p.ok, xcol);
+  load_col<R, B>(V, p.j, p.k, p.ok, vcol);
+  double mcol[R];
+#pragma unroll
+  for (int a = 0; a < R; ++a) mcol[a] = fma(scale, vcol[a], xcol[a]);
+  double Mf[R][B];
+  quad_gather<R, B>(mcol, Mf);
+  qf_inplace<R, D>(Mf);
+  double oc[R];
+  select_col<R, B>(Mf, p.k, oc);
+  store_vec<R>(out, off, own, oc);
+  if (g != nullptr) {
+    double gcol[R], hcol[R];
+    load_col<R, B>(g, p.j, p.k, p.ok, gcol);
+    load_col<R, B>(HV, p.j, p.k, p.ok, hcol);
+    double ge = 0.0, eh = 0.0;
+#pragma unroll
+    for (int a = 0; a < R; ++a) {
+      ge = fma(gcol[a], vcol[a], ge);
+      eh = fma(vcol[a], hcol[a], eh);
+    }
+    double parts[2] = {own ? ge : 0.0, own ? eh : 0.0};
+    block_partials<2>(parts, c.partials, p.tile);
+  }
+}
+
+// out = P_X(V) (ROPTLIB ProductManifold::Projection, A.2)
+template <int R, int B>
+__global__ __launch_bounds__(kThreads) void k_tangent(LaunchCtx c, const double* __restrict__ X,
+                                                      const double* __restrict__ V,
+                                                      double* __restrict__ out) {
+  const PoseLane p = pose_lane<B>(c);
+  if (tile_skipped(c, p.agent)) return;
+  const bool own = p.ok && p.k < B;
+  const long off = p.j * (R * B) + p.k * R;
+  double xcol[R], vcol[R];
+  load_col<R, B>(X, p.j, p.k, p.ok, xcol);
+  load_col<R, B>(V, p.j, p.k, p.ok, vcol);
+  double Xf[R][B], Vf[R][B];
+  quad_gather<R, B>(xcol, Xf);
+  quad_gather<R, B>(vcol, Vf);
+  tangent_project_pose<R, B>(Xf, Vf);
+  double oc[R];
+  select_col<R, B>(Vf, p.k, oc);
+  store_vec<R>(out, off, own, oc);
+}
+
+// out = P_X(V Minv) (QuadraticProblem::PreConditioner, block-Jacobi)
+template <int R, int B>
+__global__ __launch_bounds__(kThreads) void k_precond(LaunchCtx c, const double* __restrict__ X,
+                                                      const double* __restrict__ Minv, int pmode,
+                                                      const double* __restrict__ V,
+                                                      double* __restrict__ out) {
+  const PoseLane p = pose_lane<B>(c);
+  if (tile_skipped(c, p.agent)) return;
+  const bool own = p.ok && p.k < B;
+  const long off = p.j * (R * B) + p.k * R;
+  double xcol[R], vcol[R];
+  load_col<R, B>(X, p.j, p.k, p.ok, xcol);
+  load_col<R, B>(V, p.j, p.k, p.ok, vcol);
+  double Xf[R][B], Vf[R][B], Zf[R][B];
+  quad_gather<R, B>(xcol, Xf);
+  quad_gather<R, B>(vcol, Vf);
+  precond_pose<R, B>(Xf, Minv, p.j, p.ok, pmode, Vf, Zf);
+  double oc[R];
+  select_col<R, B>(Zf, p.k, oc);
+  store_vec<R>(out, off, own, oc);
+}
+
+// out = LiftedSEManifold::project(ca A + cb B) with per-agent coefficients (cb ignored if B null)
+// (src/manifold/LiftedSEManifold.cpp:34-45; Nesterov updateY/updateV src/PGOAgent.cpp:1075-1091)
+template <int R, int B>
+__global__ __launch_bounds__(kThreads) void k_polar_comb(LaunchCtx c, const double* __restrict__ A,
+                                                         const double* __restrict__ Bv,
+                                                         const double* __restrict__ ca,
+                                                         const double* __restrict__ cb,
+                                                         double* __restrict__ out) {
+  constexpr int D = B - 1;
+  const PoseLane p = pose_lane<B>(c);
+  if (tile_skipped(c, p.agent)) return;
+  const bool own = p.ok && p.k < B;
+  const long off = p.j * (R * B) + p.k * R;
+  const double a0 = ca ? ca[p.agent] : 1.0;
+  double acol[R];
+  load_col<R, B>(A, p.j, p.k, p.ok, acol);
+  if (Bv != nullptr) {
+    const double b0 = cb[p.agent];
+    double bcol[R];
+    load_col<R, B>(Bv, p.j, p.k, p.ok, bcol);
+#pragma unroll
+    for (int a = 0; a < R; ++a) acol[a] = a0 * acol[a] + b0 * bcol[a];
+  } else if (a0 != 1.0) {
+#pragma unroll
+    for (int a = 0; a < R; ++a) acol[a] = a0 * acol[a];
+  }
+  double Mf[R][B];
+  quad_gather<R, B>(acol, Mf);
+  polar_inplace<R, D>(Mf);
+  double oc[R];
+  select_col<R, B>(Mf, p.k, oc);
+  // translation column passes through unchanged
+  if (p.k == D) {
+#pragma unroll
+    for (int a = 0; a < R; ++a) oc[a] = acol[a];
+  }
+  store_vec<R>(out, off, own, oc);
+}
+
+// out = sel ? A : B per agent; partial |out - ref|^2
+template <int R, int B>
+__global__ __launch_bounds__(kThreads) void k_select(LaunchCtx c, const double* __restrict__ A,
+                                                     const double* __restrict__ Bv,
+                                                     const int* __restrict__ use_a,
+                                                     const double* __restrict__ ref,
+                                                     double* __restrict__ out) {
+  const PoseLane p = pose_lane<B>(c);
+  if (tile_skipped(c, p.agent)) return;
+  const bool own = p.ok && p.k < B;
+  const long off = p.j * (R * B) + p.k * R;
+  const bool ua = use_a[p.agent] != 0;
+  double dd = 0.0;
+  if (own) {
+#pragma unroll
+    for (int a = 0; a < R; ++a) {
+      const double v = ua ? A[off + a] : Bv[off + a];
+      const double df = v - ref[off + a];
+      dd = fma(df, df, dd);
+      out[off + a] = v;
+    }
+  }
+  double parts[1] = {dd};
+  block_partials<1>(parts, c.partials, p.tile);
+}
+
+// accepted RTR step in a multi-iteration Run: x1 <- x2, g <- g2, S <- S2
+template <int R, int B>
+__global__ __launch_bounds__(kThreads) void k_accept(LaunchCtx c, const double* __restrict__ x2,
+                                                     const double* __restrict__ g2,
+                                                     const double* __restrict__ S2,
+                                                     double* __restrict__ x1, double* __restrict__ g,
+                                                     double* __restrict__ S) {
+  constexpr int D = B - 1;
+  const PoseLane p = pose_lane<B>(c);
+  if (c.state[p.agent].copy_pending == 0) return;
+  if (!(p.ok && p.k < B)) return;
+  const long off = p.j * (R * B) + p.k * R;
+#pragma unroll
+  for (int a = 0; a < R; ++a) {
+    x1[off + a] = x2[off + a];
+    g[off + a] = g2[off + a];
+  }
+  if (p.k < D) {
+#pragma unroll
+    for (int v = 0; v < D; ++v) S[p.j * (D * D) + p.k * D + v] = S2[p.j * (D * D) + p.k * D + v];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-agent finalize: reduce tile partials in a fixed order, run the scalar logic of the
+// RTR / tCG state machine (A.4) on device.  grid = #agents, block = 256.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
+  const int agent = blockIdx.x;
+  const int t0 = f.agent_tile_off[agent], t1 = f.agent_tile_off[agent + 1];
+  __shared__ double red[kThreads];
+  __shared__ double tot[4];
+  const int nq = f.nq_a + f.nq_b;
+  for (int q = 0; q < nq; ++q) {
+    const double* src = q < f.nq_a ? f.pa : f.pb;
+    const int qq = q < f.nq_a ? q : q - f.nq_a;
+    double s = 0.0;
+    for (int t = t0 + threadIdx.x; t < t1; t += kThreads) s += src[t * kPartialStride + qq];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = kThreads / 2; w > 0; w >>= 1) {
+      if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) tot[q] = red[0];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  AgentState& s = f.state[agent];
+  const OptScalars& o = f.opt;
+  switch (f.op) {
+    case OP_EVAL_INIT: {  // after EVAL at the initial iterate
+      s.f1 = tot[0];
+      s.ngf = sqrt(tot[1]);
+      s.f_init = s.f1;
+      s.ngf_init = s.ngf;
+      s.f2 = s.f1;
+      s.ngf2 = s.ngf;
+      s.Delta = o.Delta0;
+      s.Delta_max = o.Delta_max;
+      s.run_active = f.agent_enabled ? (f.agent_enabled[agent] != 0 && !(s.ngf < o.tol)) : !(s.ngf < o.tol);
+      s.accepted = 0;
+      s.runs = 0;
+      s.outer_iters = 0;
+      s.gave_up = 0;
+      s.tcg_status = -1;
+      s.tcg_iters = 0;
+      s.tcg_active = 0;
+      s.tcg_mode = 2;
+      break;
+    }
+    case OP_EVAL: {
+      s.f1 = tot[0];
+      s.ngf = sqrt(tot[1]);
+      break;
+    }
+    case OP_TCG_INIT: {
+      s.copy_pending = 0;
+      if (!s.run_active) {
+        s.tcg_active = 0;
+        s.tcg_mode = 2;
+        break;
+      }
+      s.z_r = tot[0];
+      s.d_Pd = s.z_r;
+      s.e_Pe = 0.0;
+      s.e_Pd = 0.0;
+      s.norm_r0 = sqrt(tot[1]);
+      s.tcg_active = 1;
+      s.tcg_mode = 2;
+      s.tcg_status = TCG_MAXITER;
+      s.tcg_iters = 0;
+      break;
+    }
+    case OP_TCG_STEP: {  // after k_spmm<HESS>: tot[0] = <delta, H delta>
+      if (!s.tcg_active) {
+        s.tcg_mode = 2;
+        break;
+      }
+      const double d_Hd = tot[0];
+      const double alpha = s.z_r / d_Hd;
+      const double e_Pe_new = s.e_Pe + 2.0 * alpha * s.e_Pd + alpha * alpha * s.d_Pd;
+      const double D2 = s.Delta * s.Delta;
+      s.alpha = alpha;
+      s.tcg_iters += 1;
+      if (d_Hd <= 0.0 || e_Pe_new >= D2) {
+        const double tau = (-s.e_Pd + sqrt(s.e_Pd * s.e_Pd + s.d_Pd * (D2 - s.e_Pe))) / s.d_Pd;
+        s.tau = tau;
+        s.step = tau;
+        s.tcg_mode = 1;
+        s.tcg_status = d_Hd <= 0.0 ? TCG_NEGCURVTURE : TCG_EXCREGION;
+        s.tcg_active = 0;
+      } else {
+        s.e_Pe = e_Pe_new;
+        s.step = alpha;
+        s.tcg_mode = 0;
+      }
+      break;
+    }
+    case OP_TCG_CHECK: {  // after k_tcg_update: tot[0] = <z,r>, tot[1] = |r|^2
+      if (s.tcg_mode != 0) break;
+      const double norm_r = sqrt(tot[1]);
+      const int j = s.tcg_iters - 1;
+      const double r0t = pow(s.norm_r0, o.theta);
+      if (j >= o.min_inner && norm_r <= s.norm_r0 * fmin(r0t, o.kappa)) {
+        s.tcg_status = o.kappa < r0t ? TCG_LCON : TCG_SCON;
+        s.tcg_active = 0;
+        break;
+      }
+      const double z_r_new = tot[0];
+      const double beta = z_r_new / s.z_r;
+      s.beta = beta;
+      s.e_Pd = beta * (s.e_Pd + s.alpha * s.d_Pd);
+      s.d_Pd = z_r_new + beta * beta * s.d_Pd;
+      s.z_r = z_r_new;
+      break;
+    }
+    case OP_RHO: {  // pa: <g,eta>, <eta,Heta> ; pb: f(x2), |grad(x2)|^2
+      if (!s.run_active) break;
+      s.tcg_active = 0;
+      s.tcg_mode = 2;
+      s.g_eta = tot[0];
+      s.eta_Heta = tot[1];
+      s.f2 = tot[2];
+      s.ngf2 = sqrt(tot[3]);
+      const double denom = -s.g_eta - 0.5 * s.eta_Heta;
+      s.rho = (s.f1 - s.f2) / denom;
+      s.accepted = s.rho > 0.1 ? 1 : 0;
+      if (s.rho < 0.25) {
+        s.Delta = 0.25 * s.Delta;
+      } else if (s.rho > 0.75 && (s.tcg_status == TCG_EXCREGION || s.tcg_status == TCG_NEGCURVTURE)) {
+        s.Delta = fmin(2.0 * s.Delta, s.Delta_max);
+      }
+      s.outer_iters += 1;
+      s.copy_pending = o.single_run ? 0 : s.accepted;
+      if (o.single_run) {
+        // QuadraticOptimizer::trustRegion Max_Iteration == 1 wrapper (src/QuadraticOptimizer.cpp:92-110)
+        s.runs += 1;
+        if (s.accepted) {
+          s.run_active = 0;
+        } else if (s.runs - 1 > 10) {
+          s.gave_up = 1;
+          s.run_active = 0;
+        } else {
+          const double radius = s.Delta_max / 4.0;
+          s.Delta = radius;
+          s.Delta_max = radius;
+        }
+      } else {
+        if (s.accepted) {
+          s.f1 = s.f2;
+          s.ngf = s.ngf2;
+        }
+        if (s.ngf < o.tol || s.outer_iters >= o.max_iter) s.run_active = 0;
+      }
+      break;
+    }
+    case OP_REL_CHANGE: {
+      s.rel_change = sqrt(tot[0] / static_cast<double>(f.agent_num_poses[agent]));
+      break;
+    }
+    case OP_SUM: {
+      f.out_sums[agent * 4 + 0] = tot[0];
+      if (nq > 1) f.out_sums[agent * 4 + 1] = tot[1];
+      if (nq > 2) f.out_sums[agent * 4 + 2] = tot[2];
+      if (nq > 3) f.out_sums[agent * 4 + 3] = tot[3];
+      break;
+    }
+    default:
+      break;
+  }
+}
+
+// --- block-Jacobi inverse of (Q_jj + shift I), computed on device from the BSR diagonal ---
+template <int B>
+__global__ __launch_bounds__(kThreads) void k_bj_inverse(int n, QView q, double shift,
+                                                         double* __restrict__ Minv) {
+  const long j = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  double A[B][2 * B];
+#pragma unroll
+  for (int u = 0; u < B; ++u)
+#pragma unroll
+    for (int w = 0; w < 2 * B; ++w) A[u][w] = (w - B == u) ? 1.0 : 0.0;
+  const int beg = q.rowptr[j], end = q.rowptr[j + 1];
+  for (int nz = beg; nz < end; ++nz) {
+    if (q.col[nz] == j) {
+      // block (j,j) column-major: element (u,w) at w*B + u
+#pragma unroll
+      for (int u = 0; u < B; ++u)
+#pragma unroll
+        for (int w = 0; w < B; ++w) A[u][w] += q.blocks[static_cast<long>(nz) * B * B + w * B + u];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < B; ++u) A[u][u] += shift;
+  // Gauss-Jordan with partial pivoting (SPD, so pivoting is a safety net)
+#pragma unroll
+  for (int col = 0; col < B; ++col) {
+    int piv = col;
+    double best = fabs(A[col][col]);
+#pragma unroll
+    for (int u = col + 1; u < B; ++u)
+      if (fabs(A[u][col]) > best) {
+        best = fabs(A[u][col]);
+        piv = u;
+      }
+#pragma unroll
+    for (int u = col + 1; u < B; ++u) {
+      if (u == piv) {
+#pragma unroll
+        for (int w = 0; w < 2 * B; ++w) {
+          const double t = A[col][w];
+          A[col][w] = A[u][w];
+          A[u][w] = t;
+        }
+      }
+    }
+    const double inv = 1.0 / A[col][col];
+#pragma unroll
+    for (int w = 0; w < 2 * B; ++w) A[col][w] *= inv;
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      if (u != col) {
+        const double fct = A[u][col];
+#pragma unroll
+        for (int w = 0; w < 2 * B; ++w) A[u][w] = fma(-fct, A[col][w], A[u][w]);
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < B; ++u)
+#pragma unroll
+    for (int w = 0; w < B; ++w) Minv[j * (B * B) + u * B + w] = A[u][B + w];
+}
+
+// ------------------------------------------------------------------------------------------
+// Host-side launchers with (r, b) dispatch
+// ------------------------------------------------------------------------------------------
+#define DPGO_DISPATCH(R_, B_, CALL)                        \
+  switch ((R_) * 8 + (B_)) {                               \
+    case 2 * 8 + 3: { constexpr int R = 2, B = 3; CALL; break; } \
+    case 3 * 8 + 3: { constexpr int R = 3, B = 3; CALL; break; } \
+    case 4 * 8 + 3: { constexpr int R = 4, B = 3; CALL; break; } \
+    case 5 * 8 + 3: { constexpr int R = 5, B = 3; CALL; break; } \
+    case 6 * 8 + 3: { constexpr int R = 6, B = 3; CALL; break; } \
+    case 7 * 8 + 3: { constexpr int R = 7, B = 3; CALL; break; } \
+    case 8 * 8 + 3: { constexpr int R = 8, B = 3; CALL; break; } \
+    case 3 * 8 + 4: { constexpr int R = 3, B = 4; CALL; break; } \
+    case 4 * 8 + 4: { constexpr int R = 4, B = 4; CALL; break; } \
+    case 5 * 8 + 4: { constexpr int R = 5, B = 4; CALL; break; } \
+    case 6 * 8 + 4: { constexpr int R = 6, B = 4; CALL; break; } \
+    case 7 * 8 + 4: { constexpr int R = 7, B = 4; CALL; break; } \
+    case 8 * 8 + 4: { constexpr int R = 8, B = 4; CALL; break; } \
+    default: return hipErrorInvalidValue;                  \
+  }
+
+bool supported_rb(int r, int b) {
+  if (b == 3) return r >= 2 && r <= 8;
+  if (b == 4) return r >= 3 && r <= 8;
+  return false;
+}
+
+hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const QView& q, const double* in,
+                       const int* gidx, const double* gblk, const double* X, const double* S_in,
+                       double* out, double* S_out) {
+  if (c.num_tiles == 0) return hipSuccess;
+  dim3 grid(c.num_tiles), block(kThreads);
+  switch (mode) {
+    case MODE_XQ:
+      DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_XQ><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
+      break;
+    case MODE_XQ_G:
+      DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_XQ_G><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
+      break;
+    case MODE_EVAL:
+      DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_EVAL><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
+      break;
+    case MODE_HESS:
+      DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_HESS><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_tcg_init(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
+                           const double* g, double* eta, double* Heta, double* rv, double* z, double* delta) {
+  if (c.num_tiles == 0) return hipSuccess;
+  DPGO_DISPATCH(r, b, (k_tcg_init<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, Minv, pmode, g, eta, Heta, rv, z, delta)));
+  return hipGetLastError();
+}
+
+hipError_t launch_tcg_update(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
+                             const double* delta, const double* Hdelta, double* eta, double* Heta, double* rv,
+                             double* z) {
+  if (c.num_tiles == 0) return hipSuccess;
+  DPGO_DISPATCH(r, b, (k_tcg_update<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, Minv, pmode, delta, Hdelta, eta, Heta, rv, z)));
+  return hipGetLastError();
+}
+
+hipError_t launch_tcg_dir(int r, int b, const LaunchCtx& c, const double* z, double* delta) {
+  if (c.num_tiles == 0) return hipSuccess;
+  DPGO_DISPATCH(r, b, (k_tcg_dir<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, z, delta)));
+  return hipGetLastError();
+}
+
+hipError_t launch_retract(int r, int b, const LaunchCtx& c, const double* X, const double* V, double scale,
+                          double* out, const double* g, const double* HV) {
+  if (c.num_tiles == 0) return hipSuccess;
+  DPGO_DISPATCH(r, b, (k_retract<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, V, scale, out, g, HV)));
+  return hipGetLastError();
+}
+
+hipError_t launch_tangent(int r, int b, const LaunchCtx& c, const double* X, const double* V, double* out) {
+  if (c.num_tiles == 0) return hipSuccess;
+  DPGO_DISPATCH(r, b, (k_tangent<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, V, out)));
+  return hipGetLastError();
+}
+
+hipError_t launch_precond(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
+                          const double* V, double* out) {
+  if (c.num_tiles == 0) return hipSuccess;
+  DPGO_DISPATCH(r, b, (k_precond<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, Minv, pmode, V, out)));
+  return hipGetLastError();
+}
+
+hipError_t launch_polar_comb(int r, int b, const LaunchCtx& c, const double* A, const double* Bv,
+                             const double* ca, const double* cb, double* out) {
+  if (c.num_tiles == 0) return hipSuccess;
+  DPGO_DISPATCH(r, b, (k_polar_comb<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, A, Bv, ca, cb, out)));
+  return hipGetLastError();
+}
+
+hipError_t launch_select(int r, int b, const LaunchCtx& c, const double* A, const double* Bv, const int* use_a,
+                         const double* ref, double* out) {
+  if (c.num_tiles == 0) return hipSuccess;
+  DPGO_DISPATCH(r, b, (k_select<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, A, Bv, use_a, ref, out)));
+  return hipGetLastError();
+}
+
+hipError_t launch_accept(int r, int b, const LaunchCtx& c, const double* x2, const double* g2, const double* S2,
+                         double* x1, double* g, double* S) {
+  if (c.num_tiles == 0) return hipSuccess;
+  DPGO_DISPATCH(r, b, (k_accept<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, x2, g2, S2, x1, g, S)));
+  return hipGetLastError();
+}
+
+hipError_t launch_finalize(const FinalizeArgs& f, int num_agents, hipStream_t stream) {
+  if (num_agents == 0) return hipSuccess;
+  k_finalize<<<num_agents, kThreads, 0, stream>>>(f);
+  return hipGetLastError();
+}
+
+hipError_t launch_bj_inverse(int b, int n, const QView& q, double shift, double* Minv, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const int blocks = (n + kThreads - 1) / kThreads;
+  if (b == 3)
+    k_bj_inverse<3><<<blocks, kThreads, 0, stream>>>(n, q, shift, Minv);
+  else if (b == 4)
+    k_bj_inverse<4><<<blocks, kThreads, 0, stream>>>(n, q, shift, Minv);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+}  // namespace dpgo

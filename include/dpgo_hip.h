@@ -1,0 +1,174 @@
+/*
+ * dpgo_hip.h -- C ABI of the MI355X-native DPGO RBCD hot path (libdpgo_hip.so).
+ *
+ * This is the drop-in boundary that sits under the reference's C++ API
+ * (QuadraticProblem / QuadraticOptimizer / LiftedSEManifold / PGOAgent::updateX).
+ * Every entry point cites the reference interface it replaces (paths relative to the
+ * lajoiepy/dpgo source root).  The C++ shim classes in dpgo_amd/cpp keep the reference
+ * signatures and forward here; INTEGRATION.md shows the binding a maintainer would add.
+ *
+ * Conventions
+ *  - All arithmetic is fp64.  d in {2,3}, b = d+1, r = relaxation rank, 2 <= r <= 8, r >= d.
+ *  - Pose matrices use the reference layout: X is r x (b n), column-major, so pose j is the
+ *    contiguous r*b doubles [Y_j (r x d, col-major) | p_j (r)]   (tests/testEigenMap.cpp:19-35).
+ *  - A problem handle holds one or more *agents* (independent RBCD blocks) whose poses are
+ *    concatenated in agent order; single-agent handles reproduce QuadraticProblem exactly.
+ *    Per-agent outputs (f, norms, results) are arrays of length num_agents.
+ *  - Host-pointer entry points copy in/out and synchronise; *_dev entry points take device
+ *    pointers, run asynchronously on the handle's stream and never synchronise unless stated.
+ *  - Return value: 0 (DPGO_HIP_OK) or a negative error code; dpgo_hip_last_error() returns a
+ *    thread-local message.  No C++ exception crosses this boundary.  There is no CPU fallback:
+ *    without a usable gfx950 device every compute call returns DPGO_HIP_ENODEV.
+ */
+#ifndef DPGO_HIP_H
+#define DPGO_HIP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPGO_HIP_OK 0
+#define DPGO_HIP_EINVAL (-1)
+#define DPGO_HIP_ENODEV (-2)
+#define DPGO_HIP_EDEVICE (-3)
+#define DPGO_HIP_ENOMEM (-4)
+#define DPGO_HIP_ESTATE (-5)
+
+/* Preconditioner modes (QuadraticProblem::PreConditioner, src/QuadraticProblem.cpp:75-87).
+ * EXACT (the reference's CHOLMOD factor of Q + 0.1 I) is SURVEY 8f "next" and currently returns
+ * DPGO_HIP_EINVAL; BLOCK_JACOBI applies the per-pose (Q_jj + 0.1 I)^-1 (north_star deviation). */
+#define DPGO_PRECON_EXACT 0
+#define DPGO_PRECON_BLOCK_JACOBI 1
+#define DPGO_PRECON_NONE 2
+
+/* ROPTALG (include/DPGO/DPGO_types.h:29-35) */
+#define DPGO_ALG_RTR 0
+#define DPGO_ALG_RGD 1
+
+/* ROPTLIB tCGstatusSet */
+#define DPGO_TCG_NEGCURVTURE 0
+#define DPGO_TCG_EXCREGION 1
+#define DPGO_TCG_LCON 2
+#define DPGO_TCG_SCON 3
+#define DPGO_TCG_MAXITER 4
+
+typedef struct dpgo_hip_problem_s* dpgo_hip_problem;
+
+/* QuadraticOptimizer setters (include/DPGO/QuadraticOptimizer.h:34-71, defaults
+ * src/QuadraticOptimizer.cpp:20-30) plus the preconditioner mode. */
+typedef struct {
+  int algorithm;             /* DPGO_ALG_RTR / DPGO_ALG_RGD */
+  double rgd_stepsize;       /* setGradientDescentStepsize (1e-3) */
+  int tr_iterations;         /* setTrustRegionIterations (1) */
+  double tr_tolerance;       /* setTrustRegionTolerance (1e-2) */
+  double tr_initial_radius;  /* setTrustRegionInitialRadius (10) */
+  int tr_max_inner;          /* setTrustRegionMaxInnerIterations (50) */
+  int verbose;               /* setVerbose */
+  int precon;                /* DPGO_PRECON_* (BLOCK_JACOBI) */
+} dpgo_opt_params;
+
+/* ROPTResult (include/DPGO/DPGO_types.h:40-59) + solver counters */
+typedef struct {
+  int success;
+  double fInit, gradNormInit, fOpt, gradNormOpt, relativeChange, elapsedMs;
+  int tCGStatus;      /* DPGO_TCG_* of the last tCG, -1 if no tCG ran */
+  int runs;           /* RTR Run() calls (radius-shrink retries) */
+  int outer_iters;    /* RTR outer iterations */
+  int inner_iters;    /* tCG iterations of the last tCG */
+  int gave_up;        /* "Too many RTR rejections" (returned the input) */
+} dpgo_opt_result;
+
+/* ---- library ---------------------------------------------------------------------------*/
+const char* dpgo_hip_version(void);
+const char* dpgo_hip_last_error(void);
+/* Number of usable gfx950 devices (0 if none). */
+int dpgo_hip_device_count(void);
+void dpgo_hip_default_params(dpgo_opt_params* p);
+
+/* ---- problem lifecycle (QuadraticProblem ctor/dtor, src/QuadraticProblem.cpp:16-29) ----*/
+int dpgo_hip_problem_create(int n, int d, int r, dpgo_hip_problem* out);
+/* num_agents independent blocks with poses_per_agent[a] poses each (batched RBCD). */
+int dpgo_hip_problem_create_batch(int num_agents, const int* poses_per_agent, int d, int r,
+                                  dpgo_hip_problem* out);
+int dpgo_hip_problem_destroy(dpgo_hip_problem h);
+/* Launch on a caller-owned hipStream_t (NULL = the handle's own stream). */
+int dpgo_hip_problem_set_stream(dpgo_hip_problem h, void* stream);
+int dpgo_hip_problem_info(dpgo_hip_problem h, int* num_agents, int* total_poses, int* d, int* r);
+int dpgo_hip_set_precon(dpgo_hip_problem h, int mode);
+
+/* ---- problem data ------------------------------------------------------------------------*/
+/* QuadraticProblem::setQ (src/QuadraticProblem.cpp:31-42): Q of one agent in the reference's
+ * Eigen RowMajor CSR (include/DPGO/DPGO_types.h:23), (b n_a) x (b n_a), int32 indices. */
+int dpgo_hip_set_Q_csr(dpgo_hip_problem h, int agent, int nrows, const int* rowptr,
+                       const int* colidx, const double* vals);
+/* Same data as block-sparse rows: block (j, colidx[k]) stored column-major (b*b doubles).
+ * nbrows == n_a; column indices are agent-local pose indices. */
+int dpgo_hip_set_Q_bsr(dpgo_hip_problem h, int agent, int nbrows, const int* browptr,
+                       const int* bcolidx, const double* blocks);
+/* QuadraticProblem::setG (src/QuadraticProblem.cpp:44-48) in sparse form: count pose blocks
+ * (r x b column-major) at agent-local poses pose_idx[]; all other columns of G are zero. */
+int dpgo_hip_set_G(dpgo_hip_problem h, int agent, int count, const int* pose_idx,
+                   const double* blocks);
+/* Dense r x (b n_a) G for one agent (column-major). */
+int dpgo_hip_set_G_dense(dpgo_hip_problem h, int agent, const double* G);
+
+/* ---- evaluations (QuadraticProblem, src/QuadraticProblem.cpp:50-101) ---------------------*/
+/* f(X) = 0.5 <XQ, X> + <X, G> per agent (:50-60) */
+int dpgo_hip_f(dpgo_hip_problem h, const double* X, double* f_out);
+/* EucGrad: X Q + G (:62-66) */
+int dpgo_hip_egrad(dpgo_hip_problem h, const double* X, double* EG);
+/* EucHessianEta: V Q (:68-73) */
+int dpgo_hip_ehvp(dpgo_hip_problem h, const double* V, double* HV);
+/* RieGrad / RieGradNorm (:89-101): P_X(XQ + G), per-agent Frobenius norms; f_out optional */
+int dpgo_hip_riegrad(dpgo_hip_problem h, const double* X, double* RG, double* norms,
+                     double* f_out);
+/* Riemannian Hessian at X applied to tangent V (ROPTLIB HessianEta = EucHessianEta + EucHvToHv) */
+int dpgo_hip_rhvp(dpgo_hip_problem h, const double* X, const double* V, double* HV);
+/* PreConditioner (:75-87) with the handle's mode */
+int dpgo_hip_precondition(dpgo_hip_problem h, const double* X, const double* V, double* out);
+
+/* ---- manifold (LiftedSEManifold / ROPTLIB Stiefel Set3), stateless ----------------------*/
+/* ProductManifold::Projection: V_Y - Y sym(Y^T V_Y), V_p */
+int dpgo_hip_tangent_project(int r, int d, int n, const double* X, const double* V, double* out);
+/* QF retraction of scale*V at X: [qf(Y + s V_Y) | p + s V_p] */
+int dpgo_hip_retract_qf(int r, int d, int n, const double* X, const double* V, double scale,
+                        double* out);
+/* LiftedSEManifold::project (src/manifold/LiftedSEManifold.cpp:34-45) */
+int dpgo_hip_project_polar(int r, int d, int n, const double* in, double* out);
+
+/* ---- optimisation (QuadraticOptimizer::optimize, src/QuadraticOptimizer.cpp:34-149) -----*/
+/* Runs every agent of the handle; results[num_agents].  agent_enabled (optional, device or
+ * host per variant) skips agents (their X_out = X_in, result.success = 0). */
+int dpgo_hip_optimize(dpgo_hip_problem h, const dpgo_opt_params* params, const double* X_in,
+                      double* X_out, dpgo_opt_result* results);
+
+/* ---- device-pointer variants (asynchronous on the handle's stream) -----------------------*/
+int dpgo_hip_f_dev(dpgo_hip_problem h, const double* X, double* f_out_host);
+int dpgo_hip_egrad_dev(dpgo_hip_problem h, const double* X, double* EG);
+int dpgo_hip_ehvp_dev(dpgo_hip_problem h, const double* V, double* HV);
+int dpgo_hip_riegrad_dev(dpgo_hip_problem h, const double* X, double* RG);
+int dpgo_hip_rhvp_dev(dpgo_hip_problem h, const double* X, const double* V, double* HV);
+int dpgo_hip_project_polar_dev(dpgo_hip_problem h, const double* in, double* out);
+/* out = project(ca[a] * A + cb[a] * B) per agent a (Nesterov updateY / updateV,
+ * src/PGOAgent.cpp:1075-1091); ca/cb host arrays[num_agents]. */
+int dpgo_hip_polar_combine_dev(dpgo_hip_problem h, const double* A, const double* B,
+                               const double* ca, const double* cb, double* out);
+/* Synchronises once per RTR Run (radius-shrink bookkeeping); results host array (may be NULL). */
+int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, const double* X_in,
+                          double* X_out, const int* agent_enabled_host, dpgo_opt_result* results);
+/* Device buffer of the last tCG / RTR scalar state (for profiling / tests) */
+int dpgo_hip_synchronize(dpgo_hip_problem h);
+
+/* ---- measurement helpers ----------------------------------------------------------------*/
+/* Algorithmic HBM bytes of one X.Q SpMM over this handle (BSR blocks + indices + X + Y). */
+double dpgo_hip_spmm_bytes(dpgo_hip_problem h);
+/* Time `reps` back-to-back X.Q SpMM launches with HIP events on the handle's stream; returns the
+ * average milliseconds per launch in *ms. */
+int dpgo_hip_bench_spmm(dpgo_hip_problem h, const double* X_dev, double* Y_dev, int reps, double* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPGO_HIP_H */

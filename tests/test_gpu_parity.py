@@ -1,0 +1,136 @@
+"""GPU parity: HIP kernels through the C ABI vs the CPU oracle (oracle/dpgo_oracle.py).
+
+Tolerances (north_star): per-evaluation f / grad / HVP values 1e-12 relative (Frobenius norm of
+the difference over the norm of the oracle value); final cost after optimisation 1e-9 relative.
+"""
+import numpy as np
+import pytest
+
+from oracle import dpgo_oracle as O
+from tests._common import load_meas, random_point, random_tangent, seeded_G, rel
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def hip():
+    from dpgo_amd import hip as H
+    assert H.device_count() >= 1, "no gfx950 device"
+    return H
+
+
+CASES = [("tinyGrid3D", 5), ("smallGrid3D", 5), ("smallGrid3D", 3), ("sphere2500", 5),
+         ("input_INTEL_g2o", 5), ("input_INTEL_g2o", 2), ("city10000", 3)]
+
+
+@pytest.mark.parametrize("name,r", CASES)
+def test_evaluations(hip, name, r):
+    meas = load_meas(name)
+    d, n = meas.d, meas.num_poses
+    Q = O.connection_laplacian(meas, n)
+    P = O.QuadraticProblem(n, d, r)
+    P.set_Q(Q)
+    X = random_point(r, d, n, 11)
+    V = random_tangent(X, d, 12)
+    G = seeded_G(X, d, r, n, 13)
+    P.set_G(G)
+    H = hip.Problem(n, d, r)
+    H.set_Q_scipy(0, Q)
+    H.set_G_dense(0, G)
+    f = H.f(X)[0]
+    assert abs(f - P.f(X)) <= TOL * max(1.0, abs(P.f(X)))
+    assert rel(H.egrad(X), P.egrad(X)) <= TOL
+    assert rel(H.ehvp(V), P.ehvp(V)) <= TOL
+    RG, norms, fv = H.riegrad(X)
+    assert rel(RG, P.riegrad(X)) <= TOL
+    assert abs(norms[0] - P.riegrad_norm(X)) <= TOL * P.riegrad_norm(X)
+    assert rel(H.rhvp(X, V), P.rhvp(X, V)) <= TOL
+    assert rel(H.precondition(X, V), P.precondition(X, V, O.PRECON_BLOCK_JACOBI)) <= TOL
+
+
+@pytest.mark.parametrize("name,r", [("smallGrid3D", 5), ("input_INTEL_g2o", 2), ("sphere2500", 3)])
+def test_manifold_ops(hip, name, r):
+    meas = load_meas(name)
+    d, n = meas.d, meas.num_poses
+    X = random_point(r, d, n, 21)
+    V = random_tangent(X, d, 22)
+    assert rel(hip.tangent_project(X, V + X, d), O.tangent_project(X, V + X, d)) <= TOL
+    assert rel(hip.retract_qf(X, V, d), O.retract_qf(X, V, d)) <= 1e-13
+    assert rel(hip.retract_qf(X, V, d, scale=-0.25), O.retract_qf(X, -0.25 * V, d)) <= 1e-13
+    M = X + 0.3 * V
+    assert rel(hip.project_polar(M, d), O.lifted_project(M, d)) <= 1e-13
+
+
+def _single_rtr(hip, name, r, iters, tol, radius, inner):
+    meas = load_meas(name)
+    d, n = meas.d, meas.num_poses
+    Q = O.connection_laplacian(meas, n)
+    P = O.QuadraticProblem(n, d, r)
+    P.set_Q(Q)
+    P.precon_mode = O.PRECON_BLOCK_JACOBI
+    X0 = O.lifting_matrix(d, r) @ O.chordal_initialization(d, n, meas)
+    trace = []
+    Xo, res = O.optimize(P, X0, O.OptParams(tr_iterations=iters, tr_tolerance=tol,
+                                            tr_initial_radius=radius, tr_max_inner=inner), trace)
+    H = hip.Problem(n, d, r)
+    H.set_Q_scipy(0, Q)
+    p = hip.default_params(tr_iterations=iters, tr_tolerance=tol, tr_initial_radius=radius,
+                           tr_max_inner=inner, precon=hip.PRECON_BLOCK_JACOBI)
+    Xh, rh = H.optimize(X0, p)
+    return Xo, res, trace, Xh, rh[0]
+
+
+@pytest.mark.parametrize("name,r", [("smallGrid3D", 5), ("tinyGrid3D", 3), ("sphere2500", 3)])
+def test_rtr_single_agent(hip, name, r):
+    """PGOAgent::localPoseGraphOptimization settings (src/PGOAgent.cpp:975-984)."""
+    Xo, res, trace, Xh, rh = _single_rtr(hip, name, r, 10, 1e-1, 10.0, 50)
+    assert abs(rh["fInit"] - res["fInit"]) <= 1e-12 * abs(res["fInit"])
+    assert abs(rh["fOpt"] - res["fOpt"]) <= 1e-9 * abs(res["fOpt"])
+    assert rh["outer_iters"] == len(trace)
+    assert rh["tCGStatus"] == res["tCGStatus"]
+    assert rel(Xh, Xo) <= 1e-8
+
+
+def test_rtr_rbcd_settings(hip):
+    """PGOAgent::updateX settings: 1 iteration, 10 inner, radius 100, tol 1e-2 (:1131-1137)."""
+    Xo, res, trace, Xh, rh = _single_rtr(hip, "smallGrid3D", 5, 1, 1e-2, 100.0, 10)
+    assert rh["runs"] == res["runs"]
+    assert abs(rh["fOpt"] - res["fOpt"]) <= 1e-11 * abs(res["fOpt"])
+    assert abs(rh["gradNormOpt"] - res["gradNormOpt"]) <= 1e-9 * res["gradNormOpt"]
+    assert abs(rh["relativeChange"] - res["relativeChange"]) <= 1e-9 * res["relativeChange"]
+    assert rel(Xh, Xo) <= 1e-10
+
+
+def test_batched_agents_match_independent(hip):
+    """A batch of agents = independent QuadraticProblems solved in one set of launches."""
+    meas = load_meas("smallGrid3D")
+    d, r = 3, 5
+    parts, robot_of, local, start = O.partition_contiguous(meas, meas.num_poses, 5)
+    X0 = O.lifting_matrix(d, r) @ O.chordal_initialization(d, meas.num_poses, meas)
+    b = d + 1
+    H = hip.Problem(None, d, r, poses_per_agent=[int(start[k + 1] - start[k]) for k in range(5)])
+    oracle_out = []
+    for k in range(5):
+        ag = O.Agent(k, O.AgentParams(d, r, 5, robust="L2", precon=O.PRECON_BLOCK_JACOBI))
+        ag.set_pose_graph(*parts[k], n=int(start[k + 1] - start[k]))
+        ag.set_X(X0[:, start[k] * b:start[k + 1] * b])
+        nd = {}
+        for j in range(5):
+            if j != k:
+                nd.update({pid: X0[:, (start[pid[0]] + pid[1]) * b:(start[pid[0]] + pid[1] + 1) * b]
+                           for pid in ag.neighbor_shared if pid[0] == j})
+        ag.neighbor_pose = nd
+        assert ag.construct_G(nd)
+        H.set_Q_scipy(k, ag.problem.Q)
+        H.set_G_dense(k, ag.problem.G)
+        Xk, rk = O.optimize(ag.problem, ag.X, O.OptParams(tr_iterations=1, tr_tolerance=1e-2,
+                                                          tr_initial_radius=100.0, tr_max_inner=10))
+        oracle_out.append((Xk, rk))
+    Xh, rh = H.optimize(X0, hip.default_params(tr_iterations=1, tr_tolerance=1e-2,
+                                               tr_initial_radius=100.0, tr_max_inner=10))
+    for k in range(5):
+        Xk, rk = oracle_out[k]
+        assert abs(rh[k]["fOpt"] - rk["fOpt"]) <= 1e-10 * max(1.0, abs(rk["fOpt"]))
+        assert rel(Xh[:, start[k] * b:start[k + 1] * b], Xk) <= 1e-10
