@@ -1,0 +1,162 @@
+#!/usr/bin/env python3
+"""bench.py -- RBCD throughput + X.Q SpMM HBM roofline on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[4] / SURVEY 8d C5): synthetic 3D grid, k^3 = 10^6 poses, r = 5,
+64 agents (4 x 4 x 4 sub-cubes of 25^3 poses), Nesterov-accelerated RBCD (as
+examples/MultiRobotExample.cpp) with the L2 cost, colour-class schedule (2 colours).
+One *step* = one sweep over both colours = every agent updated once (64 agent updates, each an
+RTR(1 outer, 10 tCG) solve as PGOAgent::updateX configures it) plus the public-pose exchange.
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "RBCD iters/sec + X·Q SpMM HBM GB/s, 1M-pose synth grid r=5, 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def super_cube_ranks(A, world):
+    """Agents -> ranks: 2x2x2 super-cubes of agents (8 groups), merged for world < 8."""
+    ranks = np.zeros(A ** 3, np.int32)
+    h = max(A // 2, 1)
+    for az in range(A):
+        for ay in range(A):
+            for ax in range(A):
+                sup = (ax // h) + 2 * ((ay // h) + 2 * (az // h))
+                ranks[ax + A * (ay + A * az)] = (sup * world) // 8 if A >= 2 else 0
+    return ranks
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--k", type=int, default=100, help="grid side (k^3 poses)")
+    ap.add_argument("--agents-per-axis", type=int, default=4)
+    ap.add_argument("--r", type=int, default=5)
+    ap.add_argument("--accel", type=int, default=1)
+    ap.add_argument("--spmm-reps", type=int, default=20)
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-sample-updates", type=int, default=40)
+    ap.add_argument("--verify", type=int, default=0, help="central cost before/after (slow)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from dpgo_amd import hip as H
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        world = max(world, 1)
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    t_setup = time.time()
+    g = H.Graph.grid3d(args.k, seed=0)
+    A = args.agents_per_axis
+    aop = g.grid_partition(A)
+    num_agents = A ** 3
+    agent_rank = super_cube_ranks(A, world)
+    params = H.rbcd_params(r=args.r, acceleration=args.accel)
+    eng = H.Rbcd(g, aop, agent_rank, rank, world, params)
+    stream = torch.cuda.current_stream(dev)
+    eng.set_stream(stream.cuda_stream)
+    YLift = H.lifting_matrix(3, args.r)
+    X0 = g.chain_init_dev_layout(args.r, YLift)
+    eng.set_X(X0)
+    send = torch.empty(max(int(eng.send_counts.sum()), 1), dtype=torch.float64, device=dev)
+    recv = torch.empty(max(int(eng.recv_counts.sum()), 1), dtype=torch.float64, device=dev)
+    in_splits = [int(x) for x in eng.send_counts]
+    out_splits = [int(x) for x in eng.recv_counts]
+    setup_s = time.time() - t_setup
+
+    def step():
+        for c in range(eng.num_colors):
+            eng.pre_exchange(c)
+            if world > 1:
+                eng.pack(send.data_ptr())
+                dist.all_to_all_single(recv, send, out_splits, in_splits)
+            eng.update(c, recv.data_ptr() if world > 1 else None)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # ---- roofline of the dominant kernel (X.Q SpMM over one colour class, HIP events)
+    spmm_bytes, spmm_ms = eng.bench_spmm(0, args.spmm_reps)
+    achieved = spmm_bytes / (spmm_ms * 1e-3) / 1e9 if spmm_ms > 0 else 0.0
+
+    agent_updates = num_agents * args.steps
+    value = agent_updates / elapsed
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "RBCD agent-updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (repo-defined grid3d, SplitMix64 seed 0; no reference data at this size)",
+        "config": {"workload": f"grid3d k={args.k} ({args.k ** 3} poses), r={args.r}, "
+                               f"{num_agents} agents ({A}^3 sub-cubes), Nesterov={bool(args.accel)}, "
+                               f"L2 cost, colour schedule ({eng.num_colors} colours), "
+                               f"RTR 1x10 tCG, block-Jacobi precond",
+                   "poses": g.n, "edges": g.m, "agents": num_agents,
+                   "parallelism": f"agents over {world} GPU(s), RCCL all_to_all halo"},
+        "rounds_per_s": args.steps / elapsed,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "k_spmm<5,4,MODE_XQ> (X.Q over colour class 0 on rank 0)",
+                     "algorithmic_bytes_per_launch": spmm_bytes, "avg_launch_ms": spmm_ms},
+        "setup_s": setup_s,
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        try:
+            from oracle import cpu_port
+            out["cpu_baseline"] = cpu_port.baseline(g, aop, X0, args.r, bool(args.accel),
+                                                    num_agents, args.cpu_sample_updates)
+        except Exception as exc:  # reported, never silently replaced
+            out["cpu_baseline"] = {"error": repr(exc)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

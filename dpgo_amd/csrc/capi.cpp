@@ -15,12 +15,11 @@
 #include <string>
 #include <vector>
 
-#include "../../include/dpgo_hip.h"
-#include "kernels.h"
+#include "problem_internal.h"
 
 using dpgo::AgentState;
 
-namespace {
+namespace dpgo {
 
 thread_local std::string g_last_error;
 
@@ -28,19 +27,6 @@ int fail(int code, const std::string& msg) {
   g_last_error = msg;
   return code;
 }
-
-#define HIP_TRY(expr)                                                                        \
-  do {                                                                                       \
-    hipError_t _e = (expr);                                                                  \
-    if (_e != hipSuccess)                                                                    \
-      return fail(DPGO_HIP_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));      \
-  } while (0)
-
-#define DPGO_TRY(expr)          \
-  do {                          \
-    int _rc = (expr);           \
-    if (_rc != DPGO_HIP_OK) return _rc; \
-  } while (0)
 
 int g_devices = -1;
 
@@ -57,76 +43,11 @@ int usable_devices() {
   return ok;
 }
 
-struct HostBSR {
-  std::vector<int> rowptr, col;
-  std::vector<double> blocks;
-};
+}  // namespace dpgo
 
-template <typename T>
-struct DevBuf {
-  T* p = nullptr;
-  size_t n = 0;
-  DevBuf() = default;
-  DevBuf(const DevBuf&) = delete;
-  DevBuf& operator=(const DevBuf&) = delete;
-  ~DevBuf() { release(); }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    n = 0;
-  }
-  hipError_t ensure(size_t count) {
-    if (count <= n && p) return hipSuccess;
-    release();
-    n = std::max<size_t>(count, 1);
-    return hipMalloc(reinterpret_cast<void**>(&p), n * sizeof(T));
-  }
-};
+using namespace dpgo;
 
-}  // namespace
-
-struct dpgo_hip_problem_s {
-  int K = 0, d = 0, r = 0, b = 0;
-  long N = 0;  // total poses
-  std::vector<int> n_agent;
-  std::vector<long> pose_off;
-  hipStream_t stream = nullptr;
-  hipStream_t own_stream = nullptr;
-
-  // tiles
-  std::vector<int> h_tile_agent, h_tile_start, h_tile_count, h_agent_tile_off;
-  int num_tiles = 0;
-  DevBuf<int> tile_agent, tile_start, tile_count, agent_tile_off, agent_np, enabled, use_a;
-
-  // Q (per-agent host copies, concatenated on upload)
-  std::vector<HostBSR> q_agent;
-  bool q_dirty = true;
-  DevBuf<int> rowptr, col;
-  DevBuf<double> blocks, minv;
-  long nnzb = 0;
-
-  // G (sparse pose blocks per agent)
-  std::vector<std::map<int, std::vector<double>>> g_agent;
-  bool g_dirty = true;
-  DevBuf<int> gidx;
-  DevBuf<double> gblk;
-  int num_gslots = 0;
-
-  int precon = DPGO_PRECON_BLOCK_JACOBI;
-
-  // work
-  DevBuf<double> x1, x2, g, g2, S, S2, eta, Heta, rv, z, delta, Hdelta, tA, tB;
-  DevBuf<double> pa, pb, sums, coef_a, coef_b;
-  DevBuf<AgentState> state;
-  std::vector<AgentState> h_state;
-  std::vector<double> h_sums;
-
-  size_t vec_len() const { return static_cast<size_t>(N) * r * b; }
-  size_t vec_bytes() const { return vec_len() * sizeof(double); }
-  size_t s_len() const { return static_cast<size_t>(N) * (b - 1) * (b - 1); }
-};
-
-namespace {
+namespace dpgo {
 
 dpgo::LaunchCtx make_ctx(dpgo_hip_problem h, int flag_kind, double* partials) {
   dpgo::LaunchCtx c;
@@ -140,6 +61,10 @@ dpgo::LaunchCtx make_ctx(dpgo_hip_problem h, int flag_kind, double* partials) {
   c.stream = h->stream;
   return c;
 }
+
+}  // namespace dpgo
+
+namespace {
 
 dpgo::QView qview(dpgo_hip_problem h) { return dpgo::QView{h->rowptr.p, h->col.p, h->blocks.p}; }
 
@@ -228,6 +153,15 @@ int ready(dpgo_hip_problem h) {
   return DPGO_HIP_OK;
 }
 
+}  // namespace
+
+namespace dpgo {
+int problem_ready(dpgo_hip_problem h) { return ready(h); }
+int ensure_work_public(dpgo_hip_problem h) { return ensure_work(h); }
+}  // namespace dpgo
+
+namespace {
+
 int finalize(dpgo_hip_problem h, int op, const double* pa, int nqa, const double* pb, int nqb,
              const dpgo::OptScalars* opt = nullptr, const int* enabled = nullptr) {
   dpgo::FinalizeArgs f;
@@ -310,7 +244,7 @@ void fill_result(const AgentState& s, bool single, bool enabled, dpgo_opt_result
 extern "C" {
 
 const char* dpgo_hip_version(void) { return "dpgo_hip 0.1.0 (gfx950, fp64)"; }
-const char* dpgo_hip_last_error(void) { return g_last_error.c_str(); }
+const char* dpgo_hip_last_error(void) { return dpgo::g_last_error.c_str(); }
 int dpgo_hip_device_count(void) { return usable_devices(); }
 
 void dpgo_hip_default_params(dpgo_opt_params* p) {
@@ -578,6 +512,7 @@ int dpgo_hip_polar_combine_dev(dpgo_hip_problem h, const double* A, const double
   if (usable_devices() == 0) return fail(DPGO_HIP_ENODEV, "no gfx950 device available (no CPU fallback)");
   HIP_TRY(hipMemcpyAsync(h->coef_a.p, ca, sizeof(double) * h->K, hipMemcpyHostToDevice, h->stream));
   if (B) HIP_TRY(hipMemcpyAsync(h->coef_b.p, cb, sizeof(double) * h->K, hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));  // caller's host arrays may go out of scope
   auto c = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
   HIP_TRY(dpgo::launch_polar_comb(h->r, h->b, c, A, B, h->coef_a.p, B ? h->coef_b.p : nullptr, out));
   return DPGO_HIP_OK;

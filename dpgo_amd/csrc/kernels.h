@@ -60,7 +60,23 @@ struct FinalizeArgs {
   OptScalars opt;
 };
 
+// shared-edge records for G assembly, grouped by G slot (CSR)
+struct GEdges {
+  const int* slot_off;   // [nslots + 1]
+  const int* src;        // neighbour pose: >= 0 index into Xa, < 0 -> (-1 - src) into Xb
+  const int* outgoing;   // 1: this agent owns p1 (edge leaves the agent)
+  const double* R;       // [d*d] row-major per edge
+  const double* t;       // [d]
+  const double* kappa;
+  const double* tau;
+  const double* w;
+};
+
 bool supported_rb(int r, int b);
+hipError_t launch_gather_poses(int count, int rb, const int* idx, const double* A, const double* Bsrc, double* dst,
+                               hipStream_t stream);
+hipError_t launch_assemble_G(int r, int b, const GEdges& e, int nslots, const double* Xa, const double* Xb,
+                             double* gblk, hipStream_t stream);
 hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const QView& q, const double* in,
                        const int* gidx, const double* gblk, const double* X, const double* S_in,
                        double* out, double* S_out);
@@ -76,7 +92,8 @@ hipError_t launch_tangent(int r, int b, const LaunchCtx& c, const double* X, con
 hipError_t launch_precond(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
                           const double* V, double* out);
 hipError_t launch_polar_comb(int r, int b, const LaunchCtx& c, const double* A, const double* Bv,
-                             const double* ca, const double* cb, double* out);
+                             const double* ca, const double* cb, double* out, const double* Cv = nullptr,
+                             double sa = 1.0, double sb = 0.0);
 hipError_t launch_select(int r, int b, const LaunchCtx& c, const double* A, const double* Bv, const int* use_a,
                          const double* ref, double* out);
 hipError_t launch_accept(int r, int b, const LaunchCtx& c, const double* x2, const double* g2, const double* S2,

@@ -453,17 +453,28 @@ __global__ __launch_bounds__(kThreads) void k_polar_comb(LaunchCtx c, const doub
                                                          const double* __restrict__ Bv,
                                                          const double* __restrict__ ca,
                                                          const double* __restrict__ cb,
-                                                         double* __restrict__ out) {
+                                                         double* __restrict__ out,
+                                                         const double* __restrict__ Cv, double sa,
+                                                         double sb) {
   constexpr int D = B - 1;
   const PoseLane p = pose_lane<B>(c);
   if (tile_skipped(c, p.agent)) return;
   const bool own = p.ok && p.k < B;
   const long off = p.j * (R * B) + p.k * R;
-  const double a0 = ca ? ca[p.agent] : 1.0;
+  const double a0 = ca ? ca[p.agent] : sa;
   double acol[R];
   load_col<R, B>(A, p.j, p.k, p.ok, acol);
-  if (Bv != nullptr) {
-    const double b0 = cb[p.agent];
+  if (Cv != nullptr) {
+    // A + cb (B - C)   (updateV: V + gamma (X - Y), src/PGOAgent.cpp:1086-1091)
+    const double b0 = cb ? cb[p.agent] : sb;
+    double bcol[R], ccol[R];
+    load_col<R, B>(Bv, p.j, p.k, p.ok, bcol);
+    load_col<R, B>(Cv, p.j, p.k, p.ok, ccol);
+#pragma unroll
+    for (int a = 0; a < R; ++a) acol[a] = acol[a] + b0 * (bcol[a] - ccol[a]);
+  } else if (Bv != nullptr) {
+    // ca A + cb B   (updateY: (1 - alpha) X + alpha V, src/PGOAgent.cpp:1077-1084)
+    const double b0 = cb ? cb[p.agent] : sb;
     double bcol[R];
     load_col<R, B>(Bv, p.j, p.k, p.ok, bcol);
 #pragma unroll
@@ -768,6 +779,74 @@ __global__ __launch_bounds__(kThreads) void k_bj_inverse(int n, QView q, double 
 }
 
 // ------------------------------------------------------------------------------------------
+// Public-pose exchange helpers (PGOAgent::getSharedPoseDict / updateNeighborPoses,
+// src/PGOAgent.cpp:95-118, 434-479): dst[s] = pose idx[s] of A (idx >= 0) or of B (-1 - idx).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_gather_poses(int count, int rb, const int* __restrict__ idx,
+                                                           const double* __restrict__ A,
+                                                           const double* __restrict__ Bsrc,
+                                                           double* __restrict__ dst) {
+  const long t = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= static_cast<long>(count) * rb) return;
+  const int s = static_cast<int>(t / rb), e = static_cast<int>(t % rb);
+  const int i = idx[s];
+  dst[t] = i >= 0 ? A[static_cast<long>(i) * rb + e] : Bsrc[static_cast<long>(-1 - i) * rb + e];
+}
+
+// G assembly (PGOAgent::constructGMatrix, src/PGOAgent.cpp:783-859).  For G slot s (a public
+// pose of an agent) sum over its shared edges e:
+//   outgoing (agent owns p1):  L = -X_nbr Omega T^T = -[k Y R^T + t p t^T | t p]
+//   incoming (agent owns p2):  L = -X_nbr T Omega   = -[k Y R | t (Y t + p)]
+// with k = w kappa, t = w tau.  One thread per (slot, row a).
+template <int R, int B>
+__global__ __launch_bounds__(kThreads) void k_assemble_G(GEdges e, int nslots, const double* __restrict__ Xa,
+                                                         const double* __restrict__ Xb,
+                                                         double* __restrict__ gblk) {
+  constexpr int D = B - 1;
+  const long t = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= static_cast<long>(nslots) * R) return;
+  const int s = static_cast<int>(t / R), a = static_cast<int>(t % R);
+  double L[B];
+#pragma unroll
+  for (int c = 0; c < B; ++c) L[c] = 0.0;
+  for (int q = e.slot_off[s]; q < e.slot_off[s + 1]; ++q) {
+    const int src = e.src[q];
+    const double* P = src >= 0 ? Xa + static_cast<long>(src) * (R * B) : Xb + static_cast<long>(-1 - src) * (R * B);
+    double Y[D], p;
+#pragma unroll
+    for (int v = 0; v < D; ++v) Y[v] = P[v * R + a];
+    p = P[D * R + a];
+    const double k = e.w[q] * e.kappa[q], ta = e.w[q] * e.tau[q];
+    const double* Rm = e.R + static_cast<long>(q) * D * D;  // row-major
+    const double* tv = e.t + static_cast<long>(q) * D;
+    if (e.outgoing[q]) {
+#pragma unroll
+      for (int c = 0; c < D; ++c) {
+        double yr = 0.0;
+#pragma unroll
+        for (int v = 0; v < D; ++v) yr = fma(Y[v], Rm[c * D + v], yr);
+        L[c] -= k * yr + ta * p * tv[c];
+      }
+      L[D] -= ta * p;
+    } else {
+#pragma unroll
+      for (int c = 0; c < D; ++c) {
+        double yr = 0.0;
+#pragma unroll
+        for (int v = 0; v < D; ++v) yr = fma(Y[v], Rm[v * D + c], yr);
+        L[c] -= k * yr;
+      }
+      double yt = 0.0;
+#pragma unroll
+      for (int v = 0; v < D; ++v) yt = fma(Y[v], tv[v], yt);
+      L[D] -= ta * (yt + p);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < B; ++c) gblk[static_cast<long>(s) * (R * B) + c * R + a] = L[c];
+}
+
+// ------------------------------------------------------------------------------------------
 // Host-side launchers with (r, b) dispatch
 // ------------------------------------------------------------------------------------------
 #define DPGO_DISPATCH(R_, B_, CALL)                        \
@@ -860,9 +939,10 @@ hipError_t launch_precond(int r, int b, const LaunchCtx& c, const double* X, con
 }
 
 hipError_t launch_polar_comb(int r, int b, const LaunchCtx& c, const double* A, const double* Bv,
-                             const double* ca, const double* cb, double* out) {
+                             const double* ca, const double* cb, double* out, const double* Cv, double sa,
+                             double sb) {
   if (c.num_tiles == 0) return hipSuccess;
-  DPGO_DISPATCH(r, b, (k_polar_comb<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, A, Bv, ca, cb, out)));
+  DPGO_DISPATCH(r, b, (k_polar_comb<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, A, Bv, ca, cb, out, Cv, sa, sb)));
   return hipGetLastError();
 }
 
@@ -877,6 +957,23 @@ hipError_t launch_accept(int r, int b, const LaunchCtx& c, const double* x2, con
                          double* x1, double* g, double* S) {
   if (c.num_tiles == 0) return hipSuccess;
   DPGO_DISPATCH(r, b, (k_accept<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, x2, g2, S2, x1, g, S)));
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_poses(int count, int rb, const int* idx, const double* A, const double* Bsrc, double* dst,
+                               hipStream_t stream) {
+  if (count == 0) return hipSuccess;
+  const long total = static_cast<long>(count) * rb;
+  k_gather_poses<<<static_cast<int>((total + kThreads - 1) / kThreads), kThreads, 0, stream>>>(count, rb, idx, A, Bsrc, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_assemble_G(int r, int b, const GEdges& e, int nslots, const double* Xa, const double* Xb,
+                             double* gblk, hipStream_t stream) {
+  if (nslots == 0) return hipSuccess;
+  const long total = static_cast<long>(nslots) * r;
+  const int grid = static_cast<int>((total + kThreads - 1) / kThreads);
+  DPGO_DISPATCH(r, b, (k_assemble_G<R, B><<<grid, kThreads, 0, stream>>>(e, nslots, Xa, Xb, gblk)));
   return hipGetLastError();
 }
 

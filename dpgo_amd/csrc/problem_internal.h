@@ -1,0 +1,106 @@
+// Internal (non-ABI) view of a dpgo_hip_problem, shared by capi.cpp and rbcd.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/dpgo_hip.h"
+#include "kernels.h"
+
+namespace dpgo {
+
+int fail(int code, const std::string& msg);
+int usable_devices();
+
+#define HIP_TRY(expr)                                                                        \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess)                                                                    \
+      return ::dpgo::fail(DPGO_HIP_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+#define DPGO_TRY(expr)                  \
+  do {                                  \
+    int _rc = (expr);                   \
+    if (_rc != DPGO_HIP_OK) return _rc; \
+  } while (0)
+
+struct HostBSR {
+  std::vector<int> rowptr, col;
+  std::vector<double> blocks;
+};
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  hipError_t ensure(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    release();
+    n = std::max<size_t>(count, 1);
+    return hipMalloc(reinterpret_cast<void**>(&p), n * sizeof(T));
+  }
+};
+
+}  // namespace dpgo
+
+struct dpgo_hip_problem_s {
+  int K = 0, d = 0, r = 0, b = 0;
+  long N = 0;  // total poses
+  std::vector<int> n_agent;
+  std::vector<long> pose_off;
+  hipStream_t stream = nullptr;
+  hipStream_t own_stream = nullptr;
+
+  // tiles
+  std::vector<int> h_tile_agent, h_tile_start, h_tile_count, h_agent_tile_off;
+  int num_tiles = 0;
+  dpgo::DevBuf<int> tile_agent, tile_start, tile_count, agent_tile_off, agent_np, enabled, use_a;
+
+  // Q (per-agent host copies, concatenated on upload)
+  std::vector<dpgo::HostBSR> q_agent;
+  bool q_dirty = true;
+  dpgo::DevBuf<int> rowptr, col;
+  dpgo::DevBuf<double> blocks, minv;
+  long nnzb = 0;
+
+  // G (sparse pose blocks per agent)
+  std::vector<std::map<int, std::vector<double>>> g_agent;
+  bool g_dirty = true;
+  dpgo::DevBuf<int> gidx;
+  dpgo::DevBuf<double> gblk;
+  int num_gslots = 0;
+
+  int precon = DPGO_PRECON_BLOCK_JACOBI;
+
+  // work
+  dpgo::DevBuf<double> x1, x2, g, g2, S, S2, eta, Heta, rv, z, delta, Hdelta, tA, tB;
+  dpgo::DevBuf<double> pa, pb, sums, coef_a, coef_b;
+  dpgo::DevBuf<dpgo::AgentState> state;
+  std::vector<dpgo::AgentState> h_state;
+  std::vector<double> h_sums;
+
+  size_t vec_len() const { return static_cast<size_t>(N) * r * b; }
+  size_t vec_bytes() const { return vec_len() * sizeof(double); }
+  size_t s_len() const { return static_cast<size_t>(N) * (b - 1) * (b - 1); }
+};
+
+
+namespace dpgo {
+// helpers implemented in capi.cpp
+LaunchCtx make_ctx(dpgo_hip_problem h, int flag_kind, double* partials);
+int problem_ready(dpgo_hip_problem h);
+int ensure_work_public(dpgo_hip_problem h);
+}  // namespace dpgo

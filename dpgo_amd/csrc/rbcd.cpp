@@ -1,0 +1,535 @@
+// Multi-agent RBCD round engine (include/dpgo_rbcd.h).
+//
+// Mirrors, per agent, PGOAgent::iterate (src/PGOAgent.cpp:642-718) with updateX (:1093-1165),
+// constructQMatrix (:720-781), constructGMatrix (:783-859) and the Nesterov updates (:1033-1091),
+// under a colour-class schedule: in iteration t the agents of colour c_t are selected
+// (doOptimization = true) and every other agent runs iterate(false).  All selected agents of a
+// colour that live on this GPU are ONE batched dpgo_hip_problem.  Public poses move between
+// ranks through caller-owned device buffers; same-rank neighbours are read in place.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <set>
+#include <vector>
+
+#include "graph_internal.h"
+
+using namespace dpgo;
+
+struct dpgo_rbcd_s {
+  int d = 0, r = 0, b = 0, rank = 0, world = 1, K = 0, ncolors = 0;
+  dpgo_rbcd_params P;
+  std::vector<int> color;                 // per global agent
+  std::vector<int> owned;                 // owned global agents, colour-major
+  std::vector<int> color_off;             // [ncolors + 1] into owned
+  std::vector<long> own_pose_off;         // [owned + 1] pose offsets into owned buffers
+  long Nown = 0;
+  std::vector<int> own_global;            // owned buffer pose index -> global pose id
+  hipStream_t stream = nullptr;
+  std::vector<dpgo_hip_problem> prob;     // per colour (nullptr if none owned)
+  DevBuf<double> X, Y, V, Xprev;
+  // exchange
+  std::vector<long long> send_counts, recv_counts, send_off, recv_off;  // doubles
+  long n_send_items = 0, n_recv_poses = 0;
+  DevBuf<int> pack_idx, unpack_x, unpack_y;
+  DevBuf<double> RX, RY;
+  // per colour G assembly tables
+  struct GTab {
+    DevBuf<int> slot_off, src, outgoing;
+    DevBuf<double> R, t, kappa, tau, w;
+    int nslots = 0;
+  };
+  std::vector<GTab*> gt;
+  double gamma = 0.0, alpha = 0.0;
+  long iteration = 0;
+  long long agent_updates = 0;
+
+  ~dpgo_rbcd_s() {
+    for (auto* p : prob)
+      if (p) dpgo_hip_problem_destroy(p);
+    for (auto* g : gt) delete g;
+  }
+  size_t rb() const { return static_cast<size_t>(r) * b; }
+};
+
+namespace {
+
+template <typename T>
+int upload_vec(DevBuf<T>& dst, const std::vector<T>& src, hipStream_t s) {
+  HIP_TRY(dst.ensure(std::max<size_t>(src.size(), 1)));
+  if (!src.empty()) HIP_TRY(hipMemcpyAsync(dst.p, src.data(), sizeof(T) * src.size(), hipMemcpyHostToDevice, s));
+  return DPGO_HIP_OK;
+}
+
+double* color_ptr(dpgo_rbcd e, DevBuf<double>& buf, int c) {
+  return buf.p + static_cast<size_t>(e->own_pose_off[e->color_off[c]]) * e->rb();
+}
+
+int polar(dpgo_rbcd e, int c, const double* A, const double* B, double ca, double cb, double* out,
+          const double* C = nullptr) {
+  dpgo_hip_problem h = e->prob[c];
+  if (!h) return DPGO_HIP_OK;
+  // uniform Nesterov coefficients travel as kernel arguments
+  auto ctx = make_ctx(h, FLAG_NONE, h->pa.p);
+  HIP_TRY(launch_polar_comb(e->r, e->b, ctx, A, B, nullptr, nullptr, out, C, ca, cb));
+  return DPGO_HIP_OK;
+}
+
+int copy_poses(dpgo_rbcd e, double* dst, const double* src, long first_pose, long count) {
+  if (count <= 0) return DPGO_HIP_OK;
+  HIP_TRY(hipMemcpyAsync(dst + first_pose * e->rb(), src + first_pose * e->rb(), sizeof(double) * count * e->rb(),
+                         hipMemcpyDeviceToDevice, e->stream));
+  return DPGO_HIP_OK;
+}
+
+long color_first_pose(dpgo_rbcd e, int c) { return e->own_pose_off[e->color_off[c]]; }
+long color_num_poses(dpgo_rbcd e, int c) { return e->own_pose_off[e->color_off[c + 1]] - e->own_pose_off[e->color_off[c]]; }
+
+int assemble_G(dpgo_rbcd e, int c, bool aux) {
+  dpgo_hip_problem h = e->prob[c];
+  if (!h || e->gt[c]->nslots == 0) return DPGO_HIP_OK;
+  auto* t = e->gt[c];
+  GEdges ge{t->slot_off.p, t->src.p, t->outgoing.p, t->R.p, t->t.p, t->kappa.p, t->tau.p, t->w.p};
+  HIP_TRY(launch_assemble_G(e->r, e->b, ge, t->nslots, aux ? e->Y.p : e->X.p, aux ? e->RY.p : e->RX.p, h->gblk.p,
+                            e->stream));
+  return DPGO_HIP_OK;
+}
+
+int optimize_color(dpgo_rbcd e, int c, const double* Xin, double* Xout, dpgo_opt_result* results) {
+  dpgo_hip_problem h = e->prob[c];
+  if (!h) return DPGO_HIP_OK;
+  dpgo_opt_params p;
+  dpgo_hip_default_params(&p);
+  p.algorithm = e->P.algorithm;
+  p.tr_iterations = 1;
+  p.tr_tolerance = e->P.tolerance;
+  p.tr_max_inner = e->P.max_inner;
+  p.tr_initial_radius = e->P.initial_radius;
+  p.precon = e->P.precon;
+  DPGO_TRY(dpgo_hip_optimize_dev(h, &p, Xin, Xout, nullptr, results));
+  e->agent_updates += h->K;
+  return DPGO_HIP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void dpgo_rbcd_default_params(dpgo_rbcd_params* p) {
+  if (!p) return;
+  p->r = 5;
+  p->acceleration = 0;
+  p->restart_interval = 30;
+  p->max_inner = 10;
+  p->initial_radius = 100.0;
+  p->tolerance = 1e-2;
+  p->precon = DPGO_PRECON_BLOCK_JACOBI;
+  p->algorithm = DPGO_ALG_RTR;
+}
+
+int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, const int* agent_rank, int rank,
+                     int world, const dpgo_rbcd_params* params, dpgo_rbcd* out) {
+  if (!g || !agent_of_pose || !agent_rank || !out || num_agents <= 0 || world <= 0 || rank < 0 || rank >= world)
+    return fail(DPGO_HIP_EINVAL, "bad rbcd arguments");
+  *out = nullptr;
+  if (usable_devices() == 0) return fail(DPGO_HIP_ENODEV, "no gfx950 device available (no CPU fallback)");
+  auto* e = new dpgo_rbcd_s();
+  auto bail = [&](int rc) {
+    delete e;
+    return rc;
+  };
+  if (params)
+    e->P = *params;
+  else
+    dpgo_rbcd_default_params(&e->P);
+  e->d = g->d;
+  e->r = e->P.r;
+  e->b = g->d + 1;
+  e->rank = rank;
+  e->world = world;
+  e->K = num_agents;
+  const int n = g->n, d = g->d, b = e->b;
+  const size_t m = g->p1.size();
+  // local index of every pose inside its agent (global order)
+  std::vector<int> local(n), agent_n(num_agents, 0);
+  for (int i = 0; i < n; ++i) {
+    const int a = agent_of_pose[i];
+    if (a < 0 || a >= num_agents) return bail(fail(DPGO_HIP_EINVAL, "agent_of_pose out of range"));
+    local[i] = agent_n[a]++;
+  }
+  for (int a = 0; a < num_agents; ++a)
+    if (agent_n[a] == 0) return bail(fail(DPGO_HIP_EINVAL, "every agent needs >= 1 pose"));
+  // agent adjacency + greedy colouring in agent-id order
+  std::vector<std::set<int>> adj(num_agents);
+  for (size_t k = 0; k < m; ++k) {
+    const int a1 = agent_of_pose[g->p1[k]], a2 = agent_of_pose[g->p2[k]];
+    if (a1 != a2) {
+      adj[a1].insert(a2);
+      adj[a2].insert(a1);
+    }
+  }
+  e->color.assign(num_agents, -1);
+  for (int a = 0; a < num_agents; ++a) {
+    std::set<int> used;
+    for (int nb : adj[a])
+      if (e->color[nb] >= 0) used.insert(e->color[nb]);
+    int c = 0;
+    while (used.count(c)) ++c;
+    e->color[a] = c;
+    e->ncolors = std::max(e->ncolors, c + 1);
+  }
+  // owned agents, colour-major
+  e->color_off.assign(e->ncolors + 1, 0);
+  for (int c = 0; c < e->ncolors; ++c) {
+    for (int a = 0; a < num_agents; ++a)
+      if (agent_rank[a] == rank && e->color[a] == c) e->owned.push_back(a);
+    e->color_off[c + 1] = static_cast<int>(e->owned.size());
+  }
+  std::vector<int> owned_pos(num_agents, -1);
+  e->own_pose_off.assign(e->owned.size() + 1, 0);
+  for (size_t q = 0; q < e->owned.size(); ++q) {
+    owned_pos[e->owned[q]] = static_cast<int>(q);
+    e->own_pose_off[q + 1] = e->own_pose_off[q] + agent_n[e->owned[q]];
+  }
+  e->Nown = e->own_pose_off.back();
+  e->own_global.assign(e->Nown, -1);
+  for (int i = 0; i < n; ++i) {
+    const int q = owned_pos[agent_of_pose[i]];
+    if (q >= 0) e->own_global[e->own_pose_off[q] + local[i]] = i;
+  }
+  auto owned_index = [&](int pose) -> long {
+    const int q = owned_pos[agent_of_pose[pose]];
+    return q < 0 ? -1 : e->own_pose_off[q] + local[pose];
+  };
+  // ---- exchange plan: poses each peer needs from us / we need from each peer (sorted global ids)
+  std::vector<std::set<int>> send_set(world), recv_set(world);
+  for (size_t k = 0; k < m; ++k) {
+    const int i = g->p1[k], j = g->p2[k];
+    const int ri = agent_rank[agent_of_pose[i]], rj = agent_rank[agent_of_pose[j]];
+    if (agent_of_pose[i] == agent_of_pose[j] || ri == rj) continue;
+    if (ri == rank) {
+      send_set[rj].insert(i);
+      recv_set[rj].insert(j);
+    } else if (rj == rank) {
+      send_set[ri].insert(j);
+      recv_set[ri].insert(i);
+    }
+  }
+  const int mult = e->P.acceleration ? 2 : 1;
+  const long long rbd = static_cast<long long>(e->rb());
+  e->send_counts.assign(world, 0);
+  e->recv_counts.assign(world, 0);
+  e->send_off.assign(world + 1, 0);
+  e->recv_off.assign(world + 1, 0);
+  std::vector<int> pack_idx, unpack_x, unpack_y;
+  std::map<int, long> recv_slot;  // global pose -> recv pose index
+  long rs = 0;
+  for (int p = 0; p < world; ++p) {
+    const long cnt_s = static_cast<long>(send_set[p].size()), cnt_r = static_cast<long>(recv_set[p].size());
+    e->send_counts[p] = cnt_s * rbd * mult;
+    e->recv_counts[p] = cnt_r * rbd * mult;
+    e->send_off[p + 1] = e->send_off[p] + e->send_counts[p];
+    e->recv_off[p + 1] = e->recv_off[p] + e->recv_counts[p];
+    for (int pose : send_set[p]) pack_idx.push_back(static_cast<int>(owned_index(pose)));
+    if (mult == 2)
+      for (int pose : send_set[p]) pack_idx.push_back(-1 - static_cast<int>(owned_index(pose)));
+    const long base = e->recv_off[p] / rbd;  // recv segment start in poses
+    long s = 0;
+    for (int pose : recv_set[p]) {
+      recv_slot[pose] = rs++;
+      unpack_x.push_back(static_cast<int>(base + s));
+      if (mult == 2) unpack_y.push_back(static_cast<int>(base + cnt_r + s));
+      ++s;
+    }
+  }
+  e->n_send_items = static_cast<long>(pack_idx.size());
+  e->n_recv_poses = rs;
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
+    return bail(fail(DPGO_HIP_EDEVICE, "stream create failed"));
+  int rc = upload_vec(e->pack_idx, pack_idx, e->stream);
+  if (rc == DPGO_HIP_OK) rc = upload_vec(e->unpack_x, unpack_x, e->stream);
+  if (rc == DPGO_HIP_OK) rc = upload_vec(e->unpack_y, unpack_y, e->stream);
+  if (rc != DPGO_HIP_OK) return bail(rc);
+  if (e->RX.ensure(std::max<long>(rs, 1) * e->rb()) != hipSuccess || e->RY.ensure(std::max<long>(rs, 1) * e->rb()) != hipSuccess ||
+      e->X.ensure(std::max<long>(e->Nown, 1) * e->rb()) != hipSuccess ||
+      e->Y.ensure(std::max<long>(e->Nown, 1) * e->rb()) != hipSuccess ||
+      e->V.ensure(std::max<long>(e->Nown, 1) * e->rb()) != hipSuccess ||
+      e->Xprev.ensure(std::max<long>(e->Nown, 1) * e->rb()) != hipSuccess)
+    return bail(fail(DPGO_HIP_ENOMEM, "device allocation failed"));
+
+  // ---- per owned agent: Q (private edges + shared-edge diagonal terms) and shared edges
+  std::vector<std::vector<size_t>> agent_edges(e->owned.size());
+  for (size_t k = 0; k < m; ++k) {
+    const int q1 = owned_pos[agent_of_pose[g->p1[k]]], q2 = owned_pos[agent_of_pose[g->p2[k]]];
+    if (q1 >= 0) agent_edges[q1].push_back(k);
+    if (q2 >= 0 && q2 != q1) agent_edges[q2].push_back(k);
+  }
+  e->prob.assign(e->ncolors, nullptr);
+  e->gt.assign(e->ncolors, nullptr);
+  for (int c = 0; c < e->ncolors; ++c) {
+    e->gt[c] = new dpgo_rbcd_s::GTab();
+    const int a0 = e->color_off[c], a1 = e->color_off[c + 1];
+    if (a1 == a0) continue;
+    std::vector<int> counts;
+    for (int q = a0; q < a1; ++q) counts.push_back(agent_n[e->owned[q]]);
+    dpgo_hip_problem h = nullptr;
+    rc = dpgo_hip_problem_create_batch(a1 - a0, counts.data(), d, e->r, &h);
+    if (rc != DPGO_HIP_OK) return bail(rc);
+    e->prob[c] = h;
+    dpgo_hip_problem_set_stream(h, e->stream);
+    std::vector<int> slot_off{0}, src, outgoing;
+    std::vector<double> Rv, tv, kv, tauv, wv;
+    for (int q = a0; q < a1; ++q) {
+      const int A = e->owned[q];
+      BsrBuilder B(agent_n[A], b);
+      std::map<int, std::vector<size_t>> slots;  // local public pose -> shared edges
+      for (size_t k : agent_edges[q]) {
+        const int i = g->p1[k], j = g->p2[k];
+        if (agent_of_pose[i] == A && agent_of_pose[j] == A) {
+          B.touch(local[i], local[j]);
+          B.touch(local[j], local[i]);
+        } else {
+          slots[agent_of_pose[i] == A ? local[i] : local[j]].push_back(k);
+        }
+      }
+      B.freeze();
+      double Wii[16], Wjj[16], Wij[16], Wji[16];
+      for (size_t k : agent_edges[q]) {
+        const int i = g->p1[k], j = g->p2[k];
+        edge_blocks(d, &g->R[k * d * d], &g->t[k * d], g->kappa[k], g->tau[k], 1.0, Wii, Wjj, Wij, Wji);
+        const bool own_i = agent_of_pose[i] == A, own_j = agent_of_pose[j] == A;
+        if (own_i && own_j) {
+          B.add(local[i], local[i], Wii);
+          B.add(local[j], local[j], Wjj);
+          B.add(local[i], local[j], Wij);
+          B.add(local[j], local[i], Wji);
+        } else if (own_i) {
+          B.add(local[i], local[i], Wii);  // outgoing shared edge (:754-760)
+        } else {
+          B.add(local[j], local[j], Wjj);  // incoming shared edge (:770-775)
+        }
+      }
+      rc = dpgo_hip_set_Q_bsr(h, q - a0, agent_n[A], B.out.rowptr.data(), B.out.col.data(), B.out.blocks.data());
+      if (rc != DPGO_HIP_OK) return bail(rc);
+      std::vector<int> gpose;
+      for (auto& kv2 : slots) {
+        gpose.push_back(kv2.first);
+        for (size_t k : kv2.second) {
+          const int i = g->p1[k], j = g->p2[k];
+          const bool out_edge = agent_of_pose[i] == A;
+          const int nbr = out_edge ? j : i;
+          const long oi = owned_index(nbr);
+          src.push_back(oi >= 0 ? static_cast<int>(oi) : -1 - static_cast<int>(recv_slot.at(nbr)));
+          outgoing.push_back(out_edge ? 1 : 0);
+          Rv.insert(Rv.end(), &g->R[k * d * d], &g->R[k * d * d] + d * d);
+          tv.insert(tv.end(), &g->t[k * d], &g->t[k * d] + d);
+          kv.push_back(g->kappa[k]);
+          tauv.push_back(g->tau[k]);
+          wv.push_back(1.0);
+        }
+        slot_off.push_back(static_cast<int>(src.size()));
+      }
+      std::vector<double> zeros(gpose.size() * e->rb(), 0.0);
+      rc = dpgo_hip_set_G(h, q - a0, static_cast<int>(gpose.size()), gpose.data(), zeros.data());
+      if (rc != DPGO_HIP_OK) return bail(rc);
+    }
+    rc = problem_ready(h);  // uploads Q, block-Jacobi inverses, G slot map
+    if (rc != DPGO_HIP_OK) return bail(rc);
+    auto* t = e->gt[c];
+    t->nslots = static_cast<int>(slot_off.size()) - 1;
+    if (t->nslots != h->num_gslots) return bail(fail(DPGO_HIP_ESTATE, "G slot order mismatch"));
+    rc = upload_vec(t->slot_off, slot_off, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(t->src, src, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(t->outgoing, outgoing, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(t->R, Rv, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(t->t, tv, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(t->kappa, kv, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(t->tau, tauv, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(t->w, wv, e->stream);
+    if (rc == DPGO_HIP_OK && hipStreamSynchronize(e->stream) != hipSuccess) rc = fail(DPGO_HIP_EDEVICE, "sync");
+    if (rc != DPGO_HIP_OK) return bail(rc);
+  }
+  *out = e;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_destroy(dpgo_rbcd e) {
+  if (!e) return DPGO_HIP_OK;
+  hipStream_t s = e->stream;
+  if (s) (void)hipStreamSynchronize(s);
+  delete e;
+  if (s) (void)hipStreamDestroy(s);
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_set_stream(dpgo_rbcd e, void* stream) {
+  if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
+  if (!stream) return DPGO_HIP_OK;
+  e->stream = static_cast<hipStream_t>(stream);
+  for (auto* h : e->prob)
+    if (h) dpgo_hip_problem_set_stream(h, stream);
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_info(dpgo_rbcd e, int* num_colors, int* owned_agents, int* owned_poses, int* per_color) {
+  if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
+  if (num_colors) *num_colors = e->ncolors;
+  if (owned_agents) *owned_agents = static_cast<int>(e->owned.size());
+  if (owned_poses) *owned_poses = static_cast<int>(e->Nown);
+  if (per_color)
+    for (int c = 0; c < e->ncolors; ++c) per_color[c] = e->color_off[c + 1] - e->color_off[c];
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_color_of_agent(dpgo_rbcd e, int* color) {
+  if (!e || !color) return fail(DPGO_HIP_EINVAL, "null argument");
+  std::copy(e->color.begin(), e->color.end(), color);
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_exchange_counts(dpgo_rbcd e, long long* send_counts, long long* recv_counts) {
+  if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
+  for (int p = 0; p < e->world; ++p) {
+    if (send_counts) send_counts[p] = e->send_counts[p];
+    if (recv_counts) recv_counts[p] = e->recv_counts[p];
+  }
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_set_X(dpgo_rbcd e, const double* Xg) {
+  if (!e || !Xg) return fail(DPGO_HIP_EINVAL, "null argument");
+  const size_t rbs = e->rb();
+  std::vector<double> host(std::max<size_t>(static_cast<size_t>(e->Nown) * rbs, 1));
+  for (long q = 0; q < e->Nown; ++q)
+    std::memcpy(&host[q * rbs], Xg + static_cast<size_t>(e->own_global[q]) * rbs, sizeof(double) * rbs);
+  const size_t bytes = sizeof(double) * e->Nown * rbs;
+  if (bytes) {
+    HIP_TRY(hipMemcpyAsync(e->X.p, host.data(), bytes, hipMemcpyHostToDevice, e->stream));
+    // PGOAgent::setX -> initializeAcceleration (:55-68, :1062-1071): XPrev = V = Y = X
+    HIP_TRY(hipMemcpyAsync(e->Y.p, e->X.p, bytes, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->V.p, e->X.p, bytes, hipMemcpyDeviceToDevice, e->stream));
+    HIP_TRY(hipMemcpyAsync(e->Xprev.p, e->X.p, bytes, hipMemcpyDeviceToDevice, e->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->gamma = 0.0;
+  e->alpha = 0.0;
+  e->iteration = 0;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_get_X(dpgo_rbcd e, double* Xg) {
+  if (!e || !Xg) return fail(DPGO_HIP_EINVAL, "null argument");
+  const size_t rbs = e->rb();
+  std::vector<double> host(std::max<size_t>(static_cast<size_t>(e->Nown) * rbs, 1));
+  if (e->Nown) {
+    HIP_TRY(hipMemcpyAsync(host.data(), e->X.p, sizeof(double) * e->Nown * rbs, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+  }
+  for (long q = 0; q < e->Nown; ++q)
+    std::memcpy(Xg + static_cast<size_t>(e->own_global[q]) * rbs, &host[q * rbs], sizeof(double) * rbs);
+  return DPGO_HIP_OK;
+}
+
+static bool restart_now(dpgo_rbcd e) {
+  return e->P.acceleration && ((e->iteration + 1) % e->P.restart_interval == 0);  // shouldRestart :1033-1038
+}
+
+int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color) {
+  if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
+  e->iteration += 1;  // mIterationNumber++ (:643)
+  const long bytes = static_cast<long>(sizeof(double)) * e->Nown * static_cast<long>(e->rb());
+  if (bytes) HIP_TRY(hipMemcpyAsync(e->Xprev.p, e->X.p, bytes, hipMemcpyDeviceToDevice, e->stream));  // XPrev = X
+  if (!e->P.acceleration) return DPGO_HIP_OK;
+  const double N = static_cast<double>(e->K);
+  e->gamma = (1.0 + std::sqrt(1.0 + 4.0 * N * N * e->gamma * e->gamma)) / (2.0 * N);  // updateGamma
+  e->alpha = 1.0 / (e->gamma * N);                                                     // updateAlpha
+  const bool restart = restart_now(e);
+  for (int c = 0; c < e->ncolors; ++c) {
+    if (!e->prob[c]) continue;
+    double* Xc = color_ptr(e, e->X, c);
+    double* Yc = color_ptr(e, e->Y, c);
+    double* Vc = color_ptr(e, e->V, c);
+    // updateY: Y = project((1 - alpha) X + alpha V)  (every agent)
+    DPGO_TRY(polar(e, c, Xc, Vc, 1.0 - e->alpha, e->alpha, Yc));
+    if (c == color) continue;
+    // non-selected agents: updateX(false, true): X = Y; updateV; restart
+    DPGO_TRY(copy_poses(e, e->X.p, e->Y.p, color_first_pose(e, c), color_num_poses(e, c)));
+    DPGO_TRY(polar(e, c, Vc, Xc, 0.0, e->gamma, Vc, Yc));  // V = project(V + gamma (X - Y))
+    if (restart) {
+      DPGO_TRY(copy_poses(e, e->X.p, e->Xprev.p, color_first_pose(e, c), color_num_poses(e, c)));
+      DPGO_TRY(copy_poses(e, e->V.p, e->X.p, color_first_pose(e, c), color_num_poses(e, c)));
+      DPGO_TRY(copy_poses(e, e->Y.p, e->X.p, color_first_pose(e, c), color_num_poses(e, c)));
+    }
+  }
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_pack(dpgo_rbcd e, double* send_dev) {
+  if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
+  if (e->n_send_items == 0) return DPGO_HIP_OK;
+  HIP_TRY(launch_gather_poses(static_cast<int>(e->n_send_items), static_cast<int>(e->rb()), e->pack_idx.p, e->X.p,
+                              e->Y.p, send_dev, e->stream));
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_update(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_result* results) {
+  if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
+  const int rbs = static_cast<int>(e->rb());
+  if (e->n_recv_poses > 0) {
+    if (!recv_dev) return fail(DPGO_HIP_EINVAL, "receive buffer required");
+    HIP_TRY(launch_gather_poses(static_cast<int>(e->n_recv_poses), rbs, e->unpack_x.p, recv_dev, recv_dev, e->RX.p,
+                                e->stream));
+    if (e->P.acceleration)
+      HIP_TRY(launch_gather_poses(static_cast<int>(e->n_recv_poses), rbs, e->unpack_y.p, recv_dev, recv_dev, e->RY.p,
+                                  e->stream));
+  }
+  const bool restart = restart_now(e);
+  if (e->prob[color]) {
+    double* Xc = color_ptr(e, e->X, color);
+    double* Yc = color_ptr(e, e->Y, color);
+    double* Vc = color_ptr(e, e->V, color);
+    if (e->P.acceleration) {
+      DPGO_TRY(assemble_G(e, color, true));  // constructGMatrix(neighborAuxPoseDict)
+      DPGO_TRY(optimize_color(e, color, Yc, Xc, results));
+      DPGO_TRY(polar(e, color, Vc, Xc, 0.0, e->gamma, Vc, Yc));  // updateV
+      if (restart) {  // restartNesterovAcceleration(true) (:1040-1060)
+        DPGO_TRY(copy_poses(e, e->X.p, e->Xprev.p, color_first_pose(e, color), color_num_poses(e, color)));
+        DPGO_TRY(assemble_G(e, color, false));
+        DPGO_TRY(optimize_color(e, color, Xc, Xc, results));
+        DPGO_TRY(copy_poses(e, e->V.p, e->X.p, color_first_pose(e, color), color_num_poses(e, color)));
+        DPGO_TRY(copy_poses(e, e->Y.p, e->X.p, color_first_pose(e, color), color_num_poses(e, color)));
+      }
+    } else {
+      DPGO_TRY(assemble_G(e, color, false));  // constructGMatrix(neighborPoseDict)
+      DPGO_TRY(optimize_color(e, color, Xc, Xc, results));
+    }
+  }
+  if (restart) {
+    e->gamma = 0.0;
+    e->alpha = 0.0;
+  }
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_bench_spmm(dpgo_rbcd e, int color, int reps, double* bytes, double* ms) {
+  if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
+  dpgo_hip_problem h = e->prob[color];
+  if (!h) {
+    if (bytes) *bytes = 0.0;
+    if (ms) *ms = 0.0;
+    return DPGO_HIP_OK;
+  }
+  if (bytes) *bytes = dpgo_hip_spmm_bytes(h);
+  DPGO_TRY(ensure_work_public(h));
+  return dpgo_hip_bench_spmm(h, color_ptr(e, e->X, color), h->tA.p, reps, ms);
+}
+
+int dpgo_rbcd_counters(dpgo_rbcd e, long long* agent_updates, long long* iterations) {
+  if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
+  if (agent_updates) *agent_updates = e->agent_updates;
+  if (iterations) *iterations = e->iteration;
+  return DPGO_HIP_OK;
+}
+
+}  // extern "C"

@@ -329,3 +329,220 @@ def project_polar(M, d):
     o = np.empty_like(x)
     _check(lib().dpgo_hip_project_polar(r, d, n, xp, o.ctypes.data_as(_dp)))
     return from_dev_layout(o, r)
+
+
+# ----------------------------------------------------------------------------------------
+# Pose graphs + multi-agent RBCD engine (include/dpgo_rbcd.h)
+# ----------------------------------------------------------------------------------------
+class RbcdParams(C.Structure):
+    _fields_ = [("r", C.c_int), ("acceleration", C.c_int), ("restart_interval", C.c_int),
+                ("max_inner", C.c_int), ("initial_radius", C.c_double), ("tolerance", C.c_double),
+                ("precon", C.c_int), ("algorithm", C.c_int)]
+
+
+_lp = C.POINTER(C.c_longlong)
+_SIGS2 = [
+    ("dpgo_graph_read_g2o", [C.c_char_p, C.POINTER(C.c_void_p)], C.c_int),
+    ("dpgo_graph_grid3d", [C.c_int, C.c_ulonglong, C.c_double, C.c_double, C.POINTER(C.c_void_p)], C.c_int),
+    ("dpgo_graph_from_arrays", [C.c_int, C.c_int, C.c_int, _ip, _ip, _dp, _dp, _dp, _dp,
+                                C.POINTER(C.c_void_p)], C.c_int),
+    ("dpgo_graph_info", [C.c_void_p, _ip, _ip, _ip, _ip], C.c_int),
+    ("dpgo_graph_copy_out", [C.c_void_p, _ip, _ip, _dp, _dp, _dp, _dp], C.c_int),
+    ("dpgo_graph_destroy", [C.c_void_p], C.c_int),
+    ("dpgo_graph_laplacian_bsr", [C.c_void_p, _lp, _ip, _ip, _dp], C.c_int),
+    ("dpgo_graph_chain_init", [C.c_void_p, C.c_int, _dp, _dp], C.c_int),
+    ("dpgo_graph_grid_partition", [C.c_void_p, C.c_int, _ip], C.c_int),
+    ("dpgo_rbcd_default_params", [C.POINTER(RbcdParams)], None),
+    ("dpgo_rbcd_create", [C.c_void_p, C.c_int, _ip, _ip, C.c_int, C.c_int, C.POINTER(RbcdParams),
+                          C.POINTER(C.c_void_p)], C.c_int),
+    ("dpgo_rbcd_destroy", [C.c_void_p], C.c_int),
+    ("dpgo_rbcd_set_stream", [C.c_void_p, C.c_void_p], C.c_int),
+    ("dpgo_rbcd_info", [C.c_void_p, _ip, _ip, _ip, _ip], C.c_int),
+    ("dpgo_rbcd_color_of_agent", [C.c_void_p, _ip], C.c_int),
+    ("dpgo_rbcd_exchange_counts", [C.c_void_p, _lp, _lp], C.c_int),
+    ("dpgo_rbcd_set_X", [C.c_void_p, _dp], C.c_int),
+    ("dpgo_rbcd_get_X", [C.c_void_p, _dp], C.c_int),
+    ("dpgo_rbcd_pre_exchange", [C.c_void_p, C.c_int], C.c_int),
+    ("dpgo_rbcd_pack", [C.c_void_p, C.c_void_p], C.c_int),
+    ("dpgo_rbcd_update", [C.c_void_p, C.c_int, C.c_void_p, C.POINTER(OptResult)], C.c_int),
+    ("dpgo_rbcd_bench_spmm", [C.c_void_p, C.c_int, C.c_int, _dp, _dp], C.c_int),
+    ("dpgo_rbcd_counters", [C.c_void_p, _lp, _lp], C.c_int),
+]
+_SIGS.extend(_SIGS2)
+EXPORTED_SYMBOLS.extend(s[0] for s in _SIGS2)
+
+
+class Graph:
+    """Pose graph held by the native library (g2o reader / synthetic grid / arrays)."""
+
+    def __init__(self, handle):
+        self.h = handle
+        d, n, m, dup = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        _check(lib().dpgo_graph_info(self.h, C.byref(d), C.byref(n), C.byref(m), C.byref(dup)))
+        self.d, self.n, self.m, self.duplicates = d.value, n.value, m.value, dup.value
+
+    @classmethod
+    def read_g2o(cls, path):
+        h = C.c_void_p()
+        _check(lib().dpgo_graph_read_g2o(path.encode(), C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def grid3d(cls, k, seed=0, rot_sigma=0.2, trans_sigma=0.1):
+        h = C.c_void_p()
+        _check(lib().dpgo_graph_grid3d(int(k), int(seed), rot_sigma, trans_sigma, C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def from_arrays(cls, d, n, p1, p2, R, t, kappa, tau):
+        a1, a1p = _i32(p1)
+        a2, a2p = _i32(p2)
+        Rr, Rp = _f64(np.asarray(R).reshape(-1))
+        tt, tp = _f64(np.asarray(t).reshape(-1))
+        kk, kp = _f64(kappa)
+        ta, tap = _f64(tau)
+        h = C.c_void_p()
+        _check(lib().dpgo_graph_from_arrays(d, int(n), len(a1), a1p, a2p, Rp, tp, kp, tap, C.byref(h)))
+        return cls(h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().dpgo_graph_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def arrays(self):
+        d, m = self.d, self.m
+        p1 = np.empty(m, np.int32); p2 = np.empty(m, np.int32)
+        R = np.empty(m * d * d); t = np.empty(m * d); k = np.empty(m); ta = np.empty(m)
+        _check(lib().dpgo_graph_copy_out(self.h, p1.ctypes.data_as(_ip), p2.ctypes.data_as(_ip),
+                                         R.ctypes.data_as(_dp), t.ctypes.data_as(_dp),
+                                         k.ctypes.data_as(_dp), ta.ctypes.data_as(_dp)))
+        return dict(p1=p1, p2=p2, R=R.reshape(m, d, d), t=t.reshape(m, d), kappa=k, tau=ta)
+
+    def laplacian_bsr(self):
+        """Whole-graph Q: (browptr, bcol, blocks[nnzb, b, b] column-major)."""
+        nnz = C.c_longlong()
+        _check(lib().dpgo_graph_laplacian_bsr(self.h, C.byref(nnz), None, None, None))
+        b = self.d + 1
+        rp = np.empty(self.n + 1, np.int32); col = np.empty(nnz.value, np.int32)
+        blk = np.empty(nnz.value * b * b)
+        _check(lib().dpgo_graph_laplacian_bsr(self.h, C.byref(nnz), rp.ctypes.data_as(_ip),
+                                              col.ctypes.data_as(_ip), blk.ctypes.data_as(_dp)))
+        return rp, col, blk
+
+    def chain_init(self, r, YLift):
+        """YLift (r x d) times the odometry-chain initialisation; returns r x (d+1) n."""
+        Y, Yp = _f64(np.asarray(YLift, dtype=np.float64).T.ravel())  # column-major
+        out = np.empty(self.n * (self.d + 1) * r)
+        _check(lib().dpgo_graph_chain_init(self.h, r, Yp, out.ctypes.data_as(_dp)))
+        return from_dev_layout(out, r)
+
+    def chain_init_dev_layout(self, r, YLift):
+        Y, Yp = _f64(np.asarray(YLift, dtype=np.float64).T.ravel())
+        out = np.empty(self.n * (self.d + 1) * r)
+        _check(lib().dpgo_graph_chain_init(self.h, r, Yp, out.ctypes.data_as(_dp)))
+        return out
+
+    def grid_partition(self, agents_per_axis):
+        out = np.empty(self.n, np.int32)
+        _check(lib().dpgo_graph_grid_partition(self.h, int(agents_per_axis), out.ctypes.data_as(_ip)))
+        return out
+
+
+def lifting_matrix(d, r, seed=2):
+    """Repo-defined lifting matrix YLift in St(d, r) (replaces ROPTLIB's RNG)."""
+    M = np.random.default_rng(seed).standard_normal((r, d))
+    Qm, Rm = np.linalg.qr(M)
+    s = np.sign(np.diag(Rm))
+    s[s == 0] = 1
+    return Qm * s
+
+
+def rbcd_params(**kw) -> RbcdParams:
+    p = RbcdParams()
+    lib().dpgo_rbcd_default_params(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+class Rbcd:
+    """Colour-class RBCD over N agents; this process owns the agents with agent_rank == rank."""
+
+    def __init__(self, graph: Graph, agent_of_pose, agent_rank, rank=0, world=1, params=None):
+        self.graph = graph
+        aop, ap = _i32(agent_of_pose)
+        ar, arp = _i32(agent_rank)
+        self.num_agents = len(ar)
+        self.params = params or rbcd_params()
+        h = C.c_void_p()
+        _check(lib().dpgo_rbcd_create(graph.h, self.num_agents, ap, arp, rank, world,
+                                      C.byref(self.params), C.byref(h)))
+        self.h = h
+        self.rank, self.world = rank, world
+        nc, na, npz = C.c_int(), C.c_int(), C.c_int()
+        _check(lib().dpgo_rbcd_info(self.h, C.byref(nc), C.byref(na), C.byref(npz), None))
+        self.num_colors, self.owned_agents, self.owned_poses = nc.value, na.value, npz.value
+        per = np.empty(self.num_colors, np.int32)
+        _check(lib().dpgo_rbcd_info(self.h, None, None, None, per.ctypes.data_as(_ip)))
+        self.agents_per_color = per
+        col = np.empty(self.num_agents, np.int32)
+        _check(lib().dpgo_rbcd_color_of_agent(self.h, col.ctypes.data_as(_ip)))
+        self.color_of_agent = col
+        sc = np.empty(world, np.int64); rc = np.empty(world, np.int64)
+        _check(lib().dpgo_rbcd_exchange_counts(self.h, sc.ctypes.data_as(_lp), rc.ctypes.data_as(_lp)))
+        self.send_counts, self.recv_counts = sc, rc
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().dpgo_rbcd_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_ptr):
+        _check(lib().dpgo_rbcd_set_stream(self.h, C.c_void_p(stream_ptr)))
+
+    def set_X(self, X):
+        x, xp = _f64(to_dev_layout(X) if X.ndim == 2 else X)
+        _check(lib().dpgo_rbcd_set_X(self.h, xp))
+
+    def get_X_into(self, Xflat):
+        """Write owned poses into a global flat (device-layout) host array."""
+        assert Xflat.dtype == np.float64 and Xflat.flags.c_contiguous
+        _check(lib().dpgo_rbcd_get_X(self.h, Xflat.ctypes.data_as(_dp)))
+
+    def pre_exchange(self, color):
+        _check(lib().dpgo_rbcd_pre_exchange(self.h, int(color)))
+
+    def pack(self, send_ptr):
+        _check(lib().dpgo_rbcd_pack(self.h, C.c_void_p(send_ptr or 0)))
+
+    def update(self, color, recv_ptr, want_results=False):
+        if want_results:
+            n = int(self.agents_per_color[color])
+            res = (OptResult * max(n, 1))()
+            _check(lib().dpgo_rbcd_update(self.h, int(color), C.c_void_p(recv_ptr or 0), res))
+            return [res[i].as_dict() for i in range(n)]
+        _check(lib().dpgo_rbcd_update(self.h, int(color), C.c_void_p(recv_ptr or 0), None))
+        return None
+
+    def bench_spmm(self, color, reps):
+        b, ms = C.c_double(), C.c_double()
+        _check(lib().dpgo_rbcd_bench_spmm(self.h, int(color), int(reps), C.byref(b), C.byref(ms)))
+        return b.value, ms.value
+
+    def counters(self):
+        a, i = C.c_longlong(), C.c_longlong()
+        _check(lib().dpgo_rbcd_counters(self.h, C.byref(a), C.byref(i)))
+        return a.value, i.value

@@ -1,0 +1,92 @@
+/*
+ * dpgo_rbcd.h -- pose-graph inputs and the multi-agent RBCD round engine (libdpgo_hip.so).
+ *
+ * Graph side (host C++):
+ *   dpgo_graph_read_g2o      read_g2o_file            src/DPGO_utils.cpp:78-212 (+ SURVEY App. B fixes)
+ *   dpgo_graph_laplacian_bsr constructConnectionLaplacianSE  src/DPGO_utils.cpp:214-286
+ *   dpgo_graph_grid3d        synthetic 3D grid (replaces the missing g2o100k/1M inputs)
+ *   dpgo_graph_chain_init    odometryInitialization   src/DPGO_utils.cpp:426-447, lifted by YLift
+ *
+ * Engine side: N PGOAgents partitioned over ranks (one process per GPU).  Per RBCD iteration
+ * one colour class of the agent-adjacency graph is "selected" (doOptimization = true,
+ * src/PGOAgent.cpp:642-718); all other agents run iterate(false).  Selected agents on a GPU are
+ * solved as ONE batched dpgo_hip_problem (their Q blocks are independent).  Neighbour public poses
+ * cross ranks through caller-owned device buffers (the caller moves them with RCCL
+ * all_to_all); same-rank neighbours are read directly from device memory.
+ * Robust cost: L2 only (GNC weight updates are SURVEY 8f "next").
+ */
+#ifndef DPGO_RBCD_H
+#define DPGO_RBCD_H
+
+#include "dpgo_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct dpgo_graph_s* dpgo_graph;
+typedef struct dpgo_rbcd_s* dpgo_rbcd;
+
+/* ---- pose graphs --------------------------------------------------------------------------*/
+int dpgo_graph_read_g2o(const char* path, dpgo_graph* out);
+int dpgo_graph_grid3d(int k, unsigned long long seed, double rot_sigma, double trans_sigma,
+                      dpgo_graph* out);
+int dpgo_graph_from_arrays(int d, int n, int m, const int* p1, const int* p2, const double* R,
+                           const double* t, const double* kappa, const double* tau, dpgo_graph* out);
+/* d, n = max pose index + 1, m = #edges, duplicates = #repeated (p1,p2) pairs */
+int dpgo_graph_info(dpgo_graph g, int* d, int* n, int* m, int* duplicates);
+/* R row-major d*d per edge, t d per edge; any output may be NULL */
+int dpgo_graph_copy_out(dpgo_graph g, int* p1, int* p2, double* R, double* t, double* kappa,
+                        double* tau);
+int dpgo_graph_destroy(dpgo_graph g);
+/* Whole-graph Q as BSR (block (j, bcol) column-major).  Call with browptr == NULL to get nnzb. */
+int dpgo_graph_laplacian_bsr(dpgo_graph g, long long* nnzb, int* browptr, int* bcol, double* blocks);
+/* X = YLift * T_odo, T_odo composed along the p2 = p1 + 1 edges (r x (d+1) n, column-major). */
+int dpgo_graph_chain_init(dpgo_graph g, int r, const double* YLift_colmajor, double* X_out);
+/* Grid graphs: agent = sub-cube (x/s, y/s, z/s), s = k / A; id = ax + A (ay + A az). */
+int dpgo_graph_grid_partition(dpgo_graph g, int agents_per_axis, int* agent_of_pose);
+
+/* ---- RBCD engine ----------------------------------------------------------------------------*/
+typedef struct {
+  int r;                  /* relaxation rank */
+  int acceleration;       /* Nesterov (PGOAgentParameters::acceleration) */
+  int restart_interval;   /* 30 */
+  int max_inner;          /* tCG iterations per update (10, src/PGOAgent.cpp:1135) */
+  double initial_radius;  /* 100 (src/PGOAgent.cpp:1136) */
+  double tolerance;       /* 1e-2 (src/PGOAgent.cpp:1133) */
+  int precon;             /* DPGO_PRECON_BLOCK_JACOBI */
+  int algorithm;          /* DPGO_ALG_RTR / DPGO_ALG_RGD */
+} dpgo_rbcd_params;
+
+void dpgo_rbcd_default_params(dpgo_rbcd_params* p);
+/* agent_of_pose[n] in [0, num_agents); agent_rank[num_agents] in [0, world). */
+int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, const int* agent_rank,
+                     int rank, int world, const dpgo_rbcd_params* p, dpgo_rbcd* out);
+int dpgo_rbcd_destroy(dpgo_rbcd e);
+int dpgo_rbcd_set_stream(dpgo_rbcd e, void* stream);
+/* number of colour classes, agents owned by this rank, poses owned by this rank */
+int dpgo_rbcd_info(dpgo_rbcd e, int* num_colors, int* owned_agents, int* owned_poses,
+                   int* owned_agents_per_color /* [num_colors] or NULL */);
+int dpgo_rbcd_color_of_agent(dpgo_rbcd e, int* color /* [num_agents] */);
+/* doubles this rank sends to / receives from each peer per exchange (world entries each) */
+int dpgo_rbcd_exchange_counts(dpgo_rbcd e, long long* send_counts, long long* recv_counts);
+/* global r x (d+1) n column-major host X: copy the owned poses in; (re)initialise Nesterov state */
+int dpgo_rbcd_set_X(dpgo_rbcd e, const double* X_global);
+/* write the owned poses into a global host array (other poses untouched) */
+int dpgo_rbcd_get_X(dpgo_rbcd e, double* X_global);
+/* Phase 1 of iteration with selected colour c: every non-selected agent runs iterate(false). */
+int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color);
+/* Pack the public poses peers need (X, then Y when accelerated) into send_dev. */
+int dpgo_rbcd_pack(dpgo_rbcd e, double* send_dev);
+/* Phase 2: selected agents of colour c update from the received neighbour poses. */
+int dpgo_rbcd_update(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_result* results);
+/* Algorithmic HBM bytes of one X.Q SpMM over colour class c on this rank, and the timed average
+ * of `reps` such launches (ms, HIP events on the engine stream). */
+int dpgo_rbcd_bench_spmm(dpgo_rbcd e, int color, int reps, double* bytes, double* ms);
+/* SpMM / HVP launches issued so far (for throughput accounting) */
+int dpgo_rbcd_counters(dpgo_rbcd e, long long* agent_updates, long long* iterations);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPGO_RBCD_H */

@@ -1,0 +1,449 @@
+// CPU restatement of one PGOAgent RBCD step -- TEST / BASELINE INFRASTRUCTURE, NOT PRODUCT CODE.
+//
+// A plain single-threaded C++ restatement (no Eigen / CHOLMOD / ROPTLIB: absent) of
+//   PGOAgent::iterate(true) + iterate(false)     src/PGOAgent.cpp:642-718, 1033-1165
+//   constructQMatrix / constructGMatrix          src/PGOAgent.cpp:720-859
+//   QuadraticProblem f / EucGrad / HVP / precond src/QuadraticProblem.cpp:50-101 (block-Jacobi)
+//   QuadraticOptimizer RTR (1 outer, tCG)        src/QuadraticOptimizer.cpp:34-122 + SURVEY A.4
+//   LiftedSEManifold project (one-sided Jacobi)  src/manifold/LiftedSEManifold.cpp:34-45
+// Only bench.py's cpu_baseline leg and tests/ use it (via oracle/cpu_port.py): it is the
+// timed host-core baseline ("kind": "port") beside the GPU path, never part of the product.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <vector>
+
+namespace {
+
+struct Agent {
+  int d, r, b, n;
+  std::vector<int> rowptr, col;      // BSR of Q (block (j,i) column-major)
+  std::vector<double> blk, minv;     // blocks, per-pose (Q_jj + 0.1 I)^-1 row-major
+  std::vector<int> gpose;            // poses with a G block
+  std::vector<double> gblk;          // r*b per entry (column-major)
+  std::vector<int> gslot;            // pose -> slot or -1
+  size_t L() const { return static_cast<size_t>(n) * r * b; }
+};
+
+inline double dot(const std::vector<double>& a, const std::vector<double>& c) {
+  double s = 0.0;
+  for (size_t i = 0; i < a.size(); ++i) s += a[i] * c[i];
+  return s;
+}
+
+void spmm(const Agent& A, const double* X, double* Y) {
+  const int r = A.r, b = A.b, rb = r * b;
+  for (int j = 0; j < A.n; ++j) {
+    double acc[32] = {0};
+    for (int k = A.rowptr[j]; k < A.rowptr[j + 1]; ++k) {
+      const double* Xi = X + static_cast<size_t>(A.col[k]) * rb;
+      const double* B = &A.blk[static_cast<size_t>(k) * b * b];  // block(j,i) col-major = Q_ij row-major
+      for (int u = 0; u < b; ++u)       // row u of Q_ij
+        for (int c = 0; c < b; ++c) {
+          const double q = B[u * b + c];
+          for (int a = 0; a < r; ++a) acc[c * r + a] += Xi[u * r + a] * q;
+        }
+    }
+    std::memcpy(Y + static_cast<size_t>(j) * rb, acc, sizeof(double) * rb);
+  }
+}
+
+// V_Y <- V_Y - Y sym(Y^T V_Y) per pose
+void project_pose(int r, int d, const double* X, double* V) {
+  double S[9];
+  for (int p = 0; p < d; ++p)
+    for (int q = 0; q < d; ++q) {
+      double s = 0.0;
+      for (int a = 0; a < r; ++a) s += X[p * r + a] * V[q * r + a];
+      S[p * d + q] = s;
+    }
+  double Ss[9];
+  for (int p = 0; p < d; ++p)
+    for (int q = 0; q < d; ++q) Ss[p * d + q] = 0.5 * (S[p * d + q] + S[q * d + p]);
+  for (int q = 0; q < d; ++q)
+    for (int a = 0; a < r; ++a) {
+      double s = V[q * r + a];
+      for (int p = 0; p < d; ++p) s -= X[p * r + a] * Ss[p * d + q];
+      V[q * r + a] = s;
+    }
+}
+
+void sym_yt(int r, int d, const double* X, const double* M, double* Ss) {
+  double S[9];
+  for (int p = 0; p < d; ++p)
+    for (int q = 0; q < d; ++q) {
+      double s = 0.0;
+      for (int a = 0; a < r; ++a) s += X[p * r + a] * M[q * r + a];
+      S[p * d + q] = s;
+    }
+  for (int p = 0; p < d; ++p)
+    for (int q = 0; q < d; ++q) Ss[p * d + q] = 0.5 * (S[p * d + q] + S[q * d + p]);
+}
+
+void qf_pose(int r, int d, double* M) {  // Gram-Schmidt twice, positive diagonal
+  for (int q = 0; q < d; ++q) {
+    for (int pass = 0; pass < 2; ++pass)
+      for (int p = 0; p < q; ++p) {
+        double s = 0.0;
+        for (int a = 0; a < r; ++a) s += M[p * r + a] * M[q * r + a];
+        for (int a = 0; a < r; ++a) M[q * r + a] -= s * M[p * r + a];
+      }
+    double nn = 0.0;
+    for (int a = 0; a < r; ++a) nn += M[q * r + a] * M[q * r + a];
+    const double inv = 1.0 / std::sqrt(nn);
+    for (int a = 0; a < r; ++a) M[q * r + a] *= inv;
+  }
+}
+
+void polar_pose(int r, int d, double* M) {  // one-sided Jacobi SVD -> U V^T
+  double V[9] = {0};
+  for (int p = 0; p < d; ++p) V[p * d + p] = 1.0;
+  for (int sweep = 0; sweep < 30; ++sweep) {
+    bool rot = false;
+    for (int p = 0; p < d - 1; ++p)
+      for (int q = p + 1; q < d; ++q) {
+        double al = 0, be = 0, ga = 0;
+        for (int a = 0; a < r; ++a) {
+          al += M[p * r + a] * M[p * r + a];
+          be += M[q * r + a] * M[q * r + a];
+          ga += M[p * r + a] * M[q * r + a];
+        }
+        if (ga != 0.0 && std::fabs(ga) > 1e-17 * std::sqrt(al * be)) {
+          rot = true;
+          const double z = (be - al) / (2 * ga);
+          const double t = std::copysign(1.0, z) / (std::fabs(z) + std::sqrt(1 + z * z));
+          const double c = 1 / std::sqrt(1 + t * t), s = c * t;
+          for (int a = 0; a < r; ++a) {
+            const double mp = M[p * r + a], mq = M[q * r + a];
+            M[p * r + a] = c * mp - s * mq;
+            M[q * r + a] = s * mp + c * mq;
+          }
+          for (int a = 0; a < d; ++a) {
+            const double vp = V[a * d + p], vq = V[a * d + q];
+            V[a * d + p] = c * vp - s * vq;
+            V[a * d + q] = s * vp + c * vq;
+          }
+        }
+      }
+    if (!rot) break;
+  }
+  double U[8 * 3];
+  for (int q = 0; q < d; ++q) {
+    double nn = 0;
+    for (int a = 0; a < r; ++a) nn += M[q * r + a] * M[q * r + a];
+    const double inv = nn > 0 ? 1 / std::sqrt(nn) : 0;
+    for (int a = 0; a < r; ++a) U[q * r + a] = M[q * r + a] * inv;
+  }
+  for (int q = 0; q < d; ++q)
+    for (int a = 0; a < r; ++a) {
+      double s = 0;
+      for (int p = 0; p < d; ++p) s += U[p * r + a] * V[q * d + p];
+      M[q * r + a] = s;
+    }
+}
+
+struct Work {
+  std::vector<double> x1, x2, g, g2, S, S2, eta, Heta, rv, z, delta, Hd, tmp;
+  void init(size_t L, size_t SL) {
+    for (auto* v : {&x1, &x2, &g, &g2, &eta, &Heta, &rv, &z, &delta, &Hd, &tmp}) v->assign(L, 0.0);
+    S.assign(SL, 0.0);
+    S2.assign(SL, 0.0);
+  }
+};
+
+// f, g = P_X(XQ + G), S = sym(Y^T EG_Y); returns f, sets |g|^2
+double eval(const Agent& A, const double* X, double* g, double* S, double* ng2, std::vector<double>& tmp) {
+  const int r = A.r, d = A.d, b = A.b, rb = r * b;
+  spmm(A, X, tmp.data());
+  double f = 0.0, gg = 0.0;
+  for (int j = 0; j < A.n; ++j) {
+    double* EG = &tmp[static_cast<size_t>(j) * rb];
+    const double* Xj = X + static_cast<size_t>(j) * rb;
+    const int s = A.gslot[j];
+    for (int e = 0; e < rb; ++e) {
+      const double gv = s >= 0 ? A.gblk[static_cast<size_t>(s) * rb + e] : 0.0;
+      f += (0.5 * EG[e] + gv) * Xj[e];
+      EG[e] += gv;
+    }
+    sym_yt(r, d, Xj, EG, S + static_cast<size_t>(j) * d * d);
+    double* gj = g + static_cast<size_t>(j) * rb;
+    std::memcpy(gj, EG, sizeof(double) * rb);
+    const double* Ss = S + static_cast<size_t>(j) * d * d;
+    for (int q = 0; q < d; ++q)
+      for (int a = 0; a < r; ++a) {
+        double v = gj[q * r + a];
+        for (int p = 0; p < d; ++p) v -= Xj[p * r + a] * Ss[p * d + q];
+        gj[q * r + a] = v;
+      }
+    for (int e = 0; e < rb; ++e) gg += gj[e] * gj[e];
+  }
+  *ng2 = gg;
+  return f;
+}
+
+void hess(const Agent& A, const double* X, const double* S, const double* V, double* H) {
+  const int r = A.r, d = A.d, rb = r * A.b;
+  spmm(A, V, H);
+  for (int j = 0; j < A.n; ++j) {
+    double* Hj = H + static_cast<size_t>(j) * rb;
+    const double* Vj = V + static_cast<size_t>(j) * rb;
+    const double* Ss = S + static_cast<size_t>(j) * d * d;
+    for (int q = 0; q < d; ++q)
+      for (int a = 0; a < r; ++a) {
+        double v = Hj[q * r + a];
+        for (int p = 0; p < d; ++p) v -= Vj[p * r + a] * Ss[p * d + q];
+        Hj[q * r + a] = v;
+      }
+    project_pose(r, d, X + static_cast<size_t>(j) * rb, Hj);
+  }
+}
+
+void precond(const Agent& A, const double* X, const double* V, double* Z) {
+  const int r = A.r, d = A.d, b = A.b, rb = r * b;
+  for (int j = 0; j < A.n; ++j) {
+    const double* M = &A.minv[static_cast<size_t>(j) * b * b];
+    const double* Vj = V + static_cast<size_t>(j) * rb;
+    double* Zj = Z + static_cast<size_t>(j) * rb;
+    for (int c = 0; c < b; ++c)
+      for (int a = 0; a < r; ++a) {
+        double s = 0;
+        for (int u = 0; u < b; ++u) s += Vj[u * r + a] * M[u * b + c];
+        Zj[c * r + a] = s;
+      }
+    project_pose(r, d, X + static_cast<size_t>(j) * rb, Zj);
+  }
+}
+
+// QuadraticOptimizer::optimize with RTR, 1 outer iteration, radius-shrink retries
+double optimize(const Agent& A, const double* Xin, double* Xout, int max_inner, double radius, double tol, Work& w) {
+  const size_t L = A.L();
+  const int r = A.r, d = A.d, rb = r * A.b;
+  std::memcpy(w.x1.data(), Xin, sizeof(double) * L);
+  double ng2;
+  const double f1 = eval(A, w.x1.data(), w.g.data(), w.S.data(), &ng2, w.tmp);
+  const double ngf = std::sqrt(ng2);
+  if (ngf < tol) {
+    std::memcpy(Xout, Xin, sizeof(double) * L);
+    return f1;
+  }
+  for (int run = 0; run < 12; ++run) {
+    const double Delta = radius;
+    std::fill(w.eta.begin(), w.eta.end(), 0.0);
+    std::fill(w.Heta.begin(), w.Heta.end(), 0.0);
+    w.rv = w.g;
+    precond(A, w.x1.data(), w.rv.data(), w.z.data());
+    double z_r = dot(w.z, w.rv), d_Pd = z_r, e_Pe = 0, e_Pd = 0;
+    const double nr0 = std::sqrt(dot(w.rv, w.rv));
+    int status = 4;
+    for (size_t i = 0; i < L; ++i) w.delta[i] = -w.z[i];
+    for (int j = 0; j < max_inner; ++j) {
+      hess(A, w.x1.data(), w.S.data(), w.delta.data(), w.Hd.data());
+      const double dHd = dot(w.delta, w.Hd);
+      const double alpha = z_r / dHd;
+      const double ePe_new = e_Pe + 2 * alpha * e_Pd + alpha * alpha * d_Pd;
+      if (dHd <= 0 || ePe_new >= Delta * Delta) {
+        const double tau = (-e_Pd + std::sqrt(e_Pd * e_Pd + d_Pd * (Delta * Delta - e_Pe))) / d_Pd;
+        for (size_t i = 0; i < L; ++i) {
+          w.eta[i] += tau * w.delta[i];
+          w.Heta[i] += tau * w.Hd[i];
+        }
+        status = dHd <= 0 ? 0 : 1;
+        break;
+      }
+      e_Pe = ePe_new;
+      for (size_t i = 0; i < L; ++i) {
+        w.eta[i] += alpha * w.delta[i];
+        w.Heta[i] += alpha * w.Hd[i];
+        w.rv[i] += alpha * w.Hd[i];
+      }
+      const double nr = std::sqrt(dot(w.rv, w.rv));
+      if (nr <= nr0 * std::min(nr0, 0.1)) {
+        status = 2;
+        break;
+      }
+      precond(A, w.x1.data(), w.rv.data(), w.z.data());
+      const double zr_new = dot(w.z, w.rv);
+      const double beta = zr_new / z_r;
+      for (size_t i = 0; i < L; ++i) w.delta[i] = -w.z[i] + beta * w.delta[i];
+      e_Pd = beta * (e_Pd + alpha * d_Pd);
+      d_Pd = zr_new + beta * beta * d_Pd;
+      z_r = zr_new;
+    }
+    (void)status;
+    for (int j = 0; j < A.n; ++j) {
+      for (int e = 0; e < rb; ++e) w.x2[j * rb + e] = w.x1[j * rb + e] + w.eta[j * rb + e];
+      qf_pose(r, d, &w.x2[static_cast<size_t>(j) * rb]);
+    }
+    double ng22;
+    const double f2 = eval(A, w.x2.data(), w.g2.data(), w.S2.data(), &ng22, w.tmp);
+    const double rho = (f1 - f2) / (-dot(w.g, w.eta) - 0.5 * dot(w.eta, w.Heta));
+    if (rho > 0.1) {
+      std::memcpy(Xout, w.x2.data(), sizeof(double) * L);
+      return f2;
+    }
+    radius /= 4.0;
+  }
+  std::memcpy(Xout, Xin, sizeof(double) * L);
+  return f1;
+}
+
+void edge_T(int d, const double* R, const double* t, double T[4][4]) {
+  std::memset(T, 0, sizeof(double) * 16);
+  for (int u = 0; u < d; ++u) {
+    for (int v = 0; v < d; ++v) T[u][v] = R[u * d + v];
+    T[u][d] = t[u];
+  }
+  T[d][d] = 1.0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Times `reps` RBCD steps of one agent (iterate(true) then iterate(false), Nesterov if accel)
+// on one host thread.  X is the global r x (d+1) n matrix in column-major layout.
+// Returns seconds per agent step; f_out receives f after the last optimisation.
+double dpgo_cpu_time_agent_step(int d, int r, int m, const int* p1, const int* p2, const double* R, const double* t,
+                                const double* kappa, const double* tau, int n, const int* agent_of_pose, int agent,
+                                const double* Xg, int accel, int num_agents, int reps, double* f_out) {
+  const int b = d + 1, rb = r * b;
+  Agent A;
+  A.d = d;
+  A.r = r;
+  A.b = b;
+  std::vector<int> local(n, -1), poses;
+  for (int i = 0; i < n; ++i)
+    if (agent_of_pose[i] == agent) {
+      local[i] = static_cast<int>(poses.size());
+      poses.push_back(i);
+    }
+  A.n = static_cast<int>(poses.size());
+  // ---- Q (constructQMatrix) as a map of blocks
+  std::vector<std::map<int, std::vector<double>>> rows(A.n);
+  auto add = [&](int i, int j, const double* blkcm) {
+    auto& v = rows[i][j];
+    if (v.empty()) v.assign(b * b, 0.0);
+    for (int q = 0; q < b * b; ++q) v[q] += blkcm[q];
+  };
+  std::map<int, std::vector<double>> G;
+  for (int e = 0; e < m; ++e) {
+    const int i = p1[e], j = p2[e];
+    const bool oi = agent_of_pose[i] == agent, oj = agent_of_pose[j] == agent;
+    if (!oi && !oj) continue;
+    double T[4][4], Om[4];
+    edge_T(d, &R[e * d * d], &t[e * d], T);
+    for (int u = 0; u < d; ++u) Om[u] = kappa[e];
+    Om[d] = tau[e];
+    double Wii[16], Wjj[16], Wij[16], Wji[16];
+    for (int u = 0; u < b; ++u)
+      for (int v = 0; v < b; ++v) {
+        double s = 0;
+        for (int q = 0; q < b; ++q) s += T[u][q] * Om[q] * T[v][q];
+        Wii[v * b + u] = s;
+        Wjj[v * b + u] = u == v ? Om[u] : 0.0;
+        Wij[v * b + u] = -T[u][v] * Om[v];
+        Wji[v * b + u] = -Om[u] * T[v][u];
+      }
+    if (oi && oj) {
+      add(local[i], local[i], Wii);
+      add(local[j], local[j], Wjj);
+      add(local[i], local[j], Wij);
+      add(local[j], local[i], Wji);
+    } else {
+      // constructGMatrix (:783-859) from the neighbour's current pose
+      const int own = oi ? i : j, nbr = oi ? j : i;
+      if (oi)
+        add(local[i], local[i], Wii);
+      else
+        add(local[j], local[j], Wjj);
+      auto& gv = G[local[own]];
+      if (gv.empty()) gv.assign(rb, 0.0);
+      const double* Xn = Xg + static_cast<size_t>(nbr) * rb;
+      // L = -X_n Om T^T (outgoing) or -X_n T Om (incoming); X_n is r x b column-major
+      for (int c = 0; c < b; ++c)
+        for (int a = 0; a < r; ++a) {
+          double s = 0;
+          for (int u = 0; u < b; ++u) s += Xn[u * r + a] * (oi ? Om[u] * T[c][u] : T[u][c] * Om[c]);
+          gv[c * r + a] -= s;
+        }
+    }
+  }
+  A.rowptr.assign(A.n + 1, 0);
+  for (int j = 0; j < A.n; ++j) {
+    if (rows[j].find(j) == rows[j].end()) rows[j][j].assign(b * b, 0.0);
+    A.rowptr[j + 1] = A.rowptr[j] + static_cast<int>(rows[j].size());
+    for (auto& kv : rows[j]) {
+      A.col.push_back(kv.first);
+      A.blk.insert(A.blk.end(), kv.second.begin(), kv.second.end());
+    }
+  }
+  // block-Jacobi inverses (Gauss-Jordan)
+  A.minv.assign(static_cast<size_t>(A.n) * b * b, 0.0);
+  for (int j = 0; j < A.n; ++j) {
+    double M[4][8] = {{0}};
+    const double* D = rows[j][j].data();
+    for (int u = 0; u < b; ++u) {
+      for (int v = 0; v < b; ++v) M[u][v] = D[v * b + u];
+      M[u][u] += 0.1;
+      M[u][b + u] = 1.0;
+    }
+    for (int c = 0; c < b; ++c) {
+      int piv = c;
+      for (int u = c + 1; u < b; ++u)
+        if (std::fabs(M[u][c]) > std::fabs(M[piv][c])) piv = u;
+      for (int v = 0; v < 2 * b; ++v) std::swap(M[c][v], M[piv][v]);
+      const double inv = 1.0 / M[c][c];
+      for (int v = 0; v < 2 * b; ++v) M[c][v] *= inv;
+      for (int u = 0; u < b; ++u)
+        if (u != c) {
+          const double f = M[u][c];
+          for (int v = 0; v < 2 * b; ++v) M[u][v] -= f * M[c][v];
+        }
+    }
+    for (int u = 0; u < b; ++u)
+      for (int v = 0; v < b; ++v) A.minv[static_cast<size_t>(j) * b * b + u * b + v] = M[u][b + v];
+  }
+  A.gslot.assign(A.n, -1);
+  for (auto& kv : G) {
+    A.gslot[kv.first] = static_cast<int>(A.gpose.size());
+    A.gpose.push_back(kv.first);
+    A.gblk.insert(A.gblk.end(), kv.second.begin(), kv.second.end());
+  }
+  // ---- agent state
+  const size_t L = A.L();
+  std::vector<double> X(L), Y(L), V(L), Xp(L), M(L);
+  for (int q = 0; q < A.n; ++q) std::memcpy(&X[static_cast<size_t>(q) * rb], Xg + static_cast<size_t>(poses[q]) * rb, sizeof(double) * rb);
+  Y = X;
+  V = X;
+  Work w;
+  w.init(L, static_cast<size_t>(A.n) * d * d);
+  double gamma = 0, alpha = 0, f = 0;
+  const double N = num_agents;
+  auto t0 = std::chrono::steady_clock::now();
+  for (int rep = 0; rep < reps; ++rep) {
+    for (int sel = 1; sel >= 0; --sel) {  // iterate(true), then iterate(false)
+      Xp = X;
+      if (accel) {
+        gamma = (1 + std::sqrt(1 + 4 * N * N * gamma * gamma)) / (2 * N);
+        alpha = 1 / (gamma * N);
+        for (size_t i = 0; i < L; ++i) Y[i] = (1 - alpha) * X[i] + alpha * V[i];
+        for (int j = 0; j < A.n; ++j) polar_pose(r, d, &Y[static_cast<size_t>(j) * rb]);
+        if (sel)
+          f = optimize(A, Y.data(), X.data(), 10, 100.0, 1e-2, w);
+        else
+          X = Y;
+        for (size_t i = 0; i < L; ++i) V[i] = V[i] + gamma * (X[i] - Y[i]);
+        for (int j = 0; j < A.n; ++j) polar_pose(r, d, &V[static_cast<size_t>(j) * rb]);
+      } else if (sel) {
+        f = optimize(A, X.data(), X.data(), 10, 100.0, 1e-2, w);
+      }
+    }
+  }
+  const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (f_out) *f_out = f;
+  return sec / reps;
+}
+
+}  // extern "C"

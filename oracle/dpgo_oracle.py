@@ -33,7 +33,7 @@ import scipy.sparse.linalg as spla
 
 # ----------------------------------------------------------------------------------------
 # Repo-defined deterministic RNG: SplitMix64 -> 53-bit uniform -> Box-Muller.
-# The C++ generator (dpgo_amd/cpp/src/synthetic.cpp) implements the identical stream.
+# The C++ generator (dpgo_amd/csrc/graph.cpp) implements the identical stream.
 # ----------------------------------------------------------------------------------------
 _M64 = (1 << 64) - 1
 
@@ -1183,3 +1183,75 @@ def central_cost(meas: Measurements, X, n=None):
     d = meas.d
     Qc = connection_laplacian(meas, n)
     return 0.5 * inner(np.asarray((Qc @ X.T).T), X)
+
+
+def greedy_colors(meas: Measurements, agent_of_pose, num_agents):
+    """Greedy colouring of the agent-adjacency graph in agent-id order (repo-defined schedule)."""
+    adj = [set() for _ in range(num_agents)]
+    for e in range(meas.m):
+        a1, a2 = int(agent_of_pose[meas.p1[e]]), int(agent_of_pose[meas.p2[e]])
+        if a1 != a2:
+            adj[a1].add(a2)
+            adj[a2].add(a1)
+    col = [-1] * num_agents
+    for a in range(num_agents):
+        used = {col[b2] for b2 in adj[a] if col[b2] >= 0}
+        c = 0
+        while c in used:
+            c += 1
+        col[a] = c
+    return col
+
+
+def colour_rbcd(meas: Measurements, agent_of_pose, num_agents, X0, num_iters, r,
+                acceleration=False, robust="L2", precon=PRECON_BLOCK_JACOBI, trace=None):
+    """Colour-class RBCD schedule run with the PGOAgent restatement: at iteration t the agents of
+    colour t mod C are selected; the others run iterate(false) first (their public X / aux Y are
+    then delivered, as in examples/MultiRobotExample.cpp:181-213), then the selected agents run
+    iterate(true).  Returns the global X after num_iters iterations."""
+    d = meas.d
+    b = d + 1
+    n = len(agent_of_pose)
+    agent_of_pose = np.asarray(agent_of_pose)
+    local = np.zeros(n, np.int64)
+    counts = np.zeros(num_agents, np.int64)
+    for i in range(n):
+        a = agent_of_pose[i]
+        local[i] = counts[a]
+        counts[a] += 1
+    parts = _split(meas, agent_of_pose, local, num_agents)
+    glob = [np.nonzero(agent_of_pose == a)[0] for a in range(num_agents)]
+    agents = []
+    for a in range(num_agents):
+        ag = Agent(a, AgentParams(d, r, num_agents, acceleration=acceleration, robust=robust,
+                                  precon=precon))
+        ag.set_pose_graph(*parts[a], n=int(counts[a]))
+        cols = np.concatenate([np.arange(p * b, (p + 1) * b) for p in glob[a]])
+        ag.set_X(X0[:, cols])
+        agents.append(ag)
+    colors = greedy_colors(meas, agent_of_pose, num_agents)
+    C = max(colors) + 1
+    for it in range(num_iters):
+        c = it % C
+        for ag in agents:
+            if colors[ag.id] != c:
+                ag.iterate(False)
+        for ag in agents:
+            if colors[ag.id] != c:
+                continue
+            for other in agents:
+                if other.id == ag.id:
+                    continue
+                ag.update_neighbor_poses(other.id, other.shared_pose_dict(False), aux=False)
+                if acceleration:
+                    ag.update_neighbor_poses(other.id, other.shared_pose_dict(True), aux=True)
+        for ag in agents:
+            if colors[ag.id] == c:
+                ag.iterate(True)
+                if trace is not None:
+                    trace.append((it, ag.id, ag.last_result))
+    X = np.zeros_like(X0)
+    for a, ag in enumerate(agents):
+        cols = np.concatenate([np.arange(p * b, (p + 1) * b) for p in glob[a]])
+        X[:, cols] = ag.X
+    return X, colors
