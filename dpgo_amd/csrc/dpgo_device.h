@@ -265,4 +265,52 @@ __device__ __forceinline__ void polar_inplace(double (&M)[R][D + 1]) {
     }
 }
 
+// Polar factor via Newton-Schulz  Y <- Y (3 I - Y^T Y) / 2  when Y is already near St(d, r)
+// (||Y^T Y - I||_F < 0.25: every Nesterov combination of nearby iterates), else one-sided Jacobi.
+// Both converge to the same U V^T; Newton-Schulz needs only FMAs (no fp64 sqrt / divide).
+template <int R, int D>
+__device__ __forceinline__ void polar_fast(double (&M)[R][D + 1]) {
+  bool fallback = false;
+#pragma unroll 1
+  for (int it = 0; it < 12; ++it) {
+    double A[D][D];
+    double err = 0.0;
+#pragma unroll
+    for (int p = 0; p < D; ++p)
+#pragma unroll
+      for (int q = 0; q < D; ++q) {
+        double s = 0.0;
+#pragma unroll
+        for (int a = 0; a < R; ++a) s = fma(M[a][p], M[a][q], s);
+        A[p][q] = s;
+        const double e = s - (p == q ? 1.0 : 0.0);
+        err = fma(e, e, err);
+      }
+    if (err < 1e-30) break;
+    if (it == 0 && !(err < 0.0625)) {
+      fallback = true;
+      break;
+    }
+    double T[D][D];
+#pragma unroll
+    for (int p = 0; p < D; ++p)
+#pragma unroll
+      for (int q = 0; q < D; ++q) T[p][q] = (p == q ? 1.5 : 0.0) - 0.5 * A[p][q];
+#pragma unroll
+    for (int a = 0; a < R; ++a) {
+      double row[D];
+#pragma unroll
+      for (int q = 0; q < D; ++q) {
+        double s = 0.0;
+#pragma unroll
+        for (int p = 0; p < D; ++p) s = fma(M[a][p], T[p][q], s);
+        row[q] = s;
+      }
+#pragma unroll
+      for (int q = 0; q < D; ++q) M[a][q] = row[q];
+    }
+  }
+  if (fallback) polar_inplace<R, D>(M);
+}
+
 }  // namespace dpgo

@@ -446,54 +446,64 @@ __global__ __launch_bounds__(kThreads) void k_precond(LaunchCtx c, const double*
   store_vec<R>(out, off, own, oc);
 }
 
-// out = LiftedSEManifold::project(ca A + cb B) with per-agent coefficients (cb ignored if B null)
+// out = LiftedSEManifold::project(ca A + cb B) (or A + cb (B - C)) with per-agent (or scalar)
+// coefficients.  Thread-per-pose: 64-thread workgroups, one tile each; every thread loads its
+// pose's r*b contiguous doubles (the wave reads 64 consecutive poses = one contiguous span).
 // (src/manifold/LiftedSEManifold.cpp:34-45; Nesterov updateY/updateV src/PGOAgent.cpp:1075-1091)
 template <int R, int B>
-__global__ __launch_bounds__(kThreads) void k_polar_comb(LaunchCtx c, const double* __restrict__ A,
-                                                         const double* __restrict__ Bv,
-                                                         const double* __restrict__ ca,
-                                                         const double* __restrict__ cb,
-                                                         double* __restrict__ out,
-                                                         const double* __restrict__ Cv, double sa,
-                                                         double sb) {
+__global__ __launch_bounds__(64) void k_polar_comb(LaunchCtx c, const double* __restrict__ A,
+                                                   const double* __restrict__ Bv,
+                                                   const double* __restrict__ ca,
+                                                   const double* __restrict__ cb,
+                                                   double* __restrict__ out,
+                                                   const double* __restrict__ Cv, double sa,
+                                                   double sb) {
   constexpr int D = B - 1;
-  const PoseLane p = pose_lane<B>(c);
-  if (tile_skipped(c, p.agent)) return;
-  const bool own = p.ok && p.k < B;
-  const long off = p.j * (R * B) + p.k * R;
-  const double a0 = ca ? ca[p.agent] : sa;
-  double acol[R];
-  load_col<R, B>(A, p.j, p.k, p.ok, acol);
+  const int tile = blockIdx.x;
+  const int agent = c.tile_agent[tile];
+  if (tile_skipped(c, agent)) return;
+  if (static_cast<int>(threadIdx.x) >= c.tile_count[tile]) return;
+  const long j = static_cast<long>(c.tile_start[tile]) + threadIdx.x;
+  const double a0 = ca ? ca[agent] : sa;
+  const double b0 = cb ? cb[agent] : sb;
+  double M[R][B];
+  const double* pa = A + j * (R * B);
+#pragma unroll
+  for (int cc = 0; cc < B; ++cc)
+#pragma unroll
+    for (int a = 0; a < R; ++a) M[a][cc] = pa[cc * R + a];
   if (Cv != nullptr) {
     // A + cb (B - C)   (updateV: V + gamma (X - Y), src/PGOAgent.cpp:1086-1091)
-    const double b0 = cb ? cb[p.agent] : sb;
-    double bcol[R], ccol[R];
-    load_col<R, B>(Bv, p.j, p.k, p.ok, bcol);
-    load_col<R, B>(Cv, p.j, p.k, p.ok, ccol);
+    const double* pb = Bv + j * (R * B);
+    const double* pc = Cv + j * (R * B);
 #pragma unroll
-    for (int a = 0; a < R; ++a) acol[a] = acol[a] + b0 * (bcol[a] - ccol[a]);
+    for (int cc = 0; cc < B; ++cc)
+#pragma unroll
+      for (int a = 0; a < R; ++a) M[a][cc] = M[a][cc] + b0 * (pb[cc * R + a] - pc[cc * R + a]);
   } else if (Bv != nullptr) {
     // ca A + cb B   (updateY: (1 - alpha) X + alpha V, src/PGOAgent.cpp:1077-1084)
-    const double b0 = cb ? cb[p.agent] : sb;
-    double bcol[R];
-    load_col<R, B>(Bv, p.j, p.k, p.ok, bcol);
+    const double* pb = Bv + j * (R * B);
 #pragma unroll
-    for (int a = 0; a < R; ++a) acol[a] = a0 * acol[a] + b0 * bcol[a];
+    for (int cc = 0; cc < B; ++cc)
+#pragma unroll
+      for (int a = 0; a < R; ++a) M[a][cc] = a0 * M[a][cc] + b0 * pb[cc * R + a];
   } else if (a0 != 1.0) {
 #pragma unroll
-    for (int a = 0; a < R; ++a) acol[a] = a0 * acol[a];
-  }
-  double Mf[R][B];
-  quad_gather<R, B>(acol, Mf);
-  polar_inplace<R, D>(Mf);
-  double oc[R];
-  select_col<R, B>(Mf, p.k, oc);
-  // translation column passes through unchanged
-  if (p.k == D) {
+    for (int cc = 0; cc < B; ++cc)
 #pragma unroll
-    for (int a = 0; a < R; ++a) oc[a] = acol[a];
+      for (int a = 0; a < R; ++a) M[a][cc] = a0 * M[a][cc];
   }
-  store_vec<R>(out, off, own, oc);
+  double tcol[R];
+#pragma unroll
+  for (int a = 0; a < R; ++a) tcol[a] = M[a][D];  // translation passes through unchanged
+  polar_fast<R, D>(M);
+  double* po = out + j * (R * B);
+#pragma unroll
+  for (int cc = 0; cc < D; ++cc)
+#pragma unroll
+    for (int a = 0; a < R; ++a) po[cc * R + a] = M[a][cc];
+#pragma unroll
+  for (int a = 0; a < R; ++a) po[D * R + a] = tcol[a];
 }
 
 // out = sel ? A : B per agent; partial |out - ref|^2
@@ -942,7 +952,7 @@ hipError_t launch_polar_comb(int r, int b, const LaunchCtx& c, const double* A, 
                              const double* ca, const double* cb, double* out, const double* Cv, double sa,
                              double sb) {
   if (c.num_tiles == 0) return hipSuccess;
-  DPGO_DISPATCH(r, b, (k_polar_comb<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, A, Bv, ca, cb, out, Cv, sa, sb)));
+  DPGO_DISPATCH(r, b, (k_polar_comb<R, B><<<c.num_tiles, 64, 0, c.stream>>>(c, A, Bv, ca, cb, out, Cv, sa, sb)));
   return hipGetLastError();
 }
 
