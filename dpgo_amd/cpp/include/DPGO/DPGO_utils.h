@@ -1,0 +1,31 @@
+// Host utilities on the hot path's input side (reference include/DPGO/DPGO_utils.h).
+#ifndef DPGO_AMD_UTILS_H
+#define DPGO_AMD_UTILS_H
+
+#include <DPGO/DPGO_types.h>
+#include <DPGO/RelativeSEMeasurement.h>
+
+#include <string>
+#include <vector>
+
+namespace DPGO {
+
+// src/DPGO_utils.cpp:78-212 with SURVEY App. B fixes (num_poses = max index + 1, blank lines skipped)
+std::vector<RelativeSEMeasurement> read_g2o_file(const std::string& filename, size_t& num_poses);
+// src/DPGO_utils.cpp:280-286: Q = A Omega A^T (row-major CSR, (d+1)n square)
+SparseMatrix constructConnectionLaplacianSE(const std::vector<RelativeSEMeasurement>& measurements);
+SparseMatrix constructConnectionLaplacianSE(const std::vector<RelativeSEMeasurement>& measurements, size_t n);
+// src/DPGO_utils.cpp:426-447
+Matrix odometryInitialization(size_t dimension, size_t num_poses, const std::vector<RelativeSEMeasurement>& odometry);
+// src/DPGO_utils.cpp:478-500 (host, Jacobi SVD)
+Matrix projectToRotationGroup(const Matrix& M);
+Matrix projectToStiefelManifold(const Matrix& M);
+// src/DPGO_utils.cpp:502-507: repo-defined seeded point of St(d, r) (ROPTLIB's RNG is not available)
+Matrix fixedStiefelVariable(unsigned d, unsigned r);
+// src/DPGO_utils.cpp:509-515
+double computeMeasurementError(const RelativeSEMeasurement& m, const Matrix& R1, const Matrix& t1, const Matrix& R2,
+                               const Matrix& t2);
+
+}  // namespace DPGO
+
+#endif

@@ -1,0 +1,160 @@
+// Host utilities (reference src/DPGO_utils.cpp); the g2o parser is the library's own reader.
+#include <DPGO/DPGO_utils.h>
+#include <dpgo_rbcd.h>
+
+#include <algorithm>
+#include <random>
+#include <stdexcept>
+#include <string>
+
+namespace DPGO {
+
+std::vector<RelativeSEMeasurement> read_g2o_file(const std::string& filename, size_t& num_poses) {
+  dpgo_graph g = nullptr;
+  if (dpgo_graph_read_g2o(filename.c_str(), &g) != DPGO_HIP_OK)
+    throw std::runtime_error(std::string("read_g2o_file: ") + dpgo_hip_last_error());
+  int d = 0, n = 0, m = 0, dup = 0;
+  dpgo_graph_info(g, &d, &n, &m, &dup);
+  std::vector<int> p1(m), p2(m);
+  std::vector<double> R(static_cast<size_t>(m) * d * d), t(static_cast<size_t>(m) * d), kappa(m), tau(m);
+  dpgo_graph_copy_out(g, p1.data(), p2.data(), R.data(), t.data(), kappa.data(), tau.data());
+  dpgo_graph_destroy(g);
+  std::vector<RelativeSEMeasurement> out;
+  out.reserve(m);
+  for (int e = 0; e < m; ++e) {
+    Matrix Rm(d, d), tm(d, 1);
+    for (int u = 0; u < d; ++u) {
+      for (int v = 0; v < d; ++v) Rm(u, v) = R[static_cast<size_t>(e) * d * d + u * d + v];
+      tm(u, 0) = t[static_cast<size_t>(e) * d + u];
+    }
+    out.emplace_back(0, 0, p1[e], p2[e], Rm, tm, kappa[e], tau[e]);
+  }
+  num_poses = static_cast<size_t>(n);  // App. B1 fix: max index + 1
+  return out;
+}
+
+SparseMatrix constructConnectionLaplacianSE(const std::vector<RelativeSEMeasurement>& measurements, size_t n) {
+  const size_t d = measurements.empty() ? 0 : static_cast<size_t>(measurements[0].t.rows());
+  const size_t b = d + 1;
+  std::vector<std::pair<std::pair<int, int>, double>> trip;
+  trip.reserve(measurements.size() * 4 * b * b);
+  for (const auto& m : measurements) {
+    Matrix T = Matrix::Zero(b, b), Om = Matrix::Zero(b, b);
+    T.setBlock(0, 0, m.R);
+    T.setBlock(0, d, m.t);
+    T(d, d) = 1.0;
+    for (size_t u = 0; u < d; ++u) Om(u, u) = m.weight * m.kappa;
+    Om(d, d) = m.weight * m.tau;
+    const Matrix Wii = T * Om * T.transpose(), Wij = -(T * Om), Wji = -(Om * T.transpose());
+    const int i = static_cast<int>(m.p1), j = static_cast<int>(m.p2);
+    for (size_t u = 0; u < b; ++u)
+      for (size_t v = 0; v < b; ++v) {
+        trip.push_back({{static_cast<int>(i * b + u), static_cast<int>(i * b + v)}, Wii(u, v)});
+        trip.push_back({{static_cast<int>(j * b + u), static_cast<int>(j * b + v)}, Om(u, v)});
+        trip.push_back({{static_cast<int>(i * b + u), static_cast<int>(j * b + v)}, Wij(u, v)});
+        trip.push_back({{static_cast<int>(j * b + u), static_cast<int>(i * b + v)}, Wji(u, v)});
+      }
+  }
+  SparseMatrix Q(static_cast<long>(b * n), static_cast<long>(b * n));
+  Q.setFromTriplets(trip);
+  return Q;
+}
+
+SparseMatrix constructConnectionLaplacianSE(const std::vector<RelativeSEMeasurement>& measurements) {
+  size_t n = 0;
+  for (const auto& m : measurements) n = std::max(n, std::max(m.p1, m.p2));  // :223-228
+  return constructConnectionLaplacianSE(measurements, n + 1);
+}
+
+Matrix odometryInitialization(size_t dimension, size_t num_poses, const std::vector<RelativeSEMeasurement>& odometry) {
+  const size_t d = dimension, b = d + 1;
+  Matrix T(d, num_poses * b);
+  T.setBlock(0, 0, Matrix::Identity(d, d));
+  for (size_t src = 0; src < odometry.size(); ++src) {
+    const auto& m = odometry[src];
+    if (m.p1 != src || m.p2 != src + 1) throw std::invalid_argument("odometryInitialization: not a chain");
+    const Matrix Rs = T.block(0, src * b, d, d), ts = T.block(0, src * b + d, d, 1);
+    T.setBlock(0, (src + 1) * b, Rs * m.R);
+    T.setBlock(0, (src + 1) * b + d, ts + Rs * m.t);
+  }
+  return T;
+}
+
+// one-sided Jacobi SVD of an r x c matrix (r >= c): A V = U Sigma
+static void jacobi_svd(const Matrix& M, Matrix& U, Matrix& S, Matrix& V) {
+  const long r = M.rows(), c = M.cols();
+  U = M;
+  V = Matrix::Identity(c, c);
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    bool rot = false;
+    for (long p = 0; p < c - 1; ++p)
+      for (long q = p + 1; q < c; ++q) {
+        double al = 0, be = 0, ga = 0;
+        for (long a = 0; a < r; ++a) {
+          al += U(a, p) * U(a, p);
+          be += U(a, q) * U(a, q);
+          ga += U(a, p) * U(a, q);
+        }
+        if (ga == 0.0 || std::fabs(ga) <= 1e-17 * std::sqrt(al * be)) continue;
+        rot = true;
+        const double z = (be - al) / (2 * ga);
+        const double t = std::copysign(1.0, z) / (std::fabs(z) + std::sqrt(1 + z * z));
+        const double cs = 1 / std::sqrt(1 + t * t), sn = cs * t;
+        for (long a = 0; a < r; ++a) {
+          const double up = U(a, p), uq = U(a, q);
+          U(a, p) = cs * up - sn * uq;
+          U(a, q) = sn * up + cs * uq;
+        }
+        for (long a = 0; a < c; ++a) {
+          const double vp = V(a, p), vq = V(a, q);
+          V(a, p) = cs * vp - sn * vq;
+          V(a, q) = sn * vp + cs * vq;
+        }
+      }
+    if (!rot) break;
+  }
+  S = Matrix(c, 1);
+  for (long q = 0; q < c; ++q) {
+    double nn = 0;
+    for (long a = 0; a < r; ++a) nn += U(a, q) * U(a, q);
+    S(q, 0) = std::sqrt(nn);
+    for (long a = 0; a < r; ++a) U(a, q) = S(q, 0) > 0 ? U(a, q) / S(q, 0) : 0.0;
+  }
+}
+
+Matrix projectToStiefelManifold(const Matrix& M) {
+  Matrix U, S, V;
+  jacobi_svd(M, U, S, V);
+  return U * V.transpose();
+}
+
+Matrix projectToRotationGroup(const Matrix& M) {
+  Matrix U, S, V;
+  jacobi_svd(M, U, S, V);
+  if (U.determinant() * V.determinant() < 0) {
+    // flip the direction of the smallest singular value (:486-490)
+    long k = 0;
+    for (long q = 1; q < S.rows(); ++q)
+      if (S(q, 0) < S(k, 0)) k = q;
+    for (long a = 0; a < U.rows(); ++a) U(a, k) = -U(a, k);
+  }
+  return U * V.transpose();
+}
+
+Matrix fixedStiefelVariable(unsigned d, unsigned r) {
+  std::mt19937_64 rng(1);
+  std::normal_distribution<double> N(0.0, 1.0);
+  Matrix M(r, d);
+  for (unsigned j = 0; j < d; ++j)
+    for (unsigned i = 0; i < r; ++i) M(i, j) = N(rng);
+  return projectToStiefelManifold(M);
+}
+
+double computeMeasurementError(const RelativeSEMeasurement& m, const Matrix& R1, const Matrix& t1, const Matrix& R2,
+                               const Matrix& t2) {
+  const double rot = (R1 * m.R - R2).squaredNorm();
+  const double tr = (t2 - t1 - R1 * m.t).squaredNorm();
+  return m.kappa * rot + m.tau * tr;
+}
+
+}  // namespace DPGO

@@ -106,21 +106,26 @@ void quat_to_rot_eigen(double qw, double qx, double qy, double qz, double* R) {
   std::memcpy(R, v, sizeof(v));
 }
 
+// trace(M^-1) with Eigen's fixed-size closed-form inverses (the reader calls
+// TranCov.inverse().trace(), src/DPGO_utils.cpp:131,178,185): invdet = 1/det, r_ii = cof_ii * invdet.
 bool inv_trace_2(double a, double b, double d, double* tr) {
   const double det = a * d - b * b;
   if (det == 0.0) return false;
-  *tr = (d + a) / det;
+  const double invdet = 1.0 / det;
+  *tr = d * invdet + a * invdet;
   return true;
 }
 
-bool inv_trace_3(const double M[3][3], double* tr) {
-  const double c00 = M[1][1] * M[2][2] - M[1][2] * M[2][1];
-  const double c11 = M[0][0] * M[2][2] - M[0][2] * M[2][0];
-  const double c22 = M[0][0] * M[1][1] - M[0][1] * M[1][0];
-  const double det = M[0][0] * c00 - M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]) +
-                     M[0][2] * (M[1][0] * M[2][1] - M[1][1] * M[2][0]);
+bool inv_trace_3(const double m[3][3], double* tr) {
+  const double c00 = m[1][1] * m[2][2] - m[1][2] * m[2][1];
+  const double c10 = m[2][1] * m[0][2] - m[2][2] * m[0][1];
+  const double c20 = m[0][1] * m[1][2] - m[0][2] * m[1][1];
+  const double det = c00 * m[0][0] + c10 * m[1][0] + c20 * m[2][0];
   if (det == 0.0) return false;
-  *tr = (c00 + c11 + c22) / det;
+  const double invdet = 1.0 / det;
+  const double c11 = m[2][2] * m[0][0] - m[2][0] * m[0][2];
+  const double c22 = m[0][0] * m[1][1] - m[0][1] * m[1][0];
+  *tr = c00 * invdet + c11 * invdet + c22 * invdet;
   return true;
 }
 

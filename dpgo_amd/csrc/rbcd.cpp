@@ -112,9 +112,49 @@ int optimize_color(dpgo_rbcd e, int c, const double* Xin, double* Xout, dpgo_opt
   return DPGO_HIP_OK;
 }
 
+// Public poses this rank must send to / receive from every peer: endpoints of edges that join
+// agents on different ranks, in ascending global pose id (identical on every rank).
+void exchange_plan(dpgo_graph g, const int* agent_of_pose, const int* agent_rank, int rank, int world,
+                   std::vector<std::set<int>>& send_set, std::vector<std::set<int>>& recv_set) {
+  send_set.assign(world, {});
+  recv_set.assign(world, {});
+  for (size_t k = 0; k < g->p1.size(); ++k) {
+    const int i = g->p1[k], j = g->p2[k];
+    const int ri = agent_rank[agent_of_pose[i]], rj = agent_rank[agent_of_pose[j]];
+    if (agent_of_pose[i] == agent_of_pose[j] || ri == rj) continue;
+    if (ri == rank) {
+      send_set[rj].insert(i);
+      recv_set[rj].insert(j);
+    } else if (rj == rank) {
+      send_set[ri].insert(j);
+      recv_set[ri].insert(i);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int dpgo_rbcd_plan(dpgo_graph g, int num_agents, const int* agent_of_pose, const int* agent_rank, int rank, int world,
+                   long long* send_counts, long long* recv_counts, int* send_poses, int* recv_poses) {
+  if (!g || !agent_of_pose || !agent_rank || world <= 0 || rank < 0 || rank >= world || num_agents <= 0)
+    return fail(DPGO_HIP_EINVAL, "bad plan arguments");
+  for (int i = 0; i < g->n; ++i)
+    if (agent_of_pose[i] < 0 || agent_of_pose[i] >= num_agents) return fail(DPGO_HIP_EINVAL, "agent_of_pose out of range");
+  std::vector<std::set<int>> ss, rs;
+  exchange_plan(g, agent_of_pose, agent_rank, rank, world, ss, rs);
+  long long so = 0, ro = 0;
+  for (int p = 0; p < world; ++p) {
+    if (send_counts) send_counts[p] = static_cast<long long>(ss[p].size());
+    if (recv_counts) recv_counts[p] = static_cast<long long>(rs[p].size());
+    if (send_poses)
+      for (int x : ss[p]) send_poses[so++] = x;
+    if (recv_poses)
+      for (int x : rs[p]) recv_poses[ro++] = x;
+  }
+  return DPGO_HIP_OK;
+}
 
 void dpgo_rbcd_default_params(dpgo_rbcd_params* p) {
   if (!p) return;
@@ -203,19 +243,8 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
     return q < 0 ? -1 : e->own_pose_off[q] + local[pose];
   };
   // ---- exchange plan: poses each peer needs from us / we need from each peer (sorted global ids)
-  std::vector<std::set<int>> send_set(world), recv_set(world);
-  for (size_t k = 0; k < m; ++k) {
-    const int i = g->p1[k], j = g->p2[k];
-    const int ri = agent_rank[agent_of_pose[i]], rj = agent_rank[agent_of_pose[j]];
-    if (agent_of_pose[i] == agent_of_pose[j] || ri == rj) continue;
-    if (ri == rank) {
-      send_set[rj].insert(i);
-      recv_set[rj].insert(j);
-    } else if (rj == rank) {
-      send_set[ri].insert(j);
-      recv_set[ri].insert(i);
-    }
-  }
+  std::vector<std::set<int>> send_set, recv_set;
+  exchange_plan(g, agent_of_pose, agent_rank, rank, world, send_set, recv_set);
   const int mult = e->P.acceleration ? 2 : 1;
   const long long rbd = static_cast<long long>(e->rb());
   e->send_counts.assign(world, 0);

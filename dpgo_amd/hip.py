@@ -353,6 +353,7 @@ _SIGS2 = [
     ("dpgo_graph_chain_init", [C.c_void_p, C.c_int, _dp, _dp], C.c_int),
     ("dpgo_graph_grid_partition", [C.c_void_p, C.c_int, _ip], C.c_int),
     ("dpgo_rbcd_default_params", [C.POINTER(RbcdParams)], None),
+    ("dpgo_rbcd_plan", [C.c_void_p, C.c_int, _ip, _ip, C.c_int, C.c_int, _lp, _lp, _ip, _ip], C.c_int),
     ("dpgo_rbcd_create", [C.c_void_p, C.c_int, _ip, _ip, C.c_int, C.c_int, C.POINTER(RbcdParams),
                           C.POINTER(C.c_void_p)], C.c_int),
     ("dpgo_rbcd_destroy", [C.c_void_p], C.c_int),
@@ -453,6 +454,20 @@ class Graph:
         out = np.empty(self.n, np.int32)
         _check(lib().dpgo_graph_grid_partition(self.h, int(agents_per_axis), out.ctypes.data_as(_ip)))
         return out
+
+
+def exchange_plan(graph: "Graph", agent_of_pose, agent_rank, rank, world):
+    """Host-only exchange plan (no GPU): ([send pose ids per peer], [recv pose ids per peer])."""
+    aop, ap = _i32(agent_of_pose)
+    ar, arp = _i32(agent_rank)
+    sc = np.empty(world, np.int64); rc = np.empty(world, np.int64)
+    _check(lib().dpgo_rbcd_plan(graph.h, len(ar), ap, arp, rank, world, sc.ctypes.data_as(_lp),
+                                rc.ctypes.data_as(_lp), None, None))
+    sp_ = np.empty(max(int(sc.sum()), 1), np.int32); rp_ = np.empty(max(int(rc.sum()), 1), np.int32)
+    _check(lib().dpgo_rbcd_plan(graph.h, len(ar), ap, arp, rank, world, None, None,
+                                sp_.ctypes.data_as(_ip), rp_.ctypes.data_as(_ip)))
+    so = np.concatenate([[0], np.cumsum(sc)]); ro = np.concatenate([[0], np.cumsum(rc)])
+    return ([sp_[so[p]:so[p + 1]] for p in range(world)], [rp_[ro[p]:ro[p + 1]] for p in range(world)])
 
 
 def lifting_matrix(d, r, seed=2):

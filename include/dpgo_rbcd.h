@@ -59,6 +59,11 @@ typedef struct {
 } dpgo_rbcd_params;
 
 void dpgo_rbcd_default_params(dpgo_rbcd_params* p);
+/* Host-only (no GPU needed): the public-pose exchange plan of `rank` -- poses per peer it sends /
+ * receives (counts in poses) and, if the arrays are non-NULL, the global pose ids, peer-major,
+ * ascending within a peer.  dpgo_rbcd_pack / all_to_all / dpgo_rbcd_update follow this plan. */
+int dpgo_rbcd_plan(dpgo_graph g, int num_agents, const int* agent_of_pose, const int* agent_rank, int rank,
+                   int world, long long* send_counts, long long* recv_counts, int* send_poses, int* recv_poses);
 /* agent_of_pose[n] in [0, num_agents); agent_rank[num_agents] in [0, world). */
 int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, const int* agent_rank,
                      int rank, int world, const dpgo_rbcd_params* p, dpgo_rbcd* out);

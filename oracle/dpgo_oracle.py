@@ -116,6 +116,27 @@ def quat_to_rot_eigen(qw, qx, qy, qz):
                      [txz - twy, tyz + twx, 1.0 - (txx + tyy)]])
 
 
+def eigen_inverse_trace_2(a, b, d):
+    """trace(M^-1) for M = [[a, b], [b, d]] with Eigen's fixed-size 2x2 inverse
+    (Eigen/src/LU/InverseImpl.h compute_inverse_size2: invdet = 1/det, r_ii = m_jj * invdet)."""
+    det = a * d - b * b
+    invdet = 1.0 / det
+    return d * invdet + a * invdet
+
+
+def eigen_inverse_trace_3(M):
+    """trace(M^-1) with Eigen's fixed-size 3x3 cofactor inverse (compute_inverse_size3)."""
+    m = M
+    c00 = m[1][1] * m[2][2] - m[1][2] * m[2][1]
+    c10 = m[2][1] * m[0][2] - m[2][2] * m[0][1]
+    c20 = m[0][1] * m[1][2] - m[0][2] * m[1][1]
+    det = c00 * m[0][0] + c10 * m[1][0] + c20 * m[2][0]
+    invdet = 1.0 / det
+    c11 = m[2][2] * m[0][0] - m[2][0] * m[0][2]
+    c22 = m[0][0] * m[1][1] - m[0][1] * m[1][0]
+    return c00 * invdet + c11 * invdet + c22 * invdet
+
+
 def read_g2o(path: str) -> Measurements:
     """src/DPGO_utils.cpp:78-212 with the SURVEY Appendix B fixes:
     B1 num_poses = max pose index + 1; B2 blank lines skipped, FIX / unknown tokens ignored,
@@ -133,8 +154,7 @@ def read_g2o(path: str) -> Measurements:
             ci, cj = key_to_robot_keyframe(i), key_to_robot_keyframe(j)
             c, s = math.cos(dth), math.sin(dth)
             R = np.array([[c, -s], [s, c]])
-            Tc = np.array([[I11, I12], [I12, I22]])
-            tau.append(2.0 / np.trace(np.linalg.inv(Tc)))  # :129-131
+            tau.append(2.0 / eigen_inverse_trace_2(I11, I12, I22))  # :129-131
             kap.append(I33)  # :133
             t = np.array([dx, dy])
             d = 2
@@ -147,10 +167,10 @@ def read_g2o(path: str) -> Measurements:
              I44, I45, I46, I55, I56, I66) = I
             ci, cj = key_to_robot_keyframe(i), key_to_robot_keyframe(j)
             R = quat_to_rot_eigen(qw, qx, qy, qz)
-            Tc = np.array([[I11, I12, I13], [I12, I22, I23], [I13, I23, I33]])
-            Rc = np.array([[I44, I45, I46], [I45, I55, I56], [I46, I56, I66]])
-            tau.append(3.0 / np.trace(np.linalg.inv(Tc)))  # :176-178
-            kap.append(3.0 / (2.0 * np.trace(np.linalg.inv(Rc))))  # :183-185
+            Tc = [[I11, I12, I13], [I12, I22, I23], [I13, I23, I33]]
+            Rc = [[I44, I45, I46], [I45, I55, I56], [I46, I56, I66]]
+            tau.append(3.0 / eigen_inverse_trace_3(Tc))  # :176-178
+            kap.append(3.0 / (2.0 * eigen_inverse_trace_3(Rc)))  # :183-185
             t = np.array([dx, dy, dz])
             d = 3
         else:

@@ -107,6 +107,18 @@ def main():
     log, Xf = O.multi_robot_example(meas, 5, num_iters=30, precon=O.PRECON_BLOCK_JACOBI)
     np.savez_compressed(os.path.join(HERE, "smallGrid3D.multirobot5.npz"),
                         log=np.array(log, dtype=float), Xfinal=Xf)
+    # plain-text copies for the C++ test program (tests/cpp/test_dpgo.cpp)
+    with open(os.path.join(HERE, "smallGrid3D.meas.txt"), "w") as f:
+        f.write(f"{meas.d} {meas.num_poses} {meas.m}\n")
+        for e in range(meas.m):
+            vals = [int(meas.p1[e]), int(meas.p2[e])] + [f"{x:.17g}" for x in meas.R[e].ravel()] + \
+                   [f"{x:.17g}" for x in meas.t[e]] + [f"{meas.kappa[e]:.17g}", f"{meas.tau[e]:.17g}"]
+            f.write(" ".join(str(v) for v in vals) + "\n")
+    X0 = O.lifting_matrix(3, 5) @ O.chordal_initialization(3, meas.num_poses, meas)
+    with open(os.path.join(HERE, "smallGrid3D.X0.txt"), "w") as f:
+        f.write(f"{X0.shape[0]} {X0.shape[1]}\n")
+        for row in X0:
+            f.write(" ".join(f"{x:.17g}" for x in row) + "\n")
     # synthetic grid (bitwise contract with the C++ generator)
     g = O.grid3d(4, seed=0)
     np.savez_compressed(os.path.join(HERE, "grid3d_k4.npz"), p1=g.p1, p2=g.p2, R=g.R, t=g.t,

@@ -1,0 +1,120 @@
+"""CPU checks of the native library's host side (no GPU): ABI exports, no-CPU-fallback
+behaviour, graph inputs (reader, grid generator, Laplacian) and the CPU port."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from oracle import dpgo_oracle as O
+from tests._common import GOLDEN, load_meas, rel
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def H():
+    from dpgo_amd import hip
+    return hip
+
+
+def _declared(header):
+    txt = open(os.path.join(ROOT, "include", header)).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return set(re.findall(r"^\s*(?:const\s+)?(?:int|void|double|const char\*)\s*\**\s*(dpgo_\w+)\s*\(", txt, re.M))
+
+
+def test_library_exports_every_declared_symbol(H):
+    lib = os.path.join(ROOT, "dpgo_amd", "libdpgo_hip.so")
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r" T (dpgo_\w+)", out))
+    declared = _declared("dpgo_hip.h") | _declared("dpgo_rbcd.h")
+    assert len(declared) > 40
+    missing = declared - exported
+    assert not missing, missing
+    H.lib()  # ctypes binds every symbol the Python binding uses
+    assert set(H.EXPORTED_SYMBOLS) <= exported
+
+
+def test_no_cpu_fallback_without_device(H):
+    if H.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(H.DPGOHipError, match="no gfx950 device"):
+        H.Problem(10, 3, 5)
+
+
+def test_grid3d_bitwise_identical_to_oracle(H):
+    for k, seed in [(3, 0), (4, 0), (5, 7)]:
+        g = H.Graph.grid3d(k, seed=seed)
+        o = O.grid3d(k, seed=seed)
+        a = g.arrays()
+        assert np.array_equal(a["p1"], o.p1) and np.array_equal(a["p2"], o.p2)
+        assert np.array_equal(a["R"], o.R) and np.array_equal(a["t"], o.t)
+        assert g.m == 3 * k * k * (k - 1)
+
+
+def test_grid_partition_and_chain_init(H):
+    g = H.Graph.grid3d(6, seed=1)
+    aop = g.grid_partition(3)
+    assert aop.min() == 0 and aop.max() == 26 and np.all(np.bincount(aop) == 8)
+    o = O.grid3d(6, seed=1)
+    Y = O.lifting_matrix(3, 5)
+    X = g.chain_init(5, Y)
+    Xo = Y @ O.chain_initialization(3, o.num_poses, o)
+    assert rel(X, Xo) <= 1e-12
+
+
+@pytest.mark.parametrize("name", ["smallGrid3D", "sphere2500", "input_INTEL_g2o", "kitti_00"])
+def test_laplacian_matches_oracle(H, name):
+    meas = load_meas(name)
+    g = H.Graph.from_arrays(meas.d, meas.num_poses, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau)
+    rp, col, blk = g.laplacian_bsr()
+    b = meas.d + 1
+    Q = O.connection_laplacian(meas, meas.num_poses)
+    Qb = sp.bsr_matrix((blk.reshape(-1, b, b).transpose(0, 2, 1), col, rp), shape=Q.shape)
+    assert abs(Qb - Q).max() <= 1e-12 * abs(Q).max()
+
+
+@pytest.mark.parametrize("name", ["smallGrid3D", "sphere2500", "input_INTEL_g2o", "kitti_00", "CSAIL",
+                                  "city10000"])
+def test_g2o_reader_matches_oracle(H, name):
+    path = f"/root/reference/data/{name}.g2o"
+    if not os.path.exists(path):
+        pytest.skip("reference data not mounted (GPU box)")
+    g = H.Graph.read_g2o(path)
+    o = O.read_g2o(path)
+    a = g.arrays()
+    assert g.n == o.num_poses and g.m == o.m and g.duplicates == o.duplicates
+    assert np.array_equal(a["p1"], o.p1) and np.array_equal(a["p2"], o.p2)
+    assert rel(a["R"], o.R) <= 1e-15 and rel(a["t"], o.t) <= 1e-15
+    assert rel(a["kappa"], o.kappa) <= 1e-12 and rel(a["tau"], o.tau) <= 1e-12
+
+
+def test_cpu_port_matches_oracle_agent_step():
+    """oracle/cpu (the timed baseline) agrees with the numpy oracle on one RBCD update."""
+    from oracle import cpu_port
+    g = O.grid3d(6, seed=2)
+    s = 3
+    aop = np.array([(c[0] // s) + 2 * ((c[1] // s) + 2 * (c[2] // s)) for c in g.extra["coords"]], np.int32)
+    X0 = O.lifting_matrix(3, 5) @ O.chain_initialization(3, g.num_poses, g)
+    arrays = dict(p1=g.p1, p2=g.p2, R=g.R, t=g.t, kappa=g.kappa, tau=g.tau)
+    sec, f = cpu_port.time_agent_step(3, 5, arrays, g.num_poses, aop, 0, O.to_dev(X0), False, 8, 1)
+    # oracle: agent 0, non-accelerated update with neighbour poses from X0
+    local = np.zeros(g.num_poses, np.int64)
+    cnt = np.zeros(8, np.int64)
+    for i in range(g.num_poses):
+        local[i] = cnt[aop[i]]
+        cnt[aop[i]] += 1
+    parts = O._split(g, aop, local, 8)
+    ag = O.Agent(0, O.AgentParams(3, 5, 8, robust="L2", precon=O.PRECON_BLOCK_JACOBI))
+    ag.set_pose_graph(*parts[0], n=int(cnt[0]))
+    glob = np.nonzero(aop == 0)[0]
+    cols = np.concatenate([np.arange(p * 4, p * 4 + 4) for p in glob])
+    ag.set_X(X0[:, cols])
+    for pid in ag.neighbor_shared:
+        gp = np.nonzero(aop == pid[0])[0][pid[1]]
+        ag.neighbor_pose[pid] = X0[:, gp * 4:gp * 4 + 4]
+    ag.iterate(True)
+    assert abs(f - ag.last_result["fOpt"]) <= 1e-9 * abs(ag.last_result["fOpt"])
