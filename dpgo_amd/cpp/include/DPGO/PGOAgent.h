@@ -91,7 +91,12 @@ class PGOAgent {
   unsigned instance_number() const { return 0; }
   unsigned iteration_number() const { return mIterationNumber; }
   PGOAgentState getState() const { return mState; }
-  PGOAgentStatus getStatus() const { return mStatus; }
+  PGOAgentStatus getStatus() {  // reference include/DPGO/PGOAgent.h:285-291
+    mStatus.agentID = mID;
+    mStatus.state = mState;
+    mStatus.iterationNumber = mIterationNumber;
+    return mStatus;
+  }
   void setNeighborStatus(const PGOAgentStatus& s);
   PGOAgentStatus getNeighborStatus(unsigned id) const;
   std::vector<unsigned> getNeighbors() const { return std::vector<unsigned>(neighborRobotIDs.begin(), neighborRobotIDs.end()); }
