@@ -163,9 +163,15 @@ int ensure_work_public(dpgo_hip_problem h) { return ensure_work(h); }
 namespace {
 
 int finalize(dpgo_hip_problem h, int op, const double* pa, int nqa, const double* pb, int nqb,
-             const dpgo::OptScalars* opt = nullptr, const int* enabled = nullptr) {
+             const dpgo::OptScalars* opt = nullptr, const int* enabled = nullptr, int pub_kind = 0,
+             int pub_tag = 0) {
   dpgo::FinalizeArgs f;
   std::memset(&f, 0, sizeof(f));
+  if (pub_kind) {
+    f.pub = h->pub_dev;
+    f.pub_kind = pub_kind;
+    f.pub_tag = pub_tag;
+  }
   f.op = op;
   f.nq_a = nqa;
   f.nq_b = nqb;
@@ -186,6 +192,43 @@ int download_sums(dpgo_hip_problem h) {
   HIP_TRY(hipMemcpyAsync(h->h_sums.data(), h->sums.p, sizeof(double) * h->h_sums.size(), hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
   return DPGO_HIP_OK;
+}
+
+// Spin on the host-mapped status words until every agent published `tag` or a later one (with
+// launch lookahead the next iteration's status may overwrite this one before the host looks; a
+// later status is at least as recent, so it answers the question too).  Returns whether any
+// agent's flag is set.  Falls back to a stream synchronisation after 20 s (never expected).
+int wait_published(dpgo_hip_problem h, int tag, bool* any) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (long spin = 0;; ++spin) {
+    bool all = true, a = false;
+    for (int k = 0; k < h->K; ++k) {
+      const int v = __atomic_load_n(&h->pub_host[k], __ATOMIC_ACQUIRE);
+      if ((v >> 1) < tag) {
+        all = false;
+        break;
+      }
+      a |= (v & 1) != 0;
+    }
+    if (all) {
+      *any = a;
+      return DPGO_HIP_OK;
+    }
+    if ((spin & 1023) == 1023 &&
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 20.0) {
+      HIP_TRY(hipStreamSynchronize(h->stream));
+      return fail(DPGO_HIP_ESTATE, "status flag never published");
+    }
+  }
+}
+
+int next_tag(dpgo_hip_problem h) {
+  if (h->pub_tag >= 0x3FFFFFF0) {  // keep tags monotonic: reset the words once, after draining
+    (void)hipStreamSynchronize(h->stream);
+    std::memset(h->pub_host, 0, sizeof(int) * h->K);
+    h->pub_tag = 0;
+  }
+  return ++h->pub_tag;
 }
 
 int download_state(dpgo_hip_problem h) {
@@ -316,6 +359,11 @@ int dpgo_hip_problem_create_batch(int num_agents, const int* poses_per_agent, in
       hipMemcpy(h->agent_np.p, poses_per_agent, sizeof(int) * num_agents, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(h->state.p, 0, sizeof(AgentState) * num_agents) != hipSuccess)
     return cleanup(fail(DPGO_HIP_EDEVICE, "device upload failed"));
+  if (hipHostMalloc(reinterpret_cast<void**>(&h->pub_host), sizeof(int) * num_agents,
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&h->pub_dev), h->pub_host, 0) != hipSuccess)
+    return cleanup(fail(DPGO_HIP_ENOMEM, "host-mapped status allocation failed"));
+  std::memset(h->pub_host, 0, sizeof(int) * num_agents);
   // empty Q (setQ of a zero matrix, as in the reference ctor :23-24)
   for (int a = 0; a < num_agents; ++a) h->q_agent[a].rowptr.assign(poses_per_agent[a] + 1, 0);
   *out = h;
@@ -332,6 +380,8 @@ int dpgo_hip_problem_destroy(dpgo_hip_problem h) {
     (void)hipStreamSynchronize(h->own_stream);
     (void)hipStreamDestroy(h->own_stream);
   }
+  (void)hipDeviceSynchronize();
+  if (h->pub_host) (void)hipHostFree(h->pub_host);
   delete h;
   return DPGO_HIP_OK;
 }
@@ -518,6 +568,12 @@ int dpgo_hip_polar_combine_dev(dpgo_hip_problem h, const double* A, const double
   return DPGO_HIP_OK;
 }
 
+int dpgo_hip_set_tuning(int key, int value) {
+  if (key < 0 || key >= dpgo::TUNE_COUNT) return fail(DPGO_HIP_EINVAL, "bad tuning key");
+  dpgo::g_tuning[key] = value;
+  return DPGO_HIP_OK;
+}
+
 int dpgo_hip_synchronize(dpgo_hip_problem h) {
   DPGO_TRY(check_handle(h));
   HIP_TRY(hipStreamSynchronize(h->stream));
@@ -543,10 +599,20 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
   std::vector<int> en(K, 1);
   if (agent_enabled_host)
     for (int a = 0; a < K; ++a) en[a] = agent_enabled_host[a] != 0;
-  HIP_TRY(hipMemcpyAsync(h->enabled.p, en.data(), sizeof(int) * K, hipMemcpyHostToDevice, h->stream));
-  HIP_TRY(hipMemcpyAsync(h->x1.p, X_in, h->vec_bytes(), hipMemcpyDeviceToDevice, h->stream));
+  // (a pageable H2D copy would synchronise the stream: only copy when a mask is given)
+  if (agent_enabled_host)
+    HIP_TRY(hipMemcpyAsync(h->enabled.p, en.data(), sizeof(int) * K, hipMemcpyHostToDevice, h->stream));
+  else
+    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(h->enabled.p), 1, K, h->stream));
 
   const bool single = P.algorithm == DPGO_ALG_RTR && P.tr_iterations == 1;
+  // x1 only moves in a multi-iteration Run; a single Run (the RBCD setting) reads X_in in place.
+  double* x1 = h->x1.p;
+  if (single || P.algorithm == DPGO_ALG_RGD) {
+    x1 = const_cast<double*>(X_in);
+  } else {
+    HIP_TRY(hipMemcpyAsync(h->x1.p, X_in, h->vec_bytes(), hipMemcpyDeviceToDevice, h->stream));
+  }
   dpgo::OptScalars o;
   std::memset(&o, 0, sizeof(o));
   o.tol = P.tr_tolerance;
@@ -557,21 +623,20 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
   o.min_inner = 0;
   o.max_iter = P.tr_iterations;
   o.single_run = single ? 1 : 0;
-
   // f(x1), grad(x1), S(x1)  (QuadraticOptimizer::optimize :36-37, SolversTR start)
-  DPGO_TRY(eval_at(h, h->x1.p, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_NONE));
+  DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_NONE));
   DPGO_TRY(finalize(h, dpgo::OP_EVAL_INIT, h->pa.p, 2, nullptr, 0, &o, h->enabled.p));
 
   if (P.algorithm == DPGO_ALG_RGD) {
     // one fixed-step Riemannian gradient step (QuadraticOptimizer::gradientDescent :124-149)
     auto cr = make_ctx(h, dpgo::FLAG_NONE, h->pb.p);
-    HIP_TRY(dpgo::launch_retract(r, b, cr, h->x1.p, h->g.p, -P.rgd_stepsize, h->x2.p, nullptr, nullptr));
+    HIP_TRY(dpgo::launch_retract(r, b, cr, x1, h->g.p, -P.rgd_stepsize, h->x2.p, nullptr, nullptr));
     DPGO_TRY(eval_at(h, h->x2.p, h->g2.p, h->S2.p, h->pb.p, dpgo::FLAG_NONE));
     DPGO_TRY(finalize(h, dpgo::OP_SUM, h->pb.p, 2, nullptr, 0));
     DPGO_TRY(download_sums(h));
     HIP_TRY(hipMemcpyAsync(h->use_a.p, en.data(), sizeof(int) * K, hipMemcpyHostToDevice, h->stream));
     auto cs = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
-    HIP_TRY(dpgo::launch_select(r, b, cs, h->x2.p, h->x1.p, h->use_a.p, h->x1.p, X_out));
+    HIP_TRY(dpgo::launch_select(r, b, cs, h->x2.p, x1, h->use_a.p, x1, X_out));
     DPGO_TRY(finalize(h, dpgo::OP_REL_CHANGE, h->pa.p, 1, nullptr, 0));
     DPGO_TRY(download_state(h));
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - t0).count();
@@ -593,54 +658,77 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
     return DPGO_HIP_OK;
   }
 
+  if (P.tr_max_inner == 0) HIP_TRY(hipMemsetAsync(h->eta.p, 0, h->vec_bytes(), h->stream));
+  // Host control without stream synchronisation: k_finalize publishes each agent's tCG / Run flag
+  // to host-mapped memory; the host keeps one tCG iteration of launches queued ahead of the flag
+  // it is waiting for, so the GPU never drains (agents that finished skip their tiles).
   const int max_rounds = single ? 12 : P.tr_iterations;
   for (int round = 0; round < max_rounds; ++round) {
-    DPGO_TRY(download_state(h));
-    bool any = false;
-    for (int a = 0; a < K; ++a) any |= h->h_state[a].run_active != 0;
-    if (!any) break;
     // ---- truncated CG (A.4)
     auto ci = make_ctx(h, dpgo::FLAG_RUN, h->pa.p);
-    HIP_TRY(dpgo::launch_tcg_init(r, b, ci, h->x1.p, h->minv.p, pmode, h->g.p, h->eta.p, h->Heta.p, h->rv.p,
-                                  h->z.p, h->delta.p));
+    HIP_TRY(dpgo::launch_tcg_init(r, b, ci, x1, h->minv.p, pmode, h->g.p, h->delta.p));
     DPGO_TRY(finalize(h, dpgo::OP_TCG_INIT, h->pa.p, 2, nullptr, 0, &o));
-    for (int j = 0; j < P.tr_max_inner; ++j) {
+    std::vector<int> tags;
+    auto launch_iter = [&](int j) -> int {
       auto ch = make_ctx(h, dpgo::FLAG_TCG, h->pa.p);
-      HIP_TRY(dpgo::launch_spmm(r, b, dpgo::MODE_HESS, ch, qview(h), h->delta.p, nullptr, nullptr, h->x1.p, h->S.p,
+      HIP_TRY(dpgo::launch_spmm(r, b, dpgo::MODE_HESS, ch, qview(h), h->delta.p, nullptr, nullptr, x1, h->S.p,
                                 h->Hdelta.p, nullptr));
       DPGO_TRY(finalize(h, dpgo::OP_TCG_STEP, h->pa.p, 1, nullptr, 0, &o));
       auto cu = make_ctx(h, dpgo::FLAG_TCG_MODE, h->pb.p);
-      HIP_TRY(dpgo::launch_tcg_update(r, b, cu, h->x1.p, h->minv.p, pmode, h->delta.p, h->Hdelta.p, h->eta.p,
-                                      h->Heta.p, h->rv.p, h->z.p));
-      DPGO_TRY(finalize(h, dpgo::OP_TCG_CHECK, h->pb.p, 2, nullptr, 0, &o));
-      auto cd = make_ctx(h, dpgo::FLAG_TCG, nullptr);
-      HIP_TRY(dpgo::launch_tcg_dir(r, b, cd, h->z.p, h->delta.p));
-      if (P.tr_max_inner > 10 && (j % 8) == 7) {
-        DPGO_TRY(download_state(h));
-        bool act = false;
-        for (int a = 0; a < K; ++a) act |= h->h_state[a].tcg_active != 0;
-        if (!act) break;
+      HIP_TRY(dpgo::launch_tcg_update(r, b, cu, x1, h->minv.p, pmode, h->delta.p, h->Hdelta.p, h->eta.p,
+                                      h->Heta.p, j == 0 ? h->g.p : h->rv.p, h->rv.p, h->z.p, j == 0 ? 1 : 0));
+      const int tag = next_tag(h);
+      tags.push_back(tag);
+      DPGO_TRY(finalize(h, dpgo::OP_TCG_CHECK, h->pb.p, 2, nullptr, 0, &o, nullptr, 1, tag));
+      if (j + 1 < P.tr_max_inner) {  // the last direction update is never used
+        auto cd = make_ctx(h, dpgo::FLAG_TCG, nullptr);
+        HIP_TRY(dpgo::launch_tcg_dir(r, b, cd, h->z.p, h->delta.p));
       }
+      return DPGO_HIP_OK;
+    };
+    int launched = 0;
+    if (P.tr_max_inner > 0) {
+      DPGO_TRY(launch_iter(0));
+      launched = 1;
+    }
+    for (int j = 0; j < P.tr_max_inner; ++j) {
+      if (launched < P.tr_max_inner) {  // lookahead: iteration j+1 queued before waiting on j
+        DPGO_TRY(launch_iter(launched));
+        ++launched;
+      }
+      bool act = false;
+      DPGO_TRY(wait_published(h, tags[j], &act));
+      if (!act) break;
     }
     // ---- candidate x2 = R_x1(eta), rho test, radius update
     auto cr = make_ctx(h, dpgo::FLAG_RUN, h->pa.p);
-    HIP_TRY(dpgo::launch_retract(r, b, cr, h->x1.p, h->eta.p, 1.0, h->x2.p, h->g.p, h->Heta.p));
-    DPGO_TRY(eval_at(h, h->x2.p, h->g2.p, h->S2.p, h->pb.p, dpgo::FLAG_RUN));
-    DPGO_TRY(finalize(h, dpgo::OP_RHO, h->pa.p, 2, h->pb.p, 2, &o));
+    HIP_TRY(dpgo::launch_retract(r, b, cr, x1, h->eta.p, 1.0, h->x2.p, h->g.p, h->Heta.p));
+    // single Run: only f(x2) and |grad(x2)| are consumed (fOpt / gradNormOpt)
+    DPGO_TRY(eval_at(h, h->x2.p, single ? nullptr : h->g2.p, single ? nullptr : h->S2.p, h->pb.p, dpgo::FLAG_RUN));
+    const int rtag = next_tag(h);
+    DPGO_TRY(finalize(h, dpgo::OP_RHO, h->pa.p, 2, h->pb.p, 2, &o, nullptr, 2, rtag));
     if (!single) {
       auto ca = make_ctx(h, dpgo::FLAG_NONE, nullptr);
       HIP_TRY(dpgo::launch_accept(r, b, ca, h->x2.p, h->g2.p, h->S2.p, h->x1.p, h->g.p, h->S.p));
+    } else {
+      // speculative output: X_out = accepted ? x2 : X_in (repeated after a retry Run; agents that are
+      // done skip nothing here, rejected ones copy their unchanged input)
+      auto cs = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
+      HIP_TRY(dpgo::launch_select(r, b, cs, h->x2.p, X_in, nullptr, X_in, X_out));
+    }
+    if (round + 1 < max_rounds) {  // radius-shrink retry / next outer iteration needed?
+      bool any = false;
+      DPGO_TRY(wait_published(h, rtag, &any));
+      if (!any) break;
     }
   }
-  DPGO_TRY(download_state(h));
-  std::vector<int> use(K, 0);
-  for (int a = 0; a < K; ++a) {
-    const AgentState& s = h->h_state[a];
-    use[a] = single ? (s.runs > 0 && s.accepted && !s.gave_up) : 1;
-  }
-  HIP_TRY(hipMemcpyAsync(h->use_a.p, use.data(), sizeof(int) * K, hipMemcpyHostToDevice, h->stream));
+  // X_out: accepted candidate or the input (single Run), x1 (multi-iteration)
   auto cs = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
-  HIP_TRY(dpgo::launch_select(r, b, cs, single ? h->x2.p : h->x1.p, X_in, h->use_a.p, X_in, X_out));
+  if (!single) {
+    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(h->use_a.p), 1, K, h->stream));
+    HIP_TRY(dpgo::launch_select(r, b, cs, x1, X_in, h->use_a.p, X_in, X_out));
+  }
+  if (!results && !P.verbose) return DPGO_HIP_OK;  // no host round trip needed
   DPGO_TRY(finalize(h, dpgo::OP_REL_CHANGE, h->pa.p, 1, nullptr, 0));
   DPGO_TRY(download_state(h));
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - t0).count();

@@ -58,6 +58,10 @@ struct FinalizeArgs {
   AgentState* state;
   double* out_sums;             // OP_SUM: [num_agents * 4]
   OptScalars opt;
+  // zero-copy status publication to host-mapped memory: pub[agent] = (tag << 1) | flag
+  int* pub;                     // nullptr = none
+  int pub_tag;
+  int pub_kind;                 // 1: tcg_active, 2: run_active
 };
 
 // shared-edge records for G assembly, grouped by G slot (CSR)
@@ -72,6 +76,10 @@ struct GEdges {
   const double* w;
 };
 
+// Runtime-selectable kernel variants (A/B tuning in one process; see tools/spmm_ab.py).
+enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_COUNT = 4 };
+extern int g_tuning[TUNE_COUNT];
+
 bool supported_rb(int r, int b);
 hipError_t launch_gather_poses(int count, int rb, const int* idx, const double* A, const double* Bsrc, double* dst,
                                hipStream_t stream);
@@ -81,10 +89,10 @@ hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const QView& 
                        const int* gidx, const double* gblk, const double* X, const double* S_in,
                        double* out, double* S_out);
 hipError_t launch_tcg_init(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
-                           const double* g, double* eta, double* Heta, double* rv, double* z, double* delta);
+                           const double* g, double* delta);
 hipError_t launch_tcg_update(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
-                             const double* delta, const double* Hdelta, double* eta, double* Heta, double* rv,
-                             double* z);
+                             const double* delta, const double* Hdelta, double* eta, double* Heta,
+                             const double* r_in, double* rv, double* z, int first);
 hipError_t launch_tcg_dir(int r, int b, const LaunchCtx& c, const double* z, double* delta);
 hipError_t launch_retract(int r, int b, const LaunchCtx& c, const double* X, const double* V, double scale,
                           double* out, const double* g, const double* HV);
@@ -93,7 +101,7 @@ hipError_t launch_precond(int r, int b, const LaunchCtx& c, const double* X, con
                           const double* V, double* out);
 hipError_t launch_polar_comb(int r, int b, const LaunchCtx& c, const double* A, const double* Bv,
                              const double* ca, const double* cb, double* out, const double* Cv = nullptr,
-                             double sa = 1.0, double sb = 0.0);
+                             double sa = 1.0, double sb = 0.0, double* out2 = nullptr);
 hipError_t launch_select(int r, int b, const LaunchCtx& c, const double* A, const double* Bv, const int* use_a,
                          const double* ref, double* out);
 hipError_t launch_accept(int r, int b, const LaunchCtx& c, const double* x2, const double* g2, const double* S2,

@@ -72,13 +72,21 @@ struct PoseLane {
   int kk;  // column this lane owns (k < B) else -1
 };
 
-template <int B>
+// XCD-aware bijective remap (cdna_hip_programming.md 5.5 T1): blocks b and b+8 share an XCD, so
+// give XCD slot x a contiguous range of tiles; neighbouring tiles then share that XCD's L2 for
+// the gathered X rows.  Speed only -- placement never affects results.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+template <int B, bool XCD = false>
 __device__ __forceinline__ PoseLane pose_lane(const LaunchCtx& c) {
   PoseLane p;
   p.lane = threadIdx.x & 63;
   p.wave = threadIdx.x >> 6;
   p.k = p.lane & 3;
-  p.tile = blockIdx.x;
+  p.tile = XCD ? xcd_remap(static_cast<int>(blockIdx.x), static_cast<int>(gridDim.x)) : static_cast<int>(blockIdx.x);
   p.agent = c.tile_agent[p.tile];
   p.pslot = p.wave * kPosesPerWave + (p.lane >> 2);
   p.ok = p.pslot < c.tile_count[p.tile];
@@ -97,7 +105,73 @@ __device__ __forceinline__ PoseLane pose_lane(const LaunchCtx& c) {
 // BSR storage: block-row j lists neighbours i with block (j,i) of Q column-major, which is
 // block (i,j) row-major (Q symmetric), so lane k streams row k of Q_ij: Y_j += X_i[:,k] Q_ij[k,:].
 // ------------------------------------------------------------------------------------------
-template <int R, int B, int MODE>
+// Lane k of the pose quad accumulates sum_i X_i[:,k] (x) Q_ij[k,:] over block-row j.  UNR
+// neighbours are processed per step with every load issued before the FMAs (memory-level
+// parallelism: the column-index load and the dependent X gather of UNR neighbours overlap).
+template <int R, int B, int UNR, bool NT>
+__device__ __forceinline__ void spmm_accumulate(const QView& q, const double* __restrict__ in, long j, int k,
+                                                double (&acc)[R][B]) {
+  const int beg = q.rowptr[j], end = q.rowptr[j + 1];
+  int nz = beg;
+  auto load_blk = [&](int z, double (&bb)[B]) {
+    const double* brow = q.blocks + static_cast<long>(z) * (B * B) + k * B;
+    if constexpr (B == 4) {
+      f64x2 b0, b1;
+      if constexpr (NT) {
+        b0 = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(brow));
+        b1 = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(brow) + 1);
+      } else {
+        b0 = reinterpret_cast<const f64x2*>(brow)[0];
+        b1 = reinterpret_cast<const f64x2*>(brow)[1];
+      }
+      bb[0] = b0.x; bb[1] = b0.y; bb[2] = b1.x; bb[3] = b1.y;
+    } else {
+#pragma unroll
+      for (int cc = 0; cc < B; ++cc) bb[cc] = NT ? __builtin_nontemporal_load(brow + cc) : brow[cc];
+    }
+  };
+  if constexpr (UNR > 1) {
+    for (; nz + UNR <= end; nz += UNR) {
+      long ii[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) ii[u] = q.col[nz + u];
+      double bb[UNR][B], xx[UNR][R];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) load_blk(nz + u, bb[u]);
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const double* xk = in + ii[u] * (R * B) + k * R;
+#pragma unroll
+        for (int a = 0; a < R; ++a) xx[u][a] = xk[a];
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u)
+#pragma unroll
+        for (int a = 0; a < R; ++a)
+#pragma unroll
+          for (int cc = 0; cc < B; ++cc) acc[a][cc] = fma(xx[u][a], bb[u][cc], acc[a][cc]);
+    }
+  }
+  for (; nz < end; ++nz) {
+    const long i = q.col[nz];
+    double bb[B], xx[R];
+    load_blk(nz, bb);
+    const double* xk = in + i * (R * B) + k * R;
+#pragma unroll
+    for (int a = 0; a < R; ++a) xx[a] = xk[a];
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int cc = 0; cc < B; ++cc) acc[a][cc] = fma(xx[a], bb[cc], acc[a][cc]);
+  }
+}
+
+// SpMM variants: neighbours per step, non-temporal block loads, XCD tile remap
+constexpr int var_unr(int v) { return v == 2 || v == 5 ? 2 : (v == 3 || v == 4) ? 4 : 1; }
+constexpr bool var_nt(int v) { return v == 1; }  // default-policy loads measured faster (tools/spmm_ab.py)
+constexpr bool var_xcd(int v) { return v == 4 || v == 5; }
+
+template <int R, int B, int MODE, int VAR = 0>
 __global__ __launch_bounds__(kThreads) void k_spmm(LaunchCtx c, QView q, const double* __restrict__ in,
                                                    const int* __restrict__ gidx,
                                                    const double* __restrict__ gblk,
@@ -106,7 +180,7 @@ __global__ __launch_bounds__(kThreads) void k_spmm(LaunchCtx c, QView q, const d
                                                    double* __restrict__ out,
                                                    double* __restrict__ S_out) {
   constexpr int D = B - 1;
-  const PoseLane p = pose_lane<B>(c);
+  const PoseLane p = pose_lane<B, var_xcd(VAR)>(c);
   if (tile_skipped(c, p.agent)) return;
 
   double acc[R][B];
@@ -115,29 +189,7 @@ __global__ __launch_bounds__(kThreads) void k_spmm(LaunchCtx c, QView q, const d
 #pragma unroll
     for (int cc = 0; cc < B; ++cc) acc[a][cc] = 0.0;
 
-  if (p.ok && p.k < B) {
-    const int beg = q.rowptr[p.j], end = q.rowptr[p.j + 1];
-    for (int nz = beg; nz < end; ++nz) {
-      const long i = q.col[nz];
-      const double* brow = q.blocks + static_cast<long>(nz) * (B * B) + p.k * B;
-      const double* xk = in + i * (R * B) + p.k * R;
-      double bb[B], xx[R];
-      if constexpr (B == 4) {
-        const f64x2 b0 = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(brow));
-        const f64x2 b1 = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(brow) + 1);
-        bb[0] = b0.x; bb[1] = b0.y; bb[2] = b1.x; bb[3] = b1.y;
-      } else {
-#pragma unroll
-        for (int cc = 0; cc < B; ++cc) bb[cc] = __builtin_nontemporal_load(brow + cc);
-      }
-#pragma unroll
-      for (int a = 0; a < R; ++a) xx[a] = xk[a];
-#pragma unroll
-      for (int a = 0; a < R; ++a)
-#pragma unroll
-        for (int cc = 0; cc < B; ++cc) acc[a][cc] = fma(xx[a], bb[cc], acc[a][cc]);
-    }
-  }
+  if (p.ok && p.k < B) spmm_accumulate<R, B, var_unr(VAR), var_nt(VAR)>(q, in, p.j, p.k, acc);
 #pragma unroll
   for (int a = 0; a < R; ++a)
 #pragma unroll
@@ -192,7 +244,7 @@ __global__ __launch_bounds__(kThreads) void k_spmm(LaunchCtx c, QView q, const d
     double gpart = 0.0;
 #pragma unroll
     for (int a = 0; a < R; ++a) gpart = fma(gc[a], gc[a], gpart);
-    store_vec<R>(out, off, own, gc);
+    if (out != nullptr) store_vec<R>(out, off, own, gc);
     if (p.ok && p.k == 0 && S_out != nullptr) {
 #pragma unroll
       for (int u = 0; u < D; ++u)
@@ -259,23 +311,21 @@ __device__ __forceinline__ void precond_pose(const double (&Xf)[R][B], const dou
   tangent_project_pose<R, B>(Xf, z);
 }
 
-// tCG start (A.4): eta = 0, Heta = 0, r = grad, z = Prec(r), delta = -z; partials <z,r>, |r|^2
+// tCG start (A.4): eta = 0, Heta = 0, r = grad, z = Prec(r), delta = -z; partials <z,r>, |r|^2.
+// eta, Heta and r are not materialised here: the first k_tcg_update reads r from grad and treats
+// eta / Heta as zero, so this pass only writes delta.
 template <int R, int B>
 __global__ __launch_bounds__(kThreads) void k_tcg_init(LaunchCtx c, const double* __restrict__ X,
                                                        const double* __restrict__ Minv, int pmode,
                                                        const double* __restrict__ g,
-                                                       double* __restrict__ eta, double* __restrict__ Heta,
-                                                       double* __restrict__ r, double* __restrict__ z,
                                                        double* __restrict__ delta) {
   const PoseLane p = pose_lane<B>(c);
   if (tile_skipped(c, p.agent)) return;
   const bool own = p.ok && p.k < B;
   const long off = p.j * (R * B) + p.k * R;
-  double gcol[R], xcol[R], zero[R];
+  double gcol[R], xcol[R];
   load_col<R, B>(g, p.j, p.k, p.ok, gcol);
   load_col<R, B>(X, p.j, p.k, p.ok, xcol);
-#pragma unroll
-  for (int a = 0; a < R; ++a) zero[a] = 0.0;
   double Gf[R][B], Xf[R][B], Zf[R][B];
   quad_gather<R, B>(gcol, Gf);
   quad_gather<R, B>(xcol, Xf);
@@ -289,10 +339,6 @@ __global__ __launch_bounds__(kThreads) void k_tcg_init(LaunchCtx c, const double
     rr = fma(gcol[a], gcol[a], rr);
     dc[a] = -zc[a];
   }
-  store_vec<R>(eta, off, own, zero);
-  store_vec<R>(Heta, off, own, zero);
-  store_vec<R>(r, off, own, gcol);
-  store_vec<R>(z, off, own, zc);
   store_vec<R>(delta, off, own, dc);
   double parts[2] = {own ? zr : 0.0, own ? rr : 0.0};
   block_partials<2>(parts, c.partials, p.tile);
@@ -306,7 +352,8 @@ __global__ __launch_bounds__(kThreads) void k_tcg_update(LaunchCtx c, const doub
                                                          const double* __restrict__ delta,
                                                          const double* __restrict__ Hdelta,
                                                          double* __restrict__ eta, double* __restrict__ Heta,
-                                                         double* __restrict__ r, double* __restrict__ z) {
+                                                         const double* r_in, double* r, double* __restrict__ z,
+                                                         int first) {
   const PoseLane p = pose_lane<B>(c);
   if (tile_skipped(c, p.agent)) return;  // FLAG_TCG_MODE: skips mode 2
   const AgentState& st = c.state[p.agent];
@@ -317,8 +364,13 @@ __global__ __launch_bounds__(kThreads) void k_tcg_update(LaunchCtx c, const doub
   double dcol[R], hcol[R], ecol[R], hecol[R];
   load_col<R, B>(delta, p.j, p.k, p.ok, dcol);
   load_col<R, B>(Hdelta, p.j, p.k, p.ok, hcol);
-  load_col<R, B>(eta, p.j, p.k, p.ok, ecol);
-  load_col<R, B>(Heta, p.j, p.k, p.ok, hecol);
+  if (first) {  // eta = Heta = 0 at the start of tCG
+#pragma unroll
+    for (int a = 0; a < R; ++a) ecol[a] = hecol[a] = 0.0;
+  } else {
+    load_col<R, B>(eta, p.j, p.k, p.ok, ecol);
+    load_col<R, B>(Heta, p.j, p.k, p.ok, hecol);
+  }
 #pragma unroll
   for (int a = 0; a < R; ++a) {
     ecol[a] = fma(step, dcol[a], ecol[a]);
@@ -328,7 +380,7 @@ __global__ __launch_bounds__(kThreads) void k_tcg_update(LaunchCtx c, const doub
   store_vec<R>(Heta, off, own, hecol);
   if (mode != 0) return;  // boundary step: tCG stops, r/z untouched (uniform per agent)
   double rcol[R], xcol[R];
-  load_col<R, B>(r, p.j, p.k, p.ok, rcol);
+  load_col<R, B>(r_in, p.j, p.k, p.ok, rcol);  // r_in = grad on the first step
   load_col<R, B>(X, p.j, p.k, p.ok, xcol);
 #pragma unroll
   for (int a = 0; a < R; ++a) rcol[a] = fma(step, hcol[a], rcol[a]);
@@ -457,7 +509,7 @@ __global__ __launch_bounds__(64) void k_polar_comb(LaunchCtx c, const double* __
                                                    const double* __restrict__ cb,
                                                    double* __restrict__ out,
                                                    const double* __restrict__ Cv, double sa,
-                                                   double sb) {
+                                                   double sb, double* __restrict__ out2) {
   constexpr int D = B - 1;
   const int tile = blockIdx.x;
   const int agent = c.tile_agent[tile];
@@ -504,6 +556,15 @@ __global__ __launch_bounds__(64) void k_polar_comb(LaunchCtx c, const double* __
     for (int a = 0; a < R; ++a) po[cc * R + a] = M[a][cc];
 #pragma unroll
   for (int a = 0; a < R; ++a) po[D * R + a] = tcol[a];
+  if (out2 != nullptr) {  // second copy (Nesterov iterate(false): X = Y)
+    double* p2 = out2 + j * (R * B);
+#pragma unroll
+    for (int cc = 0; cc < D; ++cc)
+#pragma unroll
+      for (int a = 0; a < R; ++a) p2[cc * R + a] = M[a][cc];
+#pragma unroll
+    for (int a = 0; a < R; ++a) p2[D * R + a] = tcol[a];
+  }
 }
 
 // out = sel ? A : B per agent; partial |out - ref|^2
@@ -517,7 +578,13 @@ __global__ __launch_bounds__(kThreads) void k_select(LaunchCtx c, const double* 
   if (tile_skipped(c, p.agent)) return;
   const bool own = p.ok && p.k < B;
   const long off = p.j * (R * B) + p.k * R;
-  const bool ua = use_a[p.agent] != 0;
+  bool ua;
+  if (use_a != nullptr) {
+    ua = use_a[p.agent] != 0;
+  } else {  // QuadraticOptimizer::trustRegion result: accepted step, else the input (:92-110)
+    const AgentState& st = c.state[p.agent];
+    ua = st.runs > 0 && st.accepted && !st.gave_up;
+  }
   double dd = 0.0;
   if (own) {
 #pragma unroll
@@ -723,6 +790,11 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
     default:
       break;
   }
+  if (f.pub != nullptr) {
+    const int flag = f.pub_kind == 1 ? s.tcg_active : s.run_active;
+    __hip_atomic_store(&f.pub[agent], (f.pub_tag << 1) | (flag ? 1 : 0), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // --- block-Jacobi inverse of (Q_jj + shift I), computed on device from the BSR diagonal ---
@@ -877,6 +949,8 @@ __global__ __launch_bounds__(kThreads) void k_assemble_G(GEdges e, int nslots, c
     default: return hipErrorInvalidValue;                  \
   }
 
+int g_tuning[TUNE_COUNT] = {0};
+
 bool supported_rb(int r, int b) {
   if (b == 3) return r >= 2 && r <= 8;
   if (b == 4) return r >= 3 && r <= 8;
@@ -890,7 +964,25 @@ hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const QView& 
   dim3 grid(c.num_tiles), block(kThreads);
   switch (mode) {
     case MODE_XQ:
-      DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_XQ><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
+      switch (g_tuning[TUNE_SPMM_VARIANT]) {
+        case 1:
+          DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_XQ, 1><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
+          break;
+        case 2:
+          DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_XQ, 2><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
+          break;
+        case 3:
+          DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_XQ, 3><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
+          break;
+        case 4:
+          DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_XQ, 4><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
+          break;
+        case 5:
+          DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_XQ, 5><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
+          break;
+        default:
+          DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_XQ, 0><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
+      }
       break;
     case MODE_XQ_G:
       DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_XQ_G><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
@@ -908,17 +1000,17 @@ hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const QView& 
 }
 
 hipError_t launch_tcg_init(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
-                           const double* g, double* eta, double* Heta, double* rv, double* z, double* delta) {
+                           const double* g, double* delta) {
   if (c.num_tiles == 0) return hipSuccess;
-  DPGO_DISPATCH(r, b, (k_tcg_init<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, Minv, pmode, g, eta, Heta, rv, z, delta)));
+  DPGO_DISPATCH(r, b, (k_tcg_init<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, Minv, pmode, g, delta)));
   return hipGetLastError();
 }
 
 hipError_t launch_tcg_update(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
-                             const double* delta, const double* Hdelta, double* eta, double* Heta, double* rv,
-                             double* z) {
+                             const double* delta, const double* Hdelta, double* eta, double* Heta,
+                             const double* r_in, double* rv, double* z, int first) {
   if (c.num_tiles == 0) return hipSuccess;
-  DPGO_DISPATCH(r, b, (k_tcg_update<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, Minv, pmode, delta, Hdelta, eta, Heta, rv, z)));
+  DPGO_DISPATCH(r, b, (k_tcg_update<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, Minv, pmode, delta, Hdelta, eta, Heta, r_in, rv, z, first)));
   return hipGetLastError();
 }
 
@@ -950,9 +1042,9 @@ hipError_t launch_precond(int r, int b, const LaunchCtx& c, const double* X, con
 
 hipError_t launch_polar_comb(int r, int b, const LaunchCtx& c, const double* A, const double* Bv,
                              const double* ca, const double* cb, double* out, const double* Cv, double sa,
-                             double sb) {
+                             double sb, double* out2) {
   if (c.num_tiles == 0) return hipSuccess;
-  DPGO_DISPATCH(r, b, (k_polar_comb<R, B><<<c.num_tiles, 64, 0, c.stream>>>(c, A, Bv, ca, cb, out, Cv, sa, sb)));
+  DPGO_DISPATCH(r, b, (k_polar_comb<R, B><<<c.num_tiles, 64, 0, c.stream>>>(c, A, Bv, ca, cb, out, Cv, sa, sb, out2)));
   return hipGetLastError();
 }
 

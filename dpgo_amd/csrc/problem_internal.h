@@ -90,6 +90,10 @@ struct dpgo_hip_problem_s {
   dpgo::DevBuf<double> pa, pb, sums, coef_a, coef_b;
   dpgo::DevBuf<dpgo::AgentState> state;
   std::vector<dpgo::AgentState> h_state;
+  // host-mapped status words written by k_finalize (zero-copy polling, no stream sync)
+  int* pub_host = nullptr;
+  int* pub_dev = nullptr;
+  int pub_tag = 0;
   std::vector<double> h_sums;
 
   size_t vec_len() const { return static_cast<size_t>(N) * r * b; }

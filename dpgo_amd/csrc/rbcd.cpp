@@ -67,12 +67,12 @@ double* color_ptr(dpgo_rbcd e, DevBuf<double>& buf, int c) {
 }
 
 int polar(dpgo_rbcd e, int c, const double* A, const double* B, double ca, double cb, double* out,
-          const double* C = nullptr) {
+          const double* C = nullptr, double* out2 = nullptr) {
   dpgo_hip_problem h = e->prob[c];
   if (!h) return DPGO_HIP_OK;
   // uniform Nesterov coefficients travel as kernel arguments
   auto ctx = make_ctx(h, FLAG_NONE, h->pa.p);
-  HIP_TRY(launch_polar_comb(e->r, e->b, ctx, A, B, nullptr, nullptr, out, C, ca, cb));
+  HIP_TRY(launch_polar_comb(e->r, e->b, ctx, A, B, nullptr, nullptr, out, C, ca, cb, out2));
   return DPGO_HIP_OK;
 }
 
@@ -467,25 +467,28 @@ static bool restart_now(dpgo_rbcd e) {
 int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color) {
   if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
   e->iteration += 1;  // mIterationNumber++ (:643)
+  const bool restart = restart_now(e);
+  // XPrev = X (:673) is only read by a restart (the relative-change status is not tracked here)
   const long bytes = static_cast<long>(sizeof(double)) * e->Nown * static_cast<long>(e->rb());
-  if (bytes) HIP_TRY(hipMemcpyAsync(e->Xprev.p, e->X.p, bytes, hipMemcpyDeviceToDevice, e->stream));  // XPrev = X
+  if (restart && bytes) HIP_TRY(hipMemcpyAsync(e->Xprev.p, e->X.p, bytes, hipMemcpyDeviceToDevice, e->stream));
   if (!e->P.acceleration) return DPGO_HIP_OK;
   const double N = static_cast<double>(e->K);
   e->gamma = (1.0 + std::sqrt(1.0 + 4.0 * N * N * e->gamma * e->gamma)) / (2.0 * N);  // updateGamma
   e->alpha = 1.0 / (e->gamma * N);                                                     // updateAlpha
-  const bool restart = restart_now(e);
   for (int c = 0; c < e->ncolors; ++c) {
     if (!e->prob[c]) continue;
     double* Xc = color_ptr(e, e->X, c);
     double* Yc = color_ptr(e, e->Y, c);
     double* Vc = color_ptr(e, e->V, c);
-    // updateY: Y = project((1 - alpha) X + alpha V)  (every agent)
-    DPGO_TRY(polar(e, c, Xc, Vc, 1.0 - e->alpha, e->alpha, Yc));
-    if (c == color) continue;
-    // non-selected agents: updateX(false, true): X = Y; updateV; restart
-    DPGO_TRY(copy_poses(e, e->X.p, e->Y.p, color_first_pose(e, c), color_num_poses(e, c)));
-    DPGO_TRY(polar(e, c, Vc, Xc, 0.0, e->gamma, Vc, Yc));  // V = project(V + gamma (X - Y))
-    if (restart) {
+    if (c == color) {
+      DPGO_TRY(polar(e, c, Xc, Vc, 1.0 - e->alpha, e->alpha, Yc));  // updateY (selected)
+      continue;
+    }
+    // non-selected agents, iterate(false): updateY, updateX(false, true): X = Y (one fused pass);
+    // updateV: V = project(V + gamma (X - Y)) = project(V) because X == Y exactly, and V already
+    // lies on the manifold (it is a previous project() output), so that pass is skipped.
+    DPGO_TRY(polar(e, c, Xc, Vc, 1.0 - e->alpha, e->alpha, Yc, nullptr, Xc));
+    if (restart) {  // restartNesterovAcceleration(false): X = XPrev, V = Y = X
       DPGO_TRY(copy_poses(e, e->X.p, e->Xprev.p, color_first_pose(e, c), color_num_poses(e, c)));
       DPGO_TRY(copy_poses(e, e->V.p, e->X.p, color_first_pose(e, c), color_num_poses(e, c)));
       DPGO_TRY(copy_poses(e, e->Y.p, e->X.p, color_first_pose(e, c), color_num_poses(e, c)));

@@ -81,6 +81,7 @@ _SIGS = [
     ("dpgo_hip_optimize_dev", [C.c_void_p, C.POINTER(OptParams), C.c_void_p, C.c_void_p, _ip,
                                C.POINTER(OptResult)], C.c_int),
     ("dpgo_hip_synchronize", [C.c_void_p], C.c_int),
+    ("dpgo_hip_set_tuning", [C.c_int, C.c_int], C.c_int),
     ("dpgo_hip_spmm_bytes", [C.c_void_p], C.c_double),
     ("dpgo_hip_bench_spmm", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, _dp], C.c_int),
 ]
@@ -94,6 +95,13 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise DPGOHipError(f"{LIB_PATH} not built: run __graft_entry__.build() (no CPU fallback)")
+        # torch-ROCm bundles its own libamdhip64 (SONAME libamdhip64.so.7, NEEDED as
+        # "libamdhip64.so").  Load torch first so our NEEDED libamdhip64.so.7 binds to that same
+        # runtime; loading ours first would put two HIP runtimes in one process.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, args, res in _SIGS:
             fn = getattr(L, name)
@@ -120,6 +128,10 @@ def _i32(a):
 
 def device_count() -> int:
     return int(lib().dpgo_hip_device_count())
+
+
+def set_tuning(key: int, value: int):
+    _check(lib().dpgo_hip_set_tuning(int(key), int(value)))
 
 
 def default_params(**kw) -> OptParams:

@@ -162,6 +162,10 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
 int dpgo_hip_synchronize(dpgo_hip_problem h);
 
 /* ---- measurement helpers ----------------------------------------------------------------*/
+/* Select a compiled kernel variant for A/B timing (key 0: X.Q SpMM neighbour-loop variant
+ * 0 = 1 neighbour/step (default), 1 = same with non-temporal block loads, 2 = 2 neighbours/step,
+ * 3 = 4 neighbours/step, 4 = 4 + XCD-aware tile remap, 5 = 2 + XCD remap). */
+int dpgo_hip_set_tuning(int key, int value);
 /* Algorithmic HBM bytes of one X.Q SpMM over this handle (BSR blocks + indices + X + Y). */
 double dpgo_hip_spmm_bytes(dpgo_hip_problem h);
 /* Time `reps` back-to-back X.Q SpMM launches with HIP events on the handle's stream; returns the
