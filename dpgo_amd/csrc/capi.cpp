@@ -15,6 +15,7 @@
 #include <string>
 #include <vector>
 
+#include "graph_internal.h"
 #include "problem_internal.h"
 
 using dpgo::AgentState;
@@ -66,10 +67,108 @@ dpgo::LaunchCtx make_ctx(dpgo_hip_problem h, int flag_kind, double* partials) {
 
 namespace {
 
-dpgo::QView qview(dpgo_hip_problem h) { return dpgo::QView{h->rowptr.p, h->col.p, h->blocks.p}; }
+dpgo::QView qview(dpgo_hip_problem h) {
+  return dpgo::QView{h->rowptr.p, h->col.p, h->blocks.p, h->inc_ptr.p, h->inc.p, h->rec.p, h->diag.p, h->rec_first.p, h->fmt};
+}
 
 int check_handle(dpgo_hip_problem h) {
   if (!h) return fail(DPGO_HIP_EINVAL, "null problem handle");
+  return DPGO_HIP_OK;
+}
+
+// Edge-stream Q: per edge M = T Omega (rows padded to 4), per pose the packed diagonal block
+// (sum of T Omega T^T over outgoing and Omega over incoming edges, shared edges included, in edge
+// order with the same arithmetic as the BSR assembly), and the pose -> incident-edge lists of the
+// edges with both endpoints in the batch.
+// Edge ids follow first-visit order (poses ascending; an edge is first visited by its lower
+// endpoint), so rec_first[j] = first id first-visited by pose j and a tile of poses [j0, j1) owns
+// the contiguous record range [rec_first[j0], rec_first[j1]) that the SpMM streams into LDS.  Each
+// pose lists its incidences by ascending id: second visits (ids below the tile's range: read
+// through L2) come before first visits.
+int sync_q_edges(dpgo_hip_problem h) {
+  const int d = h->d, b = h->b, RW = dpgo::edge_rec_width(d), DW = dpgo::diag_width(d);
+  long m = 0;
+  for (int a = 0; a < h->K; ++a) m += static_cast<long>(h->e_agent[a].p1.size());
+  if (2 * m + 1 >= (1L << 31)) return fail(DPGO_HIP_EINVAL, "too many edges for int32 indices");
+  // batch-global endpoints per edge (-1: outside the batch)
+  std::vector<int> gp1(std::max<long>(m, 1)), gp2(std::max<long>(m, 1));
+  std::vector<double> rec0(std::max<long>(m, 1) * RW, 0.0), full(static_cast<size_t>(h->N) * b * b, 0.0);
+  double Wii[16], Wjj[16], Wij[16], Wji[16];
+  {
+    long eg = 0;
+    for (int a = 0; a < h->K; ++a) {
+      const HostEdges& E = h->e_agent[a];
+      const long off = h->pose_off[a];
+      for (size_t e = 0; e < E.p1.size(); ++e, ++eg) {
+        const int i = E.p1[e] >= 0 ? static_cast<int>(off + E.p1[e]) : -1;
+        const int j = E.p2[e] >= 0 ? static_cast<int>(off + E.p2[e]) : -1;
+        gp1[eg] = i;
+        gp2[eg] = j;
+        dpgo::edge_blocks(d, &E.R[e * d * d], &E.t[e * d], E.kw[e], E.tw[e], 1.0, Wii, Wjj, Wij, Wji);
+        double* M = &rec0[eg * RW];
+        for (int u = 0; u < b; ++u)
+          for (int v = 0; v < b; ++v) M[4 * u + v] = -Wij[v * b + u];  // Wij = -(T Omega), column-major
+        if (i >= 0)
+          for (int x = 0; x < b * b; ++x) full[static_cast<size_t>(i) * b * b + x] += Wii[x];
+        if (j >= 0)
+          for (int x = 0; x < b * b; ++x) full[static_cast<size_t>(j) * b * b + x] += Wjj[x];
+      }
+    }
+  }
+  // first-visit numbering: the lower endpoint visits first; ties impossible (no self-loops)
+  std::vector<int> deg(h->N + 1, 0), lowcnt(h->N + 1, 0);
+  for (long e = 0; e < m; ++e)
+    if (gp1[e] >= 0 && gp2[e] >= 0) {
+      ++deg[gp1[e] + 1];
+      ++deg[gp2[e] + 1];
+      ++lowcnt[std::min(gp1[e], gp2[e]) + 1];
+    }
+  for (long j = 0; j < h->N; ++j) {
+    deg[j + 1] += deg[j];
+    lowcnt[j + 1] += lowcnt[j];
+  }
+  std::vector<int> newid(std::max<long>(m, 1), -1), nfill(lowcnt.begin(), lowcnt.end() - 1);
+  for (long e = 0; e < m; ++e)
+    if (gp1[e] >= 0 && gp2[e] >= 0) newid[e] = nfill[std::min(gp1[e], gp2[e])]++;
+  int next = lowcnt[h->N];
+  for (long e = 0; e < m; ++e)
+    if (newid[e] < 0) newid[e] = next++;  // shared edges: diagonal only, never visited
+  std::vector<double> rec(rec0.size());
+  for (long e = 0; e < m; ++e)
+    std::memcpy(&rec[static_cast<size_t>(newid[e]) * RW], &rec0[e * RW], sizeof(double) * RW);
+  std::vector<int2> inc(std::max(deg[h->N], 1));
+  std::vector<int> fill(deg.begin(), deg.end() - 1);
+  for (long e = 0; e < m; ++e)
+    if (gp1[e] >= 0 && gp2[e] >= 0) {
+      inc[fill[gp1[e]]++] = make_int2(2 * newid[e] + 1, gp2[e]);  // outgoing at p1
+      inc[fill[gp2[e]]++] = make_int2(2 * newid[e], gp1[e]);      // incoming at p2
+    }
+  for (long j = 0; j < h->N; ++j)
+    std::sort(inc.begin() + deg[j], inc.begin() + deg[j + 1], [](const int2& x, const int2& y) { return x.x < y.x; });
+  std::vector<double> diag(static_cast<size_t>(h->N) * DW);
+  for (long p = 0; p < h->N; ++p) {
+    int o = 0;
+    for (int u = 0; u < b; ++u)
+      for (int v = u; v < b; ++v) diag[p * DW + o++] = full[static_cast<size_t>(p) * b * b + v * b + u];
+  }
+  h->nnz_inc = deg[h->N];
+  h->num_edges = m;
+  HIP_TRY(h->inc_ptr.ensure(h->N + 1));
+  HIP_TRY(h->rec_first.ensure(h->N + 1));
+  HIP_TRY(h->inc.ensure(inc.size()));
+  HIP_TRY(h->rec.ensure(rec.size()));
+  HIP_TRY(h->diag.ensure(std::max<size_t>(diag.size(), 1)));
+  HIP_TRY(h->minv.ensure(static_cast<size_t>(h->N) * b * b));
+  HIP_TRY(hipMemcpyAsync(h->inc_ptr.p, deg.data(), sizeof(int) * (h->N + 1), hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(h->rec_first.p, lowcnt.data(), sizeof(int) * (h->N + 1), hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(h->inc.p, inc.data(), sizeof(int2) * inc.size(), hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(h->rec.p, rec.data(), sizeof(double) * rec.size(), hipMemcpyHostToDevice, h->stream));
+  if (!diag.empty())
+    HIP_TRY(hipMemcpyAsync(h->diag.p, diag.data(), sizeof(double) * diag.size(), hipMemcpyHostToDevice, h->stream));
+  h->fmt = dpgo::QFMT_EDGES;
+  HIP_TRY(dpgo::launch_bj_inverse_diag(b, static_cast<int>(h->N), qview(h), 0.1, h->minv.p, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  h->q_dirty = false;
   return DPGO_HIP_OK;
 }
 
@@ -77,6 +176,10 @@ int check_handle(dpgo_hip_problem h) {
 // block-Jacobi inverses (QuadraticProblem::setQ, src/QuadraticProblem.cpp:31-42).
 int sync_q(dpgo_hip_problem h) {
   if (!h->q_dirty) return DPGO_HIP_OK;
+  const int f0 = h->q_fmt[0];
+  for (int a = 1; a < h->K; ++a)
+    if (h->q_fmt[a] != f0) return fail(DPGO_HIP_ESTATE, "agents of one handle mix BSR and edge-stream Q");
+  if (f0 == dpgo::QFMT_EDGES) return sync_q_edges(h);
   const int b = h->b;
   long nnz = 0;
   for (int a = 0; a < h->K; ++a) nnz += static_cast<long>(h->q_agent[a].col.size());
@@ -106,6 +209,7 @@ int sync_q(dpgo_hip_problem h) {
   HIP_TRY(hipMemcpyAsync(h->rowptr.p, rowptr.data(), sizeof(int) * rowptr.size(), hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipMemcpyAsync(h->col.p, col.data(), sizeof(int) * col.size(), hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipMemcpyAsync(h->blocks.p, blocks.data(), sizeof(double) * blocks.size(), hipMemcpyHostToDevice, h->stream));
+  h->fmt = dpgo::QFMT_BSR;
   HIP_TRY(dpgo::launch_bj_inverse(b, static_cast<int>(h->N), qview(h), 0.1, h->minv.p, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
   h->q_dirty = false;
@@ -337,6 +441,8 @@ int dpgo_hip_problem_create_batch(int num_agents, const int* poses_per_agent, in
   }
   h->num_tiles = static_cast<int>(h->h_tile_agent.size());
   h->q_agent.resize(num_agents);
+  h->e_agent.resize(num_agents);
+  h->q_fmt.assign(num_agents, dpgo::QFMT_BSR);
   h->g_agent.resize(num_agents);
   auto cleanup = [&](int rc) {
     delete h;
@@ -427,6 +533,39 @@ int dpgo_hip_set_Q_bsr(dpgo_hip_problem h, int agent, int nbrows, const int* bro
     if (q.col[k] < 0 || q.col[k] >= nbrows) return fail(DPGO_HIP_EINVAL, "block column out of range");
   q.blocks.assign(blocks, blocks + static_cast<size_t>(nnz) * h->b * h->b);
   h->q_agent[agent] = std::move(q);
+  h->e_agent[agent] = HostEdges();
+  h->q_fmt[agent] = dpgo::QFMT_BSR;
+  h->q_dirty = true;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_set_Q_edges(dpgo_hip_problem h, int agent, int m, const int* p1, const int* p2, const double* R,
+                         const double* t, const double* kappa, const double* tau, const double* weight) {
+  DPGO_TRY(check_handle(h));
+  if (agent < 0 || agent >= h->K) return fail(DPGO_HIP_EINVAL, "agent out of range");
+  if (m < 0 || (m > 0 && (!p1 || !p2 || !R || !t || !kappa || !tau)))
+    return fail(DPGO_HIP_EINVAL, "null edge array");
+  const int d = h->d, na = h->n_agent[agent];
+  HostEdges E;
+  E.p1.assign(p1, p1 + m);
+  E.p2.assign(p2, p2 + m);
+  E.R.assign(R, R + static_cast<size_t>(m) * d * d);
+  E.t.assign(t, t + static_cast<size_t>(m) * d);
+  E.kw.resize(m);
+  E.tw.resize(m);
+  for (int e = 0; e < m; ++e) {
+    const int i = p1[e], j = p2[e];
+    if (i < -1 || i >= na || j < -1 || j >= na) return fail(DPGO_HIP_EINVAL, "edge endpoint out of range");
+    if (i < 0 && j < 0) return fail(DPGO_HIP_EINVAL, "edge has no endpoint in the agent");
+    if (i == j) return fail(DPGO_HIP_EINVAL, "self-loop edge");
+    const double w = weight ? weight[e] : 1.0;
+    E.kw[e] = w * kappa[e];  // the BSR assembly's Omega = diag(w kappa, w tau) (edge_blocks)
+    E.tw[e] = w * tau[e];
+  }
+  h->e_agent[agent] = std::move(E);
+  h->q_agent[agent] = HostBSR();
+  h->q_agent[agent].rowptr.assign(na + 1, 0);
+  h->q_fmt[agent] = dpgo::QFMT_EDGES;
   h->q_dirty = true;
   return DPGO_HIP_OK;
 }
@@ -876,6 +1015,18 @@ int dpgo_hip_project_polar(int r, int d, int n, const double* in, double* out) {
 double dpgo_hip_spmm_bytes(dpgo_hip_problem h) {
   if (!h) return 0.0;
   const double b = h->b;
+  if (h->q_fmt[0] == dpgo::QFMT_EDGES) {
+    // every edge record once + 8 B per incidence + row pointers + packed diagonal + X once + Y once
+    long m = 0, inc = 0;
+    for (int a = 0; a < h->K; ++a) {
+      const HostEdges& E = h->e_agent[a];
+      m += static_cast<long>(E.p1.size());
+      for (size_t e = 0; e < E.p1.size(); ++e) inc += (E.p1[e] >= 0 && E.p2[e] >= 0) ? 2 : 0;
+    }
+    return static_cast<double>(m) * dpgo::edge_rec_width(h->d) * 8.0 + static_cast<double>(inc) * 8.0 +
+           static_cast<double>(h->N + 1) * 4.0 + static_cast<double>(h->N) * dpgo::diag_width(h->d) * 8.0 +
+           2.0 * static_cast<double>(h->r) * b * static_cast<double>(h->N) * 8.0;
+  }
   long nnz = 0;
   for (int a = 0; a < h->K; ++a) nnz += static_cast<long>(h->q_agent[a].col.size());
   return static_cast<double>(nnz) * (b * b * 8.0 + 4.0) + static_cast<double>(h->N + 1) * 4.0 +

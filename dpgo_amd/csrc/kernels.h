@@ -35,11 +35,32 @@ struct LaunchCtx {
   hipStream_t stream;
 };
 
-// Block-sparse (BSR) symmetric Q over the concatenated poses of all agents in the batch.
+enum QFormat { QFMT_BSR = 0, QFMT_EDGES = 1 };
+
+// Edge record: M = T Omega (b x b, T = [R t; 0 1], Omega = diag(w kappa I_d, w tau)) with rows
+// padded to 4 doubles, so Q_{p1 p2} = -M and Q_{p2 p1} = -M^T are read straight from it.
+__host__ __device__ constexpr int edge_rec_width(int d) { return 4 * (d + 1); }
+// Packed symmetric diagonal block Q_jj (upper triangle, row-major): b (b + 1) / 2 doubles per pose.
+__host__ __device__ constexpr int diag_width(int d) { return (d + 1) * (d + 2) / 2; }
+
+// The symmetric Q over the concatenated poses of all agents in the batch, in one of two forms:
+//  QFMT_BSR    block-sparse rows: any symmetric Q (QuadraticProblem::setQ).
+//  QFMT_EDGES  the measurement stream Q = A Omega A^T is built from (src/DPGO_utils.cpp:214-286,
+//              src/PGOAgent.cpp:720-781), never materialised as blocks: each edge's M = T Omega is
+//              stored ONCE (both off-diagonal blocks are -M and -M^T) and every pose keeps its packed
+//              diagonal block.  inc[k] = {2 * edge + (j == p1), other endpoint} lists the edges with
+//              both endpoints in the batch (shared edges only feed the diagonal); edge ids follow
+//              first-visit order so a tile's first-visit records are one contiguous range.
 struct QView {
-  const int* rowptr;      // [n + 1]
-  const int* col;         // [nnzb] global pose index
-  const double* blocks;   // [nnzb * b * b], block (j, col) column-major
+  const int* rowptr;      // BSR [n + 1]
+  const int* col;         // BSR [nnzb] global pose index
+  const double* blocks;   // BSR [nnzb * b * b], block (j, col) column-major
+  const int* inc_ptr;     // EDGES [n + 1]
+  const int2* inc;        // EDGES [nnz_inc]
+  const double* rec;      // EDGES [m * edge_rec_width(d)]
+  const double* diag;     // EDGES [n * diag_width(d)]
+  const int* rec_first;   // EDGES [n + 1] first edge id first-visited by pose j (ids in visit order)
+  int fmt;                // QFormat
 };
 
 struct OptScalars {
@@ -77,7 +98,10 @@ struct GEdges {
 };
 
 // Runtime-selectable kernel variants (A/B tuning in one process; see tools/spmm_ab.py).
-enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_COUNT = 4 };
+enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_COUNT = 4 };
+// variant of the edge-stream SpMM used unless TUNE_EDGE_VARIANT overrides it (bit 0: XCD-aware
+// tile remap; v >> 1: minimum waves per SIMD the register allocation must allow, none/4/5/6)
+constexpr int kEdgeDefaultVariant = 1;
 extern int g_tuning[TUNE_COUNT];
 
 bool supported_rb(int r, int b);
@@ -108,5 +132,6 @@ hipError_t launch_accept(int r, int b, const LaunchCtx& c, const double* x2, con
                          double* x1, double* g, double* S);
 hipError_t launch_finalize(const FinalizeArgs& f, int num_agents, hipStream_t stream);
 hipError_t launch_bj_inverse(int b, int n, const QView& q, double shift, double* Minv, hipStream_t stream);
+hipError_t launch_bj_inverse_diag(int b, int n, const QView& q, double shift, double* Minv, hipStream_t stream);
 
 }  // namespace dpgo

@@ -166,13 +166,132 @@ __device__ __forceinline__ void spmm_accumulate(const QView& q, const double* __
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Edge-stream form of the same product (QFMT_EDGES).  For an edge e = (p1 -> p2) with
+// T = [R t; 0 1], Omega = diag(k I_d, tau) and M = T Omega (src/DPGO_utils.cpp:214-286):
+//   Q_{p1 p2} = -M,  Q_{p2 p1} = -M^T,  Q_{p1 p1} += T Omega T^T,  Q_{p2 p2} += Omega.
+// Lane k of pose j's quad needs row k of the block (other, j):
+//   j == p2 (incoming): block (p1, p2) = -M    -> row k of M     (offsets 4k + c)
+//   j == p1 (outgoing): block (p2, p1) = -M^T  -> column k of M  (offsets 4c + k)
+// so every lane issues the same four scalar loads with a per-incidence stride and the loop has no
+// cross-lane traffic, no selects and no divergence.  The diagonal blocks are read once per pose.
+// ------------------------------------------------------------------------------------------
+
+// Per tile, the incidence entries and the records of the edges first visited by the tile (one
+// contiguous id range, see QView) are staged in LDS with wide coalesced loads: the record stream
+// leaves HBM at full occupancy-independent MLP instead of one dependent miss per incidence.
+// Tiles whose lists do not fit fall back to global loads.
+constexpr int kIncStage = 512;
+template <int D>
+constexpr int rec_stage() { return D == 3 ? 200 : 256; }
+
+// packed upper-triangle index of (u, v) in a symmetric B x B block
+template <int B>
+__host__ __device__ constexpr int sym_index(int u, int v) {
+  return u <= v ? u * B - u * (u - 1) / 2 + (v - u) : v * B - v * (v - 1) / 2 + (u - v);
+}
+
+// acc (lane k: X_i[:,k] (x) Q_ij[k,:]) over incidences [z0, z1) of one pose.  Two register sets
+// ping-pong so the record row/column + X column of incidence z+1 are in flight while incidence z
+// is consumed; every load is unconditional (the index is clamped) so the compiler waits only for
+// the stage it consumes.  INC_LDS: entries from the LDS stage (ds_read: waiting for them never
+// drains in-flight global loads).  REC_LDS: records from the LDS stage (id - e0), else global.
+template <int R, int B, bool INC_LDS, bool REC_LDS>
+__device__ __forceinline__ void edge_loop(const QView& q, const double* __restrict__ in, int kc, int z0, int z1,
+                                          const int2* s_inc, int i0, const double* s_rec, int e0,
+                                          double (&acc)[R][B]) {
+  constexpr int RW = edge_rec_width(B - 1);
+  struct Stage {
+    double m[B];
+    double x[R];
+  };
+  auto fetch = [&](int z, Stage& st) {
+    int2 ie;
+    if constexpr (INC_LDS)
+      ie = s_inc[z - i0];
+    else
+      ie = q.inc[z];
+    const bool outg = (ie.x & 1) != 0;
+    const int off = outg ? kc : 4 * kc;  // column kc of M (outgoing) / row kc (incoming)
+    const int stride = outg ? 4 : 1;
+    const double* mr;
+    if constexpr (REC_LDS)
+      mr = s_rec + ((ie.x >> 1) - e0) * RW + off;
+    else
+      mr = q.rec + static_cast<long>(ie.x >> 1) * RW + off;
+#pragma unroll
+    for (int c = 0; c < B; ++c) st.m[c] = mr[c * stride];
+    const double* xk = in + static_cast<long>(ie.y) * (R * B) + kc * R;
+#pragma unroll
+    for (int a = 0; a < R; ++a) st.x[a] = xk[a];
+  };
+  auto consume = [&](const Stage& st) {
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int c = 0; c < B; ++c) acc[a][c] = fma(-st.x[a], st.m[c], acc[a][c]);
+  };
+  if (z0 >= z1) return;
+  Stage sa, sb;
+  fetch(z0, sa);
+  for (int nz = z0; nz < z1; nz += 2) {
+    fetch(min(nz + 1, z1 - 1), sb);
+    consume(sa);
+    if (nz + 1 >= z1) break;
+    fetch(min(nz + 2, z1 - 1), sa);
+    consume(sb);
+  }
+}
+
+// Block row j of X.Q for the edge-stream form: off-diagonal incidences (second visits through
+// L2 first, then first visits from the LDS stage), then + X_j[:,k] (x) Q_jj[k,:].  The whole quad
+// runs together; lane 3 of a d = 2 quad mirrors lane 0 and its acc is dropped.
+template <int R, int B, bool STAGED>
+__device__ __forceinline__ void spmm_accumulate_edges(const QView& q, const double* __restrict__ in, long j,
+                                                      int k, int beg, int end, const int2* s_inc, int i0,
+                                                      const double* s_rec, int e0, double (&acc)[R][B]) {
+  constexpr int DW = diag_width(B - 1);
+  const int kc = k < B ? k : 0;
+  if constexpr (STAGED) {
+    int mid = beg;  // ids ascend: the second visits (ids below the tile's range) come first
+    while (mid < end && (s_inc[mid - i0].x >> 1) < e0) ++mid;
+    edge_loop<R, B, true, false>(q, in, kc, beg, mid, s_inc, i0, s_rec, e0, acc);
+    edge_loop<R, B, true, true>(q, in, kc, mid, end, s_inc, i0, s_rec, e0, acc);
+  } else {
+    edge_loop<R, B, false, false>(q, in, kc, beg, end, s_inc, i0, s_rec, e0, acc);
+  }
+  double xj[R], dk[B];
+  const double* pj = in + j * (R * B) + kc * R;
+#pragma unroll
+  for (int a = 0; a < R; ++a) xj[a] = pj[a];
+  const double* dj = q.diag + j * DW;
+#pragma unroll
+  for (int c = 0; c < B; ++c) {
+    int o = sym_index<B>(0, c);
+    if (kc == 1) o = sym_index<B>(1, c);
+    if (kc == 2) o = sym_index<B>(2, c);
+    if (B > 3 && kc == 3) o = sym_index<B>(B > 3 ? 3 : 0, c);
+    dk[c] = dj[o];
+  }
+  const bool act = k < B;
+#pragma unroll
+  for (int a = 0; a < R; ++a)
+#pragma unroll
+    for (int c = 0; c < B; ++c) acc[a][c] = act ? fma(xj[a], dk[c], acc[a][c]) : 0.0;
+}
+
 // SpMM variants: neighbours per step, non-temporal block loads, XCD tile remap
 constexpr int var_unr(int v) { return v == 2 || v == 5 ? 2 : (v == 3 || v == 4) ? 4 : 1; }
 constexpr bool var_nt(int v) { return v == 1; }  // default-policy loads measured faster (tools/spmm_ab.py)
-constexpr bool var_xcd(int v) { return v == 4 || v == 5; }
+constexpr bool var_xcd(int v) { return v == 4 || v == 5 || v == 6; }
+// edge-stream variants: bit 0 = XCD-aware tile remap, v >> 1 = register budget (minimum waves per
+// SIMD requested from the compiler: 0 -> none, 1 -> 4, 2 -> 5, 3 -> 6)
+constexpr bool evar_xcd(int v) { return (v & 1) != 0; }
+constexpr int evar_waves(int v) { return (v >> 1) == 0 ? 1 : 3 + (v >> 1); }
 
-template <int R, int B, int MODE, int VAR = 0>
-__global__ __launch_bounds__(kThreads) void k_spmm(LaunchCtx c, QView q, const double* __restrict__ in,
+
+template <int R, int B, int MODE, int VAR = 0, int FMT = QFMT_BSR>
+__global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) void k_spmm(LaunchCtx c, QView q, const double* __restrict__ in,
                                                    const int* __restrict__ gidx,
                                                    const double* __restrict__ gblk,
                                                    const double* __restrict__ X,
@@ -180,7 +299,7 @@ __global__ __launch_bounds__(kThreads) void k_spmm(LaunchCtx c, QView q, const d
                                                    double* __restrict__ out,
                                                    double* __restrict__ S_out) {
   constexpr int D = B - 1;
-  const PoseLane p = pose_lane<B, var_xcd(VAR)>(c);
+  const PoseLane p = pose_lane<B, FMT == QFMT_EDGES ? evar_xcd(VAR) : var_xcd(VAR)>(c);
   if (tile_skipped(c, p.agent)) return;
 
   double acc[R][B];
@@ -189,7 +308,36 @@ __global__ __launch_bounds__(kThreads) void k_spmm(LaunchCtx c, QView q, const d
 #pragma unroll
     for (int cc = 0; cc < B; ++cc) acc[a][cc] = 0.0;
 
-  if (p.ok && p.k < B) spmm_accumulate<R, B, var_unr(VAR), var_nt(VAR)>(q, in, p.j, p.k, acc);
+  if constexpr (FMT == QFMT_EDGES) {
+    constexpr int RW = edge_rec_width(B - 1), NREC = rec_stage<B - 1>();
+    __shared__ int2 s_inc[kIncStage];
+    __shared__ int s_ptr[kTilePoses + 1];
+    __shared__ int s_e[2];
+    __shared__ f64x2 s_rec2[NREC * RW / 2];
+    const int t0 = c.tile_start[p.tile], cnt = c.tile_count[p.tile];
+    if (static_cast<int>(threadIdx.x) <= cnt) s_ptr[threadIdx.x] = q.inc_ptr[t0 + threadIdx.x];
+    if (threadIdx.x < 2) s_e[threadIdx.x] = q.rec_first[t0 + (threadIdx.x ? cnt : 0)];
+    __syncthreads();
+    const int i0 = s_ptr[0], ni = s_ptr[cnt] - i0, e0 = s_e[0], ne = s_e[1] - e0;
+    const bool staged = ni <= kIncStage && ne <= NREC;
+    if (staged) {
+      for (int x = threadIdx.x; x < ni; x += kThreads) s_inc[x] = q.inc[i0 + x];
+      const f64x2* src = reinterpret_cast<const f64x2*>(q.rec) + static_cast<long>(e0) * (RW / 2);
+      for (int x = threadIdx.x; x < ne * (RW / 2); x += kThreads) s_rec2[x] = src[x];
+    }
+    __syncthreads();
+    if (p.ok) {
+      const double* s_rec = reinterpret_cast<const double*>(s_rec2);
+      if (staged)
+        spmm_accumulate_edges<R, B, true>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc, i0, s_rec, e0,
+                                          acc);
+      else
+        spmm_accumulate_edges<R, B, false>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc, i0, s_rec, e0,
+                                           acc);
+    }
+  } else {
+    if (p.ok && p.k < B) spmm_accumulate<R, B, var_unr(VAR), var_nt(VAR)>(q, in, p.j, p.k, acc);
+  }
 #pragma unroll
   for (int a = 0; a < R; ++a)
 #pragma unroll
@@ -797,30 +945,11 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
   }
 }
 
-// --- block-Jacobi inverse of (Q_jj + shift I), computed on device from the BSR diagonal ---
+// --- block-Jacobi inverse of (Q_jj + shift I), computed on device from Q's diagonal blocks ---
+// In place on A = [M | I] (B x 2B): Gauss-Jordan with partial pivoting (SPD, so pivoting is a
+// safety net); on return the right half holds M^-1.
 template <int B>
-__global__ __launch_bounds__(kThreads) void k_bj_inverse(int n, QView q, double shift,
-                                                         double* __restrict__ Minv) {
-  const long j = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  double A[B][2 * B];
-#pragma unroll
-  for (int u = 0; u < B; ++u)
-#pragma unroll
-    for (int w = 0; w < 2 * B; ++w) A[u][w] = (w - B == u) ? 1.0 : 0.0;
-  const int beg = q.rowptr[j], end = q.rowptr[j + 1];
-  for (int nz = beg; nz < end; ++nz) {
-    if (q.col[nz] == j) {
-      // block (j,j) column-major: element (u,w) at w*B + u
-#pragma unroll
-      for (int u = 0; u < B; ++u)
-#pragma unroll
-        for (int w = 0; w < B; ++w) A[u][w] += q.blocks[static_cast<long>(nz) * B * B + w * B + u];
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < B; ++u) A[u][u] += shift;
-  // Gauss-Jordan with partial pivoting (SPD, so pivoting is a safety net)
+__device__ __forceinline__ void gauss_jordan(double (&A)[B][2 * B]) {
 #pragma unroll
   for (int col = 0; col < B; ++col) {
     int piv = col;
@@ -854,6 +983,53 @@ __global__ __launch_bounds__(kThreads) void k_bj_inverse(int n, QView q, double 
       }
     }
   }
+}
+
+template <int B>
+__global__ __launch_bounds__(kThreads) void k_bj_inverse(int n, QView q, double shift,
+                                                         double* __restrict__ Minv) {
+  const long j = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  double A[B][2 * B];
+#pragma unroll
+  for (int u = 0; u < B; ++u)
+#pragma unroll
+    for (int w = 0; w < 2 * B; ++w) A[u][w] = (w - B == u) ? 1.0 : 0.0;
+  const int beg = q.rowptr[j], end = q.rowptr[j + 1];
+  for (int nz = beg; nz < end; ++nz) {
+    if (q.col[nz] == j) {
+      // block (j,j) column-major: element (u,w) at w*B + u
+#pragma unroll
+      for (int u = 0; u < B; ++u)
+#pragma unroll
+        for (int w = 0; w < B; ++w) A[u][w] += q.blocks[static_cast<long>(nz) * B * B + w * B + u];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < B; ++u) A[u][u] += shift;
+  gauss_jordan<B>(A);
+#pragma unroll
+  for (int u = 0; u < B; ++u)
+#pragma unroll
+    for (int w = 0; w < B; ++w) Minv[j * (B * B) + u * B + w] = A[u][B + w];
+}
+
+// Same from the packed diagonal blocks of an edge-stream Q (one thread per pose).
+template <int B>
+__global__ __launch_bounds__(kThreads) void k_bj_inverse_diag(int n, QView q, double shift,
+                                                              double* __restrict__ Minv) {
+  constexpr int DW = diag_width(B - 1);
+  const long j = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  double A[B][2 * B];
+#pragma unroll
+  for (int u = 0; u < B; ++u)
+#pragma unroll
+    for (int w = 0; w < B; ++w) {
+      A[u][w] = q.diag[j * DW + sym_index<B>(u, w)] + (u == w ? shift : 0.0);
+      A[u][B + w] = (u == w) ? 1.0 : 0.0;
+    }
+  gauss_jordan<B>(A);
 #pragma unroll
   for (int u = 0; u < B; ++u)
 #pragma unroll
@@ -949,7 +1125,7 @@ __global__ __launch_bounds__(kThreads) void k_assemble_G(GEdges e, int nslots, c
     default: return hipErrorInvalidValue;                  \
   }
 
-int g_tuning[TUNE_COUNT] = {0};
+int g_tuning[TUNE_COUNT] = {0, -1, 0, 0};
 
 bool supported_rb(int r, int b) {
   if (b == 3) return r >= 2 && r <= 8;
@@ -957,45 +1133,60 @@ bool supported_rb(int r, int b) {
   return false;
 }
 
+namespace {
+
+template <int MODE, int VAR, int FMT>
+hipError_t spmm_rb(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const double* in, const int* gidx,
+                   const double* gblk, const double* X, const double* S_in, double* out, double* S_out) {
+  DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE, VAR, FMT><<<grid, kThreads, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
+  return hipSuccess;
+}
+
+// r = 5, d = 3 (the headline shape) only: every compiled neighbour-loop variant, for A/B timing
+template <int MODE, int FMT>
+hipError_t spmm_variant54(int var, dim3 grid, const LaunchCtx& c, const QView& q, const double* in, const int* gidx,
+                          const double* gblk, const double* X, const double* S_in, double* out, double* S_out) {
+#define DPGO_VAR(V) \
+  case V: k_spmm<5, 4, MODE, V, FMT><<<grid, kThreads, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out); break;
+  switch (var) {
+    DPGO_VAR(0) DPGO_VAR(1) DPGO_VAR(2) DPGO_VAR(3) DPGO_VAR(4) DPGO_VAR(5) DPGO_VAR(6) DPGO_VAR(7)
+    default: return hipErrorInvalidValue;
+  }
+#undef DPGO_VAR
+  return hipSuccess;
+}
+
+template <int MODE>
+hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const double* in, const int* gidx,
+                     const double* gblk, const double* X, const double* S_in, double* out, double* S_out) {
+  if (q.fmt == QFMT_EDGES) {
+    const int var = g_tuning[TUNE_EDGE_VARIANT] < 0 ? kEdgeDefaultVariant : g_tuning[TUNE_EDGE_VARIANT];
+    if (r == 5 && b == 4 && var != kEdgeDefaultVariant)
+      return spmm_variant54<MODE, QFMT_EDGES>(var, grid, c, q, in, gidx, gblk, X, S_in, out, S_out);
+    return spmm_rb<MODE, kEdgeDefaultVariant, QFMT_EDGES>(r, b, grid, c, q, in, gidx, gblk, X, S_in, out, S_out);
+  }
+  const int var = MODE == MODE_XQ ? g_tuning[TUNE_SPMM_VARIANT] : 0;
+  if (r == 5 && b == 4 && var != 0)
+    return spmm_variant54<MODE, QFMT_BSR>(var, grid, c, q, in, gidx, gblk, X, S_in, out, S_out);
+  return spmm_rb<MODE, 0, QFMT_BSR>(r, b, grid, c, q, in, gidx, gblk, X, S_in, out, S_out);
+}
+
+}  // namespace
+
 hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const QView& q, const double* in,
                        const int* gidx, const double* gblk, const double* X, const double* S_in,
                        double* out, double* S_out) {
   if (c.num_tiles == 0) return hipSuccess;
-  dim3 grid(c.num_tiles), block(kThreads);
+  const dim3 grid(c.num_tiles);
+  hipError_t e = hipErrorInvalidValue;
   switch (mode) {
-    case MODE_XQ:
-      switch (g_tuning[TUNE_SPMM_VARIANT]) {
-        case 1:
-          DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_XQ, 1><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
-          break;
-        case 2:
-          DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_XQ, 2><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
-          break;
-        case 3:
-          DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_XQ, 3><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
-          break;
-        case 4:
-          DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_XQ, 4><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
-          break;
-        case 5:
-          DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_XQ, 5><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
-          break;
-        default:
-          DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_XQ, 0><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
-      }
-      break;
-    case MODE_XQ_G:
-      DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_XQ_G><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
-      break;
-    case MODE_EVAL:
-      DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_EVAL><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
-      break;
-    case MODE_HESS:
-      DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE_HESS><<<grid, block, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
-      break;
-    default:
-      return hipErrorInvalidValue;
+    case MODE_XQ: e = spmm_mode<MODE_XQ>(r, b, grid, c, q, in, gidx, gblk, X, S_in, out, S_out); break;
+    case MODE_XQ_G: e = spmm_mode<MODE_XQ_G>(r, b, grid, c, q, in, gidx, gblk, X, S_in, out, S_out); break;
+    case MODE_EVAL: e = spmm_mode<MODE_EVAL>(r, b, grid, c, q, in, gidx, gblk, X, S_in, out, S_out); break;
+    case MODE_HESS: e = spmm_mode<MODE_HESS>(r, b, grid, c, q, in, gidx, gblk, X, S_in, out, S_out); break;
+    default: break;
   }
+  if (e != hipSuccess) return e;
   return hipGetLastError();
 }
 
@@ -1082,6 +1273,18 @@ hipError_t launch_assemble_G(int r, int b, const GEdges& e, int nslots, const do
 hipError_t launch_finalize(const FinalizeArgs& f, int num_agents, hipStream_t stream) {
   if (num_agents == 0) return hipSuccess;
   k_finalize<<<num_agents, kThreads, 0, stream>>>(f);
+  return hipGetLastError();
+}
+
+hipError_t launch_bj_inverse_diag(int b, int n, const QView& q, double shift, double* Minv, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const int blocks = (n + kThreads - 1) / kThreads;
+  if (b == 3)
+    k_bj_inverse_diag<3><<<blocks, kThreads, 0, stream>>>(n, q, shift, Minv);
+  else if (b == 4)
+    k_bj_inverse_diag<4><<<blocks, kThreads, 0, stream>>>(n, q, shift, Minv);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -33,6 +33,13 @@ struct HostBSR {
   std::vector<double> blocks;
 };
 
+// One agent's Q as its measurement stream (QFMT_EDGES): agent-local endpoints (-1 = the endpoint
+// lives in another agent), R (d*d row-major), t (d), and the weighted precisions w kappa, w tau.
+struct HostEdges {
+  std::vector<int> p1, p2;
+  std::vector<double> R, t, kw, tw;
+};
+
 template <typename T>
 struct DevBuf {
   T* p = nullptr;
@@ -71,10 +78,17 @@ struct dpgo_hip_problem_s {
 
   // Q (per-agent host copies, concatenated on upload)
   std::vector<dpgo::HostBSR> q_agent;
+  std::vector<dpgo::HostEdges> e_agent;
+  std::vector<int> q_fmt;  // per agent: QFMT_BSR / QFMT_EDGES
+  int fmt = 0;             // format of the uploaded Q (all agents agree)
   bool q_dirty = true;
   dpgo::DevBuf<int> rowptr, col;
   dpgo::DevBuf<double> blocks, minv;
   long nnzb = 0;
+  dpgo::DevBuf<int> inc_ptr, rec_first;
+  dpgo::DevBuf<int2> inc;
+  dpgo::DevBuf<double> rec, diag;
+  long nnz_inc = 0, num_edges = 0;
 
   // G (sparse pose blocks per agent)
   std::vector<std::map<int, std::vector<double>>> g_agent;

@@ -166,6 +166,7 @@ void dpgo_rbcd_default_params(dpgo_rbcd_params* p) {
   p->tolerance = 1e-2;
   p->precon = DPGO_PRECON_BLOCK_JACOBI;
   p->algorithm = DPGO_ALG_RTR;
+  p->q_format = DPGO_QFMT_EDGES;
 }
 
 int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, const int* agent_rank, int rank,
@@ -189,7 +190,7 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
   e->rank = rank;
   e->world = world;
   e->K = num_agents;
-  const int n = g->n, d = g->d, b = e->b;
+  const int n = g->n, d = g->d;
   const size_t m = g->p1.size();
   // local index of every pose inside its agent (global order)
   std::vector<int> local(n), agent_n(num_agents, 0);
@@ -311,35 +312,45 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
     std::vector<double> Rv, tv, kv, tauv, wv;
     for (int q = a0; q < a1; ++q) {
       const int A = e->owned[q];
-      BsrBuilder B(agent_n[A], b);
+      // Q_A as its measurement stream: private edges with both local endpoints, shared edges with
+      // the foreign endpoint set to -1 (diagonal terms only, :754-760 / :770-775)
       std::map<int, std::vector<size_t>> slots;  // local public pose -> shared edges
+      std::vector<int> ep1, ep2;
+      std::vector<double> eR, et, ek, etau;
       for (size_t k : agent_edges[q]) {
         const int i = g->p1[k], j = g->p2[k];
-        if (agent_of_pose[i] == A && agent_of_pose[j] == A) {
-          B.touch(local[i], local[j]);
-          B.touch(local[j], local[i]);
-        } else {
-          slots[agent_of_pose[i] == A ? local[i] : local[j]].push_back(k);
-        }
-      }
-      B.freeze();
-      double Wii[16], Wjj[16], Wij[16], Wji[16];
-      for (size_t k : agent_edges[q]) {
-        const int i = g->p1[k], j = g->p2[k];
-        edge_blocks(d, &g->R[k * d * d], &g->t[k * d], g->kappa[k], g->tau[k], 1.0, Wii, Wjj, Wij, Wji);
         const bool own_i = agent_of_pose[i] == A, own_j = agent_of_pose[j] == A;
-        if (own_i && own_j) {
-          B.add(local[i], local[i], Wii);
-          B.add(local[j], local[j], Wjj);
-          B.add(local[i], local[j], Wij);
-          B.add(local[j], local[i], Wji);
-        } else if (own_i) {
-          B.add(local[i], local[i], Wii);  // outgoing shared edge (:754-760)
-        } else {
-          B.add(local[j], local[j], Wjj);  // incoming shared edge (:770-775)
-        }
+        ep1.push_back(own_i ? local[i] : -1);
+        ep2.push_back(own_j ? local[j] : -1);
+        eR.insert(eR.end(), &g->R[k * d * d], &g->R[k * d * d] + d * d);
+        et.insert(et.end(), &g->t[k * d], &g->t[k * d] + d);
+        ek.push_back(g->kappa[k]);
+        etau.push_back(g->tau[k]);
+        if (!(own_i && own_j)) slots[own_i ? local[i] : local[j]].push_back(k);
       }
-      rc = dpgo_hip_set_Q_bsr(h, q - a0, agent_n[A], B.out.rowptr.data(), B.out.col.data(), B.out.blocks.data());
+      if (e->P.q_format == DPGO_QFMT_BSR) {  // explicit Q_A (BSR), as the reference materialises it
+        BsrBuilder B(agent_n[A], e->b);
+        for (size_t x = 0; x < ep1.size(); ++x)
+          if (ep1[x] >= 0 && ep2[x] >= 0) {
+            B.touch(ep1[x], ep2[x]);
+            B.touch(ep2[x], ep1[x]);
+          }
+        B.freeze();
+        double Wii[16], Wjj[16], Wij[16], Wji[16];
+        for (size_t x = 0; x < ep1.size(); ++x) {
+          edge_blocks(d, &eR[x * d * d], &et[x * d], ek[x], etau[x], 1.0, Wii, Wjj, Wij, Wji);
+          if (ep1[x] >= 0) B.add(ep1[x], ep1[x], Wii);
+          if (ep2[x] >= 0) B.add(ep2[x], ep2[x], Wjj);
+          if (ep1[x] >= 0 && ep2[x] >= 0) {
+            B.add(ep1[x], ep2[x], Wij);
+            B.add(ep2[x], ep1[x], Wji);
+          }
+        }
+        rc = dpgo_hip_set_Q_bsr(h, q - a0, agent_n[A], B.out.rowptr.data(), B.out.col.data(), B.out.blocks.data());
+      } else {
+        rc = dpgo_hip_set_Q_edges(h, q - a0, static_cast<int>(ep1.size()), ep1.data(), ep2.data(), eR.data(),
+                                  et.data(), ek.data(), etau.data(), nullptr);
+      }
       if (rc != DPGO_HIP_OK) return bail(rc);
       std::vector<int> gpose;
       for (auto& kv2 : slots) {

@@ -16,6 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdpgo_hip.so")
 
 PRECON_EXACT, PRECON_BLOCK_JACOBI, PRECON_NONE = 0, 1, 2
+QFMT_BSR, QFMT_EDGES = 0, 1
 ALG_RTR, ALG_RGD = 0, 1
 TCG_NAMES = {-1: "NONE", 0: "NEGCURVTURE", 1: "EXCREGION", 2: "LCON", 3: "SCON", 4: "MAXITER"}
 
@@ -59,6 +60,7 @@ _SIGS = [
     ("dpgo_hip_set_precon", [C.c_void_p, C.c_int], C.c_int),
     ("dpgo_hip_set_Q_csr", [C.c_void_p, C.c_int, C.c_int, _ip, _ip, _dp], C.c_int),
     ("dpgo_hip_set_Q_bsr", [C.c_void_p, C.c_int, C.c_int, _ip, _ip, _dp], C.c_int),
+    ("dpgo_hip_set_Q_edges", [C.c_void_p, C.c_int, C.c_int, _ip, _ip, _dp, _dp, _dp, _dp, _dp], C.c_int),
     ("dpgo_hip_set_G", [C.c_void_p, C.c_int, C.c_int, _ip, _dp], C.c_int),
     ("dpgo_hip_set_G_dense", [C.c_void_p, C.c_int, _dp], C.c_int),
     ("dpgo_hip_f", [C.c_void_p, _dp, _dp], C.c_int),
@@ -213,6 +215,20 @@ class Problem:
         Qb.sort_indices()
         self.set_Q_bsr(agent, Qb.indptr, Qb.indices, np.ascontiguousarray(Qb.data.transpose(0, 2, 1)))
 
+    def set_Q_edges(self, agent, p1, p2, R, t, kappa, tau, weight=None):
+        """Q of one agent from its measurements (agent-local endpoints, -1 = other agent)."""
+        a1, a1p = _i32(p1)
+        a2, a2p = _i32(p2)
+        Rr, Rp = _f64(np.asarray(R, dtype=np.float64).reshape(-1))
+        tt, tp = _f64(np.asarray(t, dtype=np.float64).reshape(-1))
+        kk, kp = _f64(kappa)
+        ta, tap = _f64(tau)
+        if weight is not None:
+            ww, wp = _f64(weight)
+        else:
+            wp = None
+        _check(lib().dpgo_hip_set_Q_edges(self.h, agent, len(a1), a1p, a2p, Rp, tp, kp, tap, wp))
+
     def set_G_dense(self, agent, G):
         """G: r x (b n_a) matrix."""
         g, gp = _f64(to_dev_layout(G))
@@ -349,7 +365,7 @@ def project_polar(M, d):
 class RbcdParams(C.Structure):
     _fields_ = [("r", C.c_int), ("acceleration", C.c_int), ("restart_interval", C.c_int),
                 ("max_inner", C.c_int), ("initial_radius", C.c_double), ("tolerance", C.c_double),
-                ("precon", C.c_int), ("algorithm", C.c_int)]
+                ("precon", C.c_int), ("algorithm", C.c_int), ("q_format", C.c_int)]
 
 
 _lp = C.POINTER(C.c_longlong)

@@ -43,6 +43,10 @@ extern "C" {
 #define DPGO_PRECON_BLOCK_JACOBI 1
 #define DPGO_PRECON_NONE 2
 
+/* Device form of Q: explicit block-sparse rows, or the measurement (edge) stream it is built from */
+#define DPGO_QFMT_BSR 0
+#define DPGO_QFMT_EDGES 1
+
 /* ROPTALG (include/DPGO/DPGO_types.h:29-35) */
 #define DPGO_ALG_RTR 0
 #define DPGO_ALG_RGD 1
@@ -107,6 +111,18 @@ int dpgo_hip_set_Q_csr(dpgo_hip_problem h, int agent, int nrows, const int* rowp
  * nbrows == n_a; column indices are agent-local pose indices. */
 int dpgo_hip_set_Q_bsr(dpgo_hip_problem h, int agent, int nbrows, const int* browptr,
                        const int* bcolidx, const double* blocks);
+/* Q of one agent given by the measurements it is built from, never materialised:
+ * Q = A Omega A^T (constructConnectionLaplacianSE, src/DPGO_utils.cpp:214-286) for private edges,
+ * plus the diagonal terms of shared edges (PGOAgent::constructQMatrix, src/PGOAgent.cpp:720-781).
+ * m edges with agent-local endpoints p1 -> p2; an endpoint of -1 marks a shared edge whose other
+ * end lives in another agent (it then adds T Omega T^T to Q_p1p1, or Omega to Q_p2p2, only).
+ * R: d*d row-major per edge, t: d per edge, kappa/tau: precisions, weight: NULL = 1 (GNC weight w
+ * multiplies both precisions).  The X.Q kernels then stream one 14-double record per edge
+ * (8 for d = 2) instead of two b x b off-diagonal blocks plus diagonal blocks.  Every agent of a
+ * handle must use the same form (BSR via set_Q_csr/_bsr, or edges). */
+int dpgo_hip_set_Q_edges(dpgo_hip_problem h, int agent, int m, const int* p1, const int* p2,
+                         const double* R, const double* t, const double* kappa, const double* tau,
+                         const double* weight);
 /* QuadraticProblem::setG (src/QuadraticProblem.cpp:44-48) in sparse form: count pose blocks
  * (r x b column-major) at agent-local poses pose_idx[]; all other columns of G are zero. */
 int dpgo_hip_set_G(dpgo_hip_problem h, int agent, int count, const int* pose_idx,
@@ -162,11 +178,14 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
 int dpgo_hip_synchronize(dpgo_hip_problem h);
 
 /* ---- measurement helpers ----------------------------------------------------------------*/
-/* Select a compiled kernel variant for A/B timing (key 0: X.Q SpMM neighbour-loop variant
- * 0 = 1 neighbour/step (default), 1 = same with non-temporal block loads, 2 = 2 neighbours/step,
- * 3 = 4 neighbours/step, 4 = 4 + XCD-aware tile remap, 5 = 2 + XCD remap). */
+/* Select a compiled kernel variant for A/B timing (r = 5, d = 3 only).  key 0: BSR X.Q SpMM
+ * neighbour-loop variant 0 = 1 neighbour/step (default), 1 = same with non-temporal block loads,
+ * 2 = 2 neighbours/step, 3 = 4 neighbours/step, 4 = 4 + XCD-aware tile remap, 5 = 2 + XCD remap,
+ * 6 = 1 + XCD remap.  key 1: edge-stream variant for every SpMM mode (same numbering over
+ * incidences; -1 = the compiled default). */
 int dpgo_hip_set_tuning(int key, int value);
-/* Algorithmic HBM bytes of one X.Q SpMM over this handle (BSR blocks + indices + X + Y). */
+/* Algorithmic HBM bytes of one X.Q SpMM over this handle: BSR blocks + indices + X + Y, or, for
+ * an edge-stream Q, every edge record once + 8 B per incidence + pointers + X + Y. */
 double dpgo_hip_spmm_bytes(dpgo_hip_problem h);
 /* Time `reps` back-to-back X.Q SpMM launches with HIP events on the handle's stream; returns the
  * average milliseconds per launch in *ms. */

@@ -56,6 +56,7 @@ typedef struct {
   double tolerance;       /* 1e-2 (src/PGOAgent.cpp:1133) */
   int precon;             /* DPGO_PRECON_BLOCK_JACOBI */
   int algorithm;          /* DPGO_ALG_RTR / DPGO_ALG_RGD */
+  int q_format;           /* DPGO_QFMT_EDGES (default: edge-stream Q) or DPGO_QFMT_BSR (explicit Q) */
 } dpgo_rbcd_params;
 
 void dpgo_rbcd_default_params(dpgo_rbcd_params* p);

@@ -25,8 +25,10 @@ CASES = [("tinyGrid3D", 5), ("smallGrid3D", 5), ("smallGrid3D", 3), ("sphere2500
          ("input_INTEL_g2o", 5), ("input_INTEL_g2o", 2), ("city10000", 3)]
 
 
+@pytest.mark.parametrize("fmt", ["bsr", "edges"])
 @pytest.mark.parametrize("name,r", CASES)
-def test_evaluations(hip, name, r):
+def test_evaluations(hip, name, r, fmt):
+    """Q uploaded as BSR (QuadraticProblem::setQ) or as its measurement stream (edge records)."""
     meas = load_meas(name)
     d, n = meas.d, meas.num_poses
     Q = O.connection_laplacian(meas, n)
@@ -37,7 +39,10 @@ def test_evaluations(hip, name, r):
     G = seeded_G(X, d, r, n, 13)
     P.set_G(G)
     H = hip.Problem(n, d, r)
-    H.set_Q_scipy(0, Q)
+    if fmt == "bsr":
+        H.set_Q_scipy(0, Q)
+    else:
+        H.set_Q_edges(0, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau, meas.weight)
     H.set_G_dense(0, G)
     f = H.f(X)[0]
     assert abs(f - P.f(X)) <= TOL * max(1.0, abs(P.f(X)))
@@ -135,3 +140,60 @@ def test_batched_agents_match_independent(hip):
         Xk, rk = oracle_out[k]
         assert abs(rh[k]["fOpt"] - rk["fOpt"]) <= 1e-10 * max(1.0, abs(rk["fOpt"]))
         assert rel(Xh[:, start[k] * b:start[k + 1] * b], Xk) <= 1e-10
+
+
+def _agent_edges(meas, robot_of, local, k):
+    """Agent k's measurement stream: private edges with local endpoints, shared edges with the
+    foreign endpoint = -1 (PGOAgent::constructQMatrix, src/PGOAgent.cpp:720-781)."""
+    sel = np.nonzero((robot_of[meas.p1] == k) | (robot_of[meas.p2] == k))[0]
+    p1 = np.where(robot_of[meas.p1[sel]] == k, local[meas.p1[sel]], -1)
+    p2 = np.where(robot_of[meas.p2[sel]] == k, local[meas.p2[sel]], -1)
+    return sel, p1, p2
+
+
+@pytest.mark.parametrize("name,r,robots", [("smallGrid3D", 5, 5), ("input_INTEL_g2o", 5, 4)])
+def test_agent_edge_stream_matches_agent_Q(hip, name, r, robots):
+    """Per-agent Q from the edge stream (shared edges: diagonal terms only) = the oracle's
+    PGOAgent Q; batched over all agents in one handle, f / EucGrad / HVP / RieGrad / precond."""
+    meas = load_meas(name)
+    d, n = meas.d, meas.num_poses
+    b = d + 1
+    parts, robot_of, local, start = O.partition_contiguous(meas, n, robots)
+    X = random_point(r, d, n, 31)
+    V = random_tangent(X, d, 32)
+    H = hip.Problem(None, d, r, poses_per_agent=[int(start[k + 1] - start[k]) for k in range(robots)])
+    probs = []
+    for k in range(robots):
+        ag = O.Agent(k, O.AgentParams(d, r, robots, robust="L2", precon=O.PRECON_BLOCK_JACOBI))
+        ag.set_pose_graph(*parts[k], n=int(start[k + 1] - start[k]))
+        sel, p1, p2 = _agent_edges(meas, robot_of, local, k)
+        H.set_Q_edges(k, p1, p2, meas.R[sel], meas.t[sel], meas.kappa[sel], meas.tau[sel])
+        G = seeded_G(X[:, start[k] * b:start[k + 1] * b], d, r, int(start[k + 1] - start[k]), 40 + k)
+        ag.problem.set_G(G)
+        H.set_G_dense(k, G)
+        probs.append(ag.problem)
+    fh = H.f(X)
+    EG, HV = H.egrad(X), H.ehvp(V)
+    RG, norms, _ = H.riegrad(X)
+    PC = H.precondition(X, V)
+    for k in range(robots):
+        sl = slice(start[k] * b, start[k + 1] * b)
+        P = probs[k]
+        Xk, Vk = X[:, sl], V[:, sl]
+        assert abs(fh[k] - P.f(Xk)) <= TOL * max(1.0, abs(P.f(Xk)))
+        assert rel(EG[:, sl], P.egrad(Xk)) <= TOL
+        assert rel(HV[:, sl], P.ehvp(Vk)) <= TOL
+        assert rel(RG[:, sl], P.riegrad(Xk)) <= TOL
+        assert abs(norms[k] - P.riegrad_norm(Xk)) <= TOL * P.riegrad_norm(Xk)
+        assert rel(PC[:, sl], P.precondition(Xk, Vk, O.PRECON_BLOCK_JACOBI)) <= TOL
+
+
+def test_edge_stream_rejects_bad_input(hip):
+    H = hip.Problem(4, 3, 5)
+    R = np.tile(np.eye(3), (1, 1, 1))
+    with pytest.raises(hip.DPGOHipError):
+        H.set_Q_edges(0, [0], [0], R, np.zeros((1, 3)), [1.0], [1.0])  # self-loop
+    with pytest.raises(hip.DPGOHipError):
+        H.set_Q_edges(0, [0], [7], R, np.zeros((1, 3)), [1.0], [1.0])  # out of range
+    with pytest.raises(hip.DPGOHipError):
+        H.set_Q_edges(0, [-1], [-1], R, np.zeros((1, 3)), [1.0], [1.0])  # no local endpoint

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A/B the X.Q SpMM variants in ONE process, interleaved rounds (cdna_hip_programming.md 5.4 rule 24).
+"""A/B the X.Q SpMM variants (edge-stream or BSR Q) in ONE process, interleaved rounds (cdna_hip_programming.md 5.4 rule 24).
 Workload: one colour class of the C5 problem (grid3d k=100, 64 agents -> 32 agents, 500k poses)."""
 import argparse
 import json
@@ -17,20 +17,23 @@ def main():
     ap.add_argument("--variants", default="0,1,2,3")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--qfmt", default="edges", choices=["edges", "bsr"])
     args = ap.parse_args()
     from dpgo_amd import hip as H
     g = H.Graph.grid3d(args.k, seed=0)
     aop = g.grid_partition(4)
-    eng = H.Rbcd(g, aop, np.zeros(64, np.int32), 0, 1, H.rbcd_params(r=5, acceleration=1))
+    qf = H.QFMT_EDGES if args.qfmt == "edges" else H.QFMT_BSR
+    key = 1 if args.qfmt == "edges" else 0
+    eng = H.Rbcd(g, aop, np.zeros(64, np.int32), 0, 1, H.rbcd_params(r=5, acceleration=1, q_format=qf))
     eng.set_X(g.chain_init_dev_layout(5, H.lifting_matrix(3, 5)))
     variants = [int(v) for v in args.variants.split(",")]
     res = {v: [] for v in variants}
     for rnd in range(args.rounds):
         for v in variants:
-            H.set_tuning(0, v)
+            H.set_tuning(key, v)
             b, ms = eng.bench_spmm(0, args.reps)
             res[v].append(ms)
-    H.set_tuning(0, 0)
+    H.set_tuning(key, -1 if key == 1 else 0)
     out = {}
     for v in variants:
         t = np.array(res[v])
@@ -52,7 +55,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     copy_gbs = 2 * n * 8 / (e0.elapsed_time(e1) / 20 * 1e-3) / 1e9
-    print(json.dumps({"bytes": b, "variants": out, "d2d_copy_GBps": copy_gbs}))
+    print(json.dumps({"qfmt": args.qfmt, "bytes": b, "variants": out, "d2d_copy_GBps": copy_gbs}))
 
 
 if __name__ == "__main__":
