@@ -342,11 +342,13 @@ int download_state(dpgo_hip_problem h) {
   return DPGO_HIP_OK;
 }
 
-// EVAL sweep at X: g = P_X(XQ+G), S, per-agent f and |g|^2 partials into pa
-int eval_at(dpgo_hip_problem h, const double* X, double* gout, double* Sout, double* part, int flag) {
+// EVAL sweep at X: g = P_X(XQ+G), S, per-agent f and |g|^2 partials into pa.  mode MODE_F: f only;
+// MODE_EVAL_TCG: also the tCG start delta = -Prec(g) and the <z, g> partial.
+int eval_at(dpgo_hip_problem h, const double* X, double* gout, double* Sout, double* part, int flag,
+            int mode = dpgo::MODE_EVAL, double* delta = nullptr, int pmode = dpgo::PRECON_NONE) {
   auto c = make_ctx(h, flag, part);
-  HIP_TRY(dpgo::launch_spmm(h->r, h->b, dpgo::MODE_EVAL, c, qview(h), X, h->gidx.p, h->gblk.p, X, nullptr,
-                            gout, Sout));
+  const dpgo::SpmmArgs a{X, h->gidx.p, h->gblk.p, X, nullptr, gout, Sout, h->minv.p, delta, pmode};
+  HIP_TRY(dpgo::launch_spmm(h->r, h->b, mode, c, qview(h), a));
   return DPGO_HIP_OK;
 }
 
@@ -762,9 +764,16 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
   o.min_inner = 0;
   o.max_iter = P.tr_iterations;
   o.single_run = single ? 1 : 0;
-  // f(x1), grad(x1), S(x1)  (QuadraticOptimizer::optimize :36-37, SolversTR start)
-  DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_NONE));
-  DPGO_TRY(finalize(h, dpgo::OP_EVAL_INIT, h->pa.p, 2, nullptr, 0, &o, h->enabled.p));
+  // f(x1), grad(x1), S(x1)  (QuadraticOptimizer::optimize :36-37, SolversTR start); for RTR the
+  // first tCG start (delta = -Prec(grad), <z, grad>) is fused into the same pass
+  const bool fused_tcg = P.algorithm == DPGO_ALG_RTR && P.tr_max_inner > 0;
+  if (fused_tcg) {
+    DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_NONE, dpgo::MODE_EVAL_TCG, h->delta.p, pmode));
+    DPGO_TRY(finalize(h, dpgo::OP_EVAL_TCG_INIT, h->pa.p, 3, nullptr, 0, &o, h->enabled.p));
+  } else {
+    DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_NONE));
+    DPGO_TRY(finalize(h, dpgo::OP_EVAL_INIT, h->pa.p, 2, nullptr, 0, &o, h->enabled.p));
+  }
 
   if (P.algorithm == DPGO_ALG_RGD) {
     // one fixed-step Riemannian gradient step (QuadraticOptimizer::gradientDescent :124-149)
@@ -802,11 +811,19 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
   // to host-mapped memory; the host keeps one tCG iteration of launches queued ahead of the flag
   // it is waiting for, so the GPU never drains (agents that finished skip their tiles).
   const int max_rounds = single ? 12 : P.tr_iterations;
+  // Statistics nobody asked for are not computed: without results / verbose, the x2 evaluation of
+  // a single Run needs f(x2) only (gradNormOpt is only printed, src/PGOAgent.cpp:1155-1161), and an
+  // accepted candidate is retracted straight into X_out (only agents that did not move copy X_in).
+  const bool stats = results != nullptr || P.verbose;
+  const bool direct = single && !stats && X_out != X_in;
+  double* x2 = direct ? X_out : h->x2.p;
   for (int round = 0; round < max_rounds; ++round) {
     // ---- truncated CG (A.4)
-    auto ci = make_ctx(h, dpgo::FLAG_RUN, h->pa.p);
-    HIP_TRY(dpgo::launch_tcg_init(r, b, ci, x1, h->minv.p, pmode, h->g.p, h->delta.p));
-    DPGO_TRY(finalize(h, dpgo::OP_TCG_INIT, h->pa.p, 2, nullptr, 0, &o));
+    if (round > 0 || !fused_tcg) {
+      auto ci = make_ctx(h, dpgo::FLAG_RUN, h->pa.p);
+      HIP_TRY(dpgo::launch_tcg_init(r, b, ci, x1, h->minv.p, pmode, h->g.p, h->delta.p));
+      DPGO_TRY(finalize(h, dpgo::OP_TCG_INIT, h->pa.p, 2, nullptr, 0, &o));
+    }
     std::vector<int> tags;
     auto launch_iter = [&](int j) -> int {
       auto ch = make_ctx(h, dpgo::FLAG_TCG, h->pa.p);
@@ -841,15 +858,19 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
     }
     // ---- candidate x2 = R_x1(eta), rho test, radius update
     auto cr = make_ctx(h, dpgo::FLAG_RUN, h->pa.p);
-    HIP_TRY(dpgo::launch_retract(r, b, cr, x1, h->eta.p, 1.0, h->x2.p, h->g.p, h->Heta.p));
-    // single Run: only f(x2) and |grad(x2)| are consumed (fOpt / gradNormOpt)
-    DPGO_TRY(eval_at(h, h->x2.p, single ? nullptr : h->g2.p, single ? nullptr : h->S2.p, h->pb.p, dpgo::FLAG_RUN));
+    HIP_TRY(dpgo::launch_retract(r, b, cr, x1, h->eta.p, 1.0, x2, h->g.p, h->Heta.p));
+    // single Run: only f(x2) and |grad(x2)| are consumed (fOpt / gradNormOpt), |grad(x2)| only as a
+    // statistic
+    if (single)
+      DPGO_TRY(eval_at(h, x2, nullptr, nullptr, h->pb.p, dpgo::FLAG_RUN, stats ? dpgo::MODE_EVAL : dpgo::MODE_F));
+    else
+      DPGO_TRY(eval_at(h, x2, h->g2.p, h->S2.p, h->pb.p, dpgo::FLAG_RUN));
     const int rtag = next_tag(h);
     DPGO_TRY(finalize(h, dpgo::OP_RHO, h->pa.p, 2, h->pb.p, 2, &o, nullptr, 2, rtag));
     if (!single) {
       auto ca = make_ctx(h, dpgo::FLAG_NONE, nullptr);
       HIP_TRY(dpgo::launch_accept(r, b, ca, h->x2.p, h->g2.p, h->S2.p, h->x1.p, h->g.p, h->S.p));
-    } else {
+    } else if (!direct) {
       // speculative output: X_out = accepted ? x2 : X_in (repeated after a retry Run; agents that are
       // done skip nothing here, rejected ones copy their unchanged input)
       auto cs = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
@@ -863,6 +884,10 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
   }
   // X_out: accepted candidate or the input (single Run), x1 (multi-iteration)
   auto cs = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
+  if (direct) {  // x2 already sits in X_out: agents that did not move take X_in
+    auto cm = make_ctx(h, dpgo::FLAG_MOVED, h->pa.p);
+    HIP_TRY(dpgo::launch_select(r, b, cm, X_in, X_in, nullptr, X_in, X_out));
+  }
   if (!single) {
     HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(h->use_a.p), 1, K, h->stream));
     HIP_TRY(dpgo::launch_select(r, b, cs, x1, X_in, h->use_a.p, X_in, X_out));

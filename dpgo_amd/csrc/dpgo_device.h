@@ -71,6 +71,81 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// Reduce-scatter over the quad: lane k ends with col = sum over the 4 lanes of acc[:, k].  Round 1
+// (lanes k, k^1) sums the two columns of k's parity, round 2 (lanes k, k^2) column k: the same
+// additions in the same order as qsum, so the result equals qsum's bitwise.
+template <int R, int B>
+__device__ __forceinline__ void quad_reduce_scatter(const double (&acc)[R][B], int k, double (&col)[R]) {
+  const bool odd = (k & 1) != 0, hi = (k & 2) != 0;
+#pragma unroll
+  for (int a = 0; a < R; ++a) {
+    const double c0 = acc[a][0], c1 = acc[a][1], c2 = acc[a][2];
+    const double c3 = B > 3 ? acc[a][B > 3 ? 3 : 0] : 0.0;
+    const double hA = (odd ? c1 : c0) + dpp_f64<0xB1>(odd ? c0 : c1);
+    const double hB = (odd ? c3 : c2) + dpp_f64<0xB1>(odd ? c2 : c3);
+    col[a] = (hi ? hB : hA) + dpp_f64<0x4E>(hi ? hA : hB);
+  }
+}
+
+// Y block (first D columns) of a pose on every lane of its quad: full[a][c] = column c of lane c.
+template <int R, int D>
+__device__ __forceinline__ void quad_gather_y(const double (&col)[R], double (&full)[R][D]) {
+#pragma unroll
+  for (int a = 0; a < R; ++a) {
+    full[a][0] = qbcast<0>(col[a]);
+    full[a][1] = qbcast<1>(col[a]);
+    if constexpr (D > 2) full[a][D > 2 ? 2 : 0] = qbcast<2>(col[a]);
+  }
+}
+
+// S = sym(Y^T M_Y) from lane-held columns of M: lane q computes T[:, q] = Y^T M[:, q], the quad
+// shares T, and every lane forms S (same FMA chains as sym_ytm).
+template <int R, int D>
+__device__ __forceinline__ void sym_ytm_cols(const double (&Y)[R][D], const double (&mcol)[R],
+                                             double (&S)[D][D]) {
+  double Tk[D];
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+    double s = 0.0;
+#pragma unroll
+    for (int a = 0; a < R; ++a) s = fma(Y[a][p], mcol[a], s);
+    Tk[p] = s;
+  }
+  double T[D][D];
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+    T[p][0] = qbcast<0>(Tk[p]);
+    T[p][1] = qbcast<1>(Tk[p]);
+    if constexpr (D > 2) T[p][D > 2 ? 2 : 0] = qbcast<2>(Tk[p]);
+  }
+#pragma unroll
+  for (int p = 0; p < D; ++p)
+#pragma unroll
+    for (int q = 0; q < D; ++q) S[p][q] = 0.5 * (T[p][q] + T[q][p]);
+}
+
+// Column k of M - [Y S | 0] from lane k's column of M (k = D, the translation column, passes).
+template <int R, int D>
+__device__ __forceinline__ void sub_y_times_col(const double (&Y)[R][D], const double (&S)[D][D], int k,
+                                                const double (&mcol)[R], double (&out)[R]) {
+  double Sk[D];
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+    double v0 = S[p][0], v1 = S[p][1], v2 = D > 2 ? S[p][D > 2 ? 2 : 0] : 0.0, v3 = 0.0;
+    if constexpr (D == 2) v2 = 0.0;
+    asm("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));
+    Sk[p] = (k & 2) ? ((k & 1) ? v3 : v2) : ((k & 1) ? v1 : v0);
+  }
+  const bool proj = k < D;
+#pragma unroll
+  for (int a = 0; a < R; ++a) {
+    double s = mcol[a];
+#pragma unroll
+    for (int p = 0; p < D; ++p) s = fma(-Y[a][p], Sk[p], s);
+    out[a] = proj ? s : mcol[a];
+  }
+}
+
 // Gather a full pose from per-lane columns: full[a][c] = column c held by lane c.
 template <int R, int B>
 __device__ __forceinline__ void quad_gather(const double (&col)[R], double (&full)[R][B]) {

@@ -8,8 +8,13 @@ namespace dpgo {
 
 constexpr int kPartialStride = 4;  // doubles of partial sums per tile
 
-enum SpmmMode { MODE_XQ = 0, MODE_XQ_G = 1, MODE_EVAL = 2, MODE_HESS = 3 };
-enum FlagKind { FLAG_NONE = 0, FLAG_RUN = 1, FLAG_TCG = 2, FLAG_TCG_MODE = 3 };
+// X.Q SpMM epilogues: XQ (V Q), XQ_G (X Q + G), EVAL (g = P_X(XQ+G), S, f / |g|^2 partials),
+// HESS (Riemannian Hessian), F (f partial only), EVAL_TCG (EVAL + tCG start: delta = -P_X(g Minv),
+// partial <z, g>)
+enum SpmmMode { MODE_XQ = 0, MODE_XQ_G = 1, MODE_EVAL = 2, MODE_HESS = 3, MODE_F = 4, MODE_EVAL_TCG = 5 };
+// Per-agent tile gating: RUN skips agents out of the RTR Run, TCG those whose tCG stopped, TCG_MODE
+// those with no tCG step pending, MOVED those whose single-Run candidate was accepted.
+enum FlagKind { FLAG_NONE = 0, FLAG_RUN = 1, FLAG_TCG = 2, FLAG_TCG_MODE = 3, FLAG_MOVED = 4 };
 enum PreconMode { PRECON_EXACT = 0, PRECON_BLOCK_JACOBI = 1, PRECON_NONE = 2 };
 enum TcgStatus { TCG_NEGCURVTURE = 0, TCG_EXCREGION = 1, TCG_LCON = 2, TCG_SCON = 3, TCG_MAXITER = 4 };
 enum FinalizeOp {
@@ -20,7 +25,8 @@ enum FinalizeOp {
   OP_TCG_CHECK = 4,
   OP_RHO = 5,
   OP_REL_CHANGE = 6,
-  OP_SUM = 7
+  OP_SUM = 7,
+  OP_EVAL_TCG_INIT = 8  // OP_EVAL_INIT then OP_TCG_INIT from one fused pass (f, |g|^2, <z,g>)
 };
 
 // Tile set + per-agent state for one launch.
@@ -61,6 +67,20 @@ struct QView {
   const double* diag;     // EDGES [n * diag_width(d)]
   const int* rec_first;   // EDGES [n + 1] first edge id first-visited by pose j (ids in visit order)
   int fmt;                // QFormat
+};
+
+// Operands of one SpMM launch (unused ones may be null).
+struct SpmmArgs {
+  const double* in;     // X (EVAL modes) or V
+  const int* gidx;      // G slot per pose (-1 = none)
+  const double* gblk;   // G blocks
+  const double* X;      // iterate (EVAL / HESS)
+  const double* S_in;   // cached sym(Y^T EG_Y) (HESS)
+  double* out;          // result (gradient / HVP); may be null in EVAL
+  double* S_out;        // S (EVAL)
+  const double* Minv;   // block-Jacobi inverses (EVAL_TCG)
+  double* delta;        // tCG direction (EVAL_TCG)
+  int pmode;            // PreconMode (EVAL_TCG)
 };
 
 struct OptScalars {
@@ -109,9 +129,12 @@ hipError_t launch_gather_poses(int count, int rb, const int* idx, const double* 
                                hipStream_t stream);
 hipError_t launch_assemble_G(int r, int b, const GEdges& e, int nslots, const double* Xa, const double* Xb,
                              double* gblk, hipStream_t stream);
-hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const QView& q, const double* in,
-                       const int* gidx, const double* gblk, const double* X, const double* S_in,
-                       double* out, double* S_out);
+hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const QView& q, const SpmmArgs& a);
+inline hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const QView& q, const double* in,
+                              const int* gidx, const double* gblk, const double* X, const double* S_in,
+                              double* out, double* S_out) {
+  return launch_spmm(r, b, mode, c, q, SpmmArgs{in, gidx, gblk, X, S_in, out, S_out, nullptr, nullptr, PRECON_NONE});
+}
 hipError_t launch_tcg_init(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
                            const double* g, double* delta);
 hipError_t launch_tcg_update(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,

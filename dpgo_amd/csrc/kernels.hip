@@ -21,6 +21,7 @@ __device__ __forceinline__ bool tile_skipped(const LaunchCtx& c, int agent) {
   if (c.flag_kind == FLAG_RUN) return s.run_active == 0;
   if (c.flag_kind == FLAG_TCG) return s.tcg_active == 0;
   if (c.flag_kind == FLAG_TCG_MODE) return s.tcg_mode == 2;
+  if (c.flag_kind == FLAG_MOVED) return s.runs > 0 && s.accepted && !s.gave_up;
   return false;
 }
 
@@ -291,13 +292,15 @@ constexpr int evar_waves(int v) { return (v >> 1) == 0 ? 1 : 3 + (v >> 1); }
 
 
 template <int R, int B, int MODE, int VAR = 0, int FMT = QFMT_BSR>
-__global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) void k_spmm(LaunchCtx c, QView q, const double* __restrict__ in,
-                                                   const int* __restrict__ gidx,
-                                                   const double* __restrict__ gblk,
-                                                   const double* __restrict__ X,
-                                                   const double* __restrict__ S_in,
-                                                   double* __restrict__ out,
-                                                   double* __restrict__ S_out) {
+__global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) void k_spmm(LaunchCtx c, QView q,
+                                                                                          SpmmArgs args) {
+  const double* __restrict__ in = args.in;
+  const int* __restrict__ gidx = args.gidx;
+  const double* __restrict__ gblk = args.gblk;
+  const double* __restrict__ X = args.X;
+  const double* __restrict__ S_in = args.S_in;
+  double* __restrict__ out = args.out;
+  double* __restrict__ S_out = args.S_out;
   constexpr int D = B - 1;
   const PoseLane p = pose_lane<B, FMT == QFMT_EDGES ? evar_xcd(VAR) : var_xcd(VAR)>(c);
   if (tile_skipped(c, p.agent)) return;
@@ -338,31 +341,27 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
   } else {
     if (p.ok && p.k < B) spmm_accumulate<R, B, var_unr(VAR), var_nt(VAR)>(q, in, p.j, p.k, acc);
   }
-#pragma unroll
-  for (int a = 0; a < R; ++a)
-#pragma unroll
-    for (int cc = 0; cc < B; ++cc) acc[a][cc] = qsum(acc[a][cc]);
+  // lane k keeps column k of the block row only (quad reduce-scatter; same additions, same
+  // order as a quad all-reduce, so bitwise identical to it) and the epilogues work column-locally
+  double qc[R];
+  quad_reduce_scatter<R, B>(acc, p.k, qc);
 
   const long off = p.j * (R * B) + p.k * R;
   const bool own = p.ok && p.k < B;
 
   if constexpr (MODE == MODE_XQ) {
-    double col[R];
-    select_col<R, B>(acc, p.k, col);
-    store_vec<R>(out, off, own, col);
+    store_vec<R>(out, off, own, qc);
   } else if constexpr (MODE == MODE_XQ_G) {
-    double col[R];
-    select_col<R, B>(acc, p.k, col);
     if (own && gidx != nullptr) {
       const int slot = gidx[p.j];
       if (slot >= 0) {
 #pragma unroll
-        for (int a = 0; a < R; ++a) col[a] += gblk[static_cast<long>(slot) * (R * B) + p.k * R + a];
+        for (int a = 0; a < R; ++a) qc[a] += gblk[static_cast<long>(slot) * (R * B) + p.k * R + a];
       }
     }
-    store_vec<R>(out, off, own, col);
-  } else if constexpr (MODE == MODE_EVAL) {
-    double xcol[R], gcol[R], qcol[R];
+    store_vec<R>(out, off, own, qc);
+  } else if constexpr (MODE == MODE_EVAL || MODE == MODE_F || MODE == MODE_EVAL_TCG) {
+    double xcol[R], gcol[R];
     load_col<R, B>(X, p.j, p.k, p.ok, xcol);
 #pragma unroll
     for (int a = 0; a < R; ++a) gcol[a] = 0.0;
@@ -373,34 +372,70 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
         for (int a = 0; a < R; ++a) gcol[a] = gblk[static_cast<long>(slot) * (R * B) + p.k * R + a];
       }
     }
-    select_col<R, B>(acc, p.k, qcol);
     double fpart = 0.0;
 #pragma unroll
-    for (int a = 0; a < R; ++a) fpart = fma(fma(0.5, qcol[a], gcol[a]), xcol[a], fpart);
-    double Xf[R][B], Gf[R][B];
-    quad_gather<R, B>(xcol, Xf);
-    quad_gather<R, B>(gcol, Gf);
+    for (int a = 0; a < R; ++a) fpart = fma(fma(0.5, qc[a], gcol[a]), xcol[a], fpart);
+    if constexpr (MODE == MODE_F) {  // f only (QuadraticProblem::f, :50-60)
+      double parts[2] = {own ? fpart : 0.0, 0.0};
+      block_partials<2>(parts, c.partials, p.tile);
+    } else {
+      double eg[R];  // column k of the Euclidean gradient XQ + G
 #pragma unroll
-    for (int a = 0; a < R; ++a)
+      for (int a = 0; a < R; ++a) eg[a] = qc[a] + gcol[a];
+      double Yf[R][D];
+      quad_gather_y<R, D>(xcol, Yf);
+      double S[D][D];
+      sym_ytm_cols<R, D>(Yf, eg, S);  // S = sym(Y^T EG_Y), on every lane of the quad
+      double gc[R];
+      sub_y_times_col<R, D>(Yf, S, p.k, eg, gc);  // column k of P_X(EG)
+      double gpart = 0.0;
 #pragma unroll
-      for (int cc = 0; cc < B; ++cc) acc[a][cc] += Gf[a][cc];
-    double S[D][D];
-    sym_ytm<R, B>(Xf, acc, S);
-    sub_y_times<R, B>(Xf, S, acc);
-    double gc[R];
-    select_col<R, B>(acc, p.k, gc);
-    double gpart = 0.0;
+      for (int a = 0; a < R; ++a) gpart = fma(gc[a], gc[a], gpart);
+      if (out != nullptr) store_vec<R>(out, off, own, gc);
+      if (p.ok && p.k == 0 && S_out != nullptr) {
 #pragma unroll
-    for (int a = 0; a < R; ++a) gpart = fma(gc[a], gc[a], gpart);
-    if (out != nullptr) store_vec<R>(out, off, own, gc);
-    if (p.ok && p.k == 0 && S_out != nullptr) {
+        for (int u = 0; u < D; ++u)
 #pragma unroll
-      for (int u = 0; u < D; ++u)
+          for (int v = 0; v < D; ++v) S_out[p.j * (D * D) + u * D + v] = S[u][v];
+      }
+      if constexpr (MODE == MODE_EVAL_TCG) {
+        // tCG start fused in (A.4, k_tcg_init): z = Prec(g) = P_X(g Minv), delta = -z, <z, g>
+        double zc[R];
+        if (args.pmode == PRECON_NONE) {
 #pragma unroll
-        for (int v = 0; v < D; ++v) S_out[p.j * (D * D) + u * D + v] = S[u][v];
+          for (int a = 0; a < R; ++a) zc[a] = gc[a];
+        } else {
+          double Gf[R][B];
+          quad_gather<R, B>(gc, Gf);
+          double mk[B];  // column k of Minv (row-major b x b)
+#pragma unroll
+          for (int u = 0; u < B; ++u) mk[u] = p.ok ? args.Minv[p.j * (B * B) + u * B + (p.k < B ? p.k : 0)] : 0.0;
+          double zq[R];
+#pragma unroll
+          for (int a = 0; a < R; ++a) {
+            double sacc = 0.0;
+#pragma unroll
+            for (int u = 0; u < B; ++u) sacc = fma(Gf[a][u], mk[u], sacc);
+            zq[a] = sacc;
+          }
+          double S3[D][D];
+          sym_ytm_cols<R, D>(Yf, zq, S3);
+          sub_y_times_col<R, D>(Yf, S3, p.k, zq, zc);
+        }
+        double zr = 0.0, dc[R];
+#pragma unroll
+        for (int a = 0; a < R; ++a) {
+          zr = fma(zc[a], gc[a], zr);
+          dc[a] = -zc[a];
+        }
+        store_vec<R>(args.delta, off, own, dc);
+        double parts[3] = {own ? fpart : 0.0, own ? gpart : 0.0, own ? zr : 0.0};
+        block_partials<3>(parts, c.partials, p.tile);
+      } else {
+        double parts[2] = {own ? fpart : 0.0, own ? gpart : 0.0};
+        block_partials<2>(parts, c.partials, p.tile);
+      }
     }
-    double parts[2] = {own ? fpart : 0.0, own ? gpart : 0.0};
-    block_partials<2>(parts, c.partials, p.tile);
   } else if constexpr (MODE == MODE_HESS) {
     double vcol[R], xcol[R];
     load_col<R, B>(in, p.j, p.k, p.ok, vcol);
@@ -410,13 +445,14 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     for (int u = 0; u < D; ++u)
 #pragma unroll
       for (int v = 0; v < D; ++v) S[u][v] = p.ok ? S_in[p.j * (D * D) + u * D + v] : 0.0;
-    double Vf[R][B], Xf[R][B];
-    quad_gather<R, B>(vcol, Vf);
-    quad_gather<R, B>(xcol, Xf);
-    sub_y_times<R, B>(Vf, S, acc);  // VQ - V_Y S
-    tangent_project_pose<R, B>(Xf, acc);
-    double hc[R];
-    select_col<R, B>(acc, p.k, hc);
+    double Vf[R][D], Xf[R][D];
+    quad_gather_y<R, D>(vcol, Vf);
+    quad_gather_y<R, D>(xcol, Xf);
+    double h1[R], hc[R];
+    sub_y_times_col<R, D>(Vf, S, p.k, qc, h1);  // VQ - V_Y S
+    double S2[D][D];
+    sym_ytm_cols<R, D>(Xf, h1, S2);
+    sub_y_times_col<R, D>(Xf, S2, p.k, h1, hc);  // tangent projection at X
     double dpart = 0.0;
 #pragma unroll
     for (int a = 0; a < R; ++a) dpart = fma(vcol[a], hc[a], dpart);
@@ -823,6 +859,37 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
       s.ngf = sqrt(tot[1]);
       break;
     }
+    case OP_EVAL_TCG_INIT: {  // OP_EVAL_INIT, then OP_TCG_INIT with <z, g> = tot[2], |r|^2 = |g|^2
+      s.f1 = tot[0];
+      s.ngf = sqrt(tot[1]);
+      s.f_init = s.f1;
+      s.ngf_init = s.ngf;
+      s.f2 = s.f1;
+      s.ngf2 = s.ngf;
+      s.Delta = o.Delta0;
+      s.Delta_max = o.Delta_max;
+      s.run_active = f.agent_enabled ? (f.agent_enabled[agent] != 0 && !(s.ngf < o.tol)) : !(s.ngf < o.tol);
+      s.accepted = 0;
+      s.runs = 0;
+      s.outer_iters = 0;
+      s.gave_up = 0;
+      s.tcg_status = -1;
+      s.tcg_iters = 0;
+      s.copy_pending = 0;
+      s.tcg_mode = 2;
+      if (!s.run_active) {
+        s.tcg_active = 0;
+        break;
+      }
+      s.z_r = tot[2];
+      s.d_Pd = s.z_r;
+      s.e_Pe = 0.0;
+      s.e_Pd = 0.0;
+      s.norm_r0 = sqrt(tot[1]);
+      s.tcg_active = 1;
+      s.tcg_status = TCG_MAXITER;
+      break;
+    }
     case OP_TCG_INIT: {
       s.copy_pending = 0;
       if (!s.run_active) {
@@ -1136,18 +1203,16 @@ bool supported_rb(int r, int b) {
 namespace {
 
 template <int MODE, int VAR, int FMT>
-hipError_t spmm_rb(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const double* in, const int* gidx,
-                   const double* gblk, const double* X, const double* S_in, double* out, double* S_out) {
-  DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE, VAR, FMT><<<grid, kThreads, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out)));
+hipError_t spmm_rb(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const SpmmArgs& a) {
+  DPGO_DISPATCH(r, b, (k_spmm<R, B, MODE, VAR, FMT><<<grid, kThreads, 0, c.stream>>>(c, q, a)));
   return hipSuccess;
 }
 
-// r = 5, d = 3 (the headline shape) only: every compiled neighbour-loop variant, for A/B timing
-template <int MODE, int FMT>
-hipError_t spmm_variant54(int var, dim3 grid, const LaunchCtx& c, const QView& q, const double* in, const int* gidx,
-                          const double* gblk, const double* X, const double* S_in, double* out, double* S_out) {
+// r = 5, d = 3 (the headline shape), X.Q only: every compiled neighbour-loop variant, for A/B timing
+template <int FMT>
+hipError_t spmm_variant54(int var, dim3 grid, const LaunchCtx& c, const QView& q, const SpmmArgs& a) {
 #define DPGO_VAR(V) \
-  case V: k_spmm<5, 4, MODE, V, FMT><<<grid, kThreads, 0, c.stream>>>(c, q, in, gidx, gblk, X, S_in, out, S_out); break;
+  case V: k_spmm<5, 4, MODE_XQ, V, FMT><<<grid, kThreads, 0, c.stream>>>(c, q, a); break;
   switch (var) {
     DPGO_VAR(0) DPGO_VAR(1) DPGO_VAR(2) DPGO_VAR(3) DPGO_VAR(4) DPGO_VAR(5) DPGO_VAR(6) DPGO_VAR(7)
     default: return hipErrorInvalidValue;
@@ -1157,33 +1222,31 @@ hipError_t spmm_variant54(int var, dim3 grid, const LaunchCtx& c, const QView& q
 }
 
 template <int MODE>
-hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const double* in, const int* gidx,
-                     const double* gblk, const double* X, const double* S_in, double* out, double* S_out) {
+hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const SpmmArgs& a) {
   if (q.fmt == QFMT_EDGES) {
     const int var = g_tuning[TUNE_EDGE_VARIANT] < 0 ? kEdgeDefaultVariant : g_tuning[TUNE_EDGE_VARIANT];
-    if (r == 5 && b == 4 && var != kEdgeDefaultVariant)
-      return spmm_variant54<MODE, QFMT_EDGES>(var, grid, c, q, in, gidx, gblk, X, S_in, out, S_out);
-    return spmm_rb<MODE, kEdgeDefaultVariant, QFMT_EDGES>(r, b, grid, c, q, in, gidx, gblk, X, S_in, out, S_out);
+    if (MODE == MODE_XQ && r == 5 && b == 4 && var != kEdgeDefaultVariant)
+      return spmm_variant54<QFMT_EDGES>(var, grid, c, q, a);
+    return spmm_rb<MODE, kEdgeDefaultVariant, QFMT_EDGES>(r, b, grid, c, q, a);
   }
-  const int var = MODE == MODE_XQ ? g_tuning[TUNE_SPMM_VARIANT] : 0;
-  if (r == 5 && b == 4 && var != 0)
-    return spmm_variant54<MODE, QFMT_BSR>(var, grid, c, q, in, gidx, gblk, X, S_in, out, S_out);
-  return spmm_rb<MODE, 0, QFMT_BSR>(r, b, grid, c, q, in, gidx, gblk, X, S_in, out, S_out);
+  const int var = g_tuning[TUNE_SPMM_VARIANT];
+  if (MODE == MODE_XQ && r == 5 && b == 4 && var != 0) return spmm_variant54<QFMT_BSR>(var, grid, c, q, a);
+  return spmm_rb<MODE, 0, QFMT_BSR>(r, b, grid, c, q, a);
 }
 
 }  // namespace
 
-hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const QView& q, const double* in,
-                       const int* gidx, const double* gblk, const double* X, const double* S_in,
-                       double* out, double* S_out) {
+hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const QView& q, const SpmmArgs& a) {
   if (c.num_tiles == 0) return hipSuccess;
   const dim3 grid(c.num_tiles);
   hipError_t e = hipErrorInvalidValue;
   switch (mode) {
-    case MODE_XQ: e = spmm_mode<MODE_XQ>(r, b, grid, c, q, in, gidx, gblk, X, S_in, out, S_out); break;
-    case MODE_XQ_G: e = spmm_mode<MODE_XQ_G>(r, b, grid, c, q, in, gidx, gblk, X, S_in, out, S_out); break;
-    case MODE_EVAL: e = spmm_mode<MODE_EVAL>(r, b, grid, c, q, in, gidx, gblk, X, S_in, out, S_out); break;
-    case MODE_HESS: e = spmm_mode<MODE_HESS>(r, b, grid, c, q, in, gidx, gblk, X, S_in, out, S_out); break;
+    case MODE_XQ: e = spmm_mode<MODE_XQ>(r, b, grid, c, q, a); break;
+    case MODE_XQ_G: e = spmm_mode<MODE_XQ_G>(r, b, grid, c, q, a); break;
+    case MODE_EVAL: e = spmm_mode<MODE_EVAL>(r, b, grid, c, q, a); break;
+    case MODE_HESS: e = spmm_mode<MODE_HESS>(r, b, grid, c, q, a); break;
+    case MODE_F: e = spmm_mode<MODE_F>(r, b, grid, c, q, a); break;
+    case MODE_EVAL_TCG: e = spmm_mode<MODE_EVAL_TCG>(r, b, grid, c, q, a); break;
     default: break;
   }
   if (e != hipSuccess) return e;
