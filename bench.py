@@ -25,6 +25,22 @@ METRIC = "RBCD iters/sec + X·Q SpMM HBM GB/s, 1M-pose synth grid r=5, 1/2/4/8 G
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+def measured_traffic():
+    """HBM bytes per launch of the edge-stream X.Q SpMM from the newest committed PMC summary
+    (profiles/*_pmc_traffic.json, produced by tools/pmc_traffic.py), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            t = json.load(f)
+        t["source"] = os.path.relpath(files[-1], ROOT)
+        return t
+    except (OSError, ValueError):
+        return None
+
+
 def super_cube_ranks(A, world):
     """Agents -> ranks: 2x2x2 super-cubes of agents (8 groups), merged for world < 8."""
     ranks = np.zeros(A ** 3, np.int32)
@@ -112,9 +128,12 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    # ---- roofline of the dominant kernel (X.Q SpMM over one colour class, HIP events)
-    spmm_bytes, spmm_ms = eng.bench_spmm(0, args.spmm_reps)
-    achieved = spmm_bytes / (spmm_ms * 1e-3) / 1e9 if spmm_ms > 0 else 0.0
+    # ---- roofline of the X.Q SpMM over one colour class (HIP events on the engine stream)
+    fmt_bytes, spmm_ms = eng.bench_spmm(0, args.spmm_reps)
+    bsr_bytes, _ = eng.spmm_bytes(0)
+    achieved = bsr_bytes / (spmm_ms * 1e-3) / 1e9 if spmm_ms > 0 else 0.0
+    hvp_ms = eng.bench_hvp(0, args.spmm_reps)
+    traffic = measured_traffic()
 
     agent_updates = num_agents * args.steps
     value = agent_updates / elapsed
@@ -139,9 +158,18 @@ def main():
                    "parallelism": f"agents over {world} GPU(s), RCCL all_to_all halo"},
         "rounds_per_s": args.steps / elapsed,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_spmm<5,4,MODE_XQ> (X.Q over colour class 0 on rank 0)",
-                     "algorithmic_bytes_per_launch": spmm_bytes, "avg_launch_ms": spmm_ms},
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
+                     "kernel": "k_spmm<5,4,MODE_XQ,edge-stream> (X.Q over colour class 0 on rank 0)",
+                     "algorithmic_bytes_per_launch": bsr_bytes,
+                     "algorithmic_bytes_definition": "SURVEY 8d B_spmm = nnzb(b^2 8 + 4) + (n+1) 4 + 2 r b n 8",
+                     "avg_launch_ms": spmm_ms,
+                     "format_bytes_per_launch": fmt_bytes,
+                     "format_GBps": fmt_bytes / (spmm_ms * 1e-3) / 1e9 if spmm_ms > 0 else 0.0,
+                     "traffic_source": traffic["source"] if traffic else None},
+        "hvp": {"per_s": 1e3 / hvp_ms if hvp_ms > 0 else 0.0, "avg_launch_ms": hvp_ms,
+                "agents": int(eng.agents_per_color[0]),
+                "what": "Riemannian HVP (EucHessianEta + EucHvToHv, tangent-projected) over colour class 0"},
         "setup_s": setup_s,
     }
     if rank == 0 and world == 1 and args.cpu_baseline:

@@ -1058,6 +1058,47 @@ double dpgo_hip_spmm_bytes(dpgo_hip_problem h) {
          2.0 * static_cast<double>(h->r) * b * static_cast<double>(h->N) * 8.0;
 }
 
+double dpgo_hip_spmm_bytes_bsr(dpgo_hip_problem h) {
+  if (!h) return 0.0;
+  const double b = h->b;
+  long nnzb = 0;
+  if (h->q_fmt[0] == dpgo::QFMT_EDGES) {
+    nnzb = h->N;  // one diagonal block per pose + one block per incidence
+    for (int a = 0; a < h->K; ++a) {
+      const HostEdges& E = h->e_agent[a];
+      for (size_t e = 0; e < E.p1.size(); ++e) nnzb += (E.p1[e] >= 0 && E.p2[e] >= 0) ? 2 : 0;
+    }
+  } else {
+    for (int a = 0; a < h->K; ++a) nnzb += static_cast<long>(h->q_agent[a].col.size());
+  }
+  return static_cast<double>(nnzb) * (b * b * 8.0 + 4.0) + static_cast<double>(h->N + 1) * 4.0 +
+         2.0 * static_cast<double>(h->r) * b * static_cast<double>(h->N) * 8.0;
+}
+
+int dpgo_hip_bench_hvp(dpgo_hip_problem h, const double* X_dev, double* V_dev, double* HV_dev, int reps, double* ms) {
+  DPGO_TRY(ready(h));
+  DPGO_TRY(ensure_work(h));
+  if (reps <= 0 || !ms) return fail(DPGO_HIP_EINVAL, "reps must be > 0");
+  // S and a tangent direction (the Riemannian gradient) at X
+  DPGO_TRY(eval_at(h, X_dev, V_dev, h->S.p, h->pa.p, dpgo::FLAG_NONE));
+  hipEvent_t e0, e1;
+  HIP_TRY(hipEventCreate(&e0));
+  HIP_TRY(hipEventCreate(&e1));
+  auto c = make_ctx(h, dpgo::FLAG_NONE, h->pb.p);
+  HIP_TRY(hipEventRecord(e0, h->stream));
+  for (int i = 0; i < reps; ++i)
+    HIP_TRY(dpgo::launch_spmm(h->r, h->b, dpgo::MODE_HESS, c, qview(h), V_dev, nullptr, nullptr, X_dev, h->S.p, HV_dev,
+                              nullptr));
+  HIP_TRY(hipEventRecord(e1, h->stream));
+  HIP_TRY(hipEventSynchronize(e1));
+  float t = 0.f;
+  HIP_TRY(hipEventElapsedTime(&t, e0, e1));
+  *ms = static_cast<double>(t) / reps;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return DPGO_HIP_OK;
+}
+
 int dpgo_hip_bench_spmm(dpgo_hip_problem h, const double* X_dev, double* Y_dev, int reps, double* ms) {
   DPGO_TRY(ready(h));
   if (reps <= 0 || !ms) return fail(DPGO_HIP_EINVAL, "reps must be > 0");

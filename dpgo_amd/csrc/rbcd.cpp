@@ -568,6 +568,25 @@ int dpgo_rbcd_bench_spmm(dpgo_rbcd e, int color, int reps, double* bytes, double
   return dpgo_hip_bench_spmm(h, color_ptr(e, e->X, color), h->tA.p, reps, ms);
 }
 
+int dpgo_rbcd_spmm_bytes(dpgo_rbcd e, int color, double* bsr_bytes, double* format_bytes) {
+  if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
+  dpgo_hip_problem h = e->prob[color];
+  if (bsr_bytes) *bsr_bytes = h ? dpgo_hip_spmm_bytes_bsr(h) : 0.0;
+  if (format_bytes) *format_bytes = h ? dpgo_hip_spmm_bytes(h) : 0.0;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_bench_hvp(dpgo_rbcd e, int color, int reps, double* ms) {
+  if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
+  dpgo_hip_problem h = e->prob[color];
+  if (!h) {
+    if (ms) *ms = 0.0;
+    return DPGO_HIP_OK;
+  }
+  DPGO_TRY(ensure_work_public(h));
+  return dpgo_hip_bench_hvp(h, color_ptr(e, e->X, color), h->tA.p, h->tB.p, reps, ms);
+}
+
 int dpgo_rbcd_counters(dpgo_rbcd e, long long* agent_updates, long long* iterations) {
   if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
   if (agent_updates) *agent_updates = e->agent_updates;

@@ -86,6 +86,8 @@ _SIGS = [
     ("dpgo_hip_set_tuning", [C.c_int, C.c_int], C.c_int),
     ("dpgo_hip_spmm_bytes", [C.c_void_p], C.c_double),
     ("dpgo_hip_bench_spmm", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, _dp], C.c_int),
+    ("dpgo_hip_spmm_bytes_bsr", [C.c_void_p], C.c_double),
+    ("dpgo_hip_bench_hvp", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, _dp], C.c_int),
 ]
 
 EXPORTED_SYMBOLS = [s[0] for s in _SIGS]
@@ -396,6 +398,8 @@ _SIGS2 = [
     ("dpgo_rbcd_update", [C.c_void_p, C.c_int, C.c_void_p, C.POINTER(OptResult)], C.c_int),
     ("dpgo_rbcd_bench_spmm", [C.c_void_p, C.c_int, C.c_int, _dp, _dp], C.c_int),
     ("dpgo_rbcd_counters", [C.c_void_p, _lp, _lp], C.c_int),
+    ("dpgo_rbcd_spmm_bytes", [C.c_void_p, C.c_int, _dp, _dp], C.c_int),
+    ("dpgo_rbcd_bench_hvp", [C.c_void_p, C.c_int, C.c_int, _dp], C.c_int),
 ]
 _SIGS.extend(_SIGS2)
 EXPORTED_SYMBOLS.extend(s[0] for s in _SIGS2)
@@ -584,6 +588,17 @@ class Rbcd:
         b, ms = C.c_double(), C.c_double()
         _check(lib().dpgo_rbcd_bench_spmm(self.h, int(color), int(reps), C.byref(b), C.byref(ms)))
         return b.value, ms.value
+
+    def spmm_bytes(self, color):
+        """(SURVEY 8d B_spmm for explicit blocks, bytes of the stored form) of one X.Q SpMM."""
+        bb, fb = C.c_double(), C.c_double()
+        _check(lib().dpgo_rbcd_spmm_bytes(self.h, int(color), C.byref(bb), C.byref(fb)))
+        return bb.value, fb.value
+
+    def bench_hvp(self, color, reps):
+        ms = C.c_double()
+        _check(lib().dpgo_rbcd_bench_hvp(self.h, int(color), int(reps), C.byref(ms)))
+        return ms.value
 
     def counters(self):
         a, i = C.c_longlong(), C.c_longlong()

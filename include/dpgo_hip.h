@@ -187,6 +187,12 @@ int dpgo_hip_set_tuning(int key, int value);
 /* Algorithmic HBM bytes of one X.Q SpMM over this handle: BSR blocks + indices + X + Y, or, for
  * an edge-stream Q, every edge record once + 8 B per incidence + pointers + X + Y. */
 double dpgo_hip_spmm_bytes(dpgo_hip_problem h);
+/* SURVEY 8(d)'s algorithmic bytes of one X.Q SpMM over this handle's Q as explicit b x b blocks
+ * (B_spmm = nnzb (b^2 8 + 4) + (n + 1) 4 + 2 r b n 8), whatever form the handle stores it in. */
+double dpgo_hip_spmm_bytes_bsr(dpgo_hip_problem h);
+/* Riemannian HVP timing: one EVAL at X_dev (S and the Riemannian gradient into V_dev), then `reps`
+ * back-to-back Hessian-vector products HV_dev = Hess f(X)[V]; average ms per product in *ms. */
+int dpgo_hip_bench_hvp(dpgo_hip_problem h, const double* X_dev, double* V_dev, double* HV_dev, int reps, double* ms);
 /* Time `reps` back-to-back X.Q SpMM launches with HIP events on the handle's stream; returns the
  * average milliseconds per launch in *ms. */
 int dpgo_hip_bench_spmm(dpgo_hip_problem h, const double* X_dev, double* Y_dev, int reps, double* ms);

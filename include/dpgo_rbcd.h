@@ -89,6 +89,11 @@ int dpgo_rbcd_update(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_re
 /* Algorithmic HBM bytes of one X.Q SpMM over colour class c on this rank, and the timed average
  * of `reps` such launches (ms, HIP events on the engine stream). */
 int dpgo_rbcd_bench_spmm(dpgo_rbcd e, int color, int reps, double* bytes, double* ms);
+/* Bytes of one X.Q SpMM over colour class c on this rank: SURVEY 8(d)'s B_spmm for Q as explicit
+ * blocks, and the bytes of the form the engine stores (edge stream by default). */
+int dpgo_rbcd_spmm_bytes(dpgo_rbcd e, int color, double* bsr_bytes, double* format_bytes);
+/* Average ms of one Riemannian HVP over colour class c at the current X (HIP events). */
+int dpgo_rbcd_bench_hvp(dpgo_rbcd e, int color, int reps, double* ms);
 /* SpMM / HVP launches issued so far (for throughput accounting) */
 int dpgo_rbcd_counters(dpgo_rbcd e, long long* agent_updates, long long* iterations);
 

@@ -55,7 +55,9 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     copy_gbs = 2 * n * 8 / (e0.elapsed_time(e1) / 20 * 1e-3) / 1e9
-    print(json.dumps({"qfmt": args.qfmt, "bytes": b, "variants": out, "d2d_copy_GBps": copy_gbs}))
+    bsr_b, fmt_b = eng.spmm_bytes(0)
+    print(json.dumps({"qfmt": args.qfmt, "bytes": b, "bsr_bytes": bsr_b, "format_bytes": fmt_b, "variants": out,
+                      "d2d_copy_GBps": copy_gbs}))
 
 
 if __name__ == "__main__":
