@@ -23,7 +23,9 @@ class QuadraticOptimizer {
   void setTrustRegionTolerance(double tol) { trustRegionTolerance = tol; }
   void setTrustRegionInitialRadius(double radius) { trustRegionInitialRadius = radius; }
   void setTrustRegionMaxInnerIterations(int iter) { trustRegionMaxInnerIterations = iter; }
-  // DPGO_PRECON_BLOCK_JACOBI (default) or DPGO_PRECON_NONE; see DESIGN.md section 7.
+  // Extension (the reference always uses its CHOLMOD factor): DPGO_PRECON_EXACT (default, the
+  // factor of Q + 0.1 I), DPGO_PRECON_BLOCK_JACOBI (per-pose blocks, the throughput setting) or
+  // DPGO_PRECON_NONE; see DESIGN.md section 7.
   void setPreconditioner(int mode) { preconditioner = mode; }
 
   ROPTResult getOptResult() const { return result; }

@@ -30,7 +30,7 @@ class QuadraticProblem {
   Matrix EucGrad(const Matrix& Y) const;                          // :62-66
   Matrix EucHessianEta(const Matrix& V) const;                    // :68-73
   Matrix RieHessianEta(const Matrix& Y, const Matrix& V) const;   // ROPTLIB HessianEta
-  Matrix PreConditioner(const Matrix& Y, const Matrix& V) const;  // :75-87 (block-Jacobi)
+  Matrix PreConditioner(const Matrix& Y, const Matrix& V) const;  // :75-87 (exact factor of Q + 0.1 I)
   Matrix RieGrad(const Matrix& Y) const;                          // :89-97
   double RieGradNorm(const Matrix& Y) const;                      // :99-101
 

@@ -10,7 +10,7 @@ namespace DPGO {
 QuadraticOptimizer::QuadraticOptimizer(QuadraticProblem* p)
     : problem(p), algorithm(ROPTALG::RTR), gradientDescentStepsize(1e-3), trustRegionIterations(1),
       trustRegionTolerance(1e-2), trustRegionInitialRadius(1e1), trustRegionMaxInnerIterations(50), verbose(false),
-      preconditioner(DPGO_PRECON_BLOCK_JACOBI) {
+      preconditioner(DPGO_PRECON_EXACT) {
   result.success = false;
 }
 

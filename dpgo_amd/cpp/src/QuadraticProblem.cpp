@@ -15,6 +15,8 @@ QuadraticProblem::QuadraticProblem(size_t nIn, size_t dIn, size_t rIn) : n(nIn),
   if (r < d) throw std::invalid_argument("QuadraticProblem: r < d");
   hip_check(dpgo_hip_problem_create(static_cast<int>(n), static_cast<int>(d), static_cast<int>(r), &h),
             "dpgo_hip_problem_create");
+  // PreConditioner applies the factor of Q + 0.1 I, as the reference's CHOLMOD solver (:37-41, :75-87)
+  hip_check(dpgo_hip_set_precon(h, DPGO_PRECON_EXACT), "dpgo_hip_set_precon");
   // ctor sets empty Q and G (:23-24)
   mQ = SparseMatrix(static_cast<long>((d + 1) * n), static_cast<long>((d + 1) * n));
   mG = SparseMatrix(static_cast<long>(r), static_cast<long>((d + 1) * n));

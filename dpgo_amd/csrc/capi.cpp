@@ -15,6 +15,7 @@
 #include <string>
 #include <vector>
 
+#include "chol_internal.h"
 #include "graph_internal.h"
 #include "problem_internal.h"
 
@@ -176,6 +177,7 @@ int sync_q_edges(dpgo_hip_problem h) {
 // block-Jacobi inverses (QuadraticProblem::setQ, src/QuadraticProblem.cpp:31-42).
 int sync_q(dpgo_hip_problem h) {
   if (!h->q_dirty) return DPGO_HIP_OK;
+  h->chol_state = 0;  // the exact preconditioner follows Q (setQ refactorises, :37-41)
   const int f0 = h->q_fmt[0];
   for (int a = 1; a < h->K; ++a)
     if (h->q_fmt[a] != f0) return fail(DPGO_HIP_ESTATE, "agents of one handle mix BSR and edge-stream Q");
@@ -213,6 +215,178 @@ int sync_q(dpgo_hip_problem h) {
   HIP_TRY(dpgo::launch_bj_inverse(b, static_cast<int>(h->N), qview(h), 0.1, h->minv.p, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
   h->q_dirty = false;
+  return DPGO_HIP_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Exact preconditioner: the reference factorises P = Q + 0.1 I with CHOLMOD in
+// setQ (src/QuadraticProblem.cpp:37-41).  Here the factor is built on the host the first time the
+// EXACT mode is used after a setQ, per agent (agents are independent blocks), and uploaded as
+// forward / backward block rows plus a level schedule shared by the batch (level l of every agent
+// runs in one launch).
+constexpr size_t kMaxCholBlocks = 40u * 1000u * 1000u;
+
+void agent_bsr(dpgo_hip_problem h, int a, HostBSR& out) {
+  if (h->q_fmt[a] == dpgo::QFMT_BSR) {
+    out = h->q_agent[a];
+    return;
+  }
+  const HostEdges& E = h->e_agent[a];
+  const int d = h->d, na = h->n_agent[a];
+  dpgo::BsrBuilder B(na, h->b);
+  for (size_t e = 0; e < E.p1.size(); ++e)
+    if (E.p1[e] >= 0 && E.p2[e] >= 0) {
+      B.touch(E.p1[e], E.p2[e]);
+      B.touch(E.p2[e], E.p1[e]);
+    }
+  B.freeze();
+  double Wii[16], Wjj[16], Wij[16], Wji[16];
+  for (size_t e = 0; e < E.p1.size(); ++e) {
+    dpgo::edge_blocks(d, &E.R[e * d * d], &E.t[e * d], E.kw[e], E.tw[e], 1.0, Wii, Wjj, Wij, Wji);
+    if (E.p1[e] >= 0) B.add(E.p1[e], E.p1[e], Wii);
+    if (E.p2[e] >= 0) B.add(E.p2[e], E.p2[e], Wjj);
+    if (E.p1[e] >= 0 && E.p2[e] >= 0) {
+      B.add(E.p1[e], E.p2[e], Wij);
+      B.add(E.p2[e], E.p1[e], Wji);
+    }
+  }
+  out = std::move(B.out);
+}
+
+int sync_chol(dpgo_hip_problem h) {
+  if (h->chol_state != 0) return DPGO_HIP_OK;
+  const int b = h->b, bb = b * b;
+  std::vector<int> fptr(h->N + 1, 0), bptr(h->N + 1, 0), fcol, bcol, flev(h->N, 0), blev(h->N, 0);
+  std::vector<double> fblk, bblk, linv(static_cast<size_t>(h->N) * bb, 0.0);
+  // per pose (global) forward / backward entries, collected then laid out in CSR
+  std::vector<std::vector<std::pair<int, long>>> frow(h->N), brow(h->N);
+  std::vector<dpgo::BlockCholesky> Ls(h->K);
+  long blocks = 0;
+  for (int a = 0; a < h->K; ++a) {
+    HostBSR Q;
+    agent_bsr(h, a, Q);
+    std::string err;
+    if (dpgo::block_cholesky(h->n_agent[a], b, Q.rowptr, Q.col, Q.blocks, 0.1, kMaxCholBlocks - blocks, Ls[a], err) !=
+        0) {
+      if (err.find("positive definite") != std::string::npos) {
+        // src/QuadraticProblem.cpp:81-86: the solve fails -> "Preconditioner failed", out = in
+        std::printf("[dpgo_hip] Preconditioner failed (agent %d: %s); using the identity.\n", a, err.c_str());
+        h->chol_state = 2;
+        return DPGO_HIP_OK;
+      }
+      return fail(DPGO_HIP_EINVAL, err);
+    }
+    blocks += static_cast<long>(Ls[a].rowidx.size());
+  }
+  for (int a = 0; a < h->K; ++a) {
+    const dpgo::BlockCholesky& L = Ls[a];
+    const long off = h->pose_off[a];
+    auto G = [&](int newi) { return static_cast<int>(off + L.perm[newi]); };
+    std::vector<int> lf(L.n, 0), lb(L.n, 0);
+    for (int k = 0; k < L.n; ++k) {
+      for (int p = L.colptr[k] + 1; p < L.colptr[k + 1]; ++p) {
+        const int i = L.rowidx[p];
+        lf[i] = std::max(lf[i], lf[k] + 1);
+        frow[G(i)].push_back({G(k), static_cast<long>(a) << 40 | p});  // F_ik = L_ik^T
+        brow[G(k)].push_back({G(i), static_cast<long>(a) << 40 | p});  // L_ik
+      }
+      // diagonal inverse (lower triangular) -> linv row-major
+      const double* D = &L.blocks[static_cast<size_t>(L.colptr[k]) * bb];
+      double* Iv = &linv[static_cast<size_t>(G(k)) * bb];
+      for (int c = 0; c < b; ++c) {  // column c of D^-1 by forward substitution on e_c
+        for (int u = 0; u < b; ++u) {
+          double s = (u == c) ? 1.0 : 0.0;
+          for (int w = 0; w < u; ++w) s -= D[u * b + w] * Iv[w * b + c];
+          Iv[u * b + c] = s / D[u * b + u];
+        }
+      }
+    }
+    for (int j = L.n - 1; j >= 0; --j)
+      for (int p = L.colptr[j] + 1; p < L.colptr[j + 1]; ++p) lb[j] = std::max(lb[j], lb[L.rowidx[p]] + 1);
+    for (int j = 0; j < L.n; ++j) {
+      flev[G(j)] = lf[j];
+      blev[G(j)] = lb[j];
+    }
+  }
+  auto block_of = [&](long code) -> const double* {
+    const int a = static_cast<int>(code >> 40);
+    const long p = code & ((1L << 40) - 1);
+    return &Ls[a].blocks[static_cast<size_t>(p) * bb];
+  };
+  for (long j = 0; j < h->N; ++j) {
+    for (auto& [k, code] : frow[j]) {
+      fcol.push_back(k);
+      const double* Lb = block_of(code);
+      for (int u = 0; u < b; ++u)
+        for (int v = 0; v < b; ++v) fblk.push_back(Lb[v * b + u]);  // transpose
+    }
+    fptr[j + 1] = static_cast<int>(fcol.size());
+    for (auto& [i, code] : brow[j]) {
+      bcol.push_back(i);
+      const double* Lb = block_of(code);
+      bblk.insert(bblk.end(), Lb, Lb + bb);
+    }
+    bptr[j + 1] = static_cast<int>(bcol.size());
+  }
+  auto schedule = [&](const std::vector<int>& lev, std::vector<int>& rows, std::vector<int>& lptr) {
+    int nl = 0;
+    for (int x : lev) nl = std::max(nl, x + 1);
+    lptr.assign(nl + 1, 0);
+    for (int x : lev) ++lptr[x + 1];
+    for (int l = 0; l < nl; ++l) lptr[l + 1] += lptr[l];
+    rows.assign(lev.size(), 0);
+    std::vector<int> fill(lptr.begin(), lptr.end() - 1);
+    for (long j = 0; j < static_cast<long>(lev.size()); ++j) rows[fill[lev[j]]++] = static_cast<int>(j);
+  };
+  std::vector<int> frows, brows;
+  schedule(flev, frows, h->fw_lvl);
+  schedule(blev, brows, h->bw_lvl);
+  auto up_i = [&](DevBuf<int>& d, const std::vector<int>& v) -> int {
+    HIP_TRY(d.ensure(std::max<size_t>(v.size(), 1)));
+    if (!v.empty()) HIP_TRY(hipMemcpyAsync(d.p, v.data(), sizeof(int) * v.size(), hipMemcpyHostToDevice, h->stream));
+    return DPGO_HIP_OK;
+  };
+  auto up_d = [&](DevBuf<double>& d, const std::vector<double>& v) -> int {
+    HIP_TRY(d.ensure(std::max<size_t>(v.size(), 1)));
+    if (!v.empty())
+      HIP_TRY(hipMemcpyAsync(d.p, v.data(), sizeof(double) * v.size(), hipMemcpyHostToDevice, h->stream));
+    return DPGO_HIP_OK;
+  };
+  DPGO_TRY(up_i(h->fw_ptr, fptr));
+  DPGO_TRY(up_i(h->fw_col, fcol));
+  DPGO_TRY(up_d(h->fw_blk, fblk));
+  DPGO_TRY(up_i(h->bw_ptr, bptr));
+  DPGO_TRY(up_i(h->bw_col, bcol));
+  DPGO_TRY(up_d(h->bw_blk, bblk));
+  DPGO_TRY(up_d(h->linv, linv));
+  DPGO_TRY(up_i(h->fw_rows, frows));
+  DPGO_TRY(up_i(h->bw_rows, brows));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  h->chol_blocks = blocks;
+  h->chol_state = 1;
+  return DPGO_HIP_OK;
+}
+
+// z = P_X(in (Q + 0.1 I)^-1) for every agent (QuadraticProblem::PreConditioner, :75-87): forward
+// and backward level sweeps into the tA / tB work vectors, then projection + partials <z, rref>,
+// |rref|^2 (pass rref = in).  With a failed factorisation z = in, unprojected, as the reference.
+int exact_precond(dpgo_hip_problem h, const double* in, double* z_out, double* delta_out, const double* X,
+                  const double* rref, double* partials, int flag) {
+  DPGO_TRY(sync_chol(h));
+  const double* zraw = in;
+  if (h->chol_state == 1) {
+    const dpgo::TrsvView fw{h->fw_ptr.p, h->fw_col.p, h->fw_blk.p, h->linv.p, 1};
+    const dpgo::TrsvView bw{h->bw_ptr.p, h->bw_col.p, h->bw_blk.p, h->linv.p, 0};
+    for (size_t l = 0; l + 1 < h->fw_lvl.size(); ++l)
+      HIP_TRY(dpgo::launch_trsv_level(h->r, h->b, fw, h->fw_rows.p + h->fw_lvl[l], h->fw_lvl[l + 1] - h->fw_lvl[l], in,
+                                      h->tA.p, h->stream));
+    for (size_t l = 0; l + 1 < h->bw_lvl.size(); ++l)
+      HIP_TRY(dpgo::launch_trsv_level(h->r, h->b, bw, h->bw_rows.p + h->bw_lvl[l], h->bw_lvl[l + 1] - h->bw_lvl[l],
+                                      h->tA.p, h->tB.p, h->stream));
+    zraw = h->tB.p;
+  }
+  auto c = make_ctx(h, flag, partials);
+  HIP_TRY(dpgo::launch_precond_finish(h->r, h->b, c, X, zraw, rref, h->chol_state == 1 ? 1 : 0, z_out, delta_out));
   return DPGO_HIP_OK;
 }
 
@@ -511,9 +685,8 @@ int dpgo_hip_problem_info(dpgo_hip_problem h, int* num_agents, int* total_poses,
 
 int dpgo_hip_set_precon(dpgo_hip_problem h, int mode) {
   DPGO_TRY(check_handle(h));
-  if (mode == DPGO_PRECON_EXACT)
-    return fail(DPGO_HIP_EINVAL, "exact sparse-Cholesky preconditioner not implemented yet (SURVEY 8f-1); use BLOCK_JACOBI");
-  if (mode != DPGO_PRECON_BLOCK_JACOBI && mode != DPGO_PRECON_NONE) return fail(DPGO_HIP_EINVAL, "bad preconditioner mode");
+  if (mode != DPGO_PRECON_EXACT && mode != DPGO_PRECON_BLOCK_JACOBI && mode != DPGO_PRECON_NONE)
+    return fail(DPGO_HIP_EINVAL, "bad preconditioner mode");
   h->precon = mode;
   return DPGO_HIP_OK;
 }
@@ -730,13 +903,14 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
     P = *params;
   else
     dpgo_hip_default_params(&P);
-  if (P.precon == DPGO_PRECON_EXACT)
-    return fail(DPGO_HIP_EINVAL, "exact sparse-Cholesky preconditioner not implemented yet (SURVEY 8f-1); use BLOCK_JACOBI");
   if (P.tr_iterations < 1 || P.tr_max_inner < 0) return fail(DPGO_HIP_EINVAL, "bad optimizer parameters");
   DPGO_TRY(ensure_work(h));
   const auto t0 = std::chrono::high_resolution_clock::now();
   const int r = h->r, b = h->b, K = h->K;
-  const int pmode = P.precon == DPGO_PRECON_NONE ? dpgo::PRECON_NONE : dpgo::PRECON_BLOCK_JACOBI;
+  const bool exact = P.precon == DPGO_PRECON_EXACT;
+  if (exact) DPGO_TRY(sync_chol(h));
+  // the exact solve runs as its own stages; the fused tCG kernels then see the identity
+  const int pmode = P.precon == DPGO_PRECON_BLOCK_JACOBI ? dpgo::PRECON_BLOCK_JACOBI : dpgo::PRECON_NONE;
   std::vector<int> en(K, 1);
   if (agent_enabled_host)
     for (int a = 0; a < K; ++a) en[a] = agent_enabled_host[a] != 0;
@@ -766,7 +940,7 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
   o.single_run = single ? 1 : 0;
   // f(x1), grad(x1), S(x1)  (QuadraticOptimizer::optimize :36-37, SolversTR start); for RTR the
   // first tCG start (delta = -Prec(grad), <z, grad>) is fused into the same pass
-  const bool fused_tcg = P.algorithm == DPGO_ALG_RTR && P.tr_max_inner > 0;
+  const bool fused_tcg = P.algorithm == DPGO_ALG_RTR && P.tr_max_inner > 0 && !exact;
   if (fused_tcg) {
     DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_NONE, dpgo::MODE_EVAL_TCG, h->delta.p, pmode));
     DPGO_TRY(finalize(h, dpgo::OP_EVAL_TCG_INIT, h->pa.p, 3, nullptr, 0, &o, h->enabled.p));
@@ -820,8 +994,12 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
   for (int round = 0; round < max_rounds; ++round) {
     // ---- truncated CG (A.4)
     if (round > 0 || !fused_tcg) {
-      auto ci = make_ctx(h, dpgo::FLAG_RUN, h->pa.p);
-      HIP_TRY(dpgo::launch_tcg_init(r, b, ci, x1, h->minv.p, pmode, h->g.p, h->delta.p));
+      if (exact) {  // delta = -P_X(g P^-1), partials <z, g>, |g|^2
+        DPGO_TRY(exact_precond(h, h->g.p, nullptr, h->delta.p, x1, h->g.p, h->pa.p, dpgo::FLAG_RUN));
+      } else {
+        auto ci = make_ctx(h, dpgo::FLAG_RUN, h->pa.p);
+        HIP_TRY(dpgo::launch_tcg_init(r, b, ci, x1, h->minv.p, pmode, h->g.p, h->delta.p));
+      }
       DPGO_TRY(finalize(h, dpgo::OP_TCG_INIT, h->pa.p, 2, nullptr, 0, &o));
     }
     std::vector<int> tags;
@@ -833,6 +1011,8 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
       auto cu = make_ctx(h, dpgo::FLAG_TCG_MODE, h->pb.p);
       HIP_TRY(dpgo::launch_tcg_update(r, b, cu, x1, h->minv.p, pmode, h->delta.p, h->Hdelta.p, h->eta.p,
                                       h->Heta.p, j == 0 ? h->g.p : h->rv.p, h->rv.p, h->z.p, j == 0 ? 1 : 0));
+      if (exact)  // z = Prec(r) with the factor; replaces the identity z and its partials
+        DPGO_TRY(exact_precond(h, h->rv.p, h->z.p, nullptr, x1, h->rv.p, h->pb.p, dpgo::FLAG_TCG_MODE));
       const int tag = next_tag(h);
       tags.push_back(tag);
       DPGO_TRY(finalize(h, dpgo::OP_TCG_CHECK, h->pb.p, 2, nullptr, 0, &o, nullptr, 1, tag));
@@ -984,6 +1164,11 @@ int dpgo_hip_precondition(dpgo_hip_problem h, const double* X, const double* V, 
   DPGO_TRY(io.init(h));
   DPGO_TRY(upload(io.a.p, X, h->vec_len(), h->stream));
   DPGO_TRY(upload(io.b.p, V, h->vec_len(), h->stream));
+  if (h->precon == DPGO_PRECON_EXACT) {
+    DPGO_TRY(ensure_work(h));
+    DPGO_TRY(exact_precond(h, io.b.p, io.c.p, nullptr, io.a.p, io.b.p, nullptr, dpgo::FLAG_NONE));
+    return download(out, io.c.p, h->vec_len(), h->stream);
+  }
   auto c = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
   const int pmode = h->precon == DPGO_PRECON_NONE ? dpgo::PRECON_NONE : dpgo::PRECON_BLOCK_JACOBI;
   HIP_TRY(dpgo::launch_precond(h->r, h->b, c, io.a.p, h->minv.p, pmode, io.b.p, io.c.p));

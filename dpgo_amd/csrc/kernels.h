@@ -117,6 +117,18 @@ struct GEdges {
   const double* w;
 };
 
+// One triangle of the exact preconditioner's block factor P = L L^T, as block rows over batch-global
+// pose indices (chol.cpp): forward rows hold F_jk = L_jk^T (k earlier in the elimination order),
+// backward rows hold L_ij (i later); blocks row-major so lane k reads row k.  dinv = L_jj^-1
+// row-major; the forward pass applies L_jj^-T (reads it transposed).
+struct TrsvView {
+  const int* ptr;
+  const int* col;
+  const double* blk;
+  const double* dinv;
+  int forward;
+};
+
 // Runtime-selectable kernel variants (A/B tuning in one process; see tools/spmm_ab.py).
 enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_COUNT = 4 };
 // variant of the edge-stream SpMM used unless TUNE_EDGE_VARIANT overrides it (bit 0: XCD-aware
@@ -154,6 +166,13 @@ hipError_t launch_select(int r, int b, const LaunchCtx& c, const double* A, cons
 hipError_t launch_accept(int r, int b, const LaunchCtx& c, const double* x2, const double* g2, const double* S2,
                          double* x1, double* g, double* S);
 hipError_t launch_finalize(const FinalizeArgs& f, int num_agents, hipStream_t stream);
+// sol[j] = (rhs[j] - sum_k sol[k] blk_jk) dinv_j for the `count` poses rows[] of one level
+hipError_t launch_trsv_level(int r, int b, const TrsvView& t, const int* rows, int count, const double* rhs,
+                             double* sol, hipStream_t stream);
+// z = P_X(zraw) (or z = zraw when project == 0); optional z_out / delta_out = -z; partials
+// <z, rref>, |rref|^2 per tile
+hipError_t launch_precond_finish(int r, int b, const LaunchCtx& c, const double* X, const double* zraw,
+                                 const double* rref, int project, double* z_out, double* delta_out);
 hipError_t launch_bj_inverse(int b, int n, const QView& q, double shift, double* Minv, hipStream_t stream);
 hipError_t launch_bj_inverse_diag(int b, int n, const QView& q, double shift, double* Minv, hipStream_t stream);
 

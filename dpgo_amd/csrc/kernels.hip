@@ -1104,6 +1104,107 @@ __global__ __launch_bounds__(kThreads) void k_bj_inverse_diag(int n, QView q, do
 }
 
 // ------------------------------------------------------------------------------------------
+// Exact preconditioner (QuadraticProblem::PreConditioner with the Cholesky factor of Q + 0.1 I,
+// src/QuadraticProblem.cpp:37-41, 75-87): level-scheduled block triangular solves.  In row form
+// the r right-hand sides are the pose blocks themselves: forward Y_j = (V_j - sum_k Y_k L_jk^T)
+// L_jj^-T, backward Z_j = (Y_j - sum_i Z_i L_ij) L_jj^-1.  One quad per pose row, outer-product
+// accumulation + quad reduce-scatter as in the SpMM; every row of a level is independent.
+// ------------------------------------------------------------------------------------------
+template <int R, int B>
+__global__ __launch_bounds__(kThreads) void k_trsv_level(TrsvView t, const int* __restrict__ rows, int count,
+                                                         const double* __restrict__ rhs, double* __restrict__ sol) {
+  const int k = threadIdx.x & 3;
+  const int q = blockIdx.x * (kThreads / 4) + (threadIdx.x >> 2);
+  if (q >= count) return;  // whole quad leaves together
+  const int kc = k < B ? k : 0;
+  const long j = rows[q];
+  double acc[R][B];
+#pragma unroll
+  for (int a = 0; a < R; ++a)
+#pragma unroll
+    for (int c = 0; c < B; ++c) acc[a][c] = 0.0;
+  for (int z = t.ptr[j]; z < t.ptr[j + 1]; ++z) {
+    const long i = t.col[z];
+    const double* br = t.blk + static_cast<long>(z) * (B * B) + kc * B;
+    const double* xi = sol + i * (R * B) + kc * R;
+    double x[R], bk[B];
+#pragma unroll
+    for (int a = 0; a < R; ++a) x[a] = xi[a];
+#pragma unroll
+    for (int c = 0; c < B; ++c) bk[c] = br[c];
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int c = 0; c < B; ++c) acc[a][c] = fma(x[a], bk[c], acc[a][c]);
+  }
+  const bool act = k < B;
+#pragma unroll
+  for (int a = 0; a < R; ++a)
+#pragma unroll
+    for (int c = 0; c < B; ++c) acc[a][c] = act ? acc[a][c] : 0.0;
+  double w[R];
+  quad_reduce_scatter<R, B>(acc, k, w);  // lane c: column c of sum_k sol_k blk_jk
+  const double* rj = rhs + j * (R * B) + kc * R;
+#pragma unroll
+  for (int a = 0; a < R; ++a) w[a] = rj[a] - w[a];
+  // times the diagonal inverse: lane u contributes w[:, u] (x) Dinv[u, :]
+  double dv[B];
+  const double* dj = t.dinv + j * (B * B);
+#pragma unroll
+  for (int c = 0; c < B; ++c) dv[c] = t.forward ? dj[c * B + kc] : dj[kc * B + c];
+#pragma unroll
+  for (int a = 0; a < R; ++a)
+#pragma unroll
+    for (int c = 0; c < B; ++c) acc[a][c] = act ? w[a] * dv[c] : 0.0;
+  double y[R];
+  quad_reduce_scatter<R, B>(acc, k, y);
+  if (act) {
+    double* sj = sol + j * (R * B) + k * R;
+#pragma unroll
+    for (int a = 0; a < R; ++a) sj[a] = y[a];
+  }
+}
+
+template <int R, int B>
+__global__ __launch_bounds__(kThreads) void k_precond_finish(LaunchCtx c, const double* __restrict__ X,
+                                                             const double* __restrict__ zraw,
+                                                             const double* __restrict__ rref, int project,
+                                                             double* __restrict__ z_out,
+                                                             double* __restrict__ delta_out) {
+  constexpr int D = B - 1;
+  const PoseLane p = pose_lane<B>(c);
+  if (tile_skipped(c, p.agent)) return;
+  const bool own = p.ok && p.k < B;
+  const long off = p.j * (R * B) + p.k * R;
+  double zc[R], xc[R], rc[R];
+  load_col<R, B>(zraw, p.j, p.k, p.ok, zc);
+  load_col<R, B>(X, p.j, p.k, p.ok, xc);
+  load_col<R, B>(rref, p.j, p.k, p.ok, rc);
+  double z[R];
+  if (project) {
+    double Yf[R][D];
+    quad_gather_y<R, D>(xc, Yf);
+    double S[D][D];
+    sym_ytm_cols<R, D>(Yf, zc, S);
+    sub_y_times_col<R, D>(Yf, S, p.k, zc, z);
+  } else {
+#pragma unroll
+    for (int a = 0; a < R; ++a) z[a] = zc[a];
+  }
+  double zr = 0.0, rr = 0.0, dc[R];
+#pragma unroll
+  for (int a = 0; a < R; ++a) {
+    zr = fma(z[a], rc[a], zr);
+    rr = fma(rc[a], rc[a], rr);
+    dc[a] = -z[a];
+  }
+  if (z_out != nullptr) store_vec<R>(z_out, off, own, z);
+  if (delta_out != nullptr) store_vec<R>(delta_out, off, own, dc);
+  double parts[2] = {own ? zr : 0.0, own ? rr : 0.0};
+  if (c.partials != nullptr) block_partials<2>(parts, c.partials, p.tile);
+}
+
+// ------------------------------------------------------------------------------------------
 // Public-pose exchange helpers (PGOAgent::getSharedPoseDict / updateNeighborPoses,
 // src/PGOAgent.cpp:95-118, 434-479): dst[s] = pose idx[s] of A (idx >= 0) or of B (-1 - idx).
 // ------------------------------------------------------------------------------------------
@@ -1330,6 +1431,22 @@ hipError_t launch_assemble_G(int r, int b, const GEdges& e, int nslots, const do
   const long total = static_cast<long>(nslots) * r;
   const int grid = static_cast<int>((total + kThreads - 1) / kThreads);
   DPGO_DISPATCH(r, b, (k_assemble_G<R, B><<<grid, kThreads, 0, stream>>>(e, nslots, Xa, Xb, gblk)));
+  return hipGetLastError();
+}
+
+hipError_t launch_trsv_level(int r, int b, const TrsvView& t, const int* rows, int count, const double* rhs,
+                             double* sol, hipStream_t stream) {
+  if (count == 0) return hipSuccess;
+  const int grid = (count + kThreads / 4 - 1) / (kThreads / 4);
+  DPGO_DISPATCH(r, b, (k_trsv_level<R, B><<<grid, kThreads, 0, stream>>>(t, rows, count, rhs, sol)));
+  return hipGetLastError();
+}
+
+hipError_t launch_precond_finish(int r, int b, const LaunchCtx& c, const double* X, const double* zraw,
+                                 const double* rref, int project, double* z_out, double* delta_out) {
+  if (c.num_tiles == 0) return hipSuccess;
+  DPGO_DISPATCH(r, b, (k_precond_finish<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, zraw, rref, project, z_out,
+                                                                                      delta_out)));
   return hipGetLastError();
 }
 

@@ -99,6 +99,13 @@ struct dpgo_hip_problem_s {
 
   int precon = DPGO_PRECON_BLOCK_JACOBI;
 
+  // exact preconditioner: block Cholesky of Q + 0.1 I (chol.cpp), level-scheduled solves
+  int chol_state = 0;  // 0 stale, 1 ready, 2 Q + 0.1 I not positive definite (identity, as the reference)
+  dpgo::DevBuf<int> fw_ptr, fw_col, bw_ptr, bw_col, fw_rows, bw_rows;
+  dpgo::DevBuf<double> fw_blk, bw_blk, linv;
+  std::vector<int> fw_lvl, bw_lvl;  // level pointers into fw_rows / bw_rows
+  long chol_blocks = 0;
+
   // work
   dpgo::DevBuf<double> x1, x2, g, g2, S, S2, eta, Heta, rv, z, delta, Hdelta, tA, tB;
   dpgo::DevBuf<double> pa, pb, sums, coef_a, coef_b;

@@ -37,8 +37,10 @@ extern "C" {
 #define DPGO_HIP_ESTATE (-5)
 
 /* Preconditioner modes (QuadraticProblem::PreConditioner, src/QuadraticProblem.cpp:75-87).
- * EXACT (the reference's CHOLMOD factor of Q + 0.1 I) is SURVEY 8f "next" and currently returns
- * DPGO_HIP_EINVAL; BLOCK_JACOBI applies the per-pose (Q_jj + 0.1 I)^-1 (north_star deviation). */
+ * EXACT: the reference's own -- P_X(V (Q + 0.1 I)^-1) with a block Cholesky factor built on the
+ * host once per Q (nested dissection order) and level-scheduled triangular solves on the GPU; if
+ * Q + 0.1 I is not positive definite it falls back to the identity, as the reference does (:81-86).
+ * BLOCK_JACOBI: per-pose (Q_jj + 0.1 I)^-1 (the north_star's throughput choice). NONE: identity. */
 #define DPGO_PRECON_EXACT 0
 #define DPGO_PRECON_BLOCK_JACOBI 1
 #define DPGO_PRECON_NONE 2

@@ -92,6 +92,14 @@ def rtr_fixture(name, meas, r, precon, iters, tol, radius, inner):
                                            for k, v in res.items()}))
 
 
+def multirobot_exact(meas):
+    """The same loop with the reference's own preconditioner (exact factor of Q + 0.1 I), which the
+    C++ drop-in uses by default."""
+    log, Xf = O.multi_robot_example(meas, 5, num_iters=30, precon=O.PRECON_EXACT)
+    np.savez_compressed(os.path.join(HERE, "smallGrid3D.multirobot5.exact.npz"),
+                        log=np.array(log, dtype=float), Xfinal=Xf)
+
+
 def main():
     for name in DATASETS:
         meas = O.read_g2o(os.path.join(REF_DATA, f"{name}.g2o"))
@@ -107,6 +115,7 @@ def main():
     log, Xf = O.multi_robot_example(meas, 5, num_iters=30, precon=O.PRECON_BLOCK_JACOBI)
     np.savez_compressed(os.path.join(HERE, "smallGrid3D.multirobot5.npz"),
                         log=np.array(log, dtype=float), Xfinal=Xf)
+    multirobot_exact(meas)
     # plain-text copies for the C++ test program (tests/cpp/test_dpgo.cpp)
     with open(os.path.join(HERE, "smallGrid3D.meas.txt"), "w") as f:
         f.write(f"{meas.d} {meas.num_poses} {meas.m}\n")
@@ -126,4 +135,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "multirobot_exact":
+        multirobot_exact(load_meas("smallGrid3D"))
+    else:
+        main()

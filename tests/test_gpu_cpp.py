@@ -29,12 +29,13 @@ def test_cpp_case(cpp_output, name):
 
 
 def test_cpp_multirobot_matches_oracle(cpp_output):
-    """examples/MultiRobotExample.cpp loop (5 robots, Nesterov, GNC_TLS defaults) through the C++
-    drop-in on the GPU vs the oracle's restatement: same greedy robot sequence, same costs."""
+    """examples/MultiRobotExample.cpp loop (5 robots, Nesterov, GNC_TLS defaults, the reference's exact
+    preconditioner) through the C++ drop-in on the GPU vs the oracle's restatement: same greedy robot
+    sequence, same costs."""
     rc, out = cpp_output
     rows = [l.split() for l in out.splitlines() if l.startswith("ITER ")]
     got = np.array([[float(x) for x in r[1:]] for r in rows])
-    ref = np.load(os.path.join(GOLDEN, "smallGrid3D.multirobot5.npz"))["log"]
+    ref = np.load(os.path.join(GOLDEN, "smallGrid3D.multirobot5.exact.npz"))["log"]
     assert got.shape == ref.shape
     assert np.array_equal(got[:, 1], ref[:, 1]), "greedy selection sequence differs"
     assert np.max(np.abs(got[:, 2] - ref[:, 2]) / ref[:, 2]) <= 1e-9

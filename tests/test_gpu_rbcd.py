@@ -21,9 +21,9 @@ def _graph_from_meas(H, meas):
                                meas.kappa, meas.tau)
 
 
-def _run_engine(H, g, agent_of_pose, num_agents, X0, iters, accel, r):
+def _run_engine(H, g, agent_of_pose, num_agents, X0, iters, accel, r, **kw):
     e = H.Rbcd(g, agent_of_pose, np.zeros(num_agents, np.int32), 0, 1,
-               H.rbcd_params(r=r, acceleration=int(accel)))
+               H.rbcd_params(r=r, acceleration=int(accel), **kw))
     e.set_X(X0)
     for it in range(iters):
         c = it % e.num_colors
@@ -75,3 +75,20 @@ def test_laplacian_and_reader(hip):
     Q = O.connection_laplacian(meas, meas.num_poses)
     Qb = sp.bsr_matrix((blk.reshape(-1, 4, 4).transpose(0, 2, 1), col, rp), shape=Q.shape)
     assert abs(Qb - Q).max() <= 1e-12 * abs(Q).max()
+
+
+@pytest.mark.parametrize("qfmt", ["edges", "bsr"])
+def test_grid_cubes_exact_precon(hip, qfmt):
+    """The engine with the reference's exact preconditioner (per-agent factor of Q + 0.1 I), Nesterov,
+    both device forms of Q, against the oracle's colour schedule with the exact preconditioner."""
+    k, A, r = 6, 2, 5
+    g = hip.Graph.grid3d(k, seed=3)
+    a = g.arrays()
+    meas = O.Measurements(3, np.zeros(g.m, np.int64), np.zeros(g.m, np.int64), a["p1"].astype(np.int64),
+                          a["p2"].astype(np.int64), a["R"], a["t"], a["kappa"], a["tau"], np.ones(g.m), g.n)
+    aop = g.grid_partition(A)
+    X0 = g.chain_init(r, O.lifting_matrix(3, r))
+    Xh, e = _run_engine(hip, g, aop, A ** 3, X0, 6, True, r, precon=hip.PRECON_EXACT,
+                        q_format=hip.QFMT_EDGES if qfmt == "edges" else hip.QFMT_BSR)
+    Xo, _ = O.colour_rbcd(meas, aop, A ** 3, X0, 6, r, acceleration=True, precon=O.PRECON_EXACT)
+    assert rel(Xh, Xo) <= 1e-9
