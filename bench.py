@@ -66,6 +66,9 @@ def main():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-sample-updates", type=int, default=40)
     ap.add_argument("--verify", type=int, default=0, help="central cost before/after (slow)")
+    ap.add_argument("--robust", default="L2", choices=["L2", "GNC_TLS", "TLS", "Huber", "GM", "L1"],
+                    help="robust cost (L2: throughput setting; GNC_TLS: the reference default, "
+                         "reweighting every 30 iterations on the device)")
     args = ap.parse_args()
 
     import torch
@@ -88,7 +91,7 @@ def main():
     aop = g.grid_partition(A)
     num_agents = A ** 3
     agent_rank = super_cube_ranks(A, world)
-    params = H.rbcd_params(r=args.r, acceleration=args.accel)
+    params = H.rbcd_params(r=args.r, acceleration=args.accel, robust_cost=H.ROBUST[args.robust])
     eng = H.Rbcd(g, aop, agent_rank, rank, world, params)
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
@@ -152,7 +155,7 @@ def main():
         "data": "synthetic (repo-defined grid3d, SplitMix64 seed 0; no reference data at this size)",
         "config": {"workload": f"grid3d k={args.k} ({args.k ** 3} poses), r={args.r}, "
                                f"{num_agents} agents ({A}^3 sub-cubes), Nesterov={bool(args.accel)}, "
-                               f"L2 cost, colour schedule ({eng.num_colors} colours), "
+                               f"{args.robust} cost, colour schedule ({eng.num_colors} colours), "
                                f"RTR 1x10 tCG, block-Jacobi precond",
                    "poses": g.n, "edges": g.m, "agents": num_agents,
                    "parallelism": f"agents over {world} GPU(s), RCCL all_to_all halo"},

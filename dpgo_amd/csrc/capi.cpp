@@ -146,6 +146,41 @@ int sync_q_edges(dpgo_hip_problem h) {
     }
   for (long j = 0; j < h->N; ++j)
     std::sort(inc.begin() + deg[j], inc.begin() + deg[j + 1], [](const int2& x, const int2& y) { return x.x < y.x; });
+  // reweighting tables: raw unweighted measurement per slot, edge -> slot, all incidences per pose
+  const int RAW = d * d + d + 2;
+  std::vector<double> raw(std::max<long>(m, 1) * RAW, 0.0);
+  std::vector<int> dptr(h->N + 1, 0), dinc;
+  {
+    long eg = 0;
+    for (int a = 0; a < h->K; ++a) {
+      const HostEdges& E = h->e_agent[a];
+      for (size_t e = 0; e < E.p1.size(); ++e, ++eg) {
+        double* q = &raw[static_cast<size_t>(newid[eg]) * RAW];
+        std::memcpy(q, &E.R[e * d * d], sizeof(double) * d * d);
+        std::memcpy(q + d * d, &E.t[e * d], sizeof(double) * d);
+        q[d * d + d] = E.kappa0[e];
+        q[d * d + d + 1] = E.tau0[e];
+        if (gp1[eg] >= 0) ++dptr[gp1[eg] + 1];
+        if (gp2[eg] >= 0) ++dptr[gp2[eg] + 1];
+      }
+    }
+    for (long j = 0; j < h->N; ++j) dptr[j + 1] += dptr[j];
+    dinc.assign(std::max(dptr[h->N], 1), 0);
+    std::vector<int> dfill(dptr.begin(), dptr.end() - 1);
+    for (long e = 0; e < m; ++e) {  // edge order, p1 side then p2 side, as the host accumulation
+      if (gp1[e] >= 0) dinc[dfill[gp1[e]]++] = 2 * newid[e] + 1;
+      if (gp2[e] >= 0) dinc[dfill[gp2[e]]++] = 2 * newid[e];
+    }
+  }
+  HIP_TRY(h->raw.ensure(raw.size()));
+  HIP_TRY(h->slot_of_edge.ensure(std::max<long>(m, 1)));
+  HIP_TRY(h->dinc_ptr.ensure(h->N + 1));
+  HIP_TRY(h->dinc.ensure(dinc.size()));
+  HIP_TRY(hipMemcpyAsync(h->raw.p, raw.data(), sizeof(double) * raw.size(), hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(h->slot_of_edge.p, newid.data(), sizeof(int) * std::max<long>(m, 1), hipMemcpyHostToDevice,
+                         h->stream));
+  HIP_TRY(hipMemcpyAsync(h->dinc_ptr.p, dptr.data(), sizeof(int) * (h->N + 1), hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(h->dinc.p, dinc.data(), sizeof(int) * dinc.size(), hipMemcpyHostToDevice, h->stream));
   std::vector<double> diag(static_cast<size_t>(h->N) * DW);
   for (long p = 0; p < h->N; ++p) {
     int o = 0;
@@ -255,6 +290,20 @@ void agent_bsr(dpgo_hip_problem h, int a, HostBSR& out) {
 
 int sync_chol(dpgo_hip_problem h) {
   if (h->chol_state != 0) return DPGO_HIP_OK;
+  if (h->host_weights_stale) {  // weights changed on the device: bring the host measurement copy up to date
+    std::vector<double> w(std::max<long>(h->num_edges, 1));
+    HIP_TRY(hipMemcpyAsync(w.data(), h->w_dev_last, sizeof(double) * h->num_edges, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    long eg = 0;
+    for (int a = 0; a < h->K; ++a) {
+      HostEdges& E = h->e_agent[a];
+      for (size_t e = 0; e < E.p1.size(); ++e, ++eg) {
+        E.kw[e] = w[eg] * E.kappa0[e];
+        E.tw[e] = w[eg] * E.tau0[e];
+      }
+    }
+    h->host_weights_stale = false;
+  }
   const int b = h->b, bb = b * b;
   std::vector<int> fptr(h->N + 1, 0), bptr(h->N + 1, 0), fcol, bcol, flev(h->N, 0), blev(h->N, 0);
   std::vector<double> fblk, bblk, linv(static_cast<size_t>(h->N) * bb, 0.0);
@@ -728,6 +777,8 @@ int dpgo_hip_set_Q_edges(dpgo_hip_problem h, int agent, int m, const int* p1, co
   E.t.assign(t, t + static_cast<size_t>(m) * d);
   E.kw.resize(m);
   E.tw.resize(m);
+  E.kappa0.resize(m);
+  E.tau0.resize(m);
   for (int e = 0; e < m; ++e) {
     const int i = p1[e], j = p2[e];
     if (i < -1 || i >= na || j < -1 || j >= na) return fail(DPGO_HIP_EINVAL, "edge endpoint out of range");
@@ -736,6 +787,8 @@ int dpgo_hip_set_Q_edges(dpgo_hip_problem h, int agent, int m, const int* p1, co
     const double w = weight ? weight[e] : 1.0;
     E.kw[e] = w * kappa[e];  // the BSR assembly's Omega = diag(w kappa, w tau) (edge_blocks)
     E.tw[e] = w * tau[e];
+    E.kappa0[e] = kappa[e];
+    E.tau0[e] = tau[e];
   }
   h->e_agent[agent] = std::move(E);
   h->q_agent[agent] = HostBSR();
@@ -1241,6 +1294,23 @@ double dpgo_hip_spmm_bytes(dpgo_hip_problem h) {
   for (int a = 0; a < h->K; ++a) nnz += static_cast<long>(h->q_agent[a].col.size());
   return static_cast<double>(nnz) * (b * b * 8.0 + 4.0) + static_cast<double>(h->N + 1) * 4.0 +
          2.0 * static_cast<double>(h->r) * b * static_cast<double>(h->N) * 8.0;
+}
+
+int dpgo_hip_set_edge_weights_dev(dpgo_hip_problem h, const double* w_dev) {
+  DPGO_TRY(check_handle(h));
+  if (!w_dev) return fail(DPGO_HIP_EINVAL, "null weights");
+  for (int a = 0; a < h->K; ++a)
+    if (h->q_fmt[a] != dpgo::QFMT_EDGES) return fail(DPGO_HIP_ESTATE, "edge weights need an edge-stream Q (set_Q_edges)");
+  DPGO_TRY(ready(h));
+  HIP_TRY(h->wslot.ensure(std::max<long>(h->num_edges, 1)));
+  HIP_TRY(dpgo::launch_edge_reweight(h->d, static_cast<int>(h->num_edges), static_cast<int>(h->N), h->raw.p,
+                                     h->slot_of_edge.p, w_dev, h->dinc_ptr.p, h->dinc.p, h->wslot.p, h->rec.p,
+                                     h->diag.p, h->stream));
+  HIP_TRY(dpgo::launch_bj_inverse_diag(h->b, static_cast<int>(h->N), qview(h), 0.1, h->minv.p, h->stream));
+  h->chol_state = 0;  // the exact factor follows Q
+  h->host_weights_stale = true;
+  h->w_dev_last = w_dev;
+  return DPGO_HIP_OK;
 }
 
 double dpgo_hip_spmm_bytes_bsr(dpgo_hip_problem h) {

@@ -129,6 +129,26 @@ struct TrsvView {
   int forward;
 };
 
+// Loop closures one engine colour class reweights (PGOAgent::updateLoopClosuresWeights,
+// src/PGOAgent.cpp:1181-1244): pose sources >= 0 index the engine's X buffer, < 0 -> (-1 - s) the
+// received-pose buffer; weights go to the colour problem's edge and, for shared edges, its G entry.
+struct GncEntries {
+  int n;
+  const int* prob_edge;
+  const int* g_entry;  // -1: private loop closure
+  const int* src1;
+  const int* src2;
+  const double* R;  // d*d row-major
+  const double* t;
+  const double* kappa;
+  const double* tau;
+};
+// RobustCost::weight (src/DPGO_robust.cpp:23-67) parameters; type = DPGO_ROBUST_*
+struct RobustParams {
+  int type;
+  double mu, barc, huber, tls;
+};
+
 // Runtime-selectable kernel variants (A/B tuning in one process; see tools/spmm_ab.py).
 enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_COUNT = 4 };
 // variant of the edge-stream SpMM used unless TUNE_EDGE_VARIANT overrides it (bit 0: XCD-aware
@@ -174,6 +194,13 @@ hipError_t launch_trsv_level(int r, int b, const TrsvView& t, const int* rows, i
 hipError_t launch_precond_finish(int r, int b, const LaunchCtx& c, const double* X, const double* zraw,
                                  const double* rref, int project, double* z_out, double* delta_out);
 hipError_t launch_bj_inverse(int b, int n, const QView& q, double shift, double* Minv, hipStream_t stream);
+// Rebuild the edge-stream Q on device from per-edge weights w[edge] (problem edge order): records
+// M = T diag(w kappa I, w tau) and packed diagonal blocks, the same arithmetic as the host build.
+hipError_t launch_edge_reweight(int d, int m, int n, const double* raw, const int* slot_of_edge, const double* w,
+                                const int* dinc_ptr, const int* dinc, double* wslot, double* rec, double* diag,
+                                hipStream_t stream);
+hipError_t launch_gnc_weights(int r, int b, const GncEntries& g, const double* X, const double* RX,
+                              const RobustParams& rp, double* w_prob, double* w_g, hipStream_t stream);
 hipError_t launch_bj_inverse_diag(int b, int n, const QView& q, double shift, double* Minv, hipStream_t stream);
 
 }  // namespace dpgo

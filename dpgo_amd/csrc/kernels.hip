@@ -1104,6 +1104,148 @@ __global__ __launch_bounds__(kThreads) void k_bj_inverse_diag(int n, QView q, do
 }
 
 // ------------------------------------------------------------------------------------------
+// On-device Q assembly from edge weights (PGOAgent::constructQMatrix after a GNC weight update,
+// src/PGOAgent.cpp:720-781, 1181-1244).  raw per slot = [R (row-major) | t | kappa | tau]; the
+// arithmetic mirrors edge_blocks() (graph.cpp) so the result is bitwise the host build.
+// ------------------------------------------------------------------------------------------
+template <int D>
+__device__ __forceinline__ void edge_T_Om(const double* __restrict__ q, double w, double (&T)[D + 1][D + 1],
+                                          double (&Om)[D + 1]) {
+#pragma unroll
+  for (int u = 0; u < D; ++u) {
+#pragma unroll
+    for (int v = 0; v < D; ++v) T[u][v] = q[u * D + v];
+    T[u][D] = q[D * D + u];
+    Om[u] = w * q[D * D + D];
+    T[D][u] = 0.0;
+  }
+  T[D][D] = 1.0;
+  Om[D] = w * q[D * D + D + 1];
+}
+
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_edge_records(int m, const double* __restrict__ raw,
+                                                           const int* __restrict__ slot_of_edge,
+                                                           const double* __restrict__ w, double* __restrict__ rec) {
+  constexpr int B = D + 1, RAW = D * D + D + 2, RW = edge_rec_width(D);
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= m) return;
+  const int s = slot_of_edge[e];
+  double T[B][B], Om[B];
+  edge_T_Om<D>(raw + static_cast<long>(s) * RAW, w[e], T, Om);
+  double* M = rec + static_cast<long>(s) * RW;
+#pragma unroll
+  for (int u = 0; u < B; ++u)
+#pragma unroll
+    for (int v = 0; v < B; ++v) M[4 * u + v] = -(-T[u][v] * Om[v]);  // -Wij, as the host build
+}
+
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_edge_diag(int n, const double* __restrict__ raw,
+                                                        const int* __restrict__ edge_of_slot_w,
+                                                        const double* __restrict__ wslot,
+                                                        const int* __restrict__ dinc_ptr, const int* __restrict__ dinc,
+                                                        double* __restrict__ diag) {
+  // no FMA contraction: the host build (x86-64, separate multiply and add) is reproduced bitwise
+#pragma clang fp contract(off)
+  constexpr int B = D + 1, RAW = D * D + D + 2, DW = diag_width(D);
+  const long j = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  double F[B][B];
+#pragma unroll
+  for (int u = 0; u < B; ++u)
+#pragma unroll
+    for (int v = 0; v < B; ++v) F[u][v] = 0.0;
+  for (int z = dinc_ptr[j]; z < dinc_ptr[j + 1]; ++z) {
+    const int code = dinc[z], s = code >> 1;
+    double T[B][B], Om[B];
+    edge_T_Om<D>(raw + static_cast<long>(s) * RAW, wslot[s], T, Om);
+    if (code & 1) {  // p1 side: T Omega T^T
+#pragma unroll
+      for (int u = 0; u < B; ++u)
+#pragma unroll
+        for (int v = 0; v < B; ++v) {
+          double acc = 0.0;
+#pragma unroll
+          for (int q = 0; q < B; ++q) acc += T[u][q] * Om[q] * T[v][q];
+          F[v][u] += acc;  // column-major (v * b + u), summed as the host
+        }
+    } else {  // p2 side: Omega
+#pragma unroll
+      for (int u = 0; u < B; ++u) F[u][u] += Om[u];
+    }
+  }
+  int o = 0;
+#pragma unroll
+  for (int u = 0; u < B; ++u)
+#pragma unroll
+    for (int v = u; v < B; ++v) diag[j * DW + o++] = F[v][u];
+}
+
+// RobustCost::weight (src/DPGO_robust.cpp:23-67), r = sqrt(computeMeasurementError)
+__device__ __forceinline__ double robust_weight(const RobustParams& p, double r) {
+  switch (p.type) {
+    case 1: return 1.0 / r;                                    // L1
+    case 2: return r < p.tls ? 1.0 : 0.0;                      // TLS
+    case 3: return r < p.huber ? 1.0 : p.huber / r;            // Huber
+    case 4: { const double a = 1.0 + r * r; return 1.0 / (a * a); }  // GM
+    case 5: {                                                  // GNC_TLS, eq. (14) of the GNC paper
+      const double rSq = r * r, bc = p.barc * p.barc;
+      const double upper = (p.mu + 1) / p.mu * bc, lower = p.mu / (p.mu + 1) * bc;
+      if (rSq >= upper) return 0.0;
+      if (rSq <= lower) return 1.0;
+      return sqrt(bc * p.mu * (p.mu + 1) / rSq) - p.mu;
+    }
+    default: return 1.0;                                       // L2
+  }
+}
+
+// One thread per loop closure: computeMeasurementError (src/DPGO_utils.cpp:509-515)
+//   kappa |Y1 R - Y2|^2 + tau |p2 - p1 - Y1 t|^2, residual = sqrt, weight.
+template <int R, int D>
+__global__ __launch_bounds__(kThreads) void k_gnc_weights(GncEntries g, const double* __restrict__ X,
+                                                          const double* __restrict__ RX, RobustParams rp,
+                                                          double* __restrict__ w_prob, double* __restrict__ w_g) {
+  constexpr int B = D + 1;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= g.n) return;
+  const int s1 = g.src1[e], s2 = g.src2[e];
+  const double* P1 = s1 >= 0 ? X + static_cast<long>(s1) * (R * B) : RX + static_cast<long>(-1 - s1) * (R * B);
+  const double* P2 = s2 >= 0 ? X + static_cast<long>(s2) * (R * B) : RX + static_cast<long>(-1 - s2) * (R * B);
+  const double* Rm = g.R + static_cast<long>(e) * D * D;
+  const double* tv = g.t + static_cast<long>(e) * D;
+  double rot = 0.0, tra = 0.0;
+#pragma unroll
+  for (int a = 0; a < R; ++a) {
+#pragma unroll
+    for (int c = 0; c < D; ++c) {
+      double v = 0.0;
+#pragma unroll
+      for (int u = 0; u < D; ++u) v += P1[u * R + a] * Rm[u * D + c];
+      const double df = v - P2[c * R + a];
+      rot += df * df;
+    }
+    double yt = 0.0;
+#pragma unroll
+    for (int u = 0; u < D; ++u) yt += P1[u * R + a] * tv[u];
+    const double dt = P2[D * R + a] - P1[D * R + a] - yt;
+    tra += dt * dt;
+  }
+  const double err = g.kappa[e] * rot + g.tau[e] * tra;
+  const double w = robust_weight(rp, sqrt(err));
+  w_prob[g.prob_edge[e]] = w;
+  if (g.g_entry[e] >= 0) w_g[g.g_entry[e]] = w;
+}
+
+// w per slot (scatter of the edge-order weights) for the diagonal pass
+__global__ __launch_bounds__(kThreads) void k_weights_to_slots(int m, const int* __restrict__ slot_of_edge,
+                                                               const double* __restrict__ w,
+                                                               double* __restrict__ wslot) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < m) wslot[slot_of_edge[e]] = w[e];
+}
+
+// ------------------------------------------------------------------------------------------
 // Exact preconditioner (QuadraticProblem::PreConditioner with the Cholesky factor of Q + 0.1 I,
 // src/QuadraticProblem.cpp:37-41, 75-87): level-scheduled block triangular solves.  In row form
 // the r right-hand sides are the pose blocks themselves: forward Y_j = (V_j - sum_k Y_k L_jk^T)
@@ -1453,6 +1595,35 @@ hipError_t launch_precond_finish(int r, int b, const LaunchCtx& c, const double*
 hipError_t launch_finalize(const FinalizeArgs& f, int num_agents, hipStream_t stream) {
   if (num_agents == 0) return hipSuccess;
   k_finalize<<<num_agents, kThreads, 0, stream>>>(f);
+  return hipGetLastError();
+}
+
+hipError_t launch_edge_reweight(int d, int m, int n, const double* raw, const int* slot_of_edge, const double* w,
+                                const int* dinc_ptr, const int* dinc, double* wslot, double* rec, double* diag,
+                                hipStream_t stream) {
+  if (m == 0 && n == 0) return hipSuccess;
+  const int ge = (m + kThreads - 1) / kThreads, gn = (n + kThreads - 1) / kThreads;
+  if (m > 0) {
+    k_weights_to_slots<<<ge, kThreads, 0, stream>>>(m, slot_of_edge, w, wslot);
+    if (d == 3)
+      k_edge_records<3><<<ge, kThreads, 0, stream>>>(m, raw, slot_of_edge, w, rec);
+    else
+      k_edge_records<2><<<ge, kThreads, 0, stream>>>(m, raw, slot_of_edge, w, rec);
+  }
+  if (n > 0) {
+    if (d == 3)
+      k_edge_diag<3><<<gn, kThreads, 0, stream>>>(n, raw, nullptr, wslot, dinc_ptr, dinc, diag);
+    else
+      k_edge_diag<2><<<gn, kThreads, 0, stream>>>(n, raw, nullptr, wslot, dinc_ptr, dinc, diag);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_gnc_weights(int r, int b, const GncEntries& g, const double* X, const double* RX,
+                              const RobustParams& rp, double* w_prob, double* w_g, hipStream_t stream) {
+  if (g.n == 0) return hipSuccess;
+  const int grid = (g.n + kThreads - 1) / kThreads;
+  DPGO_DISPATCH(r, b, (k_gnc_weights<R, B - 1><<<grid, kThreads, 0, stream>>>(g, X, RX, rp, w_prob, w_g)));
   return hipGetLastError();
 }
 

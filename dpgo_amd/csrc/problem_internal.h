@@ -37,7 +37,7 @@ struct HostBSR {
 // lives in another agent), R (d*d row-major), t (d), and the weighted precisions w kappa, w tau.
 struct HostEdges {
   std::vector<int> p1, p2;
-  std::vector<double> R, t, kw, tw;
+  std::vector<double> R, t, kw, tw, kappa0, tau0;  // kw = w kappa0, tw = w tau0
 };
 
 template <typename T>
@@ -89,6 +89,13 @@ struct dpgo_hip_problem_s {
   dpgo::DevBuf<int2> inc;
   dpgo::DevBuf<double> rec, diag;
   long nnz_inc = 0, num_edges = 0;
+  // on-device reweighting (dpgo_hip_set_edge_weights_dev): unweighted measurement per record slot
+  // [R | t | kappa | tau], problem edge -> slot, and per pose every incident edge incl. shared ones
+  // (slot * 2 + (pose == p1)) in edge order, for the diagonal blocks
+  dpgo::DevBuf<double> raw, wslot;
+  dpgo::DevBuf<int> slot_of_edge, dinc_ptr, dinc;
+  bool host_weights_stale = false;
+  const double* w_dev_last = nullptr;  // caller's weight array of the last device reweighting
 
   // G (sparse pose blocks per agent)
   std::vector<std::map<int, std::vector<double>>> g_agent;

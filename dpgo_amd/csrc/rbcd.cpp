@@ -41,6 +41,16 @@ struct dpgo_rbcd_s {
     int nslots = 0;
   };
   std::vector<GTab*> gt;
+  // robust cost: per colour, the loop closures its agents reweight and the colour problem's weights
+  struct Gnc {
+    DevBuf<int> prob_edge, g_entry, src1, src2;
+    DevBuf<double> R, t, kappa, tau, w_prob;
+    int n = 0;
+  };
+  std::vector<Gnc*> gnc;
+  double mu = 0.0;       // RobustCost::mu (every agent updates it at the same iterations)
+  int gnc_iter = 0;      // RobustCost::mGNCIteration
+  bool gnc_due = false;  // this iteration reweights (set in pre_exchange, used by update)
   double gamma = 0.0, alpha = 0.0;
   long iteration = 0;
   long long agent_updates = 0;
@@ -49,6 +59,7 @@ struct dpgo_rbcd_s {
     for (auto* p : prob)
       if (p) dpgo_hip_problem_destroy(p);
     for (auto* g : gt) delete g;
+    for (auto* g : gnc) delete g;
   }
   size_t rb() const { return static_cast<size_t>(r) * b; }
 };
@@ -94,6 +105,19 @@ int assemble_G(dpgo_rbcd e, int c, bool aux) {
   HIP_TRY(launch_assemble_G(e->r, e->b, ge, t->nslots, aux ? e->Y.p : e->X.p, aux ? e->RY.p : e->RX.p, h->gblk.p,
                             e->stream));
   return DPGO_HIP_OK;
+}
+
+// GNC / robust reweighting of colour c's loop closures at the current poses (own X buffer and the
+// received neighbour poses), then the on-device rebuild of the colour problem's Q.
+int reweight_color(dpgo_rbcd e, int c) {
+  dpgo_hip_problem h = e->prob[c];
+  if (!h) return DPGO_HIP_OK;
+  auto* g = e->gnc[c];
+  const GncEntries ge{g->n, g->prob_edge.p, g->g_entry.p, g->src1.p, g->src2.p,
+                      g->R.p, g->t.p, g->kappa.p, g->tau.p};
+  const RobustParams rp{e->P.robust_cost, e->mu, e->P.gnc_barc, e->P.huber_threshold, e->P.tls_threshold};
+  HIP_TRY(launch_gnc_weights(e->r, e->b, ge, e->X.p, e->RX.p, rp, g->w_prob.p, e->gt[c]->w.p, e->stream));
+  return dpgo_hip_set_edge_weights_dev(h, g->w_prob.p);
 }
 
 int optimize_color(dpgo_rbcd e, int c, const double* Xin, double* Xout, dpgo_opt_result* results) {
@@ -167,6 +191,14 @@ void dpgo_rbcd_default_params(dpgo_rbcd_params* p) {
   p->precon = DPGO_PRECON_BLOCK_JACOBI;
   p->algorithm = DPGO_ALG_RTR;
   p->q_format = DPGO_QFMT_EDGES;
+  p->robust_cost = DPGO_ROBUST_L2;
+  p->robust_opt_inner_iters = 30;
+  p->gnc_max_iters = 100;
+  p->gnc_barc = 10.0;
+  p->gnc_mu_step = 1.4;
+  p->gnc_init_mu = 1e-4;
+  p->huber_threshold = 3.0;
+  p->tls_threshold = 10.0;
 }
 
 int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, const int* agent_rank, int rank,
@@ -184,6 +216,11 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
     e->P = *params;
   else
     dpgo_rbcd_default_params(&e->P);
+  if (e->P.robust_cost != DPGO_ROBUST_L2 && e->P.q_format != DPGO_QFMT_EDGES)
+    return bail(fail(DPGO_HIP_EINVAL, "robust costs reweight an edge-stream Q (q_format DPGO_QFMT_EDGES)"));
+  if (e->P.robust_cost < DPGO_ROBUST_L2 || e->P.robust_cost > DPGO_ROBUST_GNC_TLS || e->P.robust_opt_inner_iters <= 0)
+    return bail(fail(DPGO_HIP_EINVAL, "bad robust cost parameters"));
+  e->mu = e->P.gnc_init_mu;  // RobustCost::reset (src/DPGO_robust.cpp:70-84)
   e->d = g->d;
   e->r = e->P.r;
   e->b = g->d + 1;
@@ -297,9 +334,17 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
   }
   e->prob.assign(e->ncolors, nullptr);
   e->gt.assign(e->ncolors, nullptr);
+  e->gnc.assign(e->ncolors, nullptr);
   for (int c = 0; c < e->ncolors; ++c) {
     e->gt[c] = new dpgo_rbcd_s::GTab();
+    e->gnc[c] = new dpgo_rbcd_s::Gnc();
     const int a0 = e->color_off[c], a1 = e->color_off[c + 1];
+    // loop closures this colour reweights (PGOAgent::updateLoopClosuresWeights): private ones that
+    // are not odometry (local p2 != p1 + 1, as the partition's split), and shared ones whose other
+    // agent has the larger ID (only the lower-ID agent updates its copy)
+    std::vector<int> gn_pe, gn_ge, gn_s1, gn_s2;
+    std::vector<double> gn_R, gn_t, gn_k, gn_tau;
+    long prob_edges = 0;
     if (a1 == a0) continue;
     std::vector<int> counts;
     for (int q = a0; q < a1; ++q) counts.push_back(agent_n[e->owned[q]]);
@@ -352,10 +397,12 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
                                   et.data(), ek.data(), etau.data(), nullptr);
       }
       if (rc != DPGO_HIP_OK) return bail(rc);
+      std::map<size_t, int> g_index;  // shared edge -> its entry in the colour's G table
       std::vector<int> gpose;
       for (auto& kv2 : slots) {
         gpose.push_back(kv2.first);
         for (size_t k : kv2.second) {
+          g_index[k] = static_cast<int>(src.size());
           const int i = g->p1[k], j = g->p2[k];
           const bool out_edge = agent_of_pose[i] == A;
           const int nbr = out_edge ? j : i;
@@ -370,6 +417,32 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
         }
         slot_off.push_back(static_cast<int>(src.size()));
       }
+      for (size_t x = 0; x < agent_edges[q].size(); ++x) {
+        const size_t k = agent_edges[q][x];
+        const int i = g->p1[k], j = g->p2[k];
+        const bool own_i = agent_of_pose[i] == A, own_j = agent_of_pose[j] == A;
+        int ge = -1;
+        if (own_i && own_j) {
+          if (local[j] == local[i] + 1) continue;  // odometry: never reweighted
+        } else {
+          const int other = own_i ? agent_of_pose[j] : agent_of_pose[i];
+          if (other < A) continue;  // the lower-ID agent is responsible (:1201-1235)
+          ge = g_index.at(k);
+        }
+        auto src_of = [&](int pose) -> int {
+          const long oi = owned_index(pose);
+          return oi >= 0 ? static_cast<int>(oi) : -1 - static_cast<int>(recv_slot.at(pose));
+        };
+        gn_pe.push_back(static_cast<int>(prob_edges + static_cast<long>(x)));
+        gn_ge.push_back(ge);
+        gn_s1.push_back(src_of(i));
+        gn_s2.push_back(src_of(j));
+        gn_R.insert(gn_R.end(), &g->R[k * d * d], &g->R[k * d * d] + d * d);
+        gn_t.insert(gn_t.end(), &g->t[k * d], &g->t[k * d] + d);
+        gn_k.push_back(g->kappa[k]);
+        gn_tau.push_back(g->tau[k]);
+      }
+      prob_edges += static_cast<long>(agent_edges[q].size());
       std::vector<double> zeros(gpose.size() * e->rb(), 0.0);
       rc = dpgo_hip_set_G(h, q - a0, static_cast<int>(gpose.size()), gpose.data(), zeros.data());
       if (rc != DPGO_HIP_OK) return bail(rc);
@@ -387,6 +460,17 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
     if (rc == DPGO_HIP_OK) rc = upload_vec(t->kappa, kv, e->stream);
     if (rc == DPGO_HIP_OK) rc = upload_vec(t->tau, tauv, e->stream);
     if (rc == DPGO_HIP_OK) rc = upload_vec(t->w, wv, e->stream);
+    auto* gc = e->gnc[c];
+    gc->n = static_cast<int>(gn_pe.size());
+    if (rc == DPGO_HIP_OK) rc = upload_vec(gc->prob_edge, gn_pe, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(gc->g_entry, gn_ge, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(gc->src1, gn_s1, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(gc->src2, gn_s2, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(gc->R, gn_R, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(gc->t, gn_t, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(gc->kappa, gn_k, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(gc->tau, gn_tau, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(gc->w_prob, std::vector<double>(std::max<long>(prob_edges, 1), 1.0), e->stream);
     if (rc == DPGO_HIP_OK && hipStreamSynchronize(e->stream) != hipSuccess) rc = fail(DPGO_HIP_EDEVICE, "sync");
     if (rc != DPGO_HIP_OK) return bail(rc);
   }
@@ -478,6 +562,24 @@ static bool restart_now(dpgo_rbcd e) {
 int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color) {
   if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
   e->iteration += 1;  // mIterationNumber++ (:643)
+  // shouldUpdateLoopClosureWeights (:1174-1179): every agent reweights at the start of its iterate;
+  // the non-selected ones here, the selected ones in dpgo_rbcd_update once their neighbours' poses
+  // of this iteration have arrived (the order of examples/MultiRobotExample.cpp:181-213)
+  e->gnc_due = e->P.robust_cost != DPGO_ROBUST_L2 && (e->iteration + 1) % e->P.robust_opt_inner_iters == 0;
+  if (e->gnc_due) {
+    for (int c = 0; c < e->ncolors; ++c)
+      if (c != color) DPGO_TRY(reweight_color(e, c));
+    if (e->P.acceleration) {  // initializeAcceleration (:1062-1071): XPrev = V = Y = X, gamma = alpha = 0
+      const long bytes = static_cast<long>(sizeof(double)) * e->Nown * static_cast<long>(e->rb());
+      if (bytes) {
+        HIP_TRY(hipMemcpyAsync(e->Xprev.p, e->X.p, bytes, hipMemcpyDeviceToDevice, e->stream));
+        HIP_TRY(hipMemcpyAsync(e->V.p, e->X.p, bytes, hipMemcpyDeviceToDevice, e->stream));
+        HIP_TRY(hipMemcpyAsync(e->Y.p, e->X.p, bytes, hipMemcpyDeviceToDevice, e->stream));
+      }
+      e->gamma = 0.0;
+      e->alpha = 0.0;
+    }
+  }
   const bool restart = restart_now(e);
   // XPrev = X (:673) is only read by a restart (the relative-change status is not tracked here)
   const long bytes = static_cast<long>(sizeof(double)) * e->Nown * static_cast<long>(e->rb());
@@ -528,6 +630,12 @@ int dpgo_rbcd_update(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_re
                                   e->stream));
   }
   const bool restart = restart_now(e);
+  if (e->gnc_due) {
+    DPGO_TRY(reweight_color(e, color));
+    // RobustCost::update (src/DPGO_robust.cpp:86-103): every agent once per reweighting iteration
+    if (e->P.robust_cost == DPGO_ROBUST_GNC_TLS && ++e->gnc_iter <= e->P.gnc_max_iters) e->mu *= e->P.gnc_mu_step;
+    e->gnc_due = false;
+  }
   if (e->prob[color]) {
     double* Xc = color_ptr(e, e->X, color);
     double* Yc = color_ptr(e, e->Y, color);

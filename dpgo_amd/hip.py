@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(_HERE, "libdpgo_hip.so")
 
 PRECON_EXACT, PRECON_BLOCK_JACOBI, PRECON_NONE = 0, 1, 2
 QFMT_BSR, QFMT_EDGES = 0, 1
+ROBUST = {"L2": 0, "L1": 1, "TLS": 2, "Huber": 3, "GM": 4, "GNC_TLS": 5}
 ALG_RTR, ALG_RGD = 0, 1
 TCG_NAMES = {-1: "NONE", 0: "NEGCURVTURE", 1: "EXCREGION", 2: "LCON", 3: "SCON", 4: "MAXITER"}
 
@@ -61,6 +62,7 @@ _SIGS = [
     ("dpgo_hip_set_Q_csr", [C.c_void_p, C.c_int, C.c_int, _ip, _ip, _dp], C.c_int),
     ("dpgo_hip_set_Q_bsr", [C.c_void_p, C.c_int, C.c_int, _ip, _ip, _dp], C.c_int),
     ("dpgo_hip_set_Q_edges", [C.c_void_p, C.c_int, C.c_int, _ip, _ip, _dp, _dp, _dp, _dp, _dp], C.c_int),
+    ("dpgo_hip_set_edge_weights_dev", [C.c_void_p, C.c_void_p], C.c_int),
     ("dpgo_hip_set_G", [C.c_void_p, C.c_int, C.c_int, _ip, _dp], C.c_int),
     ("dpgo_hip_set_G_dense", [C.c_void_p, C.c_int, _dp], C.c_int),
     ("dpgo_hip_f", [C.c_void_p, _dp, _dp], C.c_int),
@@ -231,6 +233,9 @@ class Problem:
             wp = None
         _check(lib().dpgo_hip_set_Q_edges(self.h, agent, len(a1), a1p, a2p, Rp, tp, kp, tap, wp))
 
+    def set_edge_weights_dev(self, w_dev_ptr: int):
+        _check(lib().dpgo_hip_set_edge_weights_dev(self.h, C.c_void_p(w_dev_ptr)))
+
     def set_G_dense(self, agent, G):
         """G: r x (b n_a) matrix."""
         g, gp = _f64(to_dev_layout(G))
@@ -367,7 +372,10 @@ def project_polar(M, d):
 class RbcdParams(C.Structure):
     _fields_ = [("r", C.c_int), ("acceleration", C.c_int), ("restart_interval", C.c_int),
                 ("max_inner", C.c_int), ("initial_radius", C.c_double), ("tolerance", C.c_double),
-                ("precon", C.c_int), ("algorithm", C.c_int), ("q_format", C.c_int)]
+                ("precon", C.c_int), ("algorithm", C.c_int), ("q_format", C.c_int),
+                ("robust_cost", C.c_int), ("robust_opt_inner_iters", C.c_int), ("gnc_max_iters", C.c_int),
+                ("gnc_barc", C.c_double), ("gnc_mu_step", C.c_double), ("gnc_init_mu", C.c_double),
+                ("huber_threshold", C.c_double), ("tls_threshold", C.c_double)]
 
 
 _lp = C.POINTER(C.c_longlong)

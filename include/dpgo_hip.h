@@ -125,6 +125,13 @@ int dpgo_hip_set_Q_bsr(dpgo_hip_problem h, int agent, int nbrows, const int* bro
 int dpgo_hip_set_Q_edges(dpgo_hip_problem h, int agent, int m, const int* p1, const int* p2,
                          const double* R, const double* t, const double* kappa, const double* tau,
                          const double* weight);
+/* Reweight an edge-stream Q on the device (PGOAgent::constructQMatrix after a GNC weight update,
+ * src/PGOAgent.cpp:720-781, 1181-1244): w_dev[e] (device, one weight per edge, agents' set_Q_edges
+ * lists concatenated in agent order) replaces each edge's weight; records, diagonal blocks and the
+ * block-Jacobi inverses are rebuilt by kernels (bitwise the host build with those weights), the
+ * exact factor is refreshed on its next use.  Asynchronous on the handle's stream; w_dev must stay
+ * valid until the next EXACT-preconditioned call. */
+int dpgo_hip_set_edge_weights_dev(dpgo_hip_problem h, const double* w_dev);
 /* QuadraticProblem::setG (src/QuadraticProblem.cpp:44-48) in sparse form: count pose blocks
  * (r x b column-major) at agent-local poses pose_idx[]; all other columns of G are zero. */
 int dpgo_hip_set_G(dpgo_hip_problem h, int agent, int count, const int* pose_idx,

@@ -13,7 +13,9 @@
  * solved as ONE batched dpgo_hip_problem (their Q blocks are independent).  Neighbour public poses
  * cross ranks through caller-owned device buffers (the caller moves them with RCCL
  * all_to_all); same-rank neighbours are read directly from device memory.
- * Robust cost: L2 only (GNC weight updates are SURVEY 8f "next").
+ * Robust cost: L2 (default, the throughput setting) or any of the reference's RobustCostType with
+ * on-device loop-closure reweighting every robust_opt_inner_iters iterations (PGOAgent::iterate +
+ * updateLoopClosuresWeights, src/PGOAgent.cpp:642-718, 1174-1244; RobustCost, src/DPGO_robust.cpp).
  */
 #ifndef DPGO_RBCD_H
 #define DPGO_RBCD_H
@@ -57,7 +59,24 @@ typedef struct {
   int precon;             /* DPGO_PRECON_BLOCK_JACOBI */
   int algorithm;          /* DPGO_ALG_RTR / DPGO_ALG_RGD */
   int q_format;           /* DPGO_QFMT_EDGES (default: edge-stream Q) or DPGO_QFMT_BSR (explicit Q) */
+  /* robust cost (RobustCostParameters, include/DPGO/DPGO_robust.h; PGOAgentParameters) */
+  int robust_cost;             /* DPGO_ROBUST_* (default L2) */
+  int robust_opt_inner_iters;  /* 30: reweight when (iteration + 1) % this == 0 */
+  int gnc_max_iters;           /* 100 */
+  double gnc_barc;             /* 10 */
+  double gnc_mu_step;          /* 1.4 */
+  double gnc_init_mu;          /* 1e-4 */
+  double huber_threshold;      /* 3 */
+  double tls_threshold;        /* 10 */
 } dpgo_rbcd_params;
+
+/* RobustCostType (include/DPGO/DPGO_robust.h): weights need an edge-stream Q (q_format EDGES) */
+#define DPGO_ROBUST_L2 0
+#define DPGO_ROBUST_L1 1
+#define DPGO_ROBUST_TLS 2
+#define DPGO_ROBUST_HUBER 3
+#define DPGO_ROBUST_GM 4
+#define DPGO_ROBUST_GNC_TLS 5
 
 void dpgo_rbcd_default_params(dpgo_rbcd_params* p);
 /* Host-only (no GPU needed): the public-pose exchange plan of `rank` -- poses per peer it sends /

@@ -1224,7 +1224,8 @@ def greedy_colors(meas: Measurements, agent_of_pose, num_agents):
 
 
 def colour_rbcd(meas: Measurements, agent_of_pose, num_agents, X0, num_iters, r,
-                acceleration=False, robust="L2", precon=PRECON_BLOCK_JACOBI, trace=None):
+                acceleration=False, robust="L2", precon=PRECON_BLOCK_JACOBI, trace=None,
+                robust_opt_inner_iters=30):
     """Colour-class RBCD schedule run with the PGOAgent restatement: at iteration t the agents of
     colour t mod C are selected; the others run iterate(false) first (their public X / aux Y are
     then delivered, as in examples/MultiRobotExample.cpp:181-213), then the selected agents run
@@ -1244,7 +1245,7 @@ def colour_rbcd(meas: Measurements, agent_of_pose, num_agents, X0, num_iters, r,
     agents = []
     for a in range(num_agents):
         ag = Agent(a, AgentParams(d, r, num_agents, acceleration=acceleration, robust=robust,
-                                  precon=precon))
+                                  precon=precon, robust_opt_inner_iters=robust_opt_inner_iters))
         ag.set_pose_graph(*parts[a], n=int(counts[a]))
         cols = np.concatenate([np.arange(p * b, (p + 1) * b) for p in glob[a]])
         ag.set_X(X0[:, cols])

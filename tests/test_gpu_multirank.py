@@ -26,7 +26,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, accel, q):
+def _worker(rank, world, port, accel, robust, q):
     import sys
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -37,7 +37,8 @@ def _worker(rank, world, port, accel, q):
         g = H.Graph.grid3d(K, seed=5)
         aop = g.grid_partition(A)
         ranks = (np.arange(A ** 3) * world // A ** 3).astype(np.int32)
-        e = H.Rbcd(g, aop, ranks, rank, world, H.rbcd_params(r=R, acceleration=int(accel)))
+        e = H.Rbcd(g, aop, ranks, rank, world, H.rbcd_params(r=R, acceleration=int(accel),
+                                                             robust_cost=H.ROBUST[robust], robust_opt_inner_iters=3))
         X0 = g.chain_init(R, O.lifting_matrix(3, R))
         e.set_X(X0)
         dev = torch.device("cuda", 0)
@@ -60,12 +61,15 @@ def _worker(rank, world, port, accel, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("robust", ["L2", "GNC_TLS"])
 @pytest.mark.parametrize("accel", [False, True])
-def test_two_ranks_match_oracle(accel):
+def test_two_ranks_match_oracle(accel, robust):
+    """GNC_TLS: shared loop closures across the two ranks are reweighted by the lower-ID agent from
+    the received neighbour poses (robust_opt_inner_iters = 3: reweightings at iterations 2 and 5)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, accel, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, accel, robust, q)) for r in range(2)]
     for p in procs:
         p.start()
     outs = [q.get(timeout=240) for _ in range(2)]
@@ -78,5 +82,6 @@ def test_two_ranks_match_oracle(accel):
     meas = O.Measurements(3, np.zeros(g.m, np.int64), np.zeros(g.m, np.int64), a["p1"].astype(np.int64),
                           a["p2"].astype(np.int64), a["R"], a["t"], a["kappa"], a["tau"], np.ones(g.m), g.n)
     X0 = g.chain_init(R, O.lifting_matrix(3, R))
-    Xo, _ = O.colour_rbcd(meas, g.grid_partition(A), A ** 3, X0, ITERS, R, acceleration=accel)
+    Xo, _ = O.colour_rbcd(meas, g.grid_partition(A), A ** 3, X0, ITERS, R, acceleration=accel, robust=robust,
+                          robust_opt_inner_iters=3)
     assert rel(H.from_dev_layout(Xflat, R), Xo) <= 1e-9

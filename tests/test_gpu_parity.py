@@ -197,3 +197,33 @@ def test_edge_stream_rejects_bad_input(hip):
         H.set_Q_edges(0, [0], [7], R, np.zeros((1, 3)), [1.0], [1.0])  # out of range
     with pytest.raises(hip.DPGOHipError):
         H.set_Q_edges(0, [-1], [-1], R, np.zeros((1, 3)), [1.0], [1.0])  # no local endpoint
+
+
+@pytest.mark.parametrize("name,r", [("smallGrid3D", 5), ("input_INTEL_g2o", 3)])
+def test_device_reweighting_matches_host_weights(hip, name, r):
+    """dpgo_hip_set_edge_weights_dev (on-device Q rebuild after a GNC update) gives bitwise the
+    problem built on the host with the same weights, and matches the oracle's weighted Q; the exact
+    preconditioner follows the new weights."""
+    import torch
+    meas = load_meas(name)
+    d, n = meas.d, meas.num_poses
+    w = np.array([O.SplitMix64(900 + e).uniform() for e in range(meas.m)])
+    X = random_point(r, d, n, 61)
+    V = random_tangent(X, d, 62)
+    Hh = hip.Problem(n, d, r)
+    Hh.set_Q_edges(0, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau, w)
+    Hd = hip.Problem(n, d, r)
+    Hd.set_Q_edges(0, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau)
+    Hd.f(X)  # upload the unweighted problem first
+    wd = torch.tensor(w, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    Hd.set_edge_weights_dev(wd.data_ptr())
+    assert np.array_equal(Hd.egrad(X), Hh.egrad(X))
+    assert np.array_equal(Hd.rhvp(X, V), Hh.rhvp(X, V))
+    assert np.array_equal(Hd.precondition(X, V), Hh.precondition(X, V))
+    mw = O.Measurements(meas.d, meas.r1, meas.r2, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau, w, n)
+    P = O.QuadraticProblem(n, d, r)
+    P.set_Q(O.connection_laplacian(mw, n))
+    assert rel(Hd.egrad(X), P.egrad(X)) <= TOL
+    Hd.set_precon(hip.PRECON_EXACT)
+    assert rel(Hd.precondition(X, V), P.precondition(X, V, O.PRECON_EXACT)) <= 1e-10
