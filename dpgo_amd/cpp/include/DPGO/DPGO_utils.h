@@ -17,6 +17,8 @@ SparseMatrix constructConnectionLaplacianSE(const std::vector<RelativeSEMeasurem
 SparseMatrix constructConnectionLaplacianSE(const std::vector<RelativeSEMeasurement>& measurements, size_t n);
 // src/DPGO_utils.cpp:426-447
 Matrix odometryInitialization(size_t dimension, size_t num_poses, const std::vector<RelativeSEMeasurement>& odometry);
+// src/DPGO_utils.cpp:377-424 (SPQR there; native host block Cholesky of the normal equations here)
+Matrix chordalInitialization(size_t dimension, size_t num_poses, const std::vector<RelativeSEMeasurement>& measurements);
 // src/DPGO_utils.cpp:478-500 (host, Jacobi SVD)
 Matrix projectToRotationGroup(const Matrix& M);
 Matrix projectToStiefelManifold(const Matrix& M);

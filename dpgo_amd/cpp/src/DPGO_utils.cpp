@@ -80,6 +80,29 @@ Matrix odometryInitialization(size_t dimension, size_t num_poses, const std::vec
   return T;
 }
 
+Matrix chordalInitialization(size_t dimension, size_t num_poses, const std::vector<RelativeSEMeasurement>& measurements) {
+  // src/DPGO_utils.cpp:377-424 -> dpgo_chordal_initialization (native host block-Cholesky solve)
+  const size_t d = dimension, m = measurements.size();
+  std::vector<int> p1(m), p2(m);
+  std::vector<double> R(m * d * d), t(m * d), kappa(m), tau(m);
+  for (size_t e = 0; e < m; ++e) {
+    const auto& x = measurements[e];
+    p1[e] = static_cast<int>(x.p1);
+    p2[e] = static_cast<int>(x.p2);
+    for (size_t u = 0; u < d; ++u) {
+      for (size_t v = 0; v < d; ++v) R[e * d * d + u * d + v] = x.R(static_cast<long>(u), static_cast<long>(v));
+      t[e * d + u] = x.t(static_cast<long>(u), 0);
+    }
+    kappa[e] = x.kappa;
+    tau[e] = x.tau;
+  }
+  Matrix T(static_cast<long>(d), static_cast<long>(num_poses * (d + 1)));
+  if (dpgo_chordal_initialization(static_cast<int>(d), static_cast<int>(num_poses), static_cast<int>(m), p1.data(),
+                                  p2.data(), R.data(), t.data(), kappa.data(), tau.data(), T.data()) != DPGO_HIP_OK)
+    throw std::runtime_error(std::string("chordalInitialization: ") + dpgo_hip_last_error());
+  return T;
+}
+
 // one-sided Jacobi SVD of an r x c matrix (r >= c): A V = U Sigma
 static void jacobi_svd(const Matrix& M, Matrix& U, Matrix& S, Matrix& V) {
   const long r = M.rows(), c = M.cols();

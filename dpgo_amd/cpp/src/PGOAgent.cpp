@@ -108,9 +108,15 @@ void PGOAgent::setPoseGraph(const std::vector<RelativeSEMeasurement>& inputOdome
   if (TInit.rows() == d && TInit.cols() == static_cast<long>((d + 1) * n)) {
     TLocalInit = TInit;
   } else {
-    // localInitialization (:952-957): chordal initialisation is out of scope here;
-    // odometry initialisation is used for every cost type.
-    TLocalInit = odometryInitialization(d, n, odometry);
+    // localInitialization (:947-962): chordal for the L2 cost; with a robust cost the loop closures
+    // are not trusted and the odometry chain is used
+    if (mParams.robustCostType == RobustCostType::L2) {
+      std::vector<RelativeSEMeasurement> ms = odometry;
+      ms.insert(ms.end(), privateLoopClosures.begin(), privateLoopClosures.end());
+      TLocalInit = chordalInitialization(d, n, ms);
+    } else {
+      TLocalInit = odometryInitialization(d, n, odometry);
+    }
   }
   mState = WAIT_FOR_INITIALIZATION;
   if (mID == 0 || !mParams.multirobot_initialization) {

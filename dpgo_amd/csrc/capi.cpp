@@ -1274,6 +1274,176 @@ int dpgo_hip_project_polar(int r, int d, int n, const double* in, double* out) {
   return stateless(r, d, n, in, nullptr, 1.0, out, 2);
 }
 
+// ----------------------------------------------------------------------- certification
+}  // extern "C"
+
+namespace {
+
+// Eigenpairs of the symmetric tridiagonal T (diag a, off-diagonal e[i] between i and i+1) by the
+// implicit QL method; Z (k x k, column-major) receives the eigenvectors.
+void tridiag_eig(std::vector<double> a, std::vector<double> e, std::vector<double>& Z) {
+  const int k = static_cast<int>(a.size());
+  Z.assign(static_cast<size_t>(k) * k, 0.0);
+  for (int i = 0; i < k; ++i) Z[static_cast<size_t>(i) * k + i] = 1.0;
+  e.resize(k, 0.0);
+  for (int l = 0; l < k; ++l) {
+    for (int iter = 0; iter < 200; ++iter) {
+      int m = l;
+      for (; m < k - 1; ++m) {
+        const double dd = std::fabs(a[m]) + std::fabs(a[m + 1]);
+        if (std::fabs(e[m]) <= 1e-16 * dd) break;
+      }
+      if (m == l) break;
+      double g = (a[l + 1] - a[l]) / (2.0 * e[l]);
+      double r = std::hypot(g, 1.0);
+      g = a[m] - a[l] + e[l] / (g + std::copysign(r, g));
+      double s = 1.0, c = 1.0, p = 0.0;
+      int i = m - 1;
+      for (; i >= l; --i) {
+        double f = s * e[i];
+        const double bb = c * e[i];
+        r = std::hypot(f, g);
+        e[i + 1] = r;
+        if (r == 0.0) {
+          a[i + 1] -= p;
+          e[m] = 0.0;
+          break;
+        }
+        s = f / r;
+        c = g / r;
+        g = a[i + 1] - p;
+        r = (a[i] - g) * s + 2.0 * c * bb;
+        p = s * r;
+        a[i + 1] = g + p;
+        g = c * r - bb;
+        for (int q = 0; q < k; ++q) {
+          f = Z[static_cast<size_t>(i + 1) * k + q];
+          Z[static_cast<size_t>(i + 1) * k + q] = s * Z[static_cast<size_t>(i) * k + q] + c * f;
+          Z[static_cast<size_t>(i) * k + q] = c * Z[static_cast<size_t>(i) * k + q] - s * f;
+        }
+      }
+      if (r == 0.0 && i >= l) continue;
+      a[l] -= p;
+      e[l] = g;
+      e[m] = 0.0;
+    }
+  }
+  // a now holds the eigenvalues; store them in Z's companion by sorting indices
+  std::vector<int> idx(k);
+  for (int i = 0; i < k; ++i) idx[i] = i;
+  std::sort(idx.begin(), idx.end(), [&](int x, int y) { return a[x] < a[y]; });
+  std::vector<double> Zs(Z.size());
+  for (int i = 0; i < k; ++i)
+    std::memcpy(&Zs[static_cast<size_t>(i) * k], &Z[static_cast<size_t>(idx[i]) * k], sizeof(double) * k);
+  Z.swap(Zs);
+  std::sort(a.begin(), a.end());
+  Z.insert(Z.end(), a.begin(), a.end());  // eigenvalues appended after the k x k vectors
+}
+
+}  // namespace
+
+extern "C" {
+
+int dpgo_hip_certify(dpgo_hip_problem h, const double* X, int max_iters, double tol, double* lambda_min,
+                     double* residual, int* iters, double* eigvec) {
+  DPGO_TRY(ready(h));
+  if (h->K != 1) return fail(DPGO_HIP_EINVAL, "certification needs a single-agent handle");
+  if (!X || !lambda_min || max_iters < 2) return fail(DPGO_HIP_EINVAL, "bad certification arguments");
+  DPGO_TRY(ensure_work(h));
+  const long L = static_cast<long>(h->vec_len());
+  const int kmax = static_cast<int>(std::min<long>(max_iters, L));
+  HostIO io;
+  DPGO_TRY(io.init(h));
+  DPGO_TRY(upload(io.a.p, X, L, h->stream));
+  // Lambda(X): S_j = sym(Y_j^T (XQ + G)_Y) (the same S the Riemannian Hessian uses)
+  DPGO_TRY(eval_at(h, io.a.p, h->tA.p, h->S.p, h->pa.p, dpgo::FLAG_NONE));
+  DevBuf<double> basis, c, part;
+  HIP_TRY(basis.ensure(static_cast<size_t>(kmax + 1) * L));
+  HIP_TRY(c.ensure(kmax + 1));
+  HIP_TRY(part.ensure(static_cast<size_t>(dpgo::kDotBlocks) * (kmax + 1)));
+  double* w = io.b.p;
+  auto dots = [&](const double* vec, const double* B, int k, std::vector<double>& out) -> int {
+    HIP_TRY(dpgo::launch_dot_multi(L, vec, B, k, part.p, h->stream));
+    std::vector<double> hp(static_cast<size_t>(dpgo::kDotBlocks) * k);
+    HIP_TRY(hipMemcpyAsync(hp.data(), part.p, sizeof(double) * hp.size(), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    out.assign(k, 0.0);
+    for (int g = 0; g < dpgo::kDotBlocks; ++g)
+      for (int j = 0; j < k; ++j) out[j] += hp[static_cast<size_t>(g) * k + j];
+    return DPGO_HIP_OK;
+  };
+  // seeded start vector (SplitMix64 uniform in [-1, 1))
+  {
+    std::vector<double> q0(L);
+    unsigned long long st = 0x5EEDULL;
+    for (long x = 0; x < L; ++x) {
+      st += 0x9E3779B97F4A7C15ULL;
+      unsigned long long z = st;
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+      z ^= z >> 31;
+      q0[x] = 2.0 * (static_cast<double>(z >> 11) * (1.0 / 9007199254740992.0)) - 1.0;
+    }
+    DPGO_TRY(upload(w, q0.data(), L, h->stream));
+    std::vector<double> nn;
+    DPGO_TRY(dots(w, w, 1, nn));
+    HIP_TRY(dpgo::launch_scale(L, w, 1.0 / std::sqrt(nn[0]), basis.p, h->stream));
+  }
+  std::vector<double> alpha, beta, Z;  // beta[j] couples q_j and q_{j+1}
+  double lam = 0.0, res = 0.0;
+  int k = 0;
+  auto ritz = [&](int kk) {
+    tridiag_eig(std::vector<double>(alpha.begin(), alpha.begin() + kk),
+                std::vector<double>(beta.begin(), beta.begin() + kk), Z);
+    lam = Z[static_cast<size_t>(kk) * kk + 0];
+    res = std::fabs(beta[kk - 1] * Z[static_cast<size_t>(0) * kk + (kk - 1)]);
+  };
+  auto c_ctx = make_ctx(h, dpgo::FLAG_NONE, nullptr);
+  for (k = 0; k < kmax; ++k) {
+    const double* qk = basis.p + static_cast<long>(k) * L;
+    const dpgo::SpmmArgs sa{qk, nullptr, nullptr, nullptr, h->S.p, w, nullptr, nullptr, nullptr, dpgo::PRECON_NONE};
+    HIP_TRY(dpgo::launch_spmm(h->r, h->b, dpgo::MODE_CERT, c_ctx, qview(h), sa));
+    // full reorthogonalisation, classical Gram-Schmidt twice; alpha_k from both passes
+    double ak = 0.0;
+    for (int pass = 0; pass < 2; ++pass) {
+      std::vector<double> cc;
+      DPGO_TRY(dots(w, basis.p, k + 1, cc));
+      ak += cc[k];
+      HIP_TRY(hipMemcpyAsync(c.p, cc.data(), sizeof(double) * (k + 1), hipMemcpyHostToDevice, h->stream));
+      HIP_TRY(dpgo::launch_axpy_multi(L, w, basis.p, k + 1, c.p, h->stream));
+    }
+    std::vector<double> nn;
+    DPGO_TRY(dots(w, w, 1, nn));
+    const double bk = std::sqrt(nn[0]);
+    alpha.push_back(ak);
+    beta.push_back(bk);
+    if ((k + 1) % 5 == 0 || k + 1 == kmax || bk <= 1e-300) {
+      ritz(k + 1);
+      const double scale = std::max(std::fabs(Z.back()), std::fabs(lam));
+      if (res <= tol * std::max(scale, 1e-300) || bk <= 1e-300) {
+        ++k;
+        break;
+      }
+    }
+    if (k + 1 < kmax + 1) HIP_TRY(dpgo::launch_scale(L, w, 1.0 / bk, basis.p + static_cast<long>(k + 1) * L, h->stream));
+  }
+  if (k > kmax) k = kmax;
+  ritz(k);
+  *lambda_min = lam;
+  if (residual) *residual = res;
+  if (iters) *iters = k;
+  if (eigvec) {  // Ritz vector sum_i z_i q_i (axpy with -z onto zero)
+    std::vector<double> negz(k);
+    for (int i = 0; i < k; ++i) negz[i] = -Z[static_cast<size_t>(0) * k + i];
+    HIP_TRY(hipMemsetAsync(w, 0, sizeof(double) * L, h->stream));
+    HIP_TRY(hipMemcpyAsync(c.p, negz.data(), sizeof(double) * k, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(dpgo::launch_axpy_multi(L, w, basis.p, k, c.p, h->stream));
+    DPGO_TRY(download(eigvec, w, L, h->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return DPGO_HIP_OK;
+}
+
 // ----------------------------------------------------------------------- measurement
 double dpgo_hip_spmm_bytes(dpgo_hip_problem h) {
   if (!h) return 0.0;

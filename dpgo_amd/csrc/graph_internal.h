@@ -1,5 +1,6 @@
 // Internal (non-ABI) pose-graph representation shared by graph.cpp and rbcd.cpp.
 #pragma once
+#include <string>
 #include <vector>
 
 #include "../../include/dpgo_rbcd.h"
@@ -32,5 +33,9 @@ struct BsrBuilder {
 
 void edge_blocks(int d, const double* R, const double* t, double kappa, double tau, double w, double* Wii,
                  double* Wjj, double* Wij, double* Wji);
+
+// chordalInitialization (src/DPGO_utils.cpp:377-424), init.cpp: T_out d x (d+1) n column-major
+int chordal_initialization(int d, int n, int m, const int* p1, const int* p2, const double* R, const double* t,
+                           const double* kappa, const double* tau, double* T_out, std::string& err);
 
 }  // namespace dpgo

@@ -11,7 +11,8 @@ constexpr int kPartialStride = 4;  // doubles of partial sums per tile
 // X.Q SpMM epilogues: XQ (V Q), XQ_G (X Q + G), EVAL (g = P_X(XQ+G), S, f / |g|^2 partials),
 // HESS (Riemannian Hessian), F (f partial only), EVAL_TCG (EVAL + tCG start: delta = -P_X(g Minv),
 // partial <z, g>)
-enum SpmmMode { MODE_XQ = 0, MODE_XQ_G = 1, MODE_EVAL = 2, MODE_HESS = 3, MODE_F = 4, MODE_EVAL_TCG = 5 };
+// CERT: V (Q - Lambda(X)) = VQ - [V_Y S | 0] (the certificate matrix, no projection)
+enum SpmmMode { MODE_XQ = 0, MODE_XQ_G = 1, MODE_EVAL = 2, MODE_HESS = 3, MODE_F = 4, MODE_EVAL_TCG = 5, MODE_CERT = 6 };
 // Per-agent tile gating: RUN skips agents out of the RTR Run, TCG those whose tCG stopped, TCG_MODE
 // those with no tCG step pending, MOVED those whose single-Run candidate was accepted.
 enum FlagKind { FLAG_NONE = 0, FLAG_RUN = 1, FLAG_TCG = 2, FLAG_TCG_MODE = 3, FLAG_MOVED = 4 };
@@ -201,6 +202,13 @@ hipError_t launch_edge_reweight(int d, int m, int n, const double* raw, const in
                                 hipStream_t stream);
 hipError_t launch_gnc_weights(int r, int b, const GncEntries& g, const double* X, const double* RX,
                               const RobustParams& rp, double* w_prob, double* w_g, hipStream_t stream);
+// Lanczos helpers over flat vectors of length len: partial[g * k + j] = sum over grid block g's
+// chunk of w . basis_j (fixed grid kDotBlocks, fixed order); w -= sum_j c_j basis_j (c on device)
+constexpr int kDotBlocks = 512;
+hipError_t launch_dot_multi(long len, const double* w, const double* basis, int k, double* partial,
+                            hipStream_t stream);
+hipError_t launch_axpy_multi(long len, double* w, const double* basis, int k, const double* c, hipStream_t stream);
+hipError_t launch_scale(long len, const double* src, double s, double* dst, hipStream_t stream);
 hipError_t launch_bj_inverse_diag(int b, int n, const QView& q, double shift, double* Minv, hipStream_t stream);
 
 }  // namespace dpgo

@@ -10,6 +10,8 @@
 // Every kernel works on a *tile set*: tile t covers up to 64 consecutive poses of one agent
 // (agents = independent RBCD blocks batched into one launch).  See dpgo_device.h for the
 // pose-quad lane mapping.
+#include <algorithm>
+
 #include "dpgo_device.h"
 #include "kernels.h"
 
@@ -436,6 +438,19 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
         block_partials<2>(parts, c.partials, p.tile);
       }
     }
+  } else if constexpr (MODE == MODE_CERT) {
+    // certificate matrix S(X) = Q - Lambda(X), Lambda_j = [S_j 0; 0 0] (S_j = sym(Y_j^T EG_Y))
+    double vcol[R];
+    load_col<R, B>(in, p.j, p.k, p.ok, vcol);
+    double S[D][D];
+#pragma unroll
+    for (int u = 0; u < D; ++u)
+#pragma unroll
+      for (int v = 0; v < D; ++v) S[u][v] = p.ok ? S_in[p.j * (D * D) + u * D + v] : 0.0;
+    double Vf[R][D], hc[R];
+    quad_gather_y<R, D>(vcol, Vf);
+    sub_y_times_col<R, D>(Vf, S, p.k, qc, hc);
+    store_vec<R>(out, off, own, hc);
   } else if constexpr (MODE == MODE_HESS) {
     double vcol[R], xcol[R];
     load_col<R, B>(in, p.j, p.k, p.ok, vcol);
@@ -1490,6 +1505,7 @@ hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const QView& 
     case MODE_HESS: e = spmm_mode<MODE_HESS>(r, b, grid, c, q, a); break;
     case MODE_F: e = spmm_mode<MODE_F>(r, b, grid, c, q, a); break;
     case MODE_EVAL_TCG: e = spmm_mode<MODE_EVAL_TCG>(r, b, grid, c, q, a); break;
+    case MODE_CERT: e = spmm_mode<MODE_CERT>(r, b, grid, c, q, a); break;
     default: break;
   }
   if (e != hipSuccess) return e;
@@ -1624,6 +1640,64 @@ hipError_t launch_gnc_weights(int r, int b, const GncEntries& g, const double* X
   if (g.n == 0) return hipSuccess;
   const int grid = (g.n + kThreads - 1) / kThreads;
   DPGO_DISPATCH(r, b, (k_gnc_weights<R, B - 1><<<grid, kThreads, 0, stream>>>(g, X, RX, rp, w_prob, w_g)));
+  return hipGetLastError();
+}
+
+// ---- Lanczos helpers (certificate) ---------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_dot_multi(long len, const double* __restrict__ w,
+                                                        const double* __restrict__ basis, int k,
+                                                        double* __restrict__ partial) {
+  __shared__ double red[kThreads / 64];
+  const long chunk = (len + gridDim.x - 1) / gridDim.x;
+  const long beg = chunk * blockIdx.x, end = min(len, beg + chunk);
+  for (int j = 0; j < k; ++j) {
+    const double* v = basis + static_cast<long>(j) * len;
+    double s = 0.0;
+    for (long x = beg + threadIdx.x; x < end; x += kThreads) s = fma(w[x], v[x], s);
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) partial[static_cast<long>(blockIdx.x) * k + j] = ((red[0] + red[1]) + red[2]) + red[3];
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_axpy_multi(long len, double* __restrict__ w,
+                                                         const double* __restrict__ basis, int k,
+                                                         const double* __restrict__ c) {
+  for (long x = static_cast<long>(blockIdx.x) * kThreads + threadIdx.x; x < len;
+       x += static_cast<long>(gridDim.x) * kThreads) {
+    double s = w[x];
+    for (int j = 0; j < k; ++j) s = fma(-c[j], basis[static_cast<long>(j) * len + x], s);
+    w[x] = s;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_scale(long len, const double* __restrict__ src, double s,
+                                                    double* __restrict__ dst) {
+  for (long x = static_cast<long>(blockIdx.x) * kThreads + threadIdx.x; x < len;
+       x += static_cast<long>(gridDim.x) * kThreads)
+    dst[x] = src[x] * s;
+}
+
+hipError_t launch_scale(long len, const double* src, double s, double* dst, hipStream_t stream) {
+  if (len == 0) return hipSuccess;
+  const long blocks = std::min<long>((len + kThreads - 1) / kThreads, 4096);
+  k_scale<<<static_cast<int>(blocks), kThreads, 0, stream>>>(len, src, s, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_dot_multi(long len, const double* w, const double* basis, int k, double* partial,
+                            hipStream_t stream) {
+  if (k == 0) return hipSuccess;
+  k_dot_multi<<<kDotBlocks, kThreads, 0, stream>>>(len, w, basis, k, partial);
+  return hipGetLastError();
+}
+
+hipError_t launch_axpy_multi(long len, double* w, const double* basis, int k, const double* c, hipStream_t stream) {
+  if (k == 0 || len == 0) return hipSuccess;
+  const long blocks = std::min<long>((len + kThreads - 1) / kThreads, 4096);
+  k_axpy_multi<<<static_cast<int>(blocks), kThreads, 0, stream>>>(len, w, basis, k, c);
   return hipGetLastError();
 }
 

@@ -89,6 +89,7 @@ _SIGS = [
     ("dpgo_hip_spmm_bytes", [C.c_void_p], C.c_double),
     ("dpgo_hip_bench_spmm", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, _dp], C.c_int),
     ("dpgo_hip_spmm_bytes_bsr", [C.c_void_p], C.c_double),
+    ("dpgo_hip_certify", [C.c_void_p, _dp, C.c_int, C.c_double, _dp, _dp, _ip, _dp], C.c_int),
     ("dpgo_hip_bench_hvp", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, _dp], C.c_int),
 ]
 
@@ -325,6 +326,15 @@ class Problem:
         _check(lib().dpgo_hip_polar_combine_dev(self.h, C.c_void_p(A_dev), C.c_void_p(B_dev or 0), ap, bp,
                                                 C.c_void_p(out_dev)))
 
+    def certify(self, X, max_iters=300, tol=1e-8, want_vector=False):
+        """lambda_min of S(X) = Q - Lambda(X) (Lanczos on the device): (lambda_min, residual, iters, vec)."""
+        x, xp = self._in(X)
+        lam, res, it = C.c_double(), C.c_double(), C.c_int()
+        v = np.empty(self.vec_len) if want_vector else None
+        _check(lib().dpgo_hip_certify(self.h, xp, int(max_iters), float(tol), C.byref(lam), C.byref(res), C.byref(it),
+                                      v.ctypes.data_as(_dp) if v is not None else None))
+        return lam.value, res.value, it.value, (from_dev_layout(v, self.r) if v is not None else None)
+
     def spmm_bytes(self) -> float:
         return float(lib().dpgo_hip_spmm_bytes(self.h))
 
@@ -389,6 +399,8 @@ _SIGS2 = [
     ("dpgo_graph_destroy", [C.c_void_p], C.c_int),
     ("dpgo_graph_laplacian_bsr", [C.c_void_p, _lp, _ip, _ip, _dp], C.c_int),
     ("dpgo_graph_chain_init", [C.c_void_p, C.c_int, _dp, _dp], C.c_int),
+    ("dpgo_graph_chordal_init", [C.c_void_p, C.c_int, _dp, _dp], C.c_int),
+    ("dpgo_chordal_initialization", [C.c_int, C.c_int, C.c_int, _ip, _ip, _dp, _dp, _dp, _dp, _dp], C.c_int),
     ("dpgo_graph_grid_partition", [C.c_void_p, C.c_int, _ip], C.c_int),
     ("dpgo_rbcd_default_params", [C.POINTER(RbcdParams)], None),
     ("dpgo_rbcd_plan", [C.c_void_p, C.c_int, _ip, _ip, C.c_int, C.c_int, _lp, _lp, _ip, _ip], C.c_int),
@@ -484,6 +496,13 @@ class Graph:
         _check(lib().dpgo_graph_chain_init(self.h, r, Yp, out.ctypes.data_as(_dp)))
         return from_dev_layout(out, r)
 
+    def chordal_init(self, r, YLift):
+        """YLift (r x d) times chordalInitialization (host); returns r x (d+1) n."""
+        Y, Yp = _f64(np.asarray(YLift, dtype=np.float64).T.ravel())
+        out = np.empty(self.n * (self.d + 1) * r)
+        _check(lib().dpgo_graph_chordal_init(self.h, r, Yp, out.ctypes.data_as(_dp)))
+        return from_dev_layout(out, r)
+
     def chain_init_dev_layout(self, r, YLift):
         Y, Yp = _f64(np.asarray(YLift, dtype=np.float64).T.ravel())
         out = np.empty(self.n * (self.d + 1) * r)
@@ -494,6 +513,19 @@ class Graph:
         out = np.empty(self.n, np.int32)
         _check(lib().dpgo_graph_grid_partition(self.h, int(agents_per_axis), out.ctypes.data_as(_ip)))
         return out
+
+
+def chordal_initialization(d, n, p1, p2, R, t, kappa, tau):
+    """chordalInitialization (src/DPGO_utils.cpp:377-424), host: T (d x (d+1) n)."""
+    a1, a1p = _i32(p1)
+    a2, a2p = _i32(p2)
+    Rr, Rp = _f64(np.asarray(R).reshape(-1))
+    tt, tp = _f64(np.asarray(t).reshape(-1))
+    kk, kp = _f64(kappa)
+    ta, tap = _f64(tau)
+    out = np.empty(d * (d + 1) * n)
+    _check(lib().dpgo_chordal_initialization(d, int(n), len(a1), a1p, a2p, Rp, tp, kp, tap, out.ctypes.data_as(_dp)))
+    return from_dev_layout(out, d)
 
 
 def exchange_plan(graph: "Graph", agent_of_pose, agent_rank, rank, world):

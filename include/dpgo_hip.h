@@ -186,6 +186,17 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
 /* Device buffer of the last tCG / RTR scalar state (for profiling / tests) */
 int dpgo_hip_synchronize(dpgo_hip_problem h);
 
+/* ---- certification (not in the reference: parity is pinned against a sparse
+ * eigensolver on the explicitly formed matrix) --------------------------------------------------
+ * Smallest eigenvalue of the certificate matrix S(X) = Q - Lambda(X), Lambda = blockdiag of
+ * [sym(Y_j^T (XQ + G)_Y) 0; 0 0]: X is a global minimiser of the rank-r relaxation iff S(X) >= 0.
+ * Lanczos with full re-orthogonalisation on the device (the operator V -> V S(X) on r x (d+1) n
+ * matrices has S's spectrum), stopping when the Ritz residual <= tol * |lambda|_max-estimate or
+ * after max_iters steps.  Single-agent handles.  eigvec (host, r x (d+1) n, optional): the Ritz
+ * vector of lambda_min. */
+int dpgo_hip_certify(dpgo_hip_problem h, const double* X, int max_iters, double tol, double* lambda_min,
+                     double* residual, int* iters, double* eigvec);
+
 /* ---- measurement helpers ----------------------------------------------------------------*/
 /* Select a compiled kernel variant for A/B timing (r = 5, d = 3 only).  key 0: BSR X.Q SpMM
  * neighbour-loop variant 0 = 1 neighbour/step (default), 1 = same with non-temporal block loads,

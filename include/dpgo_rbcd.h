@@ -45,6 +45,14 @@ int dpgo_graph_destroy(dpgo_graph g);
 int dpgo_graph_laplacian_bsr(dpgo_graph g, long long* nnzb, int* browptr, int* bcol, double* blocks);
 /* X = YLift * T_odo, T_odo composed along the p2 = p1 + 1 edges (r x (d+1) n, column-major). */
 int dpgo_graph_chain_init(dpgo_graph g, int r, const double* YLift_colmajor, double* X_out);
+/* chordalInitialization (src/DPGO_utils.cpp:377-424, PGOAgent::localInitialization for the L2 cost):
+ * rotations by least squares with R_0 = I then projectToRotationGroup, translations by least squares
+ * with t_0 = 0 (normal equations by a host block Cholesky; the reference uses SPQR, same minimiser).
+ * Host-only.  T_out: d x (d+1) n column-major ([R_i | t_i] per pose); R d*d row-major per edge. */
+int dpgo_chordal_initialization(int d, int n, int m, const int* p1, const int* p2, const double* R,
+                                const double* t, const double* kappa, const double* tau, double* T_out);
+/* X = YLift * chordal T for a graph handle (r x (d+1) n, column-major). */
+int dpgo_graph_chordal_init(dpgo_graph g, int r, const double* YLift_colmajor, double* X_out);
 /* Grid graphs: agent = sub-cube (x/s, y/s, z/s), s = k / A; id = ax + A (ay + A az). */
 int dpgo_graph_grid_partition(dpgo_graph g, int agents_per_axis, int* agent_of_pose);
 

@@ -522,6 +522,30 @@ class QuadraticProblem:
         return tangent_project(X, out, d)
 
 
+def certificate_matrix(Q, X, d):
+    """Build-defined certificate (absent from the reference so parity-unpinned
+    against it): S(X) = Q - Lambda(X), Lambda = blockdiag([sym(Y_j^T (XQ)_{Y_j}) 0; 0 0]).  With
+    f = 0.5 tr(X Q X^T) (src/QuadraticProblem.cpp:50-60), X is globally optimal for the rank-r
+    relaxation when S(X) >= 0 (the SE-Sync certificate)."""
+    Q = sp.csr_matrix(Q)
+    b = d + 1
+    n = Q.shape[0] // b
+    r = X.shape[0]
+    EG = np.asarray((Q @ X.T).T)
+    Xp, Gp = to_poses(X, r, d), to_poses(EG, r, d)
+    S = sym(np.swapaxes(Xp[:, :, :d], 1, 2) @ Gp[:, :, :d])
+    L = np.zeros((n, b, b))
+    L[:, :d, :d] = S
+    return (Q - sp.block_diag(list(L), format="csr")).tocsr()
+
+
+def certificate_min_eig(S):
+    """lambda_min of the certificate matrix (dense below 3000 rows, else ARPACK 'SA')."""
+    if S.shape[0] <= 3000:
+        return float(np.linalg.eigvalsh(S.toarray())[0])
+    return float(spla.eigsh(S, k=1, which="SA", tol=1e-12, maxiter=100000)[0][0])
+
+
 # ----------------------------------------------------------------------------------------
 # Riemannian trust region (ROPTLIB RTRNewton / SolversTR, restated in SURVEY Appendix A.4)
 # ----------------------------------------------------------------------------------------

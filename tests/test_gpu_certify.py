@@ -1,0 +1,82 @@
+"""GPU certificate lambda_min(Q - Lambda(X)).  The reference has no certification
+(SURVEY section 1, item 8), so this is pinned against the oracle's explicit matrix
+(oracle.certificate_matrix) and numpy/ARPACK eigenvalues only.
+
+Tolerances: Lanczos stops when the Ritz residual <= tol * |lambda|max; the Ritz value is then within
+residual of an eigenvalue, so |lambda_gpu - lambda_oracle| <= 1e-6 * |lambda|max is asserted, and the
+returned Ritz vector v must satisfy ||v S - lambda v|| <= 1e-6 * |lambda|max against the oracle S."""
+import numpy as np
+import pytest
+
+from oracle import dpgo_oracle as O
+from tests._common import load_meas, random_point, rel
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hip():
+    from dpgo_amd import hip as H
+    assert H.device_count() >= 1, "no gfx950 device"
+    return H
+
+
+def _check(H, Q, X, d, max_iters, tol=1e-10):
+    S = O.certificate_matrix(Q, X, d)
+    lam_o = O.certificate_min_eig(S)
+    lam_max = float(np.abs(np.linalg.eigvalsh(S.toarray())).max()) if S.shape[0] <= 3000 else \
+        float(abs(O.spla.eigsh(S, k=1, which="LM")[0][0]))
+    lam, res, it, v = H.certify(X, max_iters=max_iters, tol=tol, want_vector=True)
+    assert abs(lam - lam_o) <= 1e-6 * lam_max, (lam, lam_o, res, it)
+    assert abs(np.linalg.norm(v) - 1.0) <= 1e-8
+    Rv = np.asarray((S @ v.T).T) - lam * v
+    assert np.linalg.norm(Rv) <= 1e-6 * lam_max
+    return lam, lam_o, it
+
+
+@pytest.mark.parametrize("fmt", ["bsr", "edges"])
+@pytest.mark.parametrize("name,r", [("tinyGrid3D", 3), ("smallGrid3D", 5), ("input_INTEL_g2o", 3)])
+def test_certificate_random_point(hip, name, r, fmt):
+    """At a random point the certificate fails: lambda_min < 0, matching the explicit matrix."""
+    meas = load_meas(name)
+    d, n = meas.d, meas.num_poses
+    Q = O.connection_laplacian(meas, n)
+    X = random_point(r, d, n, 61)
+    H = hip.Problem(n, d, r)
+    if fmt == "bsr":
+        H.set_Q_scipy(0, Q)
+    else:
+        H.set_Q_edges(0, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau, meas.weight)
+    lam, lam_o, _ = _check(H, Q, X, d, max_iters=min(600, r * (d + 1) * n))
+    assert lam < 0 and lam_o < 0
+
+
+@pytest.mark.parametrize("name,r", [("tinyGrid3D", 5), ("smallGrid3D", 5)])
+def test_certificate_at_optimum(hip, name, r):
+    """After RTR from chordal initialisation on clean grids, S(X) is PSD up to rounding: the smallest
+    eigenvalue is ~0 (the rows of X span its null space)."""
+    meas = load_meas(name)
+    d, n = meas.d, meas.num_poses
+    Q = O.connection_laplacian(meas, n)
+    X0 = O.lifting_matrix(d, r) @ O.chordal_initialization(d, n, meas)
+    H = hip.Problem(n, d, r)
+    H.set_Q_scipy(0, Q)
+    Xo, _ = H.optimize(X0, hip.default_params(tr_iterations=100, tr_tolerance=1e-10, tr_max_inner=200,
+                                              precon=hip.PRECON_EXACT))
+    S = O.certificate_matrix(Q, Xo, d)
+    lam_max = float(np.abs(np.linalg.eigvalsh(S.toarray())).max())
+    lam, res, it, _ = H.certify(Xo, max_iters=600, tol=1e-10)
+    lam_o = O.certificate_min_eig(S)
+    assert abs(lam - lam_o) <= 1e-6 * lam_max
+    assert lam >= -1e-6 * lam_max
+    # X S(X) = grad f(X), ~0 at the first-order critical point RTR returns
+    P = O.QuadraticProblem(n, d, r)
+    P.set_Q(Q)
+    assert np.linalg.norm((S @ Xo.T).T) <= 1e-6 * lam_max
+    assert rel((S @ Xo.T).T, P.riegrad(Xo)) <= 1e-6 or P.riegrad_norm(Xo) < 1e-9
+
+
+def test_certificate_rejects_batched(hip):
+    H = hip.Problem(None, 3, 3, poses_per_agent=[4, 4])
+    with pytest.raises(Exception):
+        H.certify(np.zeros((3, 32)))

@@ -118,3 +118,22 @@ def test_cpu_port_matches_oracle_agent_step():
         ag.neighbor_pose[pid] = X0[:, gp * 4:gp * 4 + 4]
     ag.iterate(True)
     assert abs(f - ag.last_result["fOpt"]) <= 1e-9 * abs(ag.last_result["fOpt"])
+
+
+@pytest.mark.parametrize("name", ["tinyGrid3D", "smallGrid3D", "sphere2500", "input_INTEL_g2o", "city10000",
+                                  "kitti_00"])
+def test_chordal_initialization_matches_oracle(H, name):
+    """chordalInitialization (src/DPGO_utils.cpp:377-424): native host block-Cholesky solve of the
+    rotation / translation least squares vs the oracle's normal-equation solve (same minimiser)."""
+    from oracle import dpgo_oracle as O
+    from tests._common import load_meas, rel
+    meas = load_meas(name)
+    d, n = meas.d, meas.num_poses
+    T = H.chordal_initialization(d, n, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau)
+    To = O.chordal_initialization(d, n, meas)
+    assert rel(T, To) <= 1e-8
+    b = d + 1
+    for i in range(0, n, max(1, n // 50)):  # rotations on SO(d)
+        Ri = T[:, i * b:i * b + d]
+        assert np.abs(Ri.T @ Ri - np.eye(d)).max() <= 1e-12
+        assert np.linalg.det(Ri) > 0

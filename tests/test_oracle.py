@@ -174,3 +174,24 @@ def test_grid3d_fixture_is_reproducible():
     g = O.grid3d(4, seed=0)
     assert np.array_equal(g.R, z["R"]) and np.array_equal(g.t, z["t"]) and np.array_equal(g.p1, z["p1"])
     assert g.m == 3 * 16 * 3
+
+
+def test_certificate_matrix_properties():
+    """Build-defined certificate (no reference counterpart): at the committed RTR optimum of
+    smallGrid3D (r=5) S(X) = Q - Lambda(X) is PSD with X's rows in its null space; at a random point
+    it is indefinite; X S(X) equals the Riemannian gradient."""
+    meas = load_meas("smallGrid3D")
+    d, n = meas.d, meas.num_poses
+    Q = O.connection_laplacian(meas, n)
+    z = np.load(os.path.join(GOLDEN, "smallGrid3D.r5.rtr.npz"))
+    Xo = z["Xopt"]
+    S = O.certificate_matrix(Q, Xo, d)
+    ev = np.linalg.eigvalsh(S.toarray())
+    assert ev[0] >= -1e-6 * abs(ev[-1])
+    # X S(X) is the Riemannian gradient P_X(XQ) (the fixture stopped at gradnorm ~5e-2)
+    P = O.QuadraticProblem(n, d, 5)
+    P.set_Q(Q)
+    assert rel((S @ Xo.T).T, P.riegrad(Xo)) <= 1e-9
+    assert O.certificate_min_eig(S) == pytest.approx(ev[0], abs=1e-9 * abs(ev[-1]))
+    X = random_point(5, d, n, 61)
+    assert O.certificate_min_eig(O.certificate_matrix(Q, X, d)) < 0
