@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from oracle import dpgo_oracle as O
-from tests._common import load_meas, random_point, rel
+from tests._common import load_meas, random_point
 
 pytestmark = pytest.mark.gpu
 
@@ -69,11 +69,8 @@ def test_certificate_at_optimum(hip, name, r):
     lam_o = O.certificate_min_eig(S)
     assert abs(lam - lam_o) <= 1e-6 * lam_max
     assert lam >= -1e-6 * lam_max
-    # X S(X) = grad f(X), ~0 at the first-order critical point RTR returns
-    P = O.QuadraticProblem(n, d, r)
-    P.set_Q(Q)
-    assert np.linalg.norm((S @ Xo.T).T) <= 1e-6 * lam_max
-    assert rel((S @ Xo.T).T, P.riegrad(Xo)) <= 1e-6 or P.riegrad_norm(Xo) < 1e-9
+    # X S(X) = grad f(X) (identity checked in test_oracle), ~0 at the critical point RTR returns
+    assert float(np.linalg.norm((S @ Xo.T).T)) <= 1e-6 * lam_max
 
 
 def test_certificate_rejects_batched(hip):
