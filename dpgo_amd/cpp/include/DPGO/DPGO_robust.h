@@ -2,6 +2,8 @@
 #ifndef DPGO_AMD_ROBUST_H
 #define DPGO_AMD_ROBUST_H
 
+#include <cstddef>
+
 namespace DPGO {
 
 enum RobustCostType { L2, L1, TLS, Huber, GM, GNC_TLS };
@@ -21,6 +23,8 @@ class RobustCost {
   double weight(double r) const;
   void reset();
   void update();
+  // include/DPGO/DPGO_robust.h:107-113: sqrt(chi2inv(quantile, 6)) for 3D measurements, 1e5 at quantile >= 1
+  static double computeErrorThresholdAtQuantile(double quantile, size_t dimension);
 
  private:
   RobustCostType mCostType;

@@ -28,6 +28,25 @@ Matrix fixedStiefelVariable(unsigned d, unsigned r);
 double computeMeasurementError(const RelativeSEMeasurement& m, const Matrix& R1, const Matrix& t1, const Matrix& R2,
                                const Matrix& t2);
 
+// src/DPGO_utils.cpp:517-520 (boost::math chi-squared quantile there; regularized incomplete gamma
+// inverted by bisection here, to ~1e-14 relative)
+double chi2inv(double quantile, size_t dof);
+// src/DPGO_utils.cpp:522-531
+double angular2ChordalSO3(double rad);
+void checkRotationMatrix(const Matrix& R);
+// src/DPGO_utils.cpp:533-580: weighted averages (kappa / tau empty = all ones)
+void singleTranslationAveraging(Vector& tOpt, const std::vector<Vector>& tVec, const Vector& tau = Vector());
+void singleRotationAveraging(Matrix& ROpt, const std::vector<Matrix>& RVec, const Vector& kappa = Vector());
+void singlePoseAveraging(Matrix& ROpt, Vector& tOpt, const std::vector<Matrix>& RVec, const std::vector<Vector>& tVec,
+                         const Vector& kappa = Vector(), const Vector& tau = Vector());
+// src/DPGO_utils.cpp:582-710: GNC-TLS robust averages, inlier indices in ascending order
+void robustSingleRotationAveraging(Matrix& ROpt, std::vector<size_t>& inlierIndices, const std::vector<Matrix>& RVec,
+                                   const Vector& kappa = Vector(), double errorThreshold = 0.1);
+void robustSinglePoseAveraging(Matrix& ROpt, Vector& tOpt, std::vector<size_t>& inlierIndices,
+                               const std::vector<Matrix>& RVec, const std::vector<Vector>& tVec,
+                               const Vector& kappa = Vector(), const Vector& tau = Vector(),
+                               double errorThreshold = 0.1);
+
 }  // namespace DPGO
 
 #endif

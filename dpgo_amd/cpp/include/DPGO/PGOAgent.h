@@ -1,7 +1,7 @@
 // PGOAgent, RBCD-round portion (reference include/DPGO/PGOAgent.h:59-726, src/PGOAgent.cpp).
 // The per-round arithmetic (updateX -> QuadraticOptimizer) runs on the GPU; Q/G assembly, GNC
-// weights and Nesterov bookkeeping stay on the host, as in the reference.  Out of scope (DESIGN.md
-// section 9): async optimisation thread, robust global-frame initialisation, logging.
+// weights, Nesterov bookkeeping and the robust global-frame initialisation (:250-432) stay on the
+// host, as in the reference.  Out of scope: async optimisation thread, logging.
 #ifndef DPGO_AMD_PGOAGENT_H
 #define DPGO_AMD_PGOAGENT_H
 
@@ -83,6 +83,11 @@ class PGOAgent {
   bool getTrajectoryInLocalFrame(Matrix& Trajectory);
   Matrix localPoseGraphOptimization();
   void setGlobalAnchor(const Matrix& M) { globalAnchor = M; }
+  // robust global-frame initialisation (reference include/DPGO/PGOAgent.h:449-474)
+  Matrix computeNeighborTransform(const PoseID& nID, const Matrix& var);
+  Matrix computeRobustNeighborTransformTwoStage(unsigned neighborID, const PoseDict& poseDict);
+  Matrix computeRobustNeighborTransform(unsigned neighborID, const PoseDict& poseDict);
+  void initializeInGlobalFrame(unsigned neighborID, const PoseDict& poseDict);
 
   unsigned getID() const { return mID; }
   unsigned num_poses() const { return n; }
@@ -106,6 +111,8 @@ class PGOAgent {
   void addOdometry(const RelativeSEMeasurement& m);
   void addPrivateLoopClosure(const RelativeSEMeasurement& m);
   void addSharedLoopClosure(const RelativeSEMeasurement& m);
+  RelativeSEMeasurement& findSharedLoopClosureWithNeighbor(const PoseID& nID);
+  void collectNeighborTransforms(const PoseDict& poseDict, std::vector<Matrix>& RVec, std::vector<Vector>& tVec);
   void constructQMatrix();
   bool constructGMatrix(const PoseDict& poseDict);
   bool updateX(bool doOptimization, bool acceleration);

@@ -1,8 +1,11 @@
 // Host utilities (reference src/DPGO_utils.cpp); the g2o parser is the library's own reader.
+#include <DPGO/DPGO_robust.h>
 #include <DPGO/DPGO_utils.h>
 #include <dpgo_rbcd.h>
 
 #include <algorithm>
+#include <cassert>
+#include <cmath>
 #include <random>
 #include <stdexcept>
 #include <string>
@@ -178,6 +181,182 @@ double computeMeasurementError(const RelativeSEMeasurement& m, const Matrix& R1,
   const double rot = (R1 * m.R - R2).squaredNorm();
   const double tr = (t2 - t1 - R1 * m.t).squaredNorm();
   return m.kappa * rot + m.tau * tr;
+}
+
+}  // namespace DPGO
+
+namespace DPGO {
+
+namespace {
+
+// Regularized lower incomplete gamma P(a, x): series below a + 1, Lentz continued fraction above.
+double gamma_p(double a, double x) {
+  if (x <= 0) return 0.0;
+  const double lg = std::lgamma(a);
+  if (x < a + 1) {
+    double term = 1.0 / a, sum = term;
+    for (int k = 1; k < 10000; ++k) {
+      term *= x / (a + k);
+      sum += term;
+      if (std::fabs(term) < std::fabs(sum) * 1e-17) break;
+    }
+    return sum * std::exp(-x + a * std::log(x) - lg);
+  }
+  const double tiny = 1e-300;
+  double b = x + 1 - a, c = 1 / tiny, dd = 1 / b, h = dd;
+  for (int k = 1; k < 10000; ++k) {
+    const double an = -k * (k - a);
+    b += 2;
+    dd = an * dd + b;
+    if (std::fabs(dd) < tiny) dd = tiny;
+    c = b + an / c;
+    if (std::fabs(c) < tiny) c = tiny;
+    dd = 1 / dd;
+    const double del = dd * c;
+    h *= del;
+    if (std::fabs(del - 1) < 1e-17) break;
+  }
+  return 1.0 - std::exp(-x + a * std::log(x) - lg) * h;
+}
+
+Vector ones_or(const Vector& v, size_t n, double fill) {
+  if (static_cast<size_t>(v.rows()) == n && n > 0) return v;
+  Vector o(static_cast<long>(n), 1);
+  for (size_t i = 0; i < n; ++i) o(static_cast<long>(i), 0) = fill;
+  return o;
+}
+
+}  // namespace
+
+double chi2inv(double quantile, size_t dof) {
+  if (!(quantile > 0 && quantile < 1) || dof == 0) throw std::invalid_argument("chi2inv: quantile in (0,1), dof > 0");
+  const double a = 0.5 * static_cast<double>(dof);
+  double lo = 0, hi = std::max(1.0, 2.0 * a);
+  while (gamma_p(a, hi) < quantile) hi *= 2;
+  for (int it = 0; it < 200 && hi - lo > 1e-15 * hi; ++it) {
+    const double mid = 0.5 * (lo + hi);
+    (gamma_p(a, mid) < quantile ? lo : hi) = mid;
+  }
+  return 2.0 * 0.5 * (lo + hi);  // chi2 quantile = 2 * Gamma(k/2, 1) quantile
+}
+
+double angular2ChordalSO3(double rad) { return 2 * std::sqrt(2.0) * std::sin(rad / 2); }
+
+void checkRotationMatrix(const Matrix& R) {  // asserts in the reference (compiled out in Release)
+  const long d = R.rows();
+  assert(R.cols() == d);
+  assert(std::fabs(R.determinant() - 1.0) < 1e-8);
+  assert((R.transpose() * R - Matrix::Identity(d, d)).norm() < 1e-8);
+  (void)d;
+}
+
+void singleTranslationAveraging(Vector& tOpt, const std::vector<Vector>& tVec, const Vector& tau) {
+  const size_t n = tVec.size();
+  if (n == 0) throw std::invalid_argument("singleTranslationAveraging: empty input");
+  const Vector w = ones_or(tau, n, 1.0);
+  Vector s = Matrix::Zero(tVec[0].rows(), 1);
+  double ws = 0;
+  for (size_t i = 0; i < n; ++i) {
+    s += w(static_cast<long>(i), 0) * tVec[i];
+    ws += w(static_cast<long>(i), 0);
+  }
+  tOpt = s * (1.0 / ws);
+}
+
+void singleRotationAveraging(Matrix& ROpt, const std::vector<Matrix>& RVec, const Vector& kappa) {
+  const size_t n = RVec.size();
+  if (n == 0) throw std::invalid_argument("singleRotationAveraging: empty input");
+  const Vector w = ones_or(kappa, n, 1.0);
+  Matrix M = Matrix::Zero(RVec[0].rows(), RVec[0].cols());
+  for (size_t i = 0; i < n; ++i) M += w(static_cast<long>(i), 0) * RVec[i];
+  ROpt = projectToRotationGroup(M);
+}
+
+void singlePoseAveraging(Matrix& ROpt, Vector& tOpt, const std::vector<Matrix>& RVec, const std::vector<Vector>& tVec,
+                         const Vector& kappa, const Vector& tau) {
+  if (RVec.empty() || RVec.size() != tVec.size()) throw std::invalid_argument("singlePoseAveraging: bad input");
+  singleTranslationAveraging(tOpt, tVec, tau);
+  singleRotationAveraging(ROpt, RVec, kappa);
+}
+
+namespace {
+
+// The GNC-TLS loop shared by both robust averages (src/DPGO_utils.cpp:600-640 and :672-705):
+// mu0 = min(cbar^2 / (2 max r^2 - cbar^2), 1e-5); skipped when mu0 <= 0 (all residuals small).
+template <typename Solve, typename Residual>
+void gnc_tls_average(size_t n, double barc, unsigned maxIters, Vector& weights, Solve solve, Residual rsq) {
+  const double w_tol = 1e-8;
+  solve(weights);
+  double maxr = 0;
+  for (size_t i = 0; i < n; ++i) maxr = std::max(maxr, rsq(i));
+  const double barcSq = barc * barc;
+  const double muInit = std::min(barcSq / (2 * maxr - barcSq), 1e-5);
+  if (!(muInit > 0)) return;
+  RobustCostParameters params;
+  params.GNCBarc = barc;
+  params.GNCMaxNumIters = maxIters;
+  params.GNCInitMu = muInit;
+  RobustCost cost(GNC_TLS, params);
+  for (unsigned iter = 0; iter < maxIters; ++iter) {
+    solve(weights);
+    size_t nc = 0;
+    for (size_t i = 0; i < n; ++i) {
+      const double wi = cost.weight(std::sqrt(rsq(i)));
+      if (wi < w_tol || wi > 1 - w_tol) nc++;
+      weights(static_cast<long>(i), 0) = wi;
+    }
+    if (nc == n) break;
+    cost.update();
+  }
+}
+
+void inliers_of(const Vector& weights, std::vector<size_t>& idx) {
+  idx.clear();
+  for (long i = 0; i < weights.rows(); ++i)
+    if (weights(i, 0) > 1 - 1e-8) idx.push_back(static_cast<size_t>(i));
+}
+
+}  // namespace
+
+void robustSingleRotationAveraging(Matrix& ROpt, std::vector<size_t>& inlierIndices, const std::vector<Matrix>& RVec,
+                                   const Vector& kappa, double errorThreshold) {
+  const size_t n = RVec.size();
+  if (n == 0) throw std::invalid_argument("robustSingleRotationAveraging: empty input");
+  const Vector k = ones_or(kappa, n, 1.0);
+  for (const auto& Ri : RVec) checkRotationMatrix(Ri);
+  Vector w = ones_or(Vector(), n, 1.0);
+  auto solve = [&](const Vector& wt) {  // kappa .* w (w = 1 for the initial estimate, :600)
+    Vector kw = k;
+    for (size_t i = 0; i < n; ++i) kw(static_cast<long>(i), 0) *= wt(static_cast<long>(i), 0);
+    singleRotationAveraging(ROpt, RVec, kw);
+  };
+  auto rsq = [&](size_t i) { return k(static_cast<long>(i), 0) * (ROpt - RVec[i]).squaredNorm(); };
+  gnc_tls_average(n, errorThreshold, 1000, w, solve, rsq);
+  inliers_of(w, inlierIndices);
+}
+
+void robustSinglePoseAveraging(Matrix& ROpt, Vector& tOpt, std::vector<size_t>& inlierIndices,
+                               const std::vector<Matrix>& RVec, const std::vector<Vector>& tVec, const Vector& kappa,
+                               const Vector& tau, double errorThreshold) {
+  const size_t n = RVec.size();
+  if (n == 0 || tVec.size() != n) throw std::invalid_argument("robustSinglePoseAveraging: bad input");
+  const Vector k = ones_or(kappa, n, 10000.0), t = ones_or(tau, n, 100.0);
+  for (const auto& Ri : RVec) checkRotationMatrix(Ri);
+  Vector w = ones_or(Vector(), n, 1.0);
+  auto solve = [&](const Vector& wt) {
+    Vector kw = k, tw = t;
+    for (size_t i = 0; i < n; ++i) {
+      kw(static_cast<long>(i), 0) *= wt(static_cast<long>(i), 0);
+      tw(static_cast<long>(i), 0) *= wt(static_cast<long>(i), 0);
+    }
+    singlePoseAveraging(ROpt, tOpt, RVec, tVec, kw, tw);
+  };
+  auto rsq = [&](size_t i) {
+    return k(static_cast<long>(i), 0) * (ROpt - RVec[i]).squaredNorm() +
+           t(static_cast<long>(i), 0) * (tOpt - tVec[i]).squaredNorm();
+  };
+  gnc_tls_average(n, errorThreshold, 10000, w, solve, rsq);
+  inliers_of(w, inlierIndices);
 }
 
 }  // namespace DPGO

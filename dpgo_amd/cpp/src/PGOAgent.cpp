@@ -41,6 +41,11 @@ void RobustCost::reset() {
   mGNCIteration = 0;
 }
 
+double RobustCost::computeErrorThresholdAtQuantile(double quantile, size_t dimension) {
+  if (dimension != 3 || !(quantile > 0)) throw std::invalid_argument("computeErrorThresholdAtQuantile: 3D only");
+  return quantile < 1 ? std::sqrt(chi2inv(quantile, 6)) : 1e5;
+}
+
 void RobustCost::update() {
   if (mCostType != GNC_TLS) return;
   if (++mGNCIteration > mParams.GNCMaxNumIters) return;
@@ -174,8 +179,122 @@ void PGOAgent::setNeighborStatus(const PGOAgentStatus& s) {
 
 PGOAgentStatus PGOAgent::getNeighborStatus(unsigned id) const { return mTeamStatus.at(id); }
 
+// ---------------------------------------------------------------- global-frame initialisation
+RelativeSEMeasurement& PGOAgent::findSharedLoopClosureWithNeighbor(const PoseID& nID) {  // :922-934
+  for (auto& m : sharedLoopClosures)
+    if ((m.r1 == nID.first && m.p1 == nID.second) || (m.r2 == nID.first && m.p2 == nID.second)) return m;
+  throw std::runtime_error("Cannot find shared loop closure with neighbor.");
+}
+
+Matrix PGOAgent::computeNeighborTransform(const PoseID& nID, const Matrix& var) {  // :250-287
+  if (!YLift || !TLocalInit) throw std::logic_error("computeNeighborTransform: lifting matrix / local init missing");
+  const RelativeSEMeasurement& m = findSharedLoopClosureWithNeighbor(nID);
+  const long b = d + 1;
+  Matrix dT = Matrix::Identity(b, b);
+  dT.setBlock(0, 0, m.R);
+  dT.setBlock(0, d, m.t);
+  // the neighbour's pose rounded back to SE(d) in its (already global) frame
+  Matrix Tw2f2 = Matrix::Identity(b, b);
+  Tw2f2.setBlock(0, 0, YLift->transpose() * var);
+  Matrix Tf1f2, Tw1f1 = Matrix::Identity(b, b);
+  if (m.r1 == nID.first) {  // incoming edge: neighbour -> me
+    Tf1f2 = dT.inverse();
+    Tw1f1.setBlock(0, 0, TLocalInit->block(0, m.p2 * b, d, b));
+  } else {  // outgoing edge: me -> neighbour
+    Tf1f2 = dT;
+    Tw1f1.setBlock(0, 0, TLocalInit->block(0, m.p1 * b, d, b));
+  }
+  const Matrix Tw2w1 = Tw2f2 * Tf1f2.inverse() * Tw1f1.inverse();
+  checkRotationMatrix(Tw2w1.block(0, 0, d, d));
+  return Tw2w1;
+}
+
+void PGOAgent::collectNeighborTransforms(const PoseDict& poseDict, std::vector<Matrix>& RVec,
+                                         std::vector<Vector>& tVec) {
+  for (const auto& kv : poseDict) {
+    if (neighborSharedPoseIDs.find(kv.first) == neighborSharedPoseIDs.end()) continue;
+    const Matrix T = computeNeighborTransform(kv.first, kv.second);
+    RVec.push_back(T.block(0, 0, d, d));
+    tVec.push_back(T.block(0, d, d, 1));
+  }
+}
+
+Matrix PGOAgent::computeRobustNeighborTransformTwoStage(unsigned neighborID, const PoseDict& poseDict) {  // :289-332
+  std::vector<Matrix> RVec;
+  std::vector<Vector> tVec;
+  collectNeighborTransforms(poseDict, RVec, tVec);
+  if (RVec.empty()) throw std::runtime_error("no shared loop closure with this neighbor");
+  Matrix ROpt;
+  Vector tOpt;
+  std::vector<size_t> inliers;
+  // robust single rotation averaging with a ~30 deg chordal threshold, unit kappa
+  robustSingleRotationAveraging(ROpt, inliers, RVec, Vector(), angular2ChordalSO3(0.5));
+  if (mParams.verbose)
+    std::printf("[RobustRelativeTransform] This robot %u, neighbor %u: finds %zu inliers out of %zu measurements.\n",
+                mID, neighborID, inliers.size(), RVec.size());
+  if (inliers.empty()) throw std::runtime_error("Robust single rotation averaging returns empty inlier set!");
+  std::vector<Vector> tIn;
+  for (size_t i : inliers) tIn.push_back(tVec[i]);
+  singleTranslationAveraging(tOpt, tIn);
+  Matrix T = Matrix::Identity(d + 1, d + 1);
+  T.setBlock(0, 0, ROpt);
+  T.setBlock(0, d, tOpt);
+  return T;
+}
+
+Matrix PGOAgent::computeRobustNeighborTransform(unsigned neighborID, const PoseDict& poseDict) {  // :334-367
+  std::vector<Matrix> RVec;
+  std::vector<Vector> tVec;
+  collectNeighborTransforms(poseDict, RVec, tVec);
+  if (RVec.empty()) throw std::runtime_error("no shared loop closure with this neighbor");
+  const size_t m = RVec.size();
+  Vector kappa(static_cast<long>(m), 1), tau(static_cast<long>(m), 1);
+  for (size_t i = 0; i < m; ++i) {
+    kappa(static_cast<long>(i), 0) = 1.82;  // rotation stddev ~30 deg
+    tau(static_cast<long>(i), 0) = 0.01;    // translation stddev 10 m
+  }
+  Matrix ROpt;
+  Vector tOpt;
+  std::vector<size_t> inliers;
+  robustSinglePoseAveraging(ROpt, tOpt, inliers, RVec, tVec, kappa, tau,
+                            RobustCost::computeErrorThresholdAtQuantile(0.9, 3));
+  if (mParams.verbose)
+    std::printf("[RobustRelativeTransform] This robot %u, neighbor %u: finds %zu inliers out of %zu measurements.\n",
+                mID, neighborID, inliers.size(), m);
+  if (inliers.empty()) throw std::runtime_error("Robust single pose averaging returns empty inlier set!");
+  Matrix T = Matrix::Identity(d + 1, d + 1);
+  T.setBlock(0, 0, ROpt);
+  T.setBlock(0, d, tOpt);
+  return T;
+}
+
+void PGOAgent::initializeInGlobalFrame(unsigned neighborID, const PoseDict& poseDict) {  // :369-432
+  if (!YLift) throw std::logic_error("initializeInGlobalFrame: lifting matrix not set");
+  neighborPoseDict.clear();
+  neighborAuxPoseDict.clear();
+  Matrix Tw2w1;
+  try {
+    Tw2w1 = computeRobustNeighborTransformTwoStage(neighborID, poseDict);
+  } catch (const std::runtime_error&) {
+    std::printf("Robust initialization is not successful! Abort and wait to try again...\n");
+    return;
+  }
+  const long b = d + 1;
+  Matrix T = *TLocalInit;
+  Matrix Tw1f = Matrix::Identity(b, b);
+  for (unsigned i = 0; i < n; ++i) {
+    Tw1f.setBlock(0, 0, T.block(0, i * b, d, b));
+    T.setBlock(0, i * b, (Tw2w1 * Tw1f).block(0, 0, d, b));
+  }
+  X = (*YLift) * T;
+  XInit = X;
+  mState = INITIALIZED;
+  if (mParams.acceleration) initializeAcceleration();
+}
+
 void PGOAgent::updateNeighborPoses(unsigned neighborID, const PoseDict& poseDict) {  // :434-458
   const bool neighborInit = getNeighborStatus(neighborID).state == INITIALIZED;
+  if (mState == WAIT_FOR_INITIALIZATION && neighborInit) initializeInGlobalFrame(neighborID, poseDict);
   for (const auto& kv : poseDict) {
     if (neighborSharedPoseIDs.find(kv.first) == neighborSharedPoseIDs.end()) continue;
     if (mState == INITIALIZED && neighborInit) neighborPoseDict[kv.first] = kv.second;

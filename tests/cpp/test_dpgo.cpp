@@ -1,6 +1,6 @@
 // C++ tests of the drop-in layer, mirroring the reference's gtests (tests/*.cpp of lajoiepy/dpgo)
 // plus the multi-robot example loop (examples/MultiRobotExample.cpp:175-264).  Needs a gfx950 GPU.
-// Usage: test_dpgo <tests/golden dir>
+// Usage: test_dpgo <tests/golden dir> [--host]   (--host: only the cases that make no GPU call)
 #include <DPGO/DPGO_utils.h>
 #include <DPGO/PGOAgent.h>
 #include <DPGO/QuadraticOptimizer.h>
@@ -270,18 +270,235 @@ static void multiRobotExample(const std::string& golden) {
   EXPECT(best < 0.7 * cost0);  // (the GNC_TLS re-weighting at iteration 29 raises the unweighted cost)
 }
 
+// Eigen::Quaterniond::UnitRandom().toRotationMatrix() restated: normalised 4-D Gaussian quaternion
+static Matrix randomRotation(std::mt19937_64& rng) {
+  std::normal_distribution<double> N(0.0, 1.0);
+  double q[4], nn = 0;
+  for (double& x : q) {
+    x = N(rng);
+    nn += x * x;
+  }
+  nn = std::sqrt(nn);
+  const double w = q[0] / nn, x = q[1] / nn, y = q[2] / nn, z = q[3] / nn;
+  return rowmajor(3, 3, {1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+                         2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+                         2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)});
+}
+
+static Vector constVec(size_t n, double v) {
+  Vector o(static_cast<long>(n), 1);
+  for (size_t i = 0; i < n; ++i) o(static_cast<long>(i), 0) = v;
+  return o;
+}
+
+// tests/testUtils.cpp:55-72 (plus the tabulated quantiles chi2inv(0.95, 4), chi2inv(0.9, 6))
+static void testChi2Inv() {
+  EXPECT(std::fabs(chi2inv(0.95, 4) - 9.487729036781154) <= 1e-9);
+  EXPECT(std::fabs(chi2inv(0.9, 6) - 10.64464067566842) <= 1e-9);
+  EXPECT(std::fabs(chi2inv(0.5, 2) - 2 * std::log(2.0)) <= 1e-12);
+  const double threshold = chi2inv(0.95, 4);
+  std::mt19937 rng(7);
+  std::chi_squared_distribution<double> dist(4);
+  int count = 0;
+  for (int i = 0; i < 100000; ++i) count += dist(rng) < threshold;
+  EXPECT(std::fabs(count / 100000.0 - 0.95) <= 0.01);
+}
+
+// tests/testUtils.cpp:74-118
+static void testRobustSingleRotationAveraging() {
+  std::mt19937_64 rng(11);
+  for (int trial = 0; trial < 50; ++trial) {
+    const Matrix RTrue = randomRotation(rng);
+    Matrix ROpt;
+    std::vector<size_t> inl;
+    robustSingleRotationAveraging(ROpt, inl, {RTrue}, constVec(1, 1.0), angular2ChordalSO3(0.5));
+    EXPECT((ROpt - RTrue).norm() <= 1e-8);
+    EXPECT(inl.size() == 1 && inl[0] == 0);
+  }
+  for (int trial = 0; trial < 50; ++trial) {
+    const double tol = angular2ChordalSO3(0.02), cbar = angular2ChordalSO3(0.3);
+    const Matrix RTrue = randomRotation(rng);
+    std::vector<Matrix> RVec(10, RTrue);
+    while (RVec.size() < 50) {
+      Matrix RRand = randomRotation(rng);
+      if ((RRand - RTrue).norm() > 1.2 * cbar) RVec.push_back(RRand);
+    }
+    Matrix ROpt;
+    std::vector<size_t> inl;
+    robustSingleRotationAveraging(ROpt, inl, RVec, constVec(50, 1.0), cbar);
+    EXPECT(std::fabs(ROpt.determinant() - 1.0) < 1e-8);
+    EXPECT((ROpt - RTrue).norm() <= tol);
+    EXPECT(inl.size() == 10);
+    for (size_t i = 0; i < inl.size() && i < 10; ++i) EXPECT(inl[i] == i);
+  }
+}
+
+// tests/testUtils.cpp:120-190
+static void testRobustSinglePoseAveraging() {
+  std::mt19937_64 rng(12);
+  std::uniform_real_distribution<double> U(-1.0, 1.0);
+  const double barc = RobustCost::computeErrorThresholdAtQuantile(0.9, 3);
+  for (int trial = 0; trial < 50; ++trial) {
+    const Matrix RTrue = randomRotation(rng);
+    const Vector tTrue = Matrix::Zero(3, 1);
+    Matrix ROpt;
+    Vector tOpt;
+    std::vector<size_t> inl;
+    robustSinglePoseAveraging(ROpt, tOpt, inl, {RTrue}, {tTrue}, constVec(1, 10000), constVec(1, 100), barc);
+    EXPECT((ROpt - RTrue).norm() <= 1e-8);
+    EXPECT((tOpt - tTrue).norm() <= 1e-8);
+    EXPECT(inl.size() == 1 && inl[0] == 0);
+  }
+  for (int trial = 0; trial < 50; ++trial) {
+    const double kappa = 10000, tau = 100;
+    const Matrix RTrue = randomRotation(rng);
+    const Vector tTrue = Matrix::Zero(3, 1);
+    std::vector<Matrix> RVec(10, RTrue);
+    std::vector<Vector> tVec(10, tTrue);
+    while (RVec.size() < 50) {
+      Matrix RRand = randomRotation(rng);
+      Vector tRand(3, 1);
+      for (long i = 0; i < 3; ++i) tRand(i, 0) = U(rng);
+      const double rSq = kappa * (RTrue - RRand).squaredNorm() + tau * (tTrue - tRand).squaredNorm();
+      if (std::sqrt(rSq) > 1.2 * barc) {
+        RVec.push_back(RRand);
+        tVec.push_back(tRand);
+      }
+    }
+    Matrix ROpt;
+    Vector tOpt;
+    std::vector<size_t> inl;
+    robustSinglePoseAveraging(ROpt, tOpt, inl, RVec, tVec, constVec(50, kappa), constVec(50, tau), barc);
+    EXPECT((ROpt - RTrue).norm() <= angular2ChordalSO3(0.02));
+    EXPECT((tOpt - tTrue).norm() <= 1e-2);
+    EXPECT(inl.size() == 10);
+    for (size_t i = 0; i < inl.size() && i < 10; ++i) EXPECT(inl[i] == i);
+  }
+}
+
+// PGOAgent::initializeInGlobalFrame (src/PGOAgent.cpp:250-432) on a noise-free 3D lattice split over
+// two robots: robot 1 starts in the frame of its own first pose (chordal local init); after
+// receiving robot 0's public poses it must hold the ground truth in robot 0's frame.  Two shared
+// loop closures are corrupted and must be rejected by the robust rotation average.
+static void testMultiRobotInitialization() {
+  const unsigned d = 3, r = 5, k = 4, n = k * k * k, half = n / 2;
+  std::mt19937_64 rng(21);
+  std::vector<Matrix> Rw(n), tw(n);
+  for (unsigned i = 0; i < n; ++i) {
+    Rw[i] = randomRotation(rng);
+    tw[i] = rowmajor(3, 1, {double(i % k), double((i / k) % k), double(i / (k * k))});
+  }
+  auto meas = [&](unsigned a, unsigned b) {
+    RelativeSEMeasurement m;
+    m.r1 = a < half ? 0 : 1;
+    m.r2 = b < half ? 0 : 1;
+    m.p1 = a < half ? a : a - half;
+    m.p2 = b < half ? b : b - half;
+    m.R = Rw[a].transpose() * Rw[b];
+    m.t = Rw[a].transpose() * (tw[b] - tw[a]);
+    m.kappa = 12.5;
+    m.tau = 100;
+    return m;
+  };
+  std::vector<RelativeSEMeasurement> odo[2], priv[2], shared[2];
+  int corrupted = 0;
+  for (unsigned a = 0; a < n; ++a)
+    for (unsigned b = a + 1; b < n; ++b) {
+      const double dist = (tw[b] - tw[a]).norm();
+      if (b != a + 1 && dist > 1.0 + 1e-9) continue;  // odometry chain + lattice neighbours
+      RelativeSEMeasurement m = meas(a, b);
+      if (m.r1 == m.r2) {
+        (b == a + 1 ? odo : priv)[m.r1].push_back(m);
+      } else {
+        if (corrupted < 2 && (a % 7) == 3) {
+          m.R = randomRotation(rng);  // outlier inter-robot loop closure
+          ++corrupted;
+        }
+        shared[0].push_back(m);
+        shared[1].push_back(m);
+      }
+    }
+  PGOAgentParameters opts(d, r, 2);
+  opts.robustCostType = L2;
+  PGOAgent a0(0, opts), a1(1, opts);
+  a0.setPoseGraph(odo[0], priv[0], shared[0]);
+  a1.setPoseGraph(odo[1], priv[1], shared[1]);
+  Matrix YLift;
+  EXPECT(a0.getLiftingMatrix(YLift));
+  a1.setLiftingMatrix(YLift);
+  EXPECT(a0.getState() == INITIALIZED);
+  EXPECT(a1.getState() == WAIT_FOR_INITIALIZATION);
+  PoseDict dict;
+  EXPECT(a0.getSharedPoseDict(dict));
+  EXPECT(!dict.empty());
+  a1.setNeighborStatus(a0.getStatus());
+  Matrix Tr;
+  {  // per-public-pose transforms vs the true T_world0_frame1 (robot 1's frame = its first pose)
+    Matrix Ttrue = Matrix::Identity(4, 4);
+    Ttrue.setBlock(0, 0, Rw[0].transpose() * Rw[half]);
+    Ttrue.setBlock(0, 3, Rw[0].transpose() * (tw[half] - tw[0]));
+    std::vector<Matrix> RV;
+    std::vector<size_t> exact;
+    for (const auto& kv : dict) {
+      const Matrix T = a1.computeNeighborTransform(kv.first, kv.second);
+      if ((T - Ttrue).norm() <= 1e-12) exact.push_back(RV.size());
+      RV.push_back(T.block(0, 0, 3, 3));
+    }
+    EXPECT(exact.size() + 2 == dict.size());  // the two corrupted closures
+    Matrix Ro;
+    std::vector<size_t> inl;
+    robustSingleRotationAveraging(Ro, inl, RV, Vector(), angular2ChordalSO3(0.5));
+    EXPECT(inl == exact);
+    // GNC returns the average solved with the last-but-one weights (src/DPGO_utils.cpp:618-637), so
+    // the outliers keep a small weight in ROpt: the reference's tolerance (testUtils.cpp:95)
+    Tr = a1.computeRobustNeighborTransformTwoStage(0, dict);
+    EXPECT((Tr.block(0, 0, 3, 3) - Ttrue.block(0, 0, 3, 3)).norm() <= angular2ChordalSO3(0.02));
+    EXPECT((Tr.block(0, 0, 3, 3) - Ro).norm() <= 1e-14);
+  }
+  a1.updateNeighborPoses(0, dict);
+  EXPECT(a1.getState() == INITIALIZED);
+  Matrix X1;
+  a1.getX(X1);
+  const Matrix T1 = YLift.transpose() * X1;
+  // X1 = YLift * (Tr * T_local): robot 1's local chordal init is the ground truth in the frame of its
+  // first pose, so T1 = Tr * (T_frame1_i) exactly; and within the averaging tolerance of the truth
+  double err = 0, dev = 0;
+  Matrix Tf1 = Matrix::Identity(4, 4);
+  for (unsigned i = 0; i < n - half; ++i) {
+    Tf1.setBlock(0, 0, Rw[half].transpose() * Rw[half + i]);
+    Tf1.setBlock(0, 3, Rw[half].transpose() * (tw[half + i] - tw[half]));
+    const Matrix Ti = (Tr * Tf1).block(0, 0, 3, 4);
+    err = std::max(err, (T1.block(0, i * (d + 1), d, d + 1) - Ti).norm());
+    const Matrix R = Rw[0].transpose() * Rw[half + i];
+    const Matrix t = Rw[0].transpose() * (tw[half + i] - tw[0]);
+    dev = std::max(dev, (T1.block(0, i * (d + 1), d, d) - R).norm());
+    dev = std::max(dev, (T1.block(0, i * (d + 1) + d, d, 1) - t).norm() / 10.0);
+  }
+  EXPECT(corrupted == 2);
+  EXPECT(err <= 1e-10);
+  EXPECT(dev <= angular2ChordalSO3(0.02));
+  if (err > 1e-10 || dev > angular2ChordalSO3(0.02)) std::printf("  pose error %.3e, vs truth %.3e\n", err, dev);
+}
+
 int main(int argc, char** argv) {
   const std::string golden = argc > 1 ? argv[1] : "tests/golden";
+  const bool host_only = argc > 2 && std::string(argv[2]) == "--host";
   struct T {
     const char* name;
     std::function<void()> fn;
-  } tests[] = {{"Construction", testConstruction},
+    bool host;
+  } tests[] = {{"Chi2Inv", testChi2Inv, true},
+               {"RobustSingleRotationAveraging", testRobustSingleRotationAveraging, true},
+               {"RobustSinglePoseAveraging", testRobustSinglePoseAveraging, true},
+               {"MultiRobotInitialization", testMultiRobotInitialization, false},
+               {"Construction", testConstruction, true},
                {"MemoryLayout", testMemoryLayout},
                {"Stiefel", testStiefel},
                {"TriangleGraph", testTriangleGraph},
                {"LineGraph", testLineGraph},
                {"MultiRobotExample", [&] { multiRobotExample(golden); }}};
   for (auto& t : tests) {
+    if (host_only && !t.host) continue;
     const int before = g_fail;
     try {
       t.fn();

@@ -21,8 +21,9 @@ def cpp_output():
     return p.returncode, p.stdout + p.stderr
 
 
-@pytest.mark.parametrize("name", ["Construction", "MemoryLayout", "Stiefel", "TriangleGraph", "LineGraph",
-                                  "MultiRobotExample"])
+@pytest.mark.parametrize("name", ["Chi2Inv", "RobustSingleRotationAveraging", "RobustSinglePoseAveraging",
+                                  "MultiRobotInitialization", "Construction", "MemoryLayout", "Stiefel",
+                                  "TriangleGraph", "LineGraph", "MultiRobotExample"])
 def test_cpp_case(cpp_output, name):
     rc, out = cpp_output
     assert f"[PASS] {name}" in out, out[-3000:]

@@ -137,3 +137,19 @@ def test_chordal_initialization_matches_oracle(H, name):
         Ri = T[:, i * b:i * b + d]
         assert np.abs(Ri.T @ Ri - np.eye(d)).max() <= 1e-12
         assert np.linalg.det(Ri) > 0
+
+
+def test_cpp_host_cases():
+    """Host-only cases of the C++ drop-in tests (no GPU call): chi2inv and the robust single
+    rotation / pose averages of the global-frame initialisation, restating tests/testUtils.cpp:55-190,
+    and the connection-Laplacian construction (tests/testConstruction.cpp)."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    binary = os.path.join(root, "dpgo_amd", "cpp", "build", "test_dpgo")
+    assert os.path.exists(binary), "C++ tests not built (run __graft_entry__.build())"
+    p = subprocess.run([binary, os.path.join(root, "tests", "golden"), "--host"], capture_output=True, text=True,
+                       timeout=300)
+    out = p.stdout + p.stderr
+    assert p.returncode == 0, out[-3000:]
+    for name in ["Chi2Inv", "RobustSingleRotationAveraging", "RobustSinglePoseAveraging", "Construction"]:
+        assert f"[PASS] {name}" in out, out[-3000:]
