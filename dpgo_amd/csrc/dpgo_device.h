@@ -340,12 +340,13 @@ __device__ __forceinline__ void polar_inplace(double (&M)[R][D + 1]) {
     }
 }
 
-// Polar factor via Newton-Schulz  Y <- Y (3 I - Y^T Y) / 2  when Y is already near St(d, r)
-// (||Y^T Y - I||_F < 0.25: every Nesterov combination of nearby iterates), else one-sided Jacobi.
-// Both converge to the same U V^T; Newton-Schulz needs only FMAs (no fp64 sqrt / divide).
+// Polar factor via Newton-Schulz  Y <- Y (3 I - Y^T Y) / 2  when ||Y^T Y - I||_F < 0.7 (singular
+// values in [0.54, 1.31], inside the iteration's (0, sqrt 3) basin: at most 9 steps), else
+// one-sided Jacobi.  Both converge to the same U V^T (the iteration keeps the singular vectors, so
+// Jacobi may also finish a Newton-Schulz run); Newton-Schulz needs only FMAs.
 template <int R, int D>
 __device__ __forceinline__ void polar_fast(double (&M)[R][D + 1]) {
-  bool fallback = false;
+  bool fallback = true;
 #pragma unroll 1
   for (int it = 0; it < 12; ++it) {
     double A[D][D];
@@ -361,11 +362,11 @@ __device__ __forceinline__ void polar_fast(double (&M)[R][D + 1]) {
         const double e = s - (p == q ? 1.0 : 0.0);
         err = fma(e, e, err);
       }
-    if (err < 1e-30) break;
-    if (it == 0 && !(err < 0.0625)) {
-      fallback = true;
+    if (err < 1e-30) {
+      fallback = false;
       break;
     }
+    if (it == 0 && !(err < 0.5)) break;
     double T[D][D];
 #pragma unroll
     for (int p = 0; p < D; ++p)
@@ -383,6 +384,12 @@ __device__ __forceinline__ void polar_fast(double (&M)[R][D + 1]) {
       }
 #pragma unroll
       for (int q = 0; q < D; ++q) M[a][q] = row[q];
+    }
+    // quadratic convergence: from ||Y^T Y - I||_F <= 1e-10 this step reaches the rounding floor,
+    // where the 1e-30 test above may never fire (the floor sits near 1e-31)
+    if (err < 1e-20) {
+      fallback = false;
+      break;
     }
   }
   if (fallback) polar_inplace<R, D>(M);

@@ -698,8 +698,10 @@ __global__ __launch_bounds__(kThreads) void k_precond(LaunchCtx c, const double*
 }
 
 // out = LiftedSEManifold::project(ca A + cb B) (or A + cb (B - C)) with per-agent (or scalar)
-// coefficients.  Thread-per-pose: 64-thread workgroups, one tile each; every thread loads its
-// pose's r*b contiguous doubles (the wave reads 64 consecutive poses = one contiguous span).
+// coefficients.  A tile's 64 poses are one contiguous span of 64 r b doubles: the combination is
+// elementwise, so it is formed while the span streams through LDS with fully coalesced loads; then
+// thread t polar-projects pose t from LDS (row stride r b + 1 doubles: conflict-free b64 reads) and
+// the span streams back out coalesced (optionally to a second destination).
 // (src/manifold/LiftedSEManifold.cpp:34-45; Nesterov updateY/updateV src/PGOAgent.cpp:1075-1091)
 template <int R, int B>
 __global__ __launch_bounds__(64) void k_polar_comb(LaunchCtx c, const double* __restrict__ A,
@@ -710,59 +712,92 @@ __global__ __launch_bounds__(64) void k_polar_comb(LaunchCtx c, const double* __
                                                    const double* __restrict__ Cv, double sa,
                                                    double sb, double* __restrict__ out2) {
   constexpr int D = B - 1;
+  constexpr int PW = R * B;
+  constexpr int PS = PW + 1;
+  __shared__ double sm[64 * PS];
   const int tile = blockIdx.x;
   const int agent = c.tile_agent[tile];
   if (tile_skipped(c, agent)) return;
-  if (static_cast<int>(threadIdx.x) >= c.tile_count[tile]) return;
-  const long j = static_cast<long>(c.tile_start[tile]) + threadIdx.x;
+  const int count = c.tile_count[tile];
+  const long base = static_cast<long>(c.tile_start[tile]) * PW;
+  const int total = count * PW;
   const double a0 = ca ? ca[agent] : sa;
   const double b0 = cb ? cb[agent] : sb;
-  double M[R][B];
-  const double* pa = A + j * (R * B);
+  const int t = static_cast<int>(threadIdx.x);
+  // elementwise combination (updateV: V + gamma (X - Y), src/PGOAgent.cpp:1086-1091; updateY:
+  // (1 - alpha) X + alpha V, :1077-1084; plain project: a0 A)
+  auto comb = [&](double av, double bv, double cv) {
+    return Cv != nullptr ? av + b0 * (bv - cv) : (Bv != nullptr ? a0 * av + b0 * bv : a0 * av);
+  };
+  constexpr bool kVec = PW % 2 == 0;  // 16-byte chunks need an even pose width (aligned spans)
+  if (kVec && count == 64) {
+    // full tile: 64 r b doubles = 16-byte chunks, all loads in flight before the LDS writes
+    constexpr int NV = PW / 2;  // 16-byte chunks per lane
+    const double2* A2 = reinterpret_cast<const double2*>(A + base);
+    const double2* B2 = reinterpret_cast<const double2*>((Bv ? Bv : A) + base);
+    const double2* C2 = reinterpret_cast<const double2*>((Cv ? Cv : A) + base);
+    double2 va[NV], vb[NV], vc[NV];
 #pragma unroll
-  for (int cc = 0; cc < B; ++cc)
+    for (int i = 0; i < NV; ++i) va[i] = A2[t + 64 * i];
+    if (Bv != nullptr) {
 #pragma unroll
-    for (int a = 0; a < R; ++a) M[a][cc] = pa[cc * R + a];
-  if (Cv != nullptr) {
-    // A + cb (B - C)   (updateV: V + gamma (X - Y), src/PGOAgent.cpp:1086-1091)
-    const double* pb = Bv + j * (R * B);
-    const double* pc = Cv + j * (R * B);
+      for (int i = 0; i < NV; ++i) vb[i] = B2[t + 64 * i];
+    }
+    if (Cv != nullptr) {
 #pragma unroll
-    for (int cc = 0; cc < B; ++cc)
+      for (int i = 0; i < NV; ++i) vc[i] = C2[t + 64 * i];
+    }
 #pragma unroll
-      for (int a = 0; a < R; ++a) M[a][cc] = M[a][cc] + b0 * (pb[cc * R + a] - pc[cc * R + a]);
-  } else if (Bv != nullptr) {
-    // ca A + cb B   (updateY: (1 - alpha) X + alpha V, src/PGOAgent.cpp:1077-1084)
-    const double* pb = Bv + j * (R * B);
-#pragma unroll
-    for (int cc = 0; cc < B; ++cc)
-#pragma unroll
-      for (int a = 0; a < R; ++a) M[a][cc] = a0 * M[a][cc] + b0 * pb[cc * R + a];
-  } else if (a0 != 1.0) {
-#pragma unroll
-    for (int cc = 0; cc < B; ++cc)
-#pragma unroll
-      for (int a = 0; a < R; ++a) M[a][cc] = a0 * M[a][cc];
+    for (int i = 0; i < NV; ++i) {
+      const int x = 2 * (t + 64 * i);  // PW is even: a chunk never straddles two poses
+      double* dst = sm + (x / PW) * PS + x % PW;
+      dst[0] = comb(va[i].x, Bv ? vb[i].x : 0.0, Cv ? vc[i].x : 0.0);
+      dst[1] = comb(va[i].y, Bv ? vb[i].y : 0.0, Cv ? vc[i].y : 0.0);
+    }
+  } else {
+    for (int x = t; x < total; x += 64)
+      sm[(x / PW) * PS + x % PW] = comb(A[base + x], Bv ? Bv[base + x] : 0.0, Cv ? Cv[base + x] : 0.0);
   }
-  double tcol[R];
-#pragma unroll
-  for (int a = 0; a < R; ++a) tcol[a] = M[a][D];  // translation passes through unchanged
-  polar_fast<R, D>(M);
-  double* po = out + j * (R * B);
-#pragma unroll
-  for (int cc = 0; cc < D; ++cc)
-#pragma unroll
-    for (int a = 0; a < R; ++a) po[cc * R + a] = M[a][cc];
-#pragma unroll
-  for (int a = 0; a < R; ++a) po[D * R + a] = tcol[a];
-  if (out2 != nullptr) {  // second copy (Nesterov iterate(false): X = Y)
-    double* p2 = out2 + j * (R * B);
+  __syncthreads();
+  if (t < count) {
+    double M[R][B];
+    double* ps = sm + t * PS;
 #pragma unroll
     for (int cc = 0; cc < D; ++cc)
 #pragma unroll
-      for (int a = 0; a < R; ++a) p2[cc * R + a] = M[a][cc];
+      for (int a = 0; a < R; ++a) M[a][cc] = ps[cc * R + a];
 #pragma unroll
-    for (int a = 0; a < R; ++a) p2[D * R + a] = tcol[a];
+    for (int a = 0; a < R; ++a) M[a][D] = 0.0;
+    polar_fast<R, D>(M);  // the translation column passes through unchanged (stays in LDS)
+#pragma unroll
+    for (int cc = 0; cc < D; ++cc)
+#pragma unroll
+      for (int a = 0; a < R; ++a) ps[cc * R + a] = M[a][cc];
+  }
+  __syncthreads();
+  if (kVec && count == 64) {
+    constexpr int NV = PW / 2;
+    double2 vo[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int x = 2 * (t + 64 * i);
+      const double* src = sm + (x / PW) * PS + x % PW;
+      vo[i] = make_double2(src[0], src[1]);
+    }
+    double2* O2 = reinterpret_cast<double2*>(out + base);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) O2[t + 64 * i] = vo[i];
+    if (out2 != nullptr) {  // second copy (Nesterov iterate(false): X = Y)
+      double2* P2 = reinterpret_cast<double2*>(out2 + base);
+#pragma unroll
+      for (int i = 0; i < NV; ++i) P2[t + 64 * i] = vo[i];
+    }
+  } else {
+    for (int x = t; x < total; x += 64) {
+      const double v = sm[(x / PW) * PS + x % PW];
+      out[base + x] = v;
+      if (out2 != nullptr) out2[base + x] = v;
+    }
   }
 }
 
