@@ -102,8 +102,9 @@ int assemble_G(dpgo_rbcd e, int c, bool aux) {
   if (!h || e->gt[c]->nslots == 0) return DPGO_HIP_OK;
   auto* t = e->gt[c];
   GEdges ge{t->slot_off.p, t->src.p, t->outgoing.p, t->R.p, t->t.p, t->kappa.p, t->tau.p, t->w.p};
-  HIP_TRY(launch_assemble_G(e->r, e->b, ge, t->nslots, aux ? e->Y.p : e->X.p, aux ? e->RY.p : e->RX.p, h->gblk.p,
-                            e->stream));
+  // in-place neighbours are never in colour c, so they ran iterate(false) this iteration and their
+  // aux pose equals X (see dpgo_rbcd_pre_exchange): X is read for both dictionaries
+  HIP_TRY(launch_assemble_G(e->r, e->b, ge, t->nslots, e->X.p, aux ? e->RY.p : e->RX.p, h->gblk.p, e->stream));
   return DPGO_HIP_OK;
 }
 
@@ -597,14 +598,15 @@ int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color) {
       DPGO_TRY(polar(e, c, Xc, Vc, 1.0 - e->alpha, e->alpha, Yc));  // updateY (selected)
       continue;
     }
-    // non-selected agents, iterate(false): updateY, updateX(false, true): X = Y (one fused pass);
-    // updateV: V = project(V + gamma (X - Y)) = project(V) because X == Y exactly, and V already
-    // lies on the manifold (it is a previous project() output), so that pass is skipped.
-    DPGO_TRY(polar(e, c, Xc, Vc, 1.0 - e->alpha, e->alpha, Yc, nullptr, Xc));
-    if (restart) {  // restartNesterovAcceleration(false): X = XPrev, V = Y = X
+    // non-selected agents, iterate(false): updateY, updateX(false, true): X = Y (one fused pass,
+    // written to X only: until this agent's next updateY its Y equals X, so the G assembly and the
+    // pack read X, and Y is not stored); updateV: V = project(V + gamma (X - Y)) = project(V)
+    // because X == Y exactly, and V already lies on the manifold (a previous project() output), so
+    // that pass is skipped.
+    DPGO_TRY(polar(e, c, Xc, Vc, 1.0 - e->alpha, e->alpha, Xc));
+    if (restart) {  // restartNesterovAcceleration(false): X = XPrev, V = Y = X (Y implied, as above)
       DPGO_TRY(copy_poses(e, e->X.p, e->Xprev.p, color_first_pose(e, c), color_num_poses(e, c)));
       DPGO_TRY(copy_poses(e, e->V.p, e->X.p, color_first_pose(e, c), color_num_poses(e, c)));
-      DPGO_TRY(copy_poses(e, e->Y.p, e->X.p, color_first_pose(e, c), color_num_poses(e, c)));
     }
   }
   return DPGO_HIP_OK;
@@ -613,8 +615,10 @@ int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color) {
 int dpgo_rbcd_pack(dpgo_rbcd e, double* send_dev) {
   if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
   if (e->n_send_items == 0) return DPGO_HIP_OK;
+  // the aux poses a receiver uses come from agents outside the selected colour, whose Y equals X
+  // after dpgo_rbcd_pre_exchange (the others' entries are not read this iteration)
   HIP_TRY(launch_gather_poses(static_cast<int>(e->n_send_items), static_cast<int>(e->rb()), e->pack_idx.p, e->X.p,
-                              e->Y.p, send_dev, e->stream));
+                              e->X.p, send_dev, e->stream));
   return DPGO_HIP_OK;
 }
 
