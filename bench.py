@@ -56,8 +56,8 @@ def super_cube_ranks(A, world):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--k", type=int, default=100, help="grid side (k^3 poses)")
     ap.add_argument("--agents-per-axis", type=int, default=4)
     ap.add_argument("--r", type=int, default=5)
