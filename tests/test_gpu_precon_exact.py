@@ -104,3 +104,30 @@ def test_rbcd_settings_exact_batched(hip):
         assert rh[k]["runs"] == rk["runs"]
         assert abs(rh[k]["fOpt"] - rk["fOpt"]) <= 1e-10 * max(1.0, abs(rk["fOpt"]))
         assert rel(Xh[:, start[k] * b:start[k + 1] * b], Xk) <= 1e-9
+
+
+@pytest.mark.parametrize("name", ["torus3D", "sphere2500"])
+def test_single_agent_local_pgo(hip, name):
+    """BASELINE configs[1]: PGOAgent::localPoseGraphOptimization (src/PGOAgent.cpp:964-990) on
+    sphere2500 / torus3D at r = d = 3 with the reference's exact preconditioner, from the chordal
+    initialisation: final cost and gradient norm to 1e-9 relative, same outer-iteration count and
+    tCG status as the oracle."""
+    meas = load_meas(name)
+    d, n, r = meas.d, meas.num_poses, 3
+    Q = O.connection_laplacian(meas, n)
+    P = O.QuadraticProblem(n, d, r)
+    P.set_Q(Q)
+    P.precon_mode = O.PRECON_EXACT
+    X0 = O.lifting_matrix(d, r) @ O.chordal_initialization(d, n, meas)
+    trace = []
+    Xo, res = O.optimize(P, X0, O.OptParams(tr_iterations=10, tr_tolerance=1e-1, tr_initial_radius=10.0,
+                                            tr_max_inner=50), trace)
+    H = hip.Problem(n, d, r)
+    H.set_Q_edges(0, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau, meas.weight)
+    Xh, rh = H.optimize(X0, hip.default_params(tr_iterations=10, tr_tolerance=1e-1, tr_initial_radius=10.0,
+                                               tr_max_inner=50, precon=hip.PRECON_EXACT))
+    rh = rh[0]
+    assert abs(rh["fOpt"] - res["fOpt"]) <= 1e-9 * abs(res["fOpt"])
+    assert abs(rh["gradNormOpt"] - res["gradNormOpt"]) <= 1e-9 * max(abs(res["gradNormOpt"]), 1e-12) + 1e-12
+    assert rh["outer_iters"] == len(trace)
+    assert rh["tCGStatus"] == res["tCGStatus"]
