@@ -249,13 +249,30 @@ __device__ __forceinline__ void edge_loop(const QView& q, const double* __restri
 // Block row j of X.Q for the edge-stream form: off-diagonal incidences (second visits through
 // L2 first, then first visits from the LDS stage), then + X_j[:,k] (x) Q_jj[k,:].  The whole quad
 // runs together; lane 3 of a d = 2 quad mirrors lane 0 and its acc is dropped.
-template <int R, int B, bool STAGED>
+//
+// HALF (the f-only evaluation): tr(X Q X^T) = sum_j <X_j, X_j Q_jj> + 2 sum_edges <X_j, X_i Q_ij>, so
+// each edge is needed once: only the first visits of pose j (ids [rec_first[j], rec_first[j+1]),
+// all staged in LDS, the last entries of j's ascending list) are accumulated and the diagonal term
+// enters with weight 1/2; then f_j = <X_j, acc_j> + <G_j, X_j>.  No second-visit record loads and
+// half the neighbour gathers.
+template <int R, int B, bool STAGED, bool HALF = false>
 __device__ __forceinline__ void spmm_accumulate_edges(const QView& q, const double* __restrict__ in, long j,
                                                       int k, int beg, int end, const int2* s_inc, int i0,
                                                       const double* s_rec, int e0, double (&acc)[R][B]) {
   constexpr int DW = diag_width(B - 1);
   const int kc = k < B ? k : 0;
-  if constexpr (STAGED) {
+  if constexpr (HALF) {
+    const int rf = q.rec_first[j];
+    if constexpr (STAGED) {
+      int mid = end;  // first visits of j are the largest ids of its list
+      while (mid > beg && (s_inc[mid - 1 - i0].x >> 1) >= rf) --mid;
+      edge_loop<R, B, true, true>(q, in, kc, mid, end, s_inc, i0, s_rec, e0, acc);
+    } else {
+      int mid = end;
+      while (mid > beg && (q.inc[mid - 1].x >> 1) >= rf) --mid;
+      edge_loop<R, B, false, false>(q, in, kc, mid, end, s_inc, i0, s_rec, e0, acc);
+    }
+  } else if constexpr (STAGED) {
     int mid = beg;  // ids ascend: the second visits (ids below the tile's range) come first
     while (mid < end && (s_inc[mid - i0].x >> 1) < e0) ++mid;
     edge_loop<R, B, true, false>(q, in, kc, beg, mid, s_inc, i0, s_rec, e0, acc);
@@ -277,6 +294,8 @@ __device__ __forceinline__ void spmm_accumulate_edges(const QView& q, const doub
     dk[c] = dj[o];
   }
   const bool act = k < B;
+#pragma unroll
+  for (int a = 0; a < R; ++a) xj[a] = HALF ? 0.5 * xj[a] : xj[a];
 #pragma unroll
   for (int a = 0; a < R; ++a)
 #pragma unroll
@@ -333,12 +352,13 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     __syncthreads();
     if (p.ok) {
       const double* s_rec = reinterpret_cast<const double*>(s_rec2);
+      constexpr bool HALF = MODE == MODE_F;
       if (staged)
-        spmm_accumulate_edges<R, B, true>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc, i0, s_rec, e0,
-                                          acc);
+        spmm_accumulate_edges<R, B, true, HALF>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc, i0,
+                                                s_rec, e0, acc);
       else
-        spmm_accumulate_edges<R, B, false>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc, i0, s_rec, e0,
-                                           acc);
+        spmm_accumulate_edges<R, B, false, HALF>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc, i0,
+                                                 s_rec, e0, acc);
     }
   } else {
     if (p.ok && p.k < B) spmm_accumulate<R, B, var_unr(VAR), var_nt(VAR)>(q, in, p.j, p.k, acc);
@@ -375,8 +395,10 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
       }
     }
     double fpart = 0.0;
+    // edge-stream MODE_F accumulates the half sum (spmm_accumulate_edges HALF): qc already carries the 1/2
+    constexpr double kq = (MODE == MODE_F && FMT == QFMT_EDGES) ? 1.0 : 0.5;
 #pragma unroll
-    for (int a = 0; a < R; ++a) fpart = fma(fma(0.5, qc[a], gcol[a]), xcol[a], fpart);
+    for (int a = 0; a < R; ++a) fpart = fma(fma(kq, qc[a], gcol[a]), xcol[a], fpart);
     if constexpr (MODE == MODE_F) {  // f only (QuadraticProblem::f, :50-60)
       double parts[2] = {own ? fpart : 0.0, 0.0};
       block_partials<2>(parts, c.partials, p.tile);
