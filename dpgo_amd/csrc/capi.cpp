@@ -194,7 +194,7 @@ int sync_q_edges(dpgo_hip_problem h) {
   HIP_TRY(h->inc.ensure(inc.size()));
   HIP_TRY(h->rec.ensure(rec.size()));
   HIP_TRY(h->diag.ensure(std::max<size_t>(diag.size(), 1)));
-  HIP_TRY(h->minv.ensure(static_cast<size_t>(h->N) * b * b));
+  HIP_TRY(h->minv.ensure(static_cast<size_t>(h->N) * dpgo::diag_width(h->d)));
   HIP_TRY(hipMemcpyAsync(h->inc_ptr.p, deg.data(), sizeof(int) * (h->N + 1), hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipMemcpyAsync(h->rec_first.p, lowcnt.data(), sizeof(int) * (h->N + 1), hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipMemcpyAsync(h->inc.p, inc.data(), sizeof(int2) * inc.size(), hipMemcpyHostToDevice, h->stream));
@@ -242,7 +242,7 @@ int sync_q(dpgo_hip_problem h) {
   HIP_TRY(h->rowptr.ensure(h->N + 1));
   HIP_TRY(h->col.ensure(col.size()));
   HIP_TRY(h->blocks.ensure(blocks.size()));
-  HIP_TRY(h->minv.ensure(static_cast<size_t>(h->N) * b * b));
+  HIP_TRY(h->minv.ensure(static_cast<size_t>(h->N) * dpgo::diag_width(h->d)));
   HIP_TRY(hipMemcpyAsync(h->rowptr.p, rowptr.data(), sizeof(int) * rowptr.size(), hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipMemcpyAsync(h->col.p, col.data(), sizeof(int) * col.size(), hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipMemcpyAsync(h->blocks.p, blocks.data(), sizeof(double) * blocks.size(), hipMemcpyHostToDevice, h->stream));
