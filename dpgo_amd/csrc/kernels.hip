@@ -194,6 +194,9 @@ __host__ __device__ constexpr int sym_index(int u, int v) {
   return u <= v ? u * B - u * (u - 1) / 2 + (v - u) : v * B - v * (v - 1) / 2 + (u - v);
 }
 
+// S = sym(Y^T EG_Y) per pose, stored as its packed upper triangle (sym_index<D>)
+__host__ __device__ constexpr int s_width(int d) { return d * (d + 1) / 2; }
+
 // packed index of the block-Jacobi inverse (same packing as the diagonal blocks)
 template <int B>
 __host__ __device__ constexpr int minv_index(int u, int v) { return sym_index<B>(u, v); }
@@ -424,7 +427,7 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
 #pragma unroll
         for (int u = 0; u < D; ++u)
 #pragma unroll
-          for (int v = 0; v < D; ++v) S_out[p.j * (D * D) + u * D + v] = S[u][v];
+          for (int v = u; v < D; ++v) S_out[p.j * s_width(D) + sym_index<D>(u, v)] = S[u][v];
       }
       if constexpr (MODE == MODE_EVAL_TCG) {
         // tCG start fused in (A.4, k_tcg_init): z = Prec(g) = P_X(g Minv), delta = -z, <z, g>
@@ -473,7 +476,7 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
 #pragma unroll
     for (int u = 0; u < D; ++u)
 #pragma unroll
-      for (int v = 0; v < D; ++v) S[u][v] = p.ok ? S_in[p.j * (D * D) + u * D + v] : 0.0;
+      for (int v = 0; v < D; ++v) S[u][v] = p.ok ? S_in[p.j * s_width(D) + sym_index<D>(u, v)] : 0.0;
     double Vf[R][D], hc[R];
     quad_gather_y<R, D>(vcol, Vf);
     sub_y_times_col<R, D>(Vf, S, p.k, qc, hc);
@@ -486,7 +489,7 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
 #pragma unroll
     for (int u = 0; u < D; ++u)
 #pragma unroll
-      for (int v = 0; v < D; ++v) S[u][v] = p.ok ? S_in[p.j * (D * D) + u * D + v] : 0.0;
+      for (int v = 0; v < D; ++v) S[u][v] = p.ok ? S_in[p.j * s_width(D) + sym_index<D>(u, v)] : 0.0;
     double Vf[R][D], Xf[R][D];
     quad_gather_y<R, D>(vcol, Vf);
     quad_gather_y<R, D>(xcol, Xf);
@@ -878,9 +881,9 @@ __global__ __launch_bounds__(kThreads) void k_accept(LaunchCtx c, const double* 
     x1[off + a] = x2[off + a];
     g[off + a] = g2[off + a];
   }
-  if (p.k < D) {
+  if (p.k == 0) {
 #pragma unroll
-    for (int v = 0; v < D; ++v) S[p.j * (D * D) + p.k * D + v] = S2[p.j * (D * D) + p.k * D + v];
+    for (int v = 0; v < s_width(D); ++v) S[p.j * s_width(D) + v] = S2[p.j * s_width(D) + v];
   }
 }
 

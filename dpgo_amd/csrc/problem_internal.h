@@ -126,7 +126,7 @@ struct dpgo_hip_problem_s {
 
   size_t vec_len() const { return static_cast<size_t>(N) * r * b; }
   size_t vec_bytes() const { return vec_len() * sizeof(double); }
-  size_t s_len() const { return static_cast<size_t>(N) * (b - 1) * (b - 1); }
+  size_t s_len() const { return static_cast<size_t>(N) * (b - 1) * b / 2; }  // packed symmetric S per pose
 };
 
 
