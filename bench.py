@@ -78,11 +78,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal on a one-GPU box: every rank on device 0 and the exchange over gloo through host
+    # copies, since RCCL refuses two ranks on one device (DPGO_BENCH_ONE_DEVICE=1; never the default)
+    one_device = os.environ.get("DPGO_BENCH_ONE_DEVICE") == "1"
+    if one_device:
+        local_rank = 0
     if world != args.gpus:
         world = max(world, 1)
     torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if one_device:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
 
     t_setup = time.time()
@@ -109,7 +117,12 @@ def main():
             eng.pre_exchange(c)
             if world > 1:
                 eng.pack(send.data_ptr())
-                dist.all_to_all_single(recv, send, out_splits, in_splits)
+                if one_device:
+                    recv_h = torch.empty(recv.shape, dtype=recv.dtype)
+                    dist.all_to_all_single(recv_h, send.cpu(), out_splits, in_splits)
+                    recv.copy_(recv_h)
+                else:
+                    dist.all_to_all_single(recv, send, out_splits, in_splits)
             eng.update(c, recv.data_ptr() if world > 1 else None)
 
     for _ in range(args.warmup):
@@ -127,7 +140,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if one_device else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
@@ -175,6 +188,27 @@ def main():
                 "what": "Riemannian HVP (EucHessianEta + EucHvToHv, tangent-projected) over colour class 0"},
         "setup_s": setup_s,
     }
+    if args.verify:
+        # central cost 1/2 tr(X Q X^T) of the whole graph before and after (outside the timed region):
+        # the schedule is deterministic, so the final cost must not depend on the number of ranks
+        Xf = np.zeros(X0.size)
+        eng.get_X_into(Xf)
+        if world > 1:
+            tx = torch.from_numpy(Xf) if one_device else torch.from_numpy(Xf).to(dev)
+            dist.all_reduce(tx)
+            Xf = tx.cpu().numpy()
+        if rank == 0:
+            import scipy.sparse as sp
+            rp, col, blk = g.laplacian_bsr()
+            b = g.d + 1
+            Q = sp.bsr_matrix((np.ascontiguousarray(blk.reshape(-1, b, b).transpose(0, 2, 1)), col, rp),
+                              shape=(g.n * b, g.n * b)).tocsr()
+
+            def central(flat):
+                X = H.from_dev_layout(flat, args.r)
+                return 0.5 * float(np.sum(np.asarray(Q @ X.T).T * X))
+            out["verify"] = {"f_init": central(X0), "f_final": central(Xf),
+                             "steps_run": args.warmup + args.steps}
     if rank == 0 and world == 1 and args.cpu_baseline:
         try:
             from oracle import cpu_port
