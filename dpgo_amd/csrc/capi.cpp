@@ -1091,7 +1091,7 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
     }
     // ---- candidate x2 = R_x1(eta), rho test, radius update
     auto cr = make_ctx(h, dpgo::FLAG_RUN, h->pa.p);
-    HIP_TRY(dpgo::launch_retract(r, b, cr, x1, h->eta.p, 1.0, x2, h->g.p, h->Heta.p));
+    HIP_TRY(dpgo::launch_retract(r, b, cr, x1, h->eta.p, 1.0, x2, h->g.p, h->Heta.p, h->delta.p));
     // single Run: only f(x2) and |grad(x2)| are consumed (fOpt / gradNormOpt), |grad(x2)| only as a
     // statistic
     if (single)

@@ -36,7 +36,9 @@ struct AgentState {
   int outer_iters;  // accepted + rejected outer iterations
   int gave_up;      // too many rejections -> returns the input
   int copy_pending;  // multi-iteration Run: accepted step still to be copied into x1
-  int pad1, pad2;
+  int eta_implicit;  // tCG stopped at its first step on the boundary: eta = step delta, Heta = step Hdelta
+                     // are not materialised (k_retract reads delta; g_eta / eta_Heta set by OP_TCG_STEP)
+  int pad2;
 };
 
 // ---- DPP quad helpers -------------------------------------------------------------------

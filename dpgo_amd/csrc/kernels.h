@@ -175,10 +175,12 @@ hipError_t launch_tcg_update(int r, int b, const LaunchCtx& c, const double* X, 
                              const double* r_in, double* rv, double* z, int first);
 hipError_t launch_tcg_dir(int r, int b, const LaunchCtx& c, const double* z, double* delta);
 hipError_t launch_retract(int r, int b, const LaunchCtx& c, const double* X, const double* V, double scale,
-                          double* out, const double* g, const double* HV);
+                          double* out, const double* g, const double* HV, const double* delta_impl = nullptr);
 hipError_t launch_tangent(int r, int b, const LaunchCtx& c, const double* X, const double* V, double* out);
 hipError_t launch_precond(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
                           const double* V, double* out);
+hipError_t launch_polar_vnext(int r, int b, const LaunchCtx& c, const double* X, double* V, const double* Yv,
+                              double gv, double sa, double sb, double* out);
 hipError_t launch_polar_comb(int r, int b, const LaunchCtx& c, const double* A, const double* Bv,
                              const double* ca, const double* cb, double* out, const double* Cv = nullptr,
                              double sa = 1.0, double sb = 0.0, double* out2 = nullptr);

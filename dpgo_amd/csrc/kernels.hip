@@ -587,6 +587,7 @@ __global__ __launch_bounds__(kThreads) void k_tcg_update(LaunchCtx c, const doub
   const PoseLane p = pose_lane<B>(c);
   if (tile_skipped(c, p.agent)) return;  // FLAG_TCG_MODE: skips mode 2
   const AgentState& st = c.state[p.agent];
+  if (st.eta_implicit) return;  // first-step boundary exit: eta / Heta stay implicit (k_retract)
   const int mode = st.tcg_mode;
   const double step = st.step;
   const bool own = p.ok && p.k < B;
@@ -646,21 +647,32 @@ __global__ __launch_bounds__(kThreads) void k_tcg_dir(LaunchCtx c, const double*
   for (int a = 0; a < R; ++a) delta[off + a] = fma(beta, delta[off + a], -z[off + a]);
 }
 
-// x2 = R_x1(scale * eta) (QF retraction, A.2) with partials <g,eta>, <eta,Heta>
+// x2 = R_x1(scale * eta) (QF retraction, A.2) with partials <g,eta>, <eta,Heta>.  For agents whose
+// eta is implicit (AgentState::eta_implicit) and delta_impl is given, eta = step delta is formed here
+// (the same fma the update kernel would have stored) and the dots come from OP_TCG_STEP instead.
 template <int R, int B>
 __global__ __launch_bounds__(kThreads) void k_retract(LaunchCtx c, const double* __restrict__ X,
                                                       const double* __restrict__ V, double scale,
                                                       double* __restrict__ out,
                                                       const double* __restrict__ g,
-                                                      const double* __restrict__ HV) {
+                                                      const double* __restrict__ HV,
+                                                      const double* __restrict__ delta_impl) {
   constexpr int D = B - 1;
   const PoseLane p = pose_lane<B>(c);
   if (tile_skipped(c, p.agent)) return;
   const bool own = p.ok && p.k < B;
   const long off = p.j * (R * B) + p.k * R;
+  const bool impl = delta_impl != nullptr && c.state != nullptr && c.state[p.agent].eta_implicit;
   double xcol[R], vcol[R];
   load_col<R, B>(X, p.j, p.k, p.ok, xcol);
-  load_col<R, B>(V, p.j, p.k, p.ok, vcol);
+  if (impl) {
+    const double step = c.state[p.agent].step;
+    load_col<R, B>(delta_impl, p.j, p.k, p.ok, vcol);
+#pragma unroll
+    for (int a = 0; a < R; ++a) vcol[a] = fma(step, vcol[a], 0.0);
+  } else {
+    load_col<R, B>(V, p.j, p.k, p.ok, vcol);
+  }
   double mcol[R];
 #pragma unroll
   for (int a = 0; a < R; ++a) mcol[a] = fma(scale, vcol[a], xcol[a]);
@@ -671,14 +683,16 @@ __global__ __launch_bounds__(kThreads) void k_retract(LaunchCtx c, const double*
   select_col<R, B>(Mf, p.k, oc);
   store_vec<R>(out, off, own, oc);
   if (g != nullptr) {
-    double gcol[R], hcol[R];
-    load_col<R, B>(g, p.j, p.k, p.ok, gcol);
-    load_col<R, B>(HV, p.j, p.k, p.ok, hcol);
     double ge = 0.0, eh = 0.0;
+    if (!impl) {
+      double gcol[R], hcol[R];
+      load_col<R, B>(g, p.j, p.k, p.ok, gcol);
+      load_col<R, B>(HV, p.j, p.k, p.ok, hcol);
 #pragma unroll
-    for (int a = 0; a < R; ++a) {
-      ge = fma(gcol[a], vcol[a], ge);
-      eh = fma(vcol[a], hcol[a], eh);
+      for (int a = 0; a < R; ++a) {
+        ge = fma(gcol[a], vcol[a], ge);
+        eh = fma(vcol[a], hcol[a], eh);
+      }
     }
     double parts[2] = {own ? ge : 0.0, own ? eh : 0.0};
     block_partials<2>(parts, c.partials, p.tile);
@@ -832,6 +846,105 @@ __global__ __launch_bounds__(64) void k_polar_comb(LaunchCtx c, const double* __
   }
 }
 
+// Nesterov updateV deferred into the colour's next combination pass (one pass instead of two):
+//   V' = project(V + gv (X - Yv))   (updateV, src/PGOAgent.cpp:1086-1091, of the agent's last update)
+//   out = project(sa X + sb V')     (updateY / the iterate(false) step, :1077-1084, of the next iteration)
+// V' is written back to V.  The combinations are the expressions k_polar_comb evaluates, so the
+// results are those of the two separate passes.
+template <int R, int B>
+__global__ __launch_bounds__(64) void k_polar_vnext(LaunchCtx c, const double* __restrict__ X,
+                                                    double* __restrict__ V, const double* __restrict__ Yv,
+                                                    double gv, double sa, double sb, double* __restrict__ out) {
+  constexpr int D = B - 1;
+  constexpr int PW = R * B;
+  constexpr int PS = PW + 1;
+  __shared__ double sm[64 * PS];
+  const int tile = blockIdx.x;
+  const int agent = c.tile_agent[tile];
+  if (tile_skipped(c, agent)) return;
+  const int count = c.tile_count[tile];
+  const long base = static_cast<long>(c.tile_start[tile]) * PW;
+  const int total = count * PW;
+  const int t = static_cast<int>(threadIdx.x);
+  auto project_span = [&]() {
+    if (t < count) {
+      double M[R][B];
+      double* ps = sm + t * PS;
+#pragma unroll
+      for (int cc = 0; cc < D; ++cc)
+#pragma unroll
+        for (int a = 0; a < R; ++a) M[a][cc] = ps[cc * R + a];
+#pragma unroll
+      for (int a = 0; a < R; ++a) M[a][D] = 0.0;
+      polar_fast<R, D>(M);
+#pragma unroll
+      for (int cc = 0; cc < D; ++cc)
+#pragma unroll
+        for (int a = 0; a < R; ++a) ps[cc * R + a] = M[a][cc];
+    }
+  };
+  constexpr bool kVec = PW % 2 == 0;
+  if (kVec && count == 64) {
+    constexpr int NV = PW / 2;
+    const double2* X2 = reinterpret_cast<const double2*>(X + base);
+    const double2* V2 = reinterpret_cast<const double2*>(V + base);
+    const double2* Y2 = reinterpret_cast<const double2*>(Yv + base);
+    double2 vx[NV], vv[NV], vy[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) vx[i] = X2[t + 64 * i];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) vv[i] = V2[t + 64 * i];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) vy[i] = Y2[t + 64 * i];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int x = 2 * (t + 64 * i);
+      double* dst = sm + (x / PW) * PS + x % PW;
+      dst[0] = vv[i].x + gv * (vx[i].x - vy[i].x);
+      dst[1] = vv[i].y + gv * (vx[i].y - vy[i].y);
+    }
+    __syncthreads();
+    project_span();
+    __syncthreads();
+    double2* Vo = reinterpret_cast<double2*>(V + base);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {  // each lane re-reads exactly the LDS words it wrote above
+      const int x = 2 * (t + 64 * i);
+      double* src = sm + (x / PW) * PS + x % PW;
+      const double2 v = make_double2(src[0], src[1]);
+      Vo[t + 64 * i] = v;
+      src[0] = sa * vx[i].x + sb * v.x;
+      src[1] = sa * vx[i].y + sb * v.y;
+    }
+    __syncthreads();
+    project_span();
+    __syncthreads();
+    double2* O2 = reinterpret_cast<double2*>(out + base);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int x = 2 * (t + 64 * i);
+      const double* src = sm + (x / PW) * PS + x % PW;
+      O2[t + 64 * i] = make_double2(src[0], src[1]);
+    }
+  } else {
+    for (int x = t; x < total; x += 64)
+      sm[(x / PW) * PS + x % PW] = V[base + x] + gv * (X[base + x] - Yv[base + x]);
+    __syncthreads();
+    project_span();
+    __syncthreads();
+    for (int x = t; x < total; x += 64) {
+      double* src = sm + (x / PW) * PS + x % PW;
+      const double v = *src;
+      V[base + x] = v;
+      *src = sa * X[base + x] + sb * v;
+    }
+    __syncthreads();
+    project_span();
+    __syncthreads();
+    for (int x = t; x < total; x += 64) out[base + x] = sm[(x / PW) * PS + x % PW];
+  }
+}
+
 // out = sel ? A : B per agent; partial |out - ref|^2
 template <int R, int B>
 __global__ __launch_bounds__(kThreads) void k_select(LaunchCtx c, const double* __restrict__ A,
@@ -933,6 +1046,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
       s.tcg_iters = 0;
       s.tcg_active = 0;
       s.tcg_mode = 2;
+      s.eta_implicit = 0;
       break;
     }
     case OP_EVAL: {
@@ -958,6 +1072,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
       s.tcg_iters = 0;
       s.copy_pending = 0;
       s.tcg_mode = 2;
+      s.eta_implicit = 0;
       if (!s.run_active) {
         s.tcg_active = 0;
         break;
@@ -973,6 +1088,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
     }
     case OP_TCG_INIT: {
       s.copy_pending = 0;
+      s.eta_implicit = 0;
       if (!s.run_active) {
         s.tcg_active = 0;
         s.tcg_mode = 2;
@@ -1007,6 +1123,14 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
         s.tcg_mode = 1;
         s.tcg_status = d_Hd <= 0.0 ? TCG_NEGCURVTURE : TCG_EXCREGION;
         s.tcg_active = 0;
+        if (s.tcg_iters == 1) {
+          // first step on the boundary (the common RBCD case): eta = tau delta and Heta = tau Hdelta
+          // stay implicit.  delta = -z, so <g, eta> = -tau <z, g> and <eta, Heta> = tau^2 <delta, Hdelta>
+          // (the same products as the explicit dots up to rounding)
+          s.eta_implicit = 1;
+          s.g_eta = -tau * s.z_r;
+          s.eta_Heta = tau * tau * d_Hd;
+        }
       } else {
         s.e_Pe = e_Pe_new;
         s.step = alpha;
@@ -1036,8 +1160,10 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
       if (!s.run_active) break;
       s.tcg_active = 0;
       s.tcg_mode = 2;
-      s.g_eta = tot[0];
-      s.eta_Heta = tot[1];
+      if (!s.eta_implicit) {
+        s.g_eta = tot[0];
+        s.eta_Heta = tot[1];
+      }
       s.f2 = tot[2];
       s.ngf2 = sqrt(tot[3]);
       const double denom = -s.g_eta - 0.5 * s.eta_Heta;
@@ -1600,9 +1726,10 @@ hipError_t launch_tcg_dir(int r, int b, const LaunchCtx& c, const double* z, dou
 }
 
 hipError_t launch_retract(int r, int b, const LaunchCtx& c, const double* X, const double* V, double scale,
-                          double* out, const double* g, const double* HV) {
+                          double* out, const double* g, const double* HV, const double* delta_impl) {
   if (c.num_tiles == 0) return hipSuccess;
-  DPGO_DISPATCH(r, b, (k_retract<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, V, scale, out, g, HV)));
+  DPGO_DISPATCH(r, b,
+                (k_retract<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, V, scale, out, g, HV, delta_impl)));
   return hipGetLastError();
 }
 
@@ -1624,6 +1751,13 @@ hipError_t launch_polar_comb(int r, int b, const LaunchCtx& c, const double* A, 
                              double sb, double* out2) {
   if (c.num_tiles == 0) return hipSuccess;
   DPGO_DISPATCH(r, b, (k_polar_comb<R, B><<<c.num_tiles, 64, 0, c.stream>>>(c, A, Bv, ca, cb, out, Cv, sa, sb, out2)));
+  return hipGetLastError();
+}
+
+hipError_t launch_polar_vnext(int r, int b, const LaunchCtx& c, const double* X, double* V, const double* Yv,
+                              double gv, double sa, double sb, double* out) {
+  if (c.num_tiles == 0) return hipSuccess;
+  DPGO_DISPATCH(r, b, (k_polar_vnext<R, B><<<c.num_tiles, 64, 0, c.stream>>>(c, X, V, Yv, gv, sa, sb, out)));
   return hipGetLastError();
 }
 

@@ -52,6 +52,10 @@ struct dpgo_rbcd_s {
   int gnc_iter = 0;      // RobustCost::mGNCIteration
   bool gnc_due = false;  // this iteration reweights (set in pre_exchange, used by update)
   double gamma = 0.0, alpha = 0.0;
+  // per colour: the selected agents' updateV (src/PGOAgent.cpp:1086-1091) is deferred into that
+  // colour's next combination pass (k_polar_vnext) with the gamma it was due with
+  std::vector<char> v_pending;
+  std::vector<double> v_gamma;
   long iteration = 0;
   long long agent_updates = 0;
 
@@ -84,6 +88,21 @@ int polar(dpgo_rbcd e, int c, const double* A, const double* B, double ca, doubl
   // uniform Nesterov coefficients travel as kernel arguments
   auto ctx = make_ctx(h, FLAG_NONE, h->pa.p);
   HIP_TRY(launch_polar_comb(e->r, e->b, ctx, A, B, nullptr, nullptr, out, C, ca, cb, out2));
+  return DPGO_HIP_OK;
+}
+
+// out = project((1 - alpha) X + alpha V) for colour c, preceded by the colour's deferred updateV
+// V = project(V + gamma (X - Y)) in the same pass when one is pending
+int nesterov_comb(dpgo_rbcd e, int c, double* out) {
+  dpgo_hip_problem h = e->prob[c];
+  if (!h) return DPGO_HIP_OK;
+  double* Xc = color_ptr(e, e->X, c);
+  double* Yc = color_ptr(e, e->Y, c);
+  double* Vc = color_ptr(e, e->V, c);
+  if (!e->v_pending[c]) return polar(e, c, Xc, Vc, 1.0 - e->alpha, e->alpha, out);
+  e->v_pending[c] = 0;
+  auto ctx = make_ctx(h, FLAG_NONE, h->pa.p);
+  HIP_TRY(launch_polar_vnext(e->r, e->b, ctx, Xc, Vc, Yc, e->v_gamma[c], 1.0 - e->alpha, e->alpha, out));
   return DPGO_HIP_OK;
 }
 
@@ -325,6 +344,8 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
       e->V.ensure(std::max<long>(e->Nown, 1) * e->rb()) != hipSuccess ||
       e->Xprev.ensure(std::max<long>(e->Nown, 1) * e->rb()) != hipSuccess)
     return bail(fail(DPGO_HIP_ENOMEM, "device allocation failed"));
+  e->v_pending.assign(e->ncolors, 0);
+  e->v_gamma.assign(e->ncolors, 0.0);
 
   // ---- per owned agent: Q (private edges + shared-edge diagonal terms) and shared edges
   std::vector<std::vector<size_t>> agent_edges(e->owned.size());
@@ -540,6 +561,7 @@ int dpgo_rbcd_set_X(dpgo_rbcd e, const double* Xg) {
   e->gamma = 0.0;
   e->alpha = 0.0;
   e->iteration = 0;
+  std::fill(e->v_pending.begin(), e->v_pending.end(), 0);
   return DPGO_HIP_OK;
 }
 
@@ -579,6 +601,7 @@ int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color) {
       }
       e->gamma = 0.0;
       e->alpha = 0.0;
+      std::fill(e->v_pending.begin(), e->v_pending.end(), 0);  // V = X supersedes a deferred updateV
     }
   }
   const bool restart = restart_now(e);
@@ -593,17 +616,16 @@ int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color) {
     if (!e->prob[c]) continue;
     double* Xc = color_ptr(e, e->X, c);
     double* Yc = color_ptr(e, e->Y, c);
-    double* Vc = color_ptr(e, e->V, c);
     if (c == color) {
-      DPGO_TRY(polar(e, c, Xc, Vc, 1.0 - e->alpha, e->alpha, Yc));  // updateY (selected)
+      DPGO_TRY(nesterov_comb(e, c, Yc));  // updateY (selected)
       continue;
     }
     // non-selected agents, iterate(false): updateY, updateX(false, true): X = Y (one fused pass,
     // written to X only: until this agent's next updateY its Y equals X, so the G assembly and the
     // pack read X, and Y is not stored); updateV: V = project(V + gamma (X - Y)) = project(V)
     // because X == Y exactly, and V already lies on the manifold (a previous project() output), so
-    // that pass is skipped.
-    DPGO_TRY(polar(e, c, Xc, Vc, 1.0 - e->alpha, e->alpha, Xc));
+    // that pass is skipped.  A deferred updateV of this colour's last update runs in the same pass.
+    DPGO_TRY(nesterov_comb(e, c, Xc));
     if (restart) {  // restartNesterovAcceleration(false): X = XPrev, V = Y = X (Y implied, as above)
       DPGO_TRY(copy_poses(e, e->X.p, e->Xprev.p, color_first_pose(e, c), color_num_poses(e, c)));
       DPGO_TRY(copy_poses(e, e->V.p, e->X.p, color_first_pose(e, c), color_num_poses(e, c)));
@@ -643,12 +665,15 @@ int dpgo_rbcd_update(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_re
   if (e->prob[color]) {
     double* Xc = color_ptr(e, e->X, color);
     double* Yc = color_ptr(e, e->Y, color);
-    double* Vc = color_ptr(e, e->V, color);
     if (e->P.acceleration) {
       DPGO_TRY(assemble_G(e, color, true));  // constructGMatrix(neighborAuxPoseDict)
       DPGO_TRY(optimize_color(e, color, Yc, Xc, results));
-      DPGO_TRY(polar(e, color, Vc, Xc, 0.0, e->gamma, Vc, Yc));  // updateV
-      if (restart) {  // restartNesterovAcceleration(true) (:1040-1060)
+      if (!restart) {
+        // updateV: V = project(V + gamma (X - Y)).  Nothing reads this colour's V before its next
+        // combination pass (the next dpgo_rbcd_pre_exchange), so it runs inside that pass
+        e->v_pending[color] = 1;
+        e->v_gamma[color] = e->gamma;
+      } else {  // restartNesterovAcceleration(true) (:1040-1060); its V = X supersedes updateV
         DPGO_TRY(copy_poses(e, e->X.p, e->Xprev.p, color_first_pose(e, color), color_num_poses(e, color)));
         DPGO_TRY(assemble_G(e, color, false));
         DPGO_TRY(optimize_color(e, color, Xc, Xc, results));
