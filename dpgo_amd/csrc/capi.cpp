@@ -970,8 +970,8 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
   // (a pageable H2D copy would synchronise the stream: only copy when a mask is given)
   if (agent_enabled_host)
     HIP_TRY(hipMemcpyAsync(h->enabled.p, en.data(), sizeof(int) * K, hipMemcpyHostToDevice, h->stream));
-  else
-    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(h->enabled.p), 1, K, h->stream));
+  // without a mask every agent is enabled: k_finalize reads no mask (no fill launch)
+  const int* en_dev = agent_enabled_host ? h->enabled.p : nullptr;
 
   const bool single = P.algorithm == DPGO_ALG_RTR && P.tr_iterations == 1;
   // x1 only moves in a multi-iteration Run; a single Run (the RBCD setting) reads X_in in place.
@@ -996,10 +996,10 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
   const bool fused_tcg = P.algorithm == DPGO_ALG_RTR && P.tr_max_inner > 0 && !exact;
   if (fused_tcg) {
     DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_NONE, dpgo::MODE_EVAL_TCG, h->delta.p, pmode));
-    DPGO_TRY(finalize(h, dpgo::OP_EVAL_TCG_INIT, h->pa.p, 3, nullptr, 0, &o, h->enabled.p));
+    DPGO_TRY(finalize(h, dpgo::OP_EVAL_TCG_INIT, h->pa.p, 3, nullptr, 0, &o, en_dev));
   } else {
     DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_NONE));
-    DPGO_TRY(finalize(h, dpgo::OP_EVAL_INIT, h->pa.p, 2, nullptr, 0, &o, h->enabled.p));
+    DPGO_TRY(finalize(h, dpgo::OP_EVAL_INIT, h->pa.p, 2, nullptr, 0, &o, en_dev));
   }
 
   if (P.algorithm == DPGO_ALG_RGD) {
@@ -1055,12 +1055,16 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
       }
       DPGO_TRY(finalize(h, dpgo::OP_TCG_INIT, h->pa.p, 2, nullptr, 0, &o));
     }
-    std::vector<int> tags;
+    std::vector<int> tags, step_tags;
     auto launch_iter = [&](int j) -> int {
       auto ch = make_ctx(h, dpgo::FLAG_TCG, h->pa.p);
       HIP_TRY(dpgo::launch_spmm(r, b, dpgo::MODE_HESS, ch, qview(h), h->delta.p, nullptr, nullptr, x1, h->S.p,
                                 h->Hdelta.p, nullptr));
-      DPGO_TRY(finalize(h, dpgo::OP_TCG_STEP, h->pa.p, 1, nullptr, 0, &o));
+      // the step test publishes too: when it already stopped every agent (a boundary or
+      // negative-curvature step, the common RBCD case) the host launches no further iteration
+      const int stag = next_tag(h);
+      step_tags.push_back(stag);
+      DPGO_TRY(finalize(h, dpgo::OP_TCG_STEP, h->pa.p, 1, nullptr, 0, &o, nullptr, 1, stag));
       auto cu = make_ctx(h, dpgo::FLAG_TCG_MODE, h->pb.p);
       HIP_TRY(dpgo::launch_tcg_update(r, b, cu, x1, h->minv.p, pmode, h->delta.p, h->Hdelta.p, h->eta.p,
                                       h->Heta.p, j == 0 ? h->g.p : h->rv.p, h->rv.p, h->z.p, j == 0 ? 1 : 0));
@@ -1081,12 +1085,14 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
       launched = 1;
     }
     for (int j = 0; j < P.tr_max_inner; ++j) {
-      if (launched < P.tr_max_inner) {  // lookahead: iteration j+1 queued before waiting on j
+      bool act = false;
+      DPGO_TRY(wait_published(h, step_tags[j], &act));  // after the step test of iteration j
+      if (!act) break;
+      if (launched < P.tr_max_inner) {  // lookahead: iteration j+1 queued while j's update runs
         DPGO_TRY(launch_iter(launched));
         ++launched;
       }
-      bool act = false;
-      DPGO_TRY(wait_published(h, tags[j], &act));
+      DPGO_TRY(wait_published(h, tags[j], &act));  // after the stopping test of iteration j
       if (!act) break;
     }
     // ---- candidate x2 = R_x1(eta), rho test, radius update
