@@ -1056,15 +1056,19 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
       DPGO_TRY(finalize(h, dpgo::OP_TCG_INIT, h->pa.p, 2, nullptr, 0, &o));
     }
     std::vector<int> tags, step_tags;
-    auto launch_iter = [&](int j) -> int {
+    // iteration j's step test: Hdelta = Hess[delta] and d_Hd = <delta, Hdelta>, or (qf) d_Hd alone
+    auto launch_step = [&](bool qf) -> int {
       auto ch = make_ctx(h, dpgo::FLAG_TCG, h->pa.p);
-      HIP_TRY(dpgo::launch_spmm(r, b, dpgo::MODE_HESS, ch, qview(h), h->delta.p, nullptr, nullptr, x1, h->S.p,
-                                h->Hdelta.p, nullptr));
+      HIP_TRY(dpgo::launch_spmm(r, b, qf ? dpgo::MODE_QF : dpgo::MODE_HESS, ch, qview(h), h->delta.p, nullptr,
+                                nullptr, x1, h->S.p, qf ? nullptr : h->Hdelta.p, nullptr));
       // the step test publishes too: when it already stopped every agent (a boundary or
       // negative-curvature step, the common RBCD case) the host launches no further iteration
       const int stag = next_tag(h);
       step_tags.push_back(stag);
       DPGO_TRY(finalize(h, dpgo::OP_TCG_STEP, h->pa.p, 1, nullptr, 0, &o, nullptr, 1, stag));
+      return DPGO_HIP_OK;
+    };
+    auto launch_rest = [&](int j) -> int {
       auto cu = make_ctx(h, dpgo::FLAG_TCG_MODE, h->pb.p);
       HIP_TRY(dpgo::launch_tcg_update(r, b, cu, x1, h->minv.p, pmode, h->delta.p, h->Hdelta.p, h->eta.p,
                                       h->Heta.p, j == 0 ? h->g.p : h->rv.p, h->rv.p, h->z.p, j == 0 ? 1 : 0));
@@ -1079,17 +1083,31 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
       }
       return DPGO_HIP_OK;
     };
+    // First step: when the previous call's first step stopped every agent (predict_boundary), only
+    // d_Hd is evaluated (MODE_QF: each edge once, no Hess[delta] vector).  A boundary / negative-
+    // curvature exit needs nothing more (eta = tau delta stays implicit, <eta, Heta> = tau^2 d_Hd);
+    // agents that take a CG step get Hess[delta] from a HESS pass over their tiles only.
+    const bool qf0 = h->predict_boundary && !exact;
     int launched = 0;
     if (P.tr_max_inner > 0) {
-      DPGO_TRY(launch_iter(0));
+      DPGO_TRY(launch_step(qf0));
+      if (!qf0) DPGO_TRY(launch_rest(0));
       launched = 1;
     }
     for (int j = 0; j < P.tr_max_inner; ++j) {
       bool act = false;
       DPGO_TRY(wait_published(h, step_tags[j], &act));  // after the step test of iteration j
+      if (j == 0) h->predict_boundary = !act;
       if (!act) break;
+      if (j == 0 && qf0) {
+        auto cg = make_ctx(h, dpgo::FLAG_TCG_CG, h->pb.p);
+        HIP_TRY(dpgo::launch_spmm(r, b, dpgo::MODE_HESS, cg, qview(h), h->delta.p, nullptr, nullptr, x1, h->S.p,
+                                  h->Hdelta.p, nullptr));
+        DPGO_TRY(launch_rest(0));
+      }
       if (launched < P.tr_max_inner) {  // lookahead: iteration j+1 queued while j's update runs
-        DPGO_TRY(launch_iter(launched));
+        DPGO_TRY(launch_step(false));
+        DPGO_TRY(launch_rest(launched));
         ++launched;
       }
       DPGO_TRY(wait_published(h, tags[j], &act));  // after the stopping test of iteration j

@@ -12,10 +12,11 @@ constexpr int kPartialStride = 4;  // doubles of partial sums per tile
 // HESS (Riemannian Hessian), F (f partial only), EVAL_TCG (EVAL + tCG start: delta = -P_X(g Minv),
 // partial <z, g>)
 // CERT: V (Q - Lambda(X)) = VQ - [V_Y S | 0] (the certificate matrix, no projection)
-enum SpmmMode { MODE_XQ = 0, MODE_XQ_G = 1, MODE_EVAL = 2, MODE_HESS = 3, MODE_F = 4, MODE_EVAL_TCG = 5, MODE_CERT = 6 };
+enum SpmmMode { MODE_XQ = 0, MODE_XQ_G = 1, MODE_EVAL = 2, MODE_HESS = 3, MODE_F = 4, MODE_EVAL_TCG = 5, MODE_CERT = 6,
+                MODE_QF = 7 };
 // Per-agent tile gating: RUN skips agents out of the RTR Run, TCG those whose tCG stopped, TCG_MODE
 // those with no tCG step pending, MOVED those whose single-Run candidate was accepted.
-enum FlagKind { FLAG_NONE = 0, FLAG_RUN = 1, FLAG_TCG = 2, FLAG_TCG_MODE = 3, FLAG_MOVED = 4 };
+enum FlagKind { FLAG_NONE = 0, FLAG_RUN = 1, FLAG_TCG = 2, FLAG_TCG_MODE = 3, FLAG_MOVED = 4, FLAG_TCG_CG = 5 };
 enum PreconMode { PRECON_EXACT = 0, PRECON_BLOCK_JACOBI = 1, PRECON_NONE = 2 };
 enum TcgStatus { TCG_NEGCURVTURE = 0, TCG_EXCREGION = 1, TCG_LCON = 2, TCG_SCON = 3, TCG_MAXITER = 4 };
 enum FinalizeOp {

@@ -24,6 +24,7 @@ __device__ __forceinline__ bool tile_skipped(const LaunchCtx& c, int agent) {
   if (c.flag_kind == FLAG_TCG) return s.tcg_active == 0;
   if (c.flag_kind == FLAG_TCG_MODE) return s.tcg_mode == 2;
   if (c.flag_kind == FLAG_MOVED) return s.runs > 0 && s.accepted && !s.gave_up;
+  if (c.flag_kind == FLAG_TCG_CG) return s.tcg_mode != 0;
   return false;
 }
 
@@ -359,7 +360,7 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     __syncthreads();
     if (p.ok) {
       const double* s_rec = reinterpret_cast<const double*>(s_rec2);
-      constexpr bool HALF = MODE == MODE_F;
+      constexpr bool HALF = MODE == MODE_F || MODE == MODE_QF;
       if (staged)
         spmm_accumulate_edges<R, B, true, HALF>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc, i0,
                                                 s_rec, e0, acc);
@@ -481,6 +482,27 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     quad_gather_y<R, D>(vcol, Vf);
     sub_y_times_col<R, D>(Vf, S, p.k, qc, hc);
     store_vec<R>(out, off, own, hc);
+  } else if constexpr (MODE == MODE_QF) {
+    // d_Hd = <V, Hess[V]> = <V, VQ> - <V_Y, V_Y S> for a tangent V (A.3; P_X is self-adjoint), without
+    // forming Hess[V].  The edge stream accumulates each edge once (HALF), so <V, VQ> = 2 sum_j <V_j, acc_j>.
+    double vcol[R];
+    load_col<R, B>(in, p.j, p.k, p.ok, vcol);
+    double S[D][D];
+#pragma unroll
+    for (int u = 0; u < D; ++u)
+#pragma unroll
+      for (int v = 0; v < D; ++v) S[u][v] = p.ok ? S_in[p.j * s_width(D) + sym_index<D>(u, v)] : 0.0;
+    double Vf[R][D], w[R], hc[R];
+    quad_gather_y<R, D>(vcol, Vf);
+    constexpr double kq = FMT == QFMT_EDGES ? 2.0 : 1.0;
+#pragma unroll
+    for (int a = 0; a < R; ++a) w[a] = kq * qc[a];
+    sub_y_times_col<R, D>(Vf, S, p.k, w, hc);
+    double dpart = 0.0;
+#pragma unroll
+    for (int a = 0; a < R; ++a) dpart = fma(vcol[a], hc[a], dpart);
+    double parts[1] = {own ? dpart : 0.0};
+    block_partials<1>(parts, c.partials, p.tile);
   } else if constexpr (MODE == MODE_HESS) {
     double vcol[R], xcol[R];
     load_col<R, B>(in, p.j, p.k, p.ok, vcol);
@@ -1698,6 +1720,7 @@ hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const QView& 
     case MODE_F: e = spmm_mode<MODE_F>(r, b, grid, c, q, a); break;
     case MODE_EVAL_TCG: e = spmm_mode<MODE_EVAL_TCG>(r, b, grid, c, q, a); break;
     case MODE_CERT: e = spmm_mode<MODE_CERT>(r, b, grid, c, q, a); break;
+    case MODE_QF: e = spmm_mode<MODE_QF>(r, b, grid, c, q, a); break;
     default: break;
   }
   if (e != hipSuccess) return e;

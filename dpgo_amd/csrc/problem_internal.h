@@ -122,6 +122,10 @@ struct dpgo_hip_problem_s {
   int* pub_host = nullptr;
   int* pub_dev = nullptr;
   int pub_tag = 0;
+  // the first tCG step of the previous optimize call stopped every agent on the trust-region
+  // boundary (or negative curvature): the next call's first step evaluates only <delta, Hess delta>
+  // (MODE_QF) and forms Hess[delta] only for agents that turn out to take a CG step
+  bool predict_boundary = true;
   std::vector<double> h_sums;
 
   size_t vec_len() const { return static_cast<size_t>(N) * r * b; }
