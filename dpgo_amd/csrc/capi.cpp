@@ -491,9 +491,10 @@ namespace {
 
 int finalize(dpgo_hip_problem h, int op, const double* pa, int nqa, const double* pb, int nqb,
              const dpgo::OptScalars* opt = nullptr, const int* enabled = nullptr, int pub_kind = 0,
-             int pub_tag = 0) {
+             int pub_tag = 0, int agent_filter = 0) {
   dpgo::FinalizeArgs f;
   std::memset(&f, 0, sizeof(f));
+  f.agent_filter = agent_filter;
   if (pub_kind) {
     f.pub = h->pub_dev;
     f.pub_kind = pub_kind;
@@ -994,8 +995,13 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
   // f(x1), grad(x1), S(x1)  (QuadraticOptimizer::optimize :36-37, SolversTR start); for RTR the
   // first tCG start (delta = -Prec(grad), <z, grad>) is fused into the same pass
   const bool fused_tcg = P.algorithm == DPGO_ALG_RTR && P.tr_max_inner > 0 && !exact;
+  // grad(x1) itself is only read by a CG step (r = grad + alpha Hdelta), a retry Run or the explicit
+  // <g, eta>: when the first step is predicted to stop every agent (single Run), it is not stored and
+  // is recomputed in the rare case it is needed
+  bool g_valid = !(fused_tcg && single && h->predict_boundary && P.tr_max_inner > 0);
   if (fused_tcg) {
-    DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_NONE, dpgo::MODE_EVAL_TCG, h->delta.p, pmode));
+    DPGO_TRY(eval_at(h, x1, g_valid ? h->g.p : nullptr, h->S.p, h->pa.p, dpgo::FLAG_NONE, dpgo::MODE_EVAL_TCG,
+                     h->delta.p, pmode));
     DPGO_TRY(finalize(h, dpgo::OP_EVAL_TCG_INIT, h->pa.p, 3, nullptr, 0, &o, en_dev));
   } else {
     DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_NONE));
@@ -1047,6 +1053,10 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
   for (int round = 0; round < max_rounds; ++round) {
     // ---- truncated CG (A.4)
     if (round > 0 || !fused_tcg) {
+      if (!g_valid) {  // a retry Run restarts tCG from grad(x1), which EVAL_TCG did not store
+        DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_RUN));
+        g_valid = true;
+      }
       if (exact) {  // delta = -P_X(g P^-1), partials <z, g>, |g|^2
         DPGO_TRY(exact_precond(h, h->g.p, nullptr, h->delta.p, x1, h->g.p, h->pa.p, dpgo::FLAG_RUN));
       } else {
@@ -1087,19 +1097,46 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
     // d_Hd is evaluated (MODE_QF: each edge once, no Hess[delta] vector).  A boundary / negative-
     // curvature exit needs nothing more (eta = tau delta stays implicit, <eta, Heta> = tau^2 d_Hd);
     // agents that take a CG step get Hess[delta] from a HESS pass over their tiles only.
-    const bool qf0 = h->predict_boundary && !exact;
-    int launched = 0;
+    const bool qf0 = h->predict_boundary && !exact && P.tr_max_inner > 0;
+    // Single Run: the candidate, f(x2) and the rho test of the agents whose first step already ended
+    // tCG are queued right behind the step test, before the host learns whether any agent continues
+    // (those are retracted, evaluated and tested after their tCG: the *_EXPL launches below).
+    const bool spec = qf0 && single;
+    auto launch_candidate = [&](int run_flag, int filter) -> int {
+      auto cr = make_ctx(h, run_flag, h->pa.p);
+      HIP_TRY(dpgo::launch_retract(r, b, cr, x1, h->eta.p, 1.0, x2, h->g.p, h->Heta.p, h->delta.p));
+      // single Run: only f(x2) and |grad(x2)| are consumed (fOpt / gradNormOpt), |grad(x2)| only as a
+      // statistic
+      if (single)
+        DPGO_TRY(eval_at(h, x2, nullptr, nullptr, h->pb.p, run_flag, stats ? dpgo::MODE_EVAL : dpgo::MODE_F));
+      else
+        DPGO_TRY(eval_at(h, x2, h->g2.p, h->S2.p, h->pb.p, run_flag));
+      const int rtag = next_tag(h);
+      DPGO_TRY(finalize(h, dpgo::OP_RHO, h->pa.p, 2, h->pb.p, 2, &o, nullptr, 2, rtag, filter));
+      return rtag;
+    };
+    int launched = 0, rtag = 0;
+    bool cg_agents = !qf0;  // some agent may still be in tCG after the first step test
     if (P.tr_max_inner > 0) {
       DPGO_TRY(launch_step(qf0));
+      if (spec) {
+        rtag = launch_candidate(dpgo::FLAG_RUN_IMPL, 1);
+        if (rtag < 0) return rtag;
+      }
       if (!qf0) DPGO_TRY(launch_rest(0));
       launched = 1;
     }
     for (int j = 0; j < P.tr_max_inner; ++j) {
       bool act = false;
       DPGO_TRY(wait_published(h, step_tags[j], &act));  // after the step test of iteration j
-      if (j == 0) h->predict_boundary = !act;
+      if (j == 0) {
+        h->predict_boundary = !act;
+        cg_agents = act;
+      }
       if (!act) break;
       if (j == 0 && qf0) {
+        if (!g_valid)  // the CG-step agents' gradient (EVAL_TCG skipped storing it)
+          DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_TCG_CG));
         auto cg = make_ctx(h, dpgo::FLAG_TCG_CG, h->pb.p);
         HIP_TRY(dpgo::launch_spmm(r, b, dpgo::MODE_HESS, cg, qview(h), h->delta.p, nullptr, nullptr, x1, h->S.p,
                                   h->Hdelta.p, nullptr));
@@ -1114,16 +1151,13 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
       if (!act) break;
     }
     // ---- candidate x2 = R_x1(eta), rho test, radius update
-    auto cr = make_ctx(h, dpgo::FLAG_RUN, h->pa.p);
-    HIP_TRY(dpgo::launch_retract(r, b, cr, x1, h->eta.p, 1.0, x2, h->g.p, h->Heta.p, h->delta.p));
-    // single Run: only f(x2) and |grad(x2)| are consumed (fOpt / gradNormOpt), |grad(x2)| only as a
-    // statistic
-    if (single)
-      DPGO_TRY(eval_at(h, x2, nullptr, nullptr, h->pb.p, dpgo::FLAG_RUN, stats ? dpgo::MODE_EVAL : dpgo::MODE_F));
-    else
-      DPGO_TRY(eval_at(h, x2, h->g2.p, h->S2.p, h->pb.p, dpgo::FLAG_RUN));
-    const int rtag = next_tag(h);
-    DPGO_TRY(finalize(h, dpgo::OP_RHO, h->pa.p, 2, h->pb.p, 2, &o, nullptr, 2, rtag));
+    if (!spec) {
+      rtag = launch_candidate(dpgo::FLAG_RUN, 0);
+      if (rtag < 0) return rtag;
+    } else if (cg_agents) {
+      rtag = launch_candidate(dpgo::FLAG_RUN_EXPL, 2);
+      if (rtag < 0) return rtag;
+    }
     if (!single) {
       auto ca = make_ctx(h, dpgo::FLAG_NONE, nullptr);
       HIP_TRY(dpgo::launch_accept(r, b, ca, h->x2.p, h->g2.p, h->S2.p, h->x1.p, h->g.p, h->S.p));
@@ -1132,6 +1166,11 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
       // done skip nothing here, rejected ones copy their unchanged input)
       auto cs = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
       HIP_TRY(dpgo::launch_select(r, b, cs, h->x2.p, X_in, nullptr, X_in, X_out));
+    } else {
+      // x2 already sits in X_out: agents that did not move take X_in (queued before the retry
+      // decision; a retry Run retracts into X_out again and repeats this)
+      auto cm = make_ctx(h, dpgo::FLAG_MOVED, h->pa.p);
+      HIP_TRY(dpgo::launch_select(r, b, cm, X_in, X_in, nullptr, X_in, X_out));
     }
     if (round + 1 < max_rounds) {  // radius-shrink retry / next outer iteration needed?
       bool any = false;
@@ -1141,10 +1180,6 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
   }
   // X_out: accepted candidate or the input (single Run), x1 (multi-iteration)
   auto cs = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
-  if (direct) {  // x2 already sits in X_out: agents that did not move take X_in
-    auto cm = make_ctx(h, dpgo::FLAG_MOVED, h->pa.p);
-    HIP_TRY(dpgo::launch_select(r, b, cm, X_in, X_in, nullptr, X_in, X_out));
-  }
   if (!single) {
     HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(h->use_a.p), 1, K, h->stream));
     HIP_TRY(dpgo::launch_select(r, b, cs, x1, X_in, h->use_a.p, X_in, X_out));

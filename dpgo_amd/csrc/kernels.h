@@ -16,7 +16,8 @@ enum SpmmMode { MODE_XQ = 0, MODE_XQ_G = 1, MODE_EVAL = 2, MODE_HESS = 3, MODE_F
                 MODE_QF = 7 };
 // Per-agent tile gating: RUN skips agents out of the RTR Run, TCG those whose tCG stopped, TCG_MODE
 // those with no tCG step pending, MOVED those whose single-Run candidate was accepted.
-enum FlagKind { FLAG_NONE = 0, FLAG_RUN = 1, FLAG_TCG = 2, FLAG_TCG_MODE = 3, FLAG_MOVED = 4, FLAG_TCG_CG = 5 };
+enum FlagKind { FLAG_NONE = 0, FLAG_RUN = 1, FLAG_TCG = 2, FLAG_TCG_MODE = 3, FLAG_MOVED = 4, FLAG_TCG_CG = 5,
+                FLAG_RUN_IMPL = 6, FLAG_RUN_EXPL = 7 };  // RUN_IMPL/EXPL: FLAG_RUN and eta (not) implicit
 enum PreconMode { PRECON_EXACT = 0, PRECON_BLOCK_JACOBI = 1, PRECON_NONE = 2 };
 enum TcgStatus { TCG_NEGCURVTURE = 0, TCG_EXCREGION = 1, TCG_LCON = 2, TCG_SCON = 3, TCG_MAXITER = 4 };
 enum FinalizeOp {
@@ -105,6 +106,7 @@ struct FinalizeArgs {
   int* pub;                     // nullptr = none
   int pub_tag;
   int pub_kind;                 // 1: tcg_active, 2: run_active
+  int agent_filter;             // 0: every agent; 1 / 2: only agents whose eta is / is not implicit
 };
 
 // shared-edge records for G assembly, grouped by G slot (CSR)

@@ -25,6 +25,8 @@ __device__ __forceinline__ bool tile_skipped(const LaunchCtx& c, int agent) {
   if (c.flag_kind == FLAG_TCG_MODE) return s.tcg_mode == 2;
   if (c.flag_kind == FLAG_MOVED) return s.runs > 0 && s.accepted && !s.gave_up;
   if (c.flag_kind == FLAG_TCG_CG) return s.tcg_mode != 0;
+  if (c.flag_kind == FLAG_RUN_IMPL) return s.run_active == 0 || s.eta_implicit == 0;
+  if (c.flag_kind == FLAG_RUN_EXPL) return s.run_active == 0 || s.eta_implicit != 0;
   return false;
 }
 
@@ -1049,7 +1051,8 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
   if (threadIdx.x != 0) return;
   AgentState& s = f.state[agent];
   const OptScalars& o = f.opt;
-  switch (f.op) {
+  const bool filtered = (f.agent_filter == 1 && !s.eta_implicit) || (f.agent_filter == 2 && s.eta_implicit);
+  switch (filtered ? -1 : f.op) {
     case OP_EVAL_INIT: {  // after EVAL at the initial iterate
       s.f1 = tot[0];
       s.ngf = sqrt(tot[1]);
