@@ -188,6 +188,7 @@ __device__ __forceinline__ void spmm_accumulate(const QView& q, const double* __
 // leaves HBM at full occupancy-independent MLP instead of one dependent miss per incidence.
 // Tiles whose lists do not fit fall back to global loads.
 constexpr int kIncStage = 512;
+constexpr bool kHalfStaged = false;  // LDS stage for the half passes (MODE_F / MODE_QF)
 template <int D>
 constexpr int rec_stage() { return D == 3 ? 200 : 256; }
 
@@ -343,8 +344,13 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     for (int cc = 0; cc < B; ++cc) acc[a][cc] = 0.0;
 
   if constexpr (FMT == QFMT_EDGES) {
-    constexpr int RW = edge_rec_width(B - 1), NREC = rec_stage<B - 1>();
-    __shared__ int2 s_inc[kIncStage];
+    // The half (each-edge-once) passes read only the tile's first-visit records, each exactly once and
+    // as whole 128-byte lines per pose quad: they skip the LDS stage (less LDS, more resident waves).
+    constexpr bool HALF = MODE == MODE_F || MODE == MODE_QF;
+    constexpr bool STAGE = !HALF || kHalfStaged;
+    constexpr int RW = edge_rec_width(B - 1), NREC = STAGE ? rec_stage<B - 1>() : 2;
+    constexpr int NINC = STAGE ? kIncStage : 2;
+    __shared__ int2 s_inc[NINC];
     __shared__ int s_ptr[kTilePoses + 1];
     __shared__ int s_e[2];
     __shared__ f64x2 s_rec2[NREC * RW / 2];
@@ -353,16 +359,15 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     if (threadIdx.x < 2) s_e[threadIdx.x] = q.rec_first[t0 + (threadIdx.x ? cnt : 0)];
     __syncthreads();
     const int i0 = s_ptr[0], ni = s_ptr[cnt] - i0, e0 = s_e[0], ne = s_e[1] - e0;
-    const bool staged = ni <= kIncStage && ne <= NREC;
+    const bool staged = STAGE && ni <= NINC && ne <= NREC;
     if (staged) {
       for (int x = threadIdx.x; x < ni; x += kThreads) s_inc[x] = q.inc[i0 + x];
       const f64x2* src = reinterpret_cast<const f64x2*>(q.rec) + static_cast<long>(e0) * (RW / 2);
       for (int x = threadIdx.x; x < ne * (RW / 2); x += kThreads) s_rec2[x] = src[x];
     }
-    __syncthreads();
+    if constexpr (STAGE) __syncthreads();
     if (p.ok) {
       const double* s_rec = reinterpret_cast<const double*>(s_rec2);
-      constexpr bool HALF = MODE == MODE_F || MODE == MODE_QF;
       if (staged)
         spmm_accumulate_edges<R, B, true, HALF>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc, i0,
                                                 s_rec, e0, acc);
