@@ -306,8 +306,10 @@ class Problem:
         return from_dev_layout(o, self.r), [r.as_dict() for r in res]
 
     # --- device pointers ---------------------------------------------------------------------
-    def optimize_dev(self, X_dev: int, X_out_dev: int, params: OptParams | None = None, enabled=None):
-        res = (OptResult * self.K)()
+    def optimize_dev(self, X_dev: int, X_out_dev: int, params: OptParams | None = None, enabled=None,
+                     want_results=True):
+        """want_results=False: no statistics (the RBCD engine's call: f(x2) only, direct X_out)."""
+        res = (OptResult * self.K)() if want_results else None
         p = params or default_params()
         if enabled is not None:
             en, enp = _i32(enabled)
@@ -315,7 +317,7 @@ class Problem:
             enp = None
         _check(lib().dpgo_hip_optimize_dev(self.h, C.byref(p), C.c_void_p(X_dev), C.c_void_p(X_out_dev),
                                            enp, res))
-        return [r.as_dict() for r in res]
+        return [r.as_dict() for r in res] if want_results else None
 
     def polar_combine_dev(self, A_dev, B_dev, ca, cb, out_dev):
         a, ap = _f64(ca)

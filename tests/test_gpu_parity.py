@@ -142,6 +142,50 @@ def test_batched_agents_match_independent(hip):
         assert rel(Xh[:, start[k] * b:start[k + 1] * b], Xk) <= 1e-10
 
 
+@pytest.mark.parametrize("want_results", [True, False])
+def test_first_step_prediction_paths(hip, want_results):
+    """The first tCG step is evaluated as <delta, Hess delta> alone (MODE_QF) while the previous call's
+    first step stopped every agent; agents that take a CG step then get Hess[delta] (and the
+    gradient) recomputed, and their candidate / rho test follow the boundary agents' speculative
+    ones.  A batch mixing a near-optimal agent (CG steps) with far-off agents (boundary steps), over
+    repeated calls on one handle, must match independent oracle solves every time."""
+    import torch
+    meas = load_meas("smallGrid3D")
+    d, r, n = 3, 5, meas.num_poses
+    b = d + 1
+    Q = O.connection_laplacian(meas, n)
+    P = O.QuadraticProblem(n, d, r)
+    P.set_Q(Q)
+    P.precon_mode = O.PRECON_BLOCK_JACOBI
+    good = O.lifting_matrix(d, r) @ O.chordal_initialization(d, n, meas)
+    Xs = [good, random_point(r, d, n, 31), random_point(r, d, n, 32)]
+    H = hip.Problem(None, d, r, poses_per_agent=[n] * len(Xs))
+    for k in range(len(Xs)):
+        H.set_Q_scipy(k, Q)
+    p = hip.default_params(tr_iterations=1, tr_tolerance=1e-2, tr_initial_radius=100.0, tr_max_inner=10,
+                           precon=hip.PRECON_BLOCK_JACOBI)
+    op = O.OptParams(tr_iterations=1, tr_tolerance=1e-2, tr_initial_radius=100.0, tr_max_inner=10)
+    dev = torch.device("cuda", 0)
+    kinds = set()
+    for call in range(6):
+        if call == 4:  # every agent far off: the prediction turns back to "first step stops" (call 5)
+            Xs[0] = random_point(r, d, n, 33)
+        xin = torch.from_numpy(hip.to_dev_layout(np.hstack(Xs))).to(dev)
+        xout = torch.empty_like(xin)
+        H.optimize_dev(xin.data_ptr(), xout.data_ptr(), p, want_results=want_results)
+        torch.cuda.synchronize()
+        Xh = hip.from_dev_layout(xout.cpu().numpy(), r)
+        for k in range(len(Xs)):
+            trace = []
+            Xk, rk = O.optimize(P, Xs[k], op, trace)
+            outer = [t for t in trace if "ninner" in t]
+            if outer:  # tCG ran: did its first step end it?
+                kinds.add(outer[0]["ninner"] == 1 and outer[0]["status"] in (O.TCG_NEGCURVTURE, O.TCG_EXCREGION))
+            assert rel(Xh[:, k * n * b:(k + 1) * n * b], Xk) <= 1e-10, (call, k)
+            Xs[k] = Xk
+    assert kinds == {True, False}  # both kinds of first step occurred
+
+
 def _agent_edges(meas, robot_of, local, k):
     """Agent k's measurement stream: private edges with local endpoints, shared edges with the
     foreign endpoint = -1 (PGOAgent::constructQMatrix, src/PGOAgent.cpp:720-781)."""
