@@ -269,7 +269,8 @@ __device__ __forceinline__ void edge_loop(const QView& q, const double* __restri
 template <int R, int B, bool STAGED, bool HALF = false>
 __device__ __forceinline__ void spmm_accumulate_edges(const QView& q, const double* __restrict__ in, long j,
                                                       int k, int beg, int end, const int2* s_inc, int i0,
-                                                      const double* s_rec, int e0, double (&acc)[R][B]) {
+                                                      const double* s_rec, int e0, double (&acc)[R][B],
+                                                      double (&xown)[R]) {
   constexpr int DW = diag_width(B - 1);
   const int kc = k < B ? k : 0;
   if constexpr (HALF) {
@@ -305,6 +306,8 @@ __device__ __forceinline__ void spmm_accumulate_edges(const QView& q, const doub
     dk[c] = dj[o];
   }
   const bool act = k < B;
+#pragma unroll
+  for (int a = 0; a < R; ++a) xown[a] = act ? xj[a] : 0.0;  // column k of in_j (load_col), for the epilogues
 #pragma unroll
   for (int a = 0; a < R; ++a) xj[a] = HALF ? 0.5 * xj[a] : xj[a];
 #pragma unroll
@@ -343,6 +346,10 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
 #pragma unroll
     for (int cc = 0; cc < B; ++cc) acc[a][cc] = 0.0;
 
+  // column k of in_j: the edge stream reads it for the diagonal term and hands it to the epilogues
+  double xin[R];
+#pragma unroll
+  for (int a = 0; a < R; ++a) xin[a] = 0.0;
   if constexpr (FMT == QFMT_EDGES) {
     // The half (each-edge-once) passes read only the tile's first-visit records, each exactly once and
     // as whole 128-byte lines per pose quad: they skip the LDS stage (less LDS, more resident waves).
@@ -370,13 +377,14 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
       const double* s_rec = reinterpret_cast<const double*>(s_rec2);
       if (staged)
         spmm_accumulate_edges<R, B, true, HALF>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc, i0,
-                                                s_rec, e0, acc);
+                                                s_rec, e0, acc, xin);
       else
         spmm_accumulate_edges<R, B, false, HALF>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc, i0,
-                                                 s_rec, e0, acc);
+                                                 s_rec, e0, acc, xin);
     }
   } else {
     if (p.ok && p.k < B) spmm_accumulate<R, B, var_unr(VAR), var_nt(VAR)>(q, in, p.j, p.k, acc);
+    if constexpr (MODE != MODE_XQ && MODE != MODE_XQ_G) load_col<R, B>(in, p.j, p.k, p.ok, xin);
   }
   // lane k keeps column k of the block row only (quad reduce-scatter; same additions, same
   // order as a quad all-reduce, so bitwise identical to it) and the epilogues work column-locally
@@ -399,7 +407,12 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     store_vec<R>(out, off, own, qc);
   } else if constexpr (MODE == MODE_EVAL || MODE == MODE_F || MODE == MODE_EVAL_TCG) {
     double xcol[R], gcol[R];
-    load_col<R, B>(X, p.j, p.k, p.ok, xcol);
+    if (X == in) {  // the evaluation point is the SpMM input (always, through eval_at)
+#pragma unroll
+      for (int a = 0; a < R; ++a) xcol[a] = xin[a];
+    } else {
+      load_col<R, B>(X, p.j, p.k, p.ok, xcol);
+    }
 #pragma unroll
     for (int a = 0; a < R; ++a) gcol[a] = 0.0;
     if (own && gidx != nullptr) {
@@ -479,7 +492,8 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
   } else if constexpr (MODE == MODE_CERT) {
     // certificate matrix S(X) = Q - Lambda(X), Lambda_j = [S_j 0; 0 0] (S_j = sym(Y_j^T EG_Y))
     double vcol[R];
-    load_col<R, B>(in, p.j, p.k, p.ok, vcol);
+#pragma unroll
+    for (int a = 0; a < R; ++a) vcol[a] = xin[a];
     double S[D][D];
 #pragma unroll
     for (int u = 0; u < D; ++u)
@@ -493,7 +507,8 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     // d_Hd = <V, Hess[V]> = <V, VQ> - <V_Y, V_Y S> for a tangent V (A.3; P_X is self-adjoint), without
     // forming Hess[V].  The edge stream accumulates each edge once (HALF), so <V, VQ> = 2 sum_j <V_j, acc_j>.
     double vcol[R];
-    load_col<R, B>(in, p.j, p.k, p.ok, vcol);
+#pragma unroll
+    for (int a = 0; a < R; ++a) vcol[a] = xin[a];
     double S[D][D];
 #pragma unroll
     for (int u = 0; u < D; ++u)
@@ -512,7 +527,8 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     block_partials<1>(parts, c.partials, p.tile);
   } else if constexpr (MODE == MODE_HESS) {
     double vcol[R], xcol[R];
-    load_col<R, B>(in, p.j, p.k, p.ok, vcol);
+#pragma unroll
+    for (int a = 0; a < R; ++a) vcol[a] = xin[a];
     load_col<R, B>(X, p.j, p.k, p.ok, xcol);
     double S[D][D];
 #pragma unroll
