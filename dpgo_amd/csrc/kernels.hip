@@ -1049,28 +1049,49 @@ __global__ __launch_bounds__(kThreads) void k_accept(LaunchCtx c, const double* 
 // Per-agent finalize: reduce tile partials in a fixed order, run the scalar logic of the
 // RTR / tCG state machine (A.4) on device.  grid = #agents, block = 256.
 // ------------------------------------------------------------------------------------------
+// The summation tree is the classic 256-wide LDS halving tree (pairs t, t + w for w = 128 .. 1);
+// the two cross-wave levels go through LDS once for all quantities and the six in-wave levels are
+// shuffles (lane t adds lane t + w: the same pairs in the same order), so the sums are bitwise
+// those of a barrier-per-level tree with 1 barrier instead of 8 per quantity.  The agent's state
+// is staged in LDS while the partials load, so the scalar logic below runs on LDS, not on a chain
+// of dependent global loads.
+static_assert(kThreads == 256, "k_finalize's reduction tree assumes 4 waves of 64");
+static_assert(sizeof(AgentState) % sizeof(double) == 0, "AgentState is staged as doubles");
 __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
   const int agent = blockIdx.x;
   const int t0 = f.agent_tile_off[agent], t1 = f.agent_tile_off[agent + 1];
-  __shared__ double red[kThreads];
+  constexpr int kStateWords = static_cast<int>(sizeof(AgentState) / sizeof(double));
+  __shared__ double red[4][kThreads];
   __shared__ double tot[4];
+  __shared__ AgentState sh_state;
+  if (threadIdx.x < kStateWords)
+    reinterpret_cast<double*>(&sh_state)[threadIdx.x] = reinterpret_cast<const double*>(&f.state[agent])[threadIdx.x];
   const int nq = f.nq_a + f.nq_b;
-  for (int q = 0; q < nq; ++q) {
-    const double* src = q < f.nq_a ? f.pa : f.pb;
-    const int qq = q < f.nq_a ? q : q - f.nq_a;
-    double s = 0.0;
-    for (int t = t0 + threadIdx.x; t < t1; t += kThreads) s += src[t * kPartialStride + qq];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int w = kThreads / 2; w > 0; w >>= 1) {
-      if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-      __syncthreads();
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int t = t0 + threadIdx.x; t < t1; t += kThreads) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q >= nq) break;
+      const double* src = q < f.nq_a ? f.pa : f.pb;
+      const int qq = q < f.nq_a ? q : q - f.nq_a;
+      acc[q] += src[t * kPartialStride + qq];
     }
-    if (threadIdx.x == 0) tot[q] = red[0];
-    __syncthreads();
   }
-  if (threadIdx.x != 0) return;
-  AgentState& s = f.state[agent];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[q][threadIdx.x] = acc[q];
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  const int l = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q >= nq) break;
+    double v = (red[q][l] + red[q][l + 128]) + (red[q][l + 64] + red[q][l + 192]);
+#pragma unroll
+    for (int w = 32; w > 0; w >>= 1) v += __shfl_down(v, w, 64);
+    if (l == 0) tot[q] = v;
+  }
+  if (l != 0) return;
+  AgentState& s = sh_state;
   const OptScalars& o = f.opt;
   const bool filtered = (f.agent_filter == 1 && !s.eta_implicit) || (f.agent_filter == 2 && s.eta_implicit);
   switch (filtered ? -1 : f.op) {
@@ -1257,6 +1278,12 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
     }
     default:
       break;
+  }
+  {
+    double* dst = reinterpret_cast<double*>(&f.state[agent]);
+    const double* srcw = reinterpret_cast<const double*>(&sh_state);
+#pragma unroll
+    for (int w = 0; w < kStateWords; ++w) dst[w] = srcw[w];
   }
   if (f.pub != nullptr) {
     const int flag = f.pub_kind == 1 ? s.tcg_active : s.run_active;
