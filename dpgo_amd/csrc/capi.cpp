@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -489,9 +490,9 @@ int ensure_work_public(dpgo_hip_problem h) { return ensure_work(h); }
 
 namespace {
 
-int finalize(dpgo_hip_problem h, int op, const double* pa, int nqa, const double* pb, int nqb,
-             const dpgo::OptScalars* opt = nullptr, const int* enabled = nullptr, int pub_kind = 0,
-             int pub_tag = 0, int agent_filter = 0) {
+dpgo::FinalizeArgs make_fin(dpgo_hip_problem h, int op, const double* pa, int nqa, const double* pb, int nqb,
+                            const dpgo::OptScalars* opt = nullptr, const int* enabled = nullptr, int pub_kind = 0,
+                            int pub_tag = 0, int agent_filter = 0) {
   dpgo::FinalizeArgs f;
   std::memset(&f, 0, sizeof(f));
   f.agent_filter = agent_filter;
@@ -511,7 +512,30 @@ int finalize(dpgo_hip_problem h, int op, const double* pa, int nqa, const double
   f.state = h->state.p;
   f.out_sums = h->sums.p;
   if (opt) f.opt = *opt;
+  return f;
+}
+
+int finalize(dpgo_hip_problem h, int op, const double* pa, int nqa, const double* pb, int nqb,
+             const dpgo::OptScalars* opt = nullptr, const int* enabled = nullptr, int pub_kind = 0,
+             int pub_tag = 0, int agent_filter = 0) {
+  const dpgo::FinalizeArgs f = make_fin(h, op, pa, nqa, pb, nqb, opt, enabled, pub_kind, pub_tag, agent_filter);
   HIP_TRY(dpgo::launch_finalize(f, h->K, h->stream));
+  return DPGO_HIP_OK;
+}
+
+// An SpMM followed by finalize `fin`: fused into the SpMM's last block per agent (spmm_arrive), or as
+// a separate k_finalize launch when fusion is off.
+int spmm_then_finalize(dpgo_hip_problem h, int mode, const dpgo::LaunchCtx& c, dpgo::SpmmArgs a,
+                       const dpgo::FinalizeArgs& fin) {
+  const bool fuse = h->fuse_finalize != 0 && c.num_tiles > 0 && dpgo::spmm_fusable(mode);
+  if (fuse) {
+    a.fin_arrive = h->arrive.p;
+    a.fin_mode = h->fuse_finalize;
+    a.fin = fin;
+    a.fin.coherent = h->fuse_finalize == 2 ? 1 : 0;
+  }
+  HIP_TRY(dpgo::launch_spmm(h->r, h->b, mode, c, qview(h), a));
+  if (!fuse) HIP_TRY(dpgo::launch_finalize(fin, h->K, h->stream));
   return DPGO_HIP_OK;
 }
 
@@ -569,9 +593,11 @@ int download_state(dpgo_hip_problem h) {
 // EVAL sweep at X: g = P_X(XQ+G), S, per-agent f and |g|^2 partials into pa.  mode MODE_F: f only;
 // MODE_EVAL_TCG: also the tCG start delta = -Prec(g) and the <z, g> partial.
 int eval_at(dpgo_hip_problem h, const double* X, double* gout, double* Sout, double* part, int flag,
-            int mode = dpgo::MODE_EVAL, double* delta = nullptr, int pmode = dpgo::PRECON_NONE) {
+            int mode = dpgo::MODE_EVAL, double* delta = nullptr, int pmode = dpgo::PRECON_NONE,
+            const dpgo::FinalizeArgs* fin = nullptr) {
   auto c = make_ctx(h, flag, part);
   const dpgo::SpmmArgs a{X, h->gidx.p, h->gblk.p, X, nullptr, gout, Sout, h->minv.p, delta, pmode};
+  if (fin != nullptr) return spmm_then_finalize(h, mode, c, a, *fin);
   HIP_TRY(dpgo::launch_spmm(h->r, h->b, mode, c, qview(h), a));
   return DPGO_HIP_OK;
 }
@@ -682,15 +708,18 @@ int dpgo_hip_problem_create_batch(int num_agents, const int* poses_per_agent, in
       h->agent_tile_off.ensure(num_agents + 1) || h->agent_np.ensure(num_agents) ||
       h->enabled.ensure(num_agents) || h->use_a.ensure(num_agents) || h->pa.ensure(static_cast<size_t>(T) * dpgo::kPartialStride) ||
       h->pb.ensure(static_cast<size_t>(T) * dpgo::kPartialStride) || h->sums.ensure(static_cast<size_t>(num_agents) * 4) ||
-      h->state.ensure(num_agents) || h->coef_a.ensure(num_agents) || h->coef_b.ensure(num_agents))
+      h->state.ensure(num_agents) || h->coef_a.ensure(num_agents) || h->coef_b.ensure(num_agents) ||
+      h->arrive.ensure(num_agents))
     return cleanup(fail(DPGO_HIP_ENOMEM, "device allocation failed"));
   if (hipMemcpy(h->tile_agent.p, h->h_tile_agent.data(), sizeof(int) * T, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->tile_start.p, h->h_tile_start.data(), sizeof(int) * T, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->tile_count.p, h->h_tile_count.data(), sizeof(int) * T, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->agent_tile_off.p, h->h_agent_tile_off.data(), sizeof(int) * (num_agents + 1), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(h->agent_np.p, poses_per_agent, sizeof(int) * num_agents, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(h->state.p, 0, sizeof(AgentState) * num_agents) != hipSuccess)
+      hipMemset(h->state.p, 0, sizeof(AgentState) * num_agents) != hipSuccess ||
+      hipMemset(h->arrive.p, 0, sizeof(int) * num_agents) != hipSuccess)
     return cleanup(fail(DPGO_HIP_EDEVICE, "device upload failed"));
+  if (const char* ev = std::getenv("DPGO_FUSE_FINALIZE")) h->fuse_finalize = std::atoi(ev);
   if (hipHostMalloc(reinterpret_cast<void**>(&h->pub_host), sizeof(int) * num_agents,
                     hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer(reinterpret_cast<void**>(&h->pub_dev), h->pub_host, 0) != hipSuccess)
@@ -1000,9 +1029,9 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
   // is recomputed in the rare case it is needed
   bool g_valid = !(fused_tcg && single && h->predict_boundary && P.tr_max_inner > 0);
   if (fused_tcg) {
+    const dpgo::FinalizeArgs fin = make_fin(h, dpgo::OP_EVAL_TCG_INIT, h->pa.p, 3, nullptr, 0, &o, en_dev);
     DPGO_TRY(eval_at(h, x1, g_valid ? h->g.p : nullptr, h->S.p, h->pa.p, dpgo::FLAG_NONE, dpgo::MODE_EVAL_TCG,
-                     h->delta.p, pmode));
-    DPGO_TRY(finalize(h, dpgo::OP_EVAL_TCG_INIT, h->pa.p, 3, nullptr, 0, &o, en_dev));
+                     h->delta.p, pmode, &fin));
   } else {
     DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_NONE));
     DPGO_TRY(finalize(h, dpgo::OP_EVAL_INIT, h->pa.p, 2, nullptr, 0, &o, en_dev));
@@ -1069,14 +1098,14 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
     // iteration j's step test: Hdelta = Hess[delta] and d_Hd = <delta, Hdelta>, or (qf) d_Hd alone
     auto launch_step = [&](bool qf) -> int {
       auto ch = make_ctx(h, dpgo::FLAG_TCG, h->pa.p);
-      HIP_TRY(dpgo::launch_spmm(r, b, qf ? dpgo::MODE_QF : dpgo::MODE_HESS, ch, qview(h), h->delta.p, nullptr,
-                                nullptr, x1, h->S.p, qf ? nullptr : h->Hdelta.p, nullptr));
       // the step test publishes too: when it already stopped every agent (a boundary or
       // negative-curvature step, the common RBCD case) the host launches no further iteration
       const int stag = next_tag(h);
       step_tags.push_back(stag);
-      DPGO_TRY(finalize(h, dpgo::OP_TCG_STEP, h->pa.p, 1, nullptr, 0, &o, nullptr, 1, stag));
-      return DPGO_HIP_OK;
+      const dpgo::SpmmArgs sa{h->delta.p, nullptr, nullptr, x1, h->S.p, qf ? nullptr : h->Hdelta.p, nullptr,
+                              nullptr, nullptr, dpgo::PRECON_NONE};
+      return spmm_then_finalize(h, qf ? dpgo::MODE_QF : dpgo::MODE_HESS, ch, sa,
+                                make_fin(h, dpgo::OP_TCG_STEP, h->pa.p, 1, nullptr, 0, &o, nullptr, 1, stag));
     };
     auto launch_rest = [&](int j) -> int {
       auto cu = make_ctx(h, dpgo::FLAG_TCG_MODE, h->pb.p);
@@ -1107,12 +1136,14 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
       HIP_TRY(dpgo::launch_retract(r, b, cr, x1, h->eta.p, 1.0, x2, h->g.p, h->Heta.p, h->delta.p));
       // single Run: only f(x2) and |grad(x2)| are consumed (fOpt / gradNormOpt), |grad(x2)| only as a
       // statistic
-      if (single)
-        DPGO_TRY(eval_at(h, x2, nullptr, nullptr, h->pb.p, run_flag, stats ? dpgo::MODE_EVAL : dpgo::MODE_F));
-      else
-        DPGO_TRY(eval_at(h, x2, h->g2.p, h->S2.p, h->pb.p, run_flag));
       const int rtag = next_tag(h);
-      DPGO_TRY(finalize(h, dpgo::OP_RHO, h->pa.p, 2, h->pb.p, 2, &o, nullptr, 2, rtag, filter));
+      const dpgo::FinalizeArgs fin = make_fin(h, dpgo::OP_RHO, h->pa.p, 2, h->pb.p, 2, &o, nullptr, 2, rtag, filter);
+      if (single)
+        DPGO_TRY(eval_at(h, x2, nullptr, nullptr, h->pb.p, run_flag, stats ? dpgo::MODE_EVAL : dpgo::MODE_F,
+                         nullptr, dpgo::PRECON_NONE, &fin));
+      else
+        DPGO_TRY(eval_at(h, x2, h->g2.p, h->S2.p, h->pb.p, run_flag, dpgo::MODE_EVAL, nullptr, dpgo::PRECON_NONE,
+                         &fin));
       return rtag;
     };
     int launched = 0, rtag = 0;

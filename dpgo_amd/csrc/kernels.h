@@ -72,20 +72,6 @@ struct QView {
   int fmt;                // QFormat
 };
 
-// Operands of one SpMM launch (unused ones may be null).
-struct SpmmArgs {
-  const double* in;     // X (EVAL modes) or V
-  const int* gidx;      // G slot per pose (-1 = none)
-  const double* gblk;   // G blocks
-  const double* X;      // iterate (EVAL / HESS)
-  const double* S_in;   // cached sym(Y^T EG_Y) (HESS)
-  double* out;          // result (gradient / HVP); may be null in EVAL
-  double* S_out;        // S (EVAL)
-  const double* Minv;   // block-Jacobi inverses (EVAL_TCG)
-  double* delta;        // tCG direction (EVAL_TCG)
-  int pmode;            // PreconMode (EVAL_TCG)
-};
-
 struct OptScalars {
   double tol, Delta0, Delta_max, theta, kappa;
   int min_inner, max_iter, single_run, pad;
@@ -107,7 +93,34 @@ struct FinalizeArgs {
   int pub_tag;
   int pub_kind;                 // 1: tcg_active, 2: run_active
   int agent_filter;             // 0: every agent; 1 / 2: only agents whose eta is / is not implicit
+  int coherent;                 // read the partials with agent-scope loads (fused, SpmmArgs::fin_mode 2)
 };
+
+// SpMM modes that can run a fused finalize (SpmmArgs::fin_arrive); the others ignore it.
+__host__ __device__ constexpr bool spmm_fusable(int mode) {
+  return mode == MODE_EVAL || mode == MODE_EVAL_TCG || mode == MODE_F || mode == MODE_QF || mode == MODE_HESS;
+}
+
+// Operands of one SpMM launch (unused ones may be null).
+struct SpmmArgs {
+  const double* in;     // X (EVAL modes) or V
+  const int* gidx;      // G slot per pose (-1 = none)
+  const double* gblk;   // G blocks
+  const double* X;      // iterate (EVAL / HESS)
+  const double* S_in;   // cached sym(Y^T EG_Y) (HESS)
+  double* out;          // result (gradient / HVP); may be null in EVAL
+  double* S_out;        // S (EVAL)
+  const double* Minv;   // block-Jacobi inverses (EVAL_TCG)
+  double* delta;        // tCG direction (EVAL_TCG)
+  int pmode;            // PreconMode (EVAL_TCG)
+  // Fused finalize (null = none): the last block of each agent to arrive runs k_finalize's work for
+  // that agent (fin), so no separate k_finalize launch follows the SpMM.  fin_arrive[agent] counts
+  // arrivals and is reset to 0 by that last block.
+  int* fin_arrive;
+  int fin_mode;  // 1: device fences, 2: agent-scope partial stores and loads (see spmm_arrive)
+  FinalizeArgs fin;
+};
+
 
 // shared-edge records for G assembly, grouped by G slot (CSR)
 struct GEdges {

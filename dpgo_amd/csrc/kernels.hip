@@ -52,9 +52,10 @@ __device__ __forceinline__ void store_vec(double* __restrict__ P, long off, bool
   }
 }
 
+// coherent: agent-scope (L2-bypassing) stores, read by a fused finalize in the same launch
 template <int NQ>
 __device__ __forceinline__ void block_partials(double (&v)[NQ], double* __restrict__ partials,
-                                               int tile) {
+                                               int tile, bool coherent = false) {
   __shared__ double red[4][NQ > 0 ? NQ : 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -66,8 +67,13 @@ __device__ __forceinline__ void block_partials(double (&v)[NQ], double* __restri
   __syncthreads();
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int q = 0; q < NQ; ++q)
-      partials[tile * kPartialStride + q] = ((red[0][q] + red[1][q]) + red[2][q]) + red[3][q];
+    for (int q = 0; q < NQ; ++q) {
+      const double t = ((red[0][q] + red[1][q]) + red[2][q]) + red[3][q];
+      if (coherent)
+        __hip_atomic_store(&partials[tile * kPartialStride + q], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        partials[tile * kPartialStride + q] = t;
+    }
   }
 }
 
@@ -326,6 +332,35 @@ constexpr bool evar_xcd(int v) { return (v & 1) != 0; }
 constexpr int evar_waves(int v) { return (v >> 1) == 0 ? 1 : 3 + (v >> 1); }
 
 
+__device__ void finalize_agent(const FinalizeArgs& f, int agent);
+
+// Fused finalize (SpmmArgs::fin_arrive): every block of the launch arrives once per agent tile, after
+// its partial is written (release: fence, then the count); the block that completes its agent's
+// count runs the agent's finalize on wave 0 (acquire fence first) and resets the count.  Skipped
+// tiles arrive too, so every agent is finalized exactly as by a separate k_finalize launch.
+// fin_mode 1: device-scope fences around the count (each writes back the XCD's L2: slow).
+// fin_mode 2: partials are agent-scope stores (block_partials coherent) that complete before the count
+// (s_waitcnt vmcnt(0)); the finalize reads them with agent-scope loads; no cache maintenance.
+__device__ __forceinline__ void spmm_arrive(const SpmmArgs& a, int agent) {
+  if (a.fin_arrive == nullptr) return;
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (a.fin_mode == 2)
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this block's partial stores are acknowledged
+    else
+      __threadfence();
+    const int n = a.fin.agent_tile_off[agent + 1] - a.fin.agent_tile_off[agent];
+    const int old = atomicAdd(&a.fin_arrive[agent], 1);
+    s_last = old == n - 1 ? 1 : 0;
+    if (s_last) atomicExch(&a.fin_arrive[agent], 0);
+  }
+  __syncthreads();
+  if (s_last == 0 || threadIdx.x >= 64) return;
+  if (a.fin_mode != 2) __threadfence();
+  finalize_agent(a.fin, agent);
+}
+
 template <int R, int B, int MODE, int VAR = 0, int FMT = QFMT_BSR>
 __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) void k_spmm(LaunchCtx c, QView q,
                                                                                           SpmmArgs args) {
@@ -338,7 +373,10 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
   double* __restrict__ S_out = args.S_out;
   constexpr int D = B - 1;
   const PoseLane p = pose_lane<B, FMT == QFMT_EDGES ? evar_xcd(VAR) : var_xcd(VAR)>(c);
-  if (tile_skipped(c, p.agent)) return;
+  if (tile_skipped(c, p.agent)) {
+    if constexpr (spmm_fusable(MODE)) spmm_arrive(args, p.agent);
+    return;
+  }
 
   double acc[R][B];
 #pragma unroll
@@ -429,7 +467,7 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     for (int a = 0; a < R; ++a) fpart = fma(fma(kq, qc[a], gcol[a]), xcol[a], fpart);
     if constexpr (MODE == MODE_F) {  // f only (QuadraticProblem::f, :50-60)
       double parts[2] = {own ? fpart : 0.0, 0.0};
-      block_partials<2>(parts, c.partials, p.tile);
+      block_partials<2>(parts, c.partials, p.tile, args.fin_mode == 2);
     } else {
       double eg[R];  // column k of the Euclidean gradient XQ + G
 #pragma unroll
@@ -483,10 +521,10 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
         }
         store_vec<R>(args.delta, off, own, dc);
         double parts[3] = {own ? fpart : 0.0, own ? gpart : 0.0, own ? zr : 0.0};
-        block_partials<3>(parts, c.partials, p.tile);
+        block_partials<3>(parts, c.partials, p.tile, args.fin_mode == 2);
       } else {
         double parts[2] = {own ? fpart : 0.0, own ? gpart : 0.0};
-        block_partials<2>(parts, c.partials, p.tile);
+        block_partials<2>(parts, c.partials, p.tile, args.fin_mode == 2);
       }
     }
   } else if constexpr (MODE == MODE_CERT) {
@@ -524,7 +562,7 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
 #pragma unroll
     for (int a = 0; a < R; ++a) dpart = fma(vcol[a], hc[a], dpart);
     double parts[1] = {own ? dpart : 0.0};
-    block_partials<1>(parts, c.partials, p.tile);
+    block_partials<1>(parts, c.partials, p.tile, args.fin_mode == 2);
   } else if constexpr (MODE == MODE_HESS) {
     double vcol[R], xcol[R];
 #pragma unroll
@@ -548,8 +586,9 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     for (int a = 0; a < R; ++a) dpart = fma(vcol[a], hc[a], dpart);
     store_vec<R>(out, off, own, hc);
     double parts[1] = {own ? dpart : 0.0};
-    block_partials<1>(parts, c.partials, p.tile);
+    block_partials<1>(parts, c.partials, p.tile, args.fin_mode == 2);
   }
+  if constexpr (spmm_fusable(MODE)) spmm_arrive(args, p.agent);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1047,51 +1086,43 @@ __global__ __launch_bounds__(kThreads) void k_accept(LaunchCtx c, const double* 
 
 // ------------------------------------------------------------------------------------------
 // Per-agent finalize: reduce tile partials in a fixed order, run the scalar logic of the
-// RTR / tCG state machine (A.4) on device.  grid = #agents, block = 256.
+// RTR / tCG state machine (A.4) on device.  grid = #agents, block = one wave.
 // ------------------------------------------------------------------------------------------
-// The summation tree is the classic 256-wide LDS halving tree (pairs t, t + w for w = 128 .. 1);
-// the two cross-wave levels go through LDS once for all quantities and the six in-wave levels are
-// shuffles (lane t adds lane t + w: the same pairs in the same order), so the sums are bitwise
-// those of a barrier-per-level tree with 1 barrier instead of 8 per quantity.  The agent's state
-// is staged in LDS while the partials load, so the scalar logic below runs on LDS, not on a chain
-// of dependent global loads.
-static_assert(kThreads == 256, "k_finalize's reduction tree assumes 4 waves of 64");
-static_assert(sizeof(AgentState) % sizeof(double) == 0, "AgentState is staged as doubles");
-__global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
-  const int agent = blockIdx.x;
+// The summation tree is the classic 256-wide LDS halving tree over per-thread serial sums (thread t
+// sums tiles t, t + 256, ...; then pairs t, t + w for w = 128 .. 1).  One wave evaluates it: lane l
+// plays threads l, l + 64, l + 128, l + 192 (the two cross-wave levels in registers) and the six
+// in-wave levels are shuffles (lane t adds lane t + w: the same pairs in the same order), so the sums
+// are bitwise those of the barrier-per-level tree, with no LDS and no barrier.  Called by all 64 lanes
+// of one wave (k_finalize, or the last-arriving block of an agent in a fused k_spmm).
+static_assert(kThreads == 256, "finalize_agent restates a 256-thread reduction tree");
+// The state is read and written in place (a register copy of AgentState would cost the fused SpMMs
+// ~50 VGPRs and a wave per SIMD of occupancy).
+__device__ __forceinline__ void finalize_agent(const FinalizeArgs& f, int agent) {
+  const int l = static_cast<int>(threadIdx.x) & 63;
   const int t0 = f.agent_tile_off[agent], t1 = f.agent_tile_off[agent + 1];
-  constexpr int kStateWords = static_cast<int>(sizeof(AgentState) / sizeof(double));
-  __shared__ double red[4][kThreads];
-  __shared__ double tot[4];
-  __shared__ AgentState sh_state;
-  if (threadIdx.x < kStateWords)
-    reinterpret_cast<double*>(&sh_state)[threadIdx.x] = reinterpret_cast<const double*>(&f.state[agent])[threadIdx.x];
   const int nq = f.nq_a + f.nq_b;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int t = t0 + threadIdx.x; t < t1; t += kThreads) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (q >= nq) break;
-      const double* src = q < f.nq_a ? f.pa : f.pb;
-      const int qq = q < f.nq_a ? q : q - f.nq_a;
-      acc[q] += src[t * kPartialStride + qq];
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) red[q][threadIdx.x] = acc[q];
-  __syncthreads();
-  if (threadIdx.x >= 64) return;
-  const int l = threadIdx.x;
+  double tot[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     if (q >= nq) break;
-    double v = (red[q][l] + red[q][l + 128]) + (red[q][l + 64] + red[q][l + 192]);
+    const double* src = q < f.nq_a ? f.pa : f.pb;
+    const int qq = q < f.nq_a ? q : q - f.nq_a;
+    double a4[4];
 #pragma unroll
-    for (int w = 32; w > 0; w >>= 1) v += __shfl_down(v, w, 64);
-    if (l == 0) tot[q] = v;
+    for (int v = 0; v < 4; ++v) {
+      double sv = 0.0;
+      for (int t = t0 + l + 64 * v; t < t1; t += kThreads)
+        sv += f.coherent ? __hip_atomic_load(&src[t * kPartialStride + qq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                         : src[t * kPartialStride + qq];
+      a4[v] = sv;
+    }
+    double x = (a4[0] + a4[2]) + (a4[1] + a4[3]);
+#pragma unroll
+    for (int w = 32; w > 0; w >>= 1) x += __shfl_down(x, w, 64);
+    tot[q] = x;
   }
   if (l != 0) return;
-  AgentState& s = sh_state;
+  AgentState& s = f.state[agent];
   const OptScalars& o = f.opt;
   const bool filtered = (f.agent_filter == 1 && !s.eta_implicit) || (f.agent_filter == 2 && s.eta_implicit);
   switch (filtered ? -1 : f.op) {
@@ -1279,18 +1310,14 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
     default:
       break;
   }
-  {
-    double* dst = reinterpret_cast<double*>(&f.state[agent]);
-    const double* srcw = reinterpret_cast<const double*>(&sh_state);
-#pragma unroll
-    for (int w = 0; w < kStateWords; ++w) dst[w] = srcw[w];
-  }
   if (f.pub != nullptr) {
     const int flag = f.pub_kind == 1 ? s.tcg_active : s.run_active;
     __hip_atomic_store(&f.pub[agent], (f.pub_tag << 1) | (flag ? 1 : 0), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
+
+__global__ __launch_bounds__(64) void k_finalize(FinalizeArgs f) { finalize_agent(f, blockIdx.x); }
 
 // --- block-Jacobi inverse of (Q_jj + shift I), computed on device from Q's diagonal blocks ---
 // In place on A = [M | I] (B x 2B): Gauss-Jordan with partial pivoting (SPD, so pivoting is a
@@ -1884,7 +1911,7 @@ hipError_t launch_precond_finish(int r, int b, const LaunchCtx& c, const double*
 
 hipError_t launch_finalize(const FinalizeArgs& f, int num_agents, hipStream_t stream) {
   if (num_agents == 0) return hipSuccess;
-  k_finalize<<<num_agents, kThreads, 0, stream>>>(f);
+  k_finalize<<<num_agents, 64, 0, stream>>>(f);
   return hipGetLastError();
 }
 

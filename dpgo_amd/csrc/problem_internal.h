@@ -118,6 +118,11 @@ struct dpgo_hip_problem_s {
   dpgo::DevBuf<double> pa, pb, sums, coef_a, coef_b;
   dpgo::DevBuf<dpgo::AgentState> state;
   std::vector<dpgo::AgentState> h_state;
+  // per-agent arrival counts of a k_spmm with a fused finalize (0 between launches)
+  dpgo::DevBuf<int> arrive;
+  // finalize after an SpMM: 0 separate k_finalize launch, 1 / 2 fused into the SpMM's last block per
+  // agent (SpmmArgs::fin_mode); DPGO_FUSE_FINALIZE overrides
+  int fuse_finalize = 0;
   // host-mapped status words written by k_finalize (zero-copy polling, no stream sync)
   int* pub_host = nullptr;
   int* pub_dev = nullptr;
