@@ -1086,43 +1086,12 @@ __global__ __launch_bounds__(kThreads) void k_accept(LaunchCtx c, const double* 
 
 // ------------------------------------------------------------------------------------------
 // Per-agent finalize: reduce tile partials in a fixed order, run the scalar logic of the
-// RTR / tCG state machine (A.4) on device.  grid = #agents, block = one wave.
+// RTR / tCG state machine (A.4) on device.
 // ------------------------------------------------------------------------------------------
-// The summation tree is the classic 256-wide LDS halving tree over per-thread serial sums (thread t
-// sums tiles t, t + 256, ...; then pairs t, t + w for w = 128 .. 1).  One wave evaluates it: lane l
-// plays threads l, l + 64, l + 128, l + 192 (the two cross-wave levels in registers) and the six
-// in-wave levels are shuffles (lane t adds lane t + w: the same pairs in the same order), so the sums
-// are bitwise those of the barrier-per-level tree, with no LDS and no barrier.  Called by all 64 lanes
-// of one wave (k_finalize, or the last-arriving block of an agent in a fused k_spmm).
-static_assert(kThreads == 256, "finalize_agent restates a 256-thread reduction tree");
-// The state is read and written in place (a register copy of AgentState would cost the fused SpMMs
-// ~50 VGPRs and a wave per SIMD of occupancy).
-__device__ __forceinline__ void finalize_agent(const FinalizeArgs& f, int agent) {
-  const int l = static_cast<int>(threadIdx.x) & 63;
-  const int t0 = f.agent_tile_off[agent], t1 = f.agent_tile_off[agent + 1];
+// The RTR / tCG scalar logic of one agent on its reduced partials tot[] (one thread).
+__device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent, const double (&tot)[4],
+                                                AgentState& s) {
   const int nq = f.nq_a + f.nq_b;
-  double tot[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    if (q >= nq) break;
-    const double* src = q < f.nq_a ? f.pa : f.pb;
-    const int qq = q < f.nq_a ? q : q - f.nq_a;
-    double a4[4];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      double sv = 0.0;
-      for (int t = t0 + l + 64 * v; t < t1; t += kThreads)
-        sv += f.coherent ? __hip_atomic_load(&src[t * kPartialStride + qq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                         : src[t * kPartialStride + qq];
-      a4[v] = sv;
-    }
-    double x = (a4[0] + a4[2]) + (a4[1] + a4[3]);
-#pragma unroll
-    for (int w = 32; w > 0; w >>= 1) x += __shfl_down(x, w, 64);
-    tot[q] = x;
-  }
-  if (l != 0) return;
-  AgentState& s = f.state[agent];
   const OptScalars& o = f.opt;
   const bool filtered = (f.agent_filter == 1 && !s.eta_implicit) || (f.agent_filter == 2 && s.eta_implicit);
   switch (filtered ? -1 : f.op) {
@@ -1317,7 +1286,89 @@ __device__ __forceinline__ void finalize_agent(const FinalizeArgs& f, int agent)
   }
 }
 
-__global__ __launch_bounds__(64) void k_finalize(FinalizeArgs f) { finalize_agent(f, blockIdx.x); }
+
+// Both reductions below evaluate the classic 256-wide LDS halving tree over per-thread serial sums
+// (thread t sums tiles t, t + 256, ...; then pairs t, t + w for w = 128 .. 1), so fused and separate
+// finalizes give bitwise the same sums.
+static_assert(kThreads == 256, "the finalize reductions restate a 256-thread reduction tree");
+
+// Fused path (one wave of the last-arriving SpMM block): lane l plays threads l, l + 64, l + 128,
+// l + 192 (the two cross-wave levels in registers) and the six in-wave levels are shuffles (lane t
+// adds lane t + w: the same pairs in the same order).  No LDS and no barrier; the state is read and
+// written in place (a register copy would cost the SpMM ~50 VGPRs and a wave per SIMD of occupancy).
+__device__ __forceinline__ void finalize_agent(const FinalizeArgs& f, int agent) {
+  const int l = static_cast<int>(threadIdx.x) & 63;
+  const int t0 = f.agent_tile_off[agent], t1 = f.agent_tile_off[agent + 1];
+  const int nq = f.nq_a + f.nq_b;
+  double tot[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q >= nq) break;
+    const double* src = q < f.nq_a ? f.pa : f.pb;
+    const int qq = q < f.nq_a ? q : q - f.nq_a;
+    double a4[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      double sv = 0.0;
+      for (int t = t0 + l + 64 * v; t < t1; t += kThreads)
+        sv += f.coherent ? __hip_atomic_load(&src[t * kPartialStride + qq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                         : src[t * kPartialStride + qq];
+      a4[v] = sv;
+    }
+    double x = (a4[0] + a4[2]) + (a4[1] + a4[3]);
+#pragma unroll
+    for (int w = 32; w > 0; w >>= 1) x += __shfl_down(x, w, 64);
+    tot[q] = x;
+  }
+  if (l != 0) return;
+  finalize_scalar(f, agent, tot, f.state[agent]);
+}
+
+// Separate launch (grid = #agents, block = 256): every thread loads its tiles' partials, the two
+// cross-wave levels go through LDS once for all quantities and the in-wave levels are shuffles; the
+// agent's state is staged in LDS while the partials load and written back after the scalar logic.
+static_assert(sizeof(AgentState) % sizeof(double) == 0, "AgentState is staged as doubles");
+__global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
+  const int agent = blockIdx.x;
+  const int t0 = f.agent_tile_off[agent], t1 = f.agent_tile_off[agent + 1];
+  constexpr int kStateWords = static_cast<int>(sizeof(AgentState) / sizeof(double));
+  __shared__ double red[4][kThreads];
+  __shared__ AgentState sh_state;
+  if (threadIdx.x < kStateWords)
+    reinterpret_cast<double*>(&sh_state)[threadIdx.x] = reinterpret_cast<const double*>(&f.state[agent])[threadIdx.x];
+  const int nq = f.nq_a + f.nq_b;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int t = t0 + threadIdx.x; t < t1; t += kThreads) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q >= nq) break;
+      const double* src = q < f.nq_a ? f.pa : f.pb;
+      const int qq = q < f.nq_a ? q : q - f.nq_a;
+      acc[q] += src[t * kPartialStride + qq];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[q][threadIdx.x] = acc[q];
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  const int l = threadIdx.x;
+  double tot[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q >= nq) break;
+    double v = (red[q][l] + red[q][l + 128]) + (red[q][l + 64] + red[q][l + 192]);
+#pragma unroll
+    for (int w = 32; w > 0; w >>= 1) v += __shfl_down(v, w, 64);
+    tot[q] = v;
+  }
+  if (l != 0) return;
+  finalize_scalar(f, agent, tot, sh_state);
+  double* dst = reinterpret_cast<double*>(&f.state[agent]);
+  const double* srcw = reinterpret_cast<const double*>(&sh_state);
+#pragma unroll
+  for (int w = 0; w < kStateWords; ++w) dst[w] = srcw[w];
+}
+
 
 // --- block-Jacobi inverse of (Q_jj + shift I), computed on device from Q's diagonal blocks ---
 // In place on A = [M | I] (B x 2B): Gauss-Jordan with partial pivoting (SPD, so pivoting is a
@@ -1911,7 +1962,7 @@ hipError_t launch_precond_finish(int r, int b, const LaunchCtx& c, const double*
 
 hipError_t launch_finalize(const FinalizeArgs& f, int num_agents, hipStream_t stream) {
   if (num_agents == 0) return hipSuccess;
-  k_finalize<<<num_agents, 64, 0, stream>>>(f);
+  k_finalize<<<num_agents, kThreads, 0, stream>>>(f);
   return hipGetLastError();
 }
 
