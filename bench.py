@@ -5,7 +5,11 @@ Workload (BASELINE.json configs[4] / SURVEY 8d C5): synthetic 3D grid, k^3 = 10^
 64 agents (4 x 4 x 4 sub-cubes of 25^3 poses), Nesterov-accelerated RBCD (as
 examples/MultiRobotExample.cpp) with the L2 cost, colour-class schedule (2 colours).
 One *step* = one sweep over both colours = every agent updated once (64 agent updates, each an
-RTR(1 outer, 10 tCG) solve as PGOAgent::updateX configures it) plus the public-pose exchange.
+RTR(1 outer, 10 tCG) solve as PGOAgent::updateX configures it, plus the agent status) plus the
+public-pose exchange.
+
+The timed region starts from the odometry initialisation after `--burnin` untimed steps (the iterate
+then re-enters set_X, i.e. PGOAgent::setX: Nesterov restarts from it), then `--warmup` untimed steps.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
@@ -23,11 +27,13 @@ sys.path.insert(0, ROOT)
 
 METRIC = "RBCD iters/sec + X·Q SpMM HBM GB/s, 1M-pose synth grid r=5, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+STATS = ["calls", "early", "runs", "tcg_iters", "NEGCURVTURE", "EXCREGION", "LCON", "SCON", "MAXITER",
+         "gave_up", "cg_steps", "implicit"]
 
 
 def measured_traffic():
-    """HBM bytes per launch of the edge-stream X.Q SpMM from the newest committed PMC summary
-    (profiles/*_pmc_traffic.json, produced by tools/pmc_traffic.py), or None."""
+    """HBM bytes per launch from the newest committed PMC summary (profiles/*_pmc_traffic.json,
+    produced by tools/pmc_traffic.py), or None."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
     if not files:
@@ -58,14 +64,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--burnin", type=int, default=0, help="untimed steps before the timed run's set_X")
     ap.add_argument("--k", type=int, default=100, help="grid side (k^3 poses)")
     ap.add_argument("--agents-per-axis", type=int, default=4)
     ap.add_argument("--r", type=int, default=5)
     ap.add_argument("--accel", type=int, default=1)
     ap.add_argument("--spmm-reps", type=int, default=20)
+    ap.add_argument("--kernel-timing", type=int, default=1, help="HIP events around in-step X.Q launches")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-sample-updates", type=int, default=40)
-    ap.add_argument("--verify", type=int, default=0, help="central cost before/after (slow)")
+    ap.add_argument("--cpu-sample-updates", type=int, default=20)
     ap.add_argument("--robust", default="L2", choices=["L2", "GNC_TLS", "TLS", "Huber", "GM", "L1"],
                     help="robust cost (L2: throughput setting; GNC_TLS: the reference default, "
                          "reweighting every 30 iterations on the device)")
@@ -83,8 +90,7 @@ def main():
     one_device = os.environ.get("DPGO_BENCH_ONE_DEVICE") == "1"
     if one_device:
         local_rank = 0
-    if world != args.gpus:
-        world = max(world, 1)
+    world = max(world, 1)
     torch.cuda.set_device(local_rank)
     if world > 1:
         if one_device:
@@ -101,7 +107,8 @@ def main():
     agent_rank = super_cube_ranks(A, world)
     params = H.rbcd_params(r=args.r, acceleration=args.accel, robust_cost=H.ROBUST[args.robust])
     eng = H.Rbcd(g, aop, agent_rank, rank, world, params)
-    stream = torch.cuda.current_stream(dev)
+    # every engine launch and the exchange run on one dedicated stream (stream order = halo order)
+    stream = torch.cuda.Stream(dev)
     eng.set_stream(stream.cuda_stream)
     YLift = H.lifting_matrix(3, args.r)
     X0 = g.chain_init_dev_layout(args.r, YLift)
@@ -112,47 +119,122 @@ def main():
     out_splits = [int(x) for x in eng.recv_counts]
     setup_s = time.time() - t_setup
 
+    def exchange():
+        if world == 1:
+            return None
+        eng.pack(send.data_ptr())
+        if one_device:
+            recv_h = torch.empty(recv.shape, dtype=recv.dtype)
+            dist.all_to_all_single(recv_h, send.cpu(), out_splits, in_splits)
+            recv.copy_(recv_h)
+        else:
+            dist.all_to_all_single(recv, send, out_splits, in_splits)
+        return recv.data_ptr()
+
     def step():
         for c in range(eng.num_colors):
             eng.pre_exchange(c)
-            if world > 1:
-                eng.pack(send.data_ptr())
-                if one_device:
-                    recv_h = torch.empty(recv.shape, dtype=recv.dtype)
-                    dist.all_to_all_single(recv_h, send.cpu(), out_splits, in_splits)
-                    recv.copy_(recv_h)
-                else:
-                    dist.all_to_all_single(recv, send, out_splits, in_splits)
-            eng.update(c, recv.data_ptr() if world > 1 else None)
+            eng.update(c, exchange())
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    def central():
+        """Central cost and |RieGrad| of the whole graph (examples/MultiRobotExample.cpp:229-235)."""
+        f, gn = eng.central_eval(exchange())
+        if world > 1:
+            t = torch.tensor(np.concatenate([[f], gn]), dtype=torch.float64, device="cpu" if one_device else dev)
+            dist.all_reduce(t)
+            v = t.cpu().numpy()
+            f, gn = float(v[0]), v[1:]
+        return f, float(np.sqrt(np.sum(gn)))
+
+    def sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    with torch.cuda.stream(stream):
+        for _ in range(args.burnin):
+            step()
+        if args.burnin:
+            Xb = np.zeros(X0.size)
+            eng.get_X_into(Xb)
+            if world > 1:
+                tx = torch.from_numpy(Xb) if one_device else torch.from_numpy(Xb).to(dev)
+                dist.all_reduce(tx)  # every rank wrote only its own poses into zeros
+                Xb = tx.cpu().numpy()
+            eng.set_X(Xb)  # PGOAgent::setX: Nesterov restarts from the burnt-in iterate
+        X_start = None
+        if rank == 0 and world == 1 and args.cpu_baseline:
+            X_start = np.zeros(X0.size)
+            eng.get_X_into(X_start)
+        f_start, gn_start = central()
+        for _ in range(args.warmup):
+            step()
+        st0 = eng.stats().copy()
+        b0, evaltcg_bytes = eng.bytes()
+        eng.kernel_times()  # drop anything recorded so far
+        eng.set_kernel_timing(args.kernel_timing)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        sync()
+        elapsed = time.perf_counter() - t0
+        eng.set_kernel_timing(0)
+        ktimes = eng.kernel_times()
+        st1 = eng.stats().copy()
+        b1, _ = eng.bytes()
+        f_end, gn_end = central()
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if one_device else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    # ---- roofline of the X.Q SpMM over one colour class (HIP events on the engine stream)
+    # ---- solver statistics over the timed region (all ranks)
+    dst = (st1 - st0).astype(np.int64)
+    sums = dst.sum(axis=0)
+    if world > 1:
+        ts = torch.tensor(sums, dtype=torch.int64, device="cpu" if one_device else dev)
+        dist.all_reduce(ts)
+        sums = ts.cpu().numpy()
+    tot = dict(zip(STATS, (int(v) for v in sums)))
+    upd = max(tot["calls"], 1)
+    tcg = {"per_update": {"runs": tot["runs"] / upd, "tcg_iters": tot["tcg_iters"] / upd,
+                          "cg_steps": tot["cg_steps"] / upd, "early_return": tot["early"] / upd},
+           "exits": {k: tot[k] for k in ("NEGCURVTURE", "EXCREGION", "LCON", "SCON", "MAXITER")},
+           "first_step_boundary_runs": tot["implicit"], "runs": tot["runs"], "updates": tot["calls"],
+           "gave_up": tot["gave_up"]}
+
+    # ---- roofline: the in-step X.Q launches timed with HIP events on the engine stream
+    per_mode = {m: {"ms_total": v[0], "launches": v[1], "avg_ms": v[0] / max(v[1], 1)} for m, v in ktimes.items()}
+    step_ms = 1e3 * elapsed / args.steps
+    ev = per_mode.get("EVAL_TCG")
+    ev_bytes = float(np.mean(evaltcg_bytes)) if len(evaltcg_bytes) else 0.0
+    achieved = ev_bytes / (ev["avg_ms"] * 1e-3) / 1e9 if ev and ev["avg_ms"] > 0 else 0.0
+    dominant = max(per_mode, key=lambda m: per_mode[m]["ms_total"]) if per_mode else None
+    step_bytes = (b1 - b0) / args.steps
+    if world > 1:
+        tb = torch.tensor([step_bytes], dtype=torch.float64, device="cpu" if one_device else dev)
+        dist.all_reduce(tb)
+        step_bytes = float(tb.item())
+    traffic = measured_traffic()
+    ev_traffic = None
+    if traffic and "kernels" in traffic:
+        ev_traffic = traffic["kernels"].get("EVAL_TCG", {}).get("traffic_bytes_per_launch")
+
+    # ---- the standalone X.Q SpMM over one colour class (the metric's "X.Q SpMM HBM GB/s")
     fmt_bytes, spmm_ms = eng.bench_spmm(0, args.spmm_reps)
     bsr_bytes, _ = eng.spmm_bytes(0)
-    achieved = bsr_bytes / (spmm_ms * 1e-3) / 1e9 if spmm_ms > 0 else 0.0
     hvp_ms = eng.bench_hvp(0, args.spmm_reps)
-    traffic = measured_traffic()
 
     agent_updates = num_agents * args.steps
     value = agent_updates / elapsed
+    if world == 1:
+        par = "1 GPU, all 64 agents on it (no exchange)"
+    elif one_device:
+        par = f"{world} ranks on ONE device (rehearsal), halo all_to_all over gloo through host copies"
+    else:
+        par = f"agents over {world} GPUs (2x2x2 super-cubes), halo all_to_all_single over RCCL/xGMI"
     out = {
         "metric": METRIC,
         "value": value,
@@ -160,7 +242,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": 1e3 * elapsed / args.steps,
+        "ms_per_step": step_ms,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -169,51 +251,48 @@ def main():
         "config": {"workload": f"grid3d k={args.k} ({args.k ** 3} poses), r={args.r}, "
                                f"{num_agents} agents ({A}^3 sub-cubes), Nesterov={bool(args.accel)}, "
                                f"{args.robust} cost, colour schedule ({eng.num_colors} colours), "
-                               f"RTR 1x10 tCG, block-Jacobi precond",
-                   "poses": g.n, "edges": g.m, "agents": num_agents,
-                   "parallelism": f"agents over {world} GPU(s), RCCL all_to_all halo"},
+                               f"RTR 1x10 tCG, block-Jacobi precond, agent status on, burn-in {args.burnin} steps",
+                   "poses": g.n, "edges": g.m, "agents": num_agents, "parallelism": par},
         "rounds_per_s": args.steps / elapsed,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic["traffic_bytes_per_launch"] if traffic else None,
-                     "kernel": "k_spmm<5,4,MODE_XQ,edge-stream> (X.Q over colour class 0 on rank 0)",
-                     "algorithmic_bytes_per_launch": bsr_bytes,
-                     "algorithmic_bytes_definition": "SURVEY 8d B_spmm = nnzb(b^2 8 + 4) + (n+1) 4 + 2 r b n 8",
-                     "avg_launch_ms": spmm_ms,
-                     "format_bytes_per_launch": fmt_bytes,
-                     "format_GBps": fmt_bytes / (spmm_ms * 1e-3) / 1e9 if spmm_ms > 0 else 0.0,
+                     "traffic": ev_traffic,
+                     "kernel": "k_spmm<5,4,MODE_EVAL_TCG,edge-stream> (in-step: f, grad, S, tCG start; every agent "
+                               "of a colour per launch)",
+                     "algorithmic_bytes_per_launch": ev_bytes,
+                     "algorithmic_bytes_definition": "SURVEY 8d: Q as b x b blocks (n + 2 m_in)(b^2 8 + 4) + (n+1) 4 "
+                                                     "+ X 160 n + S 48 n + Minv 80 n + delta 160 n + G 160 per slot",
+                     "avg_launch_ms": ev["avg_ms"] if ev else None,
+                     "launches_timed": ev["launches"] if ev else 0,
+                     "traffic_frac": (ev_traffic / (ev["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                     if (ev_traffic and ev) else None,
+                     "dominant_in_step_kernel": dominant,
+                     "in_step_spmm": per_mode,
+                     "step_level": {"algorithmic_bytes_per_step": step_bytes,
+                                    "GBps": step_bytes / (step_ms * 1e-3) / 1e9,
+                                    "frac": step_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                    "definition": "all in-step kernels: SURVEY 8d bytes x exact per-agent launch "
+                                                  "counts (dpgo_rbcd_bytes)"},
                      "traffic_source": traffic["source"] if traffic else None},
+        "xq_spmm": {"kernel": "k_spmm<5,4,MODE_XQ,edge-stream> over colour class 0 (standalone reps)",
+                    "avg_launch_ms": spmm_ms, "algorithmic_bytes_per_launch": bsr_bytes,
+                    "GBps": bsr_bytes / (spmm_ms * 1e-3) / 1e9 if spmm_ms > 0 else 0.0,
+                    "frac": bsr_bytes / (spmm_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if spmm_ms > 0 else 0.0,
+                    "format_bytes_per_launch": fmt_bytes,
+                    "traffic_bytes_per_launch": traffic.get("traffic_bytes_per_launch") if traffic else None},
         "hvp": {"per_s": 1e3 / hvp_ms if hvp_ms > 0 else 0.0, "avg_launch_ms": hvp_ms,
                 "agents": int(eng.agents_per_color[0]),
                 "what": "Riemannian HVP (EucHessianEta + EucHvToHv, tangent-projected) over colour class 0"},
+        "tcg": tcg,
+        "central": {"f_start": f_start, "gradnorm_start": gn_start, "f_end": f_end, "gradnorm_end": gn_end,
+                    "steps_between": args.warmup + args.steps},
         "setup_s": setup_s,
     }
-    if args.verify:
-        # central cost 1/2 tr(X Q X^T) of the whole graph before and after (outside the timed region):
-        # the schedule is deterministic, so the final cost must not depend on the number of ranks
-        Xf = np.zeros(X0.size)
-        eng.get_X_into(Xf)
-        if world > 1:
-            tx = torch.from_numpy(Xf) if one_device else torch.from_numpy(Xf).to(dev)
-            dist.all_reduce(tx)
-            Xf = tx.cpu().numpy()
-        if rank == 0:
-            import scipy.sparse as sp
-            rp, col, blk = g.laplacian_bsr()
-            b = g.d + 1
-            Q = sp.bsr_matrix((np.ascontiguousarray(blk.reshape(-1, b, b).transpose(0, 2, 1)), col, rp),
-                              shape=(g.n * b, g.n * b)).tocsr()
-
-            def central(flat):
-                X = H.from_dev_layout(flat, args.r)
-                return 0.5 * float(np.sum(np.asarray(Q @ X.T).T * X))
-            out["verify"] = {"f_init": central(X0), "f_final": central(Xf),
-                             "steps_run": args.warmup + args.steps}
-    if rank == 0 and world == 1 and args.cpu_baseline:
+    if X_start is not None:
         try:
             from oracle import cpu_port
-            out["cpu_baseline"] = cpu_port.baseline(g, aop, X0, args.r, bool(args.accel),
-                                                    num_agents, args.cpu_sample_updates)
+            out["cpu_baseline"] = cpu_port.baseline(g, aop, X_start, args.r, bool(args.accel), num_agents,
+                                                    args.cpu_sample_updates)
         except Exception as exc:  # reported, never silently replaced
             out["cpu_baseline"] = {"error": repr(exc)}
     if rank == 0:

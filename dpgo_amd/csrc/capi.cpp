@@ -78,6 +78,50 @@ int check_handle(dpgo_hip_problem h) {
   return DPGO_HIP_OK;
 }
 
+hipError_t pooled_event(dpgo_hip_problem h, hipEvent_t* e) {
+  if (!h->ev_pool.empty()) {
+    *e = h->ev_pool.back();
+    h->ev_pool.pop_back();
+    return hipSuccess;
+  }
+  return hipEventCreate(e);
+}
+
+}  // namespace
+
+int dpgo::spmm_launch(dpgo_hip_problem h, int mode, const LaunchCtx& c, const SpmmArgs& a) {
+  if (!h->timing || c.num_tiles == 0) {
+    HIP_TRY(dpgo::launch_spmm(h->r, h->b, mode, c, qview(h), a));
+    return DPGO_HIP_OK;
+  }
+  dpgo_hip_problem_s::TimedLaunch t{mode, nullptr, nullptr};
+  HIP_TRY(pooled_event(h, &t.a));
+  HIP_TRY(pooled_event(h, &t.b));
+  HIP_TRY(hipEventRecord(t.a, c.stream));
+  HIP_TRY(dpgo::launch_spmm(h->r, h->b, mode, c, qview(h), a));
+  HIP_TRY(hipEventRecord(t.b, c.stream));
+  h->timed.push_back(t);
+  return DPGO_HIP_OK;
+}
+
+int dpgo::take_spmm_times(dpgo_hip_problem h, double* ms, long long* launches) {
+  for (auto& t : h->timed) {
+    HIP_TRY(hipEventSynchronize(t.b));
+    float v = 0.f;
+    HIP_TRY(hipEventElapsedTime(&v, t.a, t.b));
+    if (t.mode >= 0 && t.mode < 8) {
+      ms[t.mode] += v;
+      launches[t.mode] += 1;
+    }
+    h->ev_pool.push_back(t.a);
+    h->ev_pool.push_back(t.b);
+  }
+  h->timed.clear();
+  return DPGO_HIP_OK;
+}
+
+namespace {
+
 // Edge-stream Q: per edge M = T Omega (rows padded to 4), per pose the packed diagonal block
 // (sum of T Omega T^T over outgoing and Omega over incoming edges, shared edges included, in edge
 // order with the same arithmetic as the BSR assembly), and the pose -> incident-edge lists of the
@@ -512,6 +556,10 @@ dpgo::FinalizeArgs make_fin(dpgo_hip_problem h, int op, const double* pa, int nq
   f.state = h->state.p;
   f.out_sums = h->sums.p;
   if (opt) f.opt = *opt;
+  if (h->trace_cap > 0) {
+    f.trace = h->trace.p;
+    f.trace_cap = h->trace_cap;
+  }
   return f;
 }
 
@@ -534,7 +582,7 @@ int spmm_then_finalize(dpgo_hip_problem h, int mode, const dpgo::LaunchCtx& c, d
     a.fin = fin;
     a.fin.coherent = h->fuse_finalize == 2 ? 1 : 0;
   }
-  HIP_TRY(dpgo::launch_spmm(h->r, h->b, mode, c, qview(h), a));
+  DPGO_TRY(dpgo::spmm_launch(h, mode, c, a));
   if (!fuse) HIP_TRY(dpgo::launch_finalize(fin, h->K, h->stream));
   return DPGO_HIP_OK;
 }
@@ -598,7 +646,7 @@ int eval_at(dpgo_hip_problem h, const double* X, double* gout, double* Sout, dou
   auto c = make_ctx(h, flag, part);
   const dpgo::SpmmArgs a{X, h->gidx.p, h->gblk.p, X, nullptr, gout, Sout, h->minv.p, delta, pmode};
   if (fin != nullptr) return spmm_then_finalize(h, mode, c, a, *fin);
-  HIP_TRY(dpgo::launch_spmm(h->r, h->b, mode, c, qview(h), a));
+  DPGO_TRY(dpgo::spmm_launch(h, mode, c, a));
   return DPGO_HIP_OK;
 }
 
@@ -977,9 +1025,78 @@ int dpgo_hip_synchronize(dpgo_hip_problem h) {
   return DPGO_HIP_OK;
 }
 
-// --------------------------------------------------------------------------- optimisation
+int dpgo_hip_stats(dpgo_hip_problem h, int* out) {
+  DPGO_TRY(check_handle(h));
+  if (!out) return fail(DPGO_HIP_EINVAL, "null output");
+  static_assert(DPGO_STATS_INTS == dpgo::kStatsInts, "stats width");
+  DPGO_TRY(download_state(h));
+  for (int a = 0; a < h->K; ++a) std::memcpy(out + a * dpgo::kStatsInts, &h->h_state[a].st_calls, sizeof(int) * dpgo::kStatsInts);
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_set_trace(dpgo_hip_problem h, int capacity) {
+  DPGO_TRY(check_handle(h));
+  if (capacity < 0) return fail(DPGO_HIP_EINVAL, "negative trace capacity");
+  static_assert(DPGO_TRACE_WIDTH == dpgo::kTraceWidth, "trace width");
+  if (capacity > 0) HIP_TRY(h->trace.ensure(static_cast<size_t>(h->K) * capacity * dpgo::kTraceWidth));
+  // restart every agent's record count (host round trip: a setup call)
+  DPGO_TRY(download_state(h));
+  for (auto& s : h->h_state) s.trace_n = 0;
+  HIP_TRY(hipMemcpyAsync(h->state.p, h->h_state.data(), sizeof(AgentState) * h->K, hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  h->trace_cap = capacity;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_get_trace(dpgo_hip_problem h, int agent, double* out, int max_records, int* count) {
+  DPGO_TRY(check_handle(h));
+  if (agent < 0 || agent >= h->K) return fail(DPGO_HIP_EINVAL, "agent out of range");
+  DPGO_TRY(download_state(h));
+  const int n = h->h_state[agent].trace_n;
+  if (count) *count = n;
+  const int k = std::min({n, max_records, h->trace_cap});
+  if (out && k > 0) {
+    HIP_TRY(hipMemcpyAsync(out, h->trace.p + static_cast<size_t>(agent) * h->trace_cap * dpgo::kTraceWidth,
+                           sizeof(double) * k * dpgo::kTraceWidth, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+  }
+  return DPGO_HIP_OK;
+}
+
+#ifndef DPGO_SOURCE_HASH
+#define DPGO_SOURCE_HASH "unknown"
+#endif
+const char* dpgo_hip_build_id(void) { return DPGO_SOURCE_HASH; }
+
 int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, const double* X_in,
                           double* X_out, const int* agent_enabled_host, dpgo_opt_result* results) {
+  return dpgo::optimize_dev_status(h, params, X_in, X_out, agent_enabled_host, results, nullptr);
+}
+
+}  // extern "C"
+
+namespace {
+// PGOAgent status pass (src/PGOAgent.cpp:700-716): |X_out - XPrev|^2 per agent, then OP_STATUS.
+// pa already holds |X_out - st->ref|^2 when `have_partials` (the final select compared against ref).
+int status_pass(dpgo_hip_problem h, const double* X_out, const dpgo::StatusArgs& st, const dpgo::OptScalars& o0,
+                bool have_partials) {
+  if (!have_partials) {
+    auto c = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
+    HIP_TRY(dpgo::launch_sqdiff(h->r, h->b, c, X_out, st.ref));
+  }
+  dpgo::OptScalars o = o0;
+  o.rel_tol = st.rel_tol;
+  o.min_ratio = st.min_ratio;
+  dpgo::FinalizeArgs f = make_fin(h, dpgo::OP_STATUS, h->pa.p, 1, nullptr, 0, &o);
+  f.conv_ratio = st.conv_ratio;
+  HIP_TRY(dpgo::launch_finalize(f, h->K, h->stream));
+  return DPGO_HIP_OK;
+}
+}  // namespace
+
+// --------------------------------------------------------------------------- optimisation
+int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params, const double* X_in, double* X_out,
+                              const int* agent_enabled_host, dpgo_opt_result* results, const StatusArgs* st) {
   DPGO_TRY(ready(h));
   dpgo_opt_params P;
   if (params)
@@ -1025,8 +1142,10 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
   // first tCG start (delta = -Prec(grad), <z, grad>) is fused into the same pass
   const bool fused_tcg = P.algorithm == DPGO_ALG_RTR && P.tr_max_inner > 0 && !exact;
   // grad(x1) itself is only read by a CG step (r = grad + alpha Hdelta), a retry Run or the explicit
-  // <g, eta>: when the first step is predicted to stop every agent (single Run), it is not stored and
-  // is recomputed in the rare case it is needed
+  // <g, eta>: when the previous call's first step stopped every agent (single Run), it is not stored
+  // and is recomputed, by the same MODE_EVAL_TCG pass (bitwise the same g), if it is needed.  This
+  // only chooses between storing and recomputing identical values: no result depends on it, so an
+  // agent's arithmetic does not depend on which other agents share its handle.
   bool g_valid = !(fused_tcg && single && h->predict_boundary && P.tr_max_inner > 0);
   if (fused_tcg) {
     const dpgo::FinalizeArgs fin = make_fin(h, dpgo::OP_EVAL_TCG_INIT, h->pa.p, 3, nullptr, 0, &o, en_dev);
@@ -1041,13 +1160,21 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
     // one fixed-step Riemannian gradient step (QuadraticOptimizer::gradientDescent :124-149)
     auto cr = make_ctx(h, dpgo::FLAG_NONE, h->pb.p);
     HIP_TRY(dpgo::launch_retract(r, b, cr, x1, h->g.p, -P.rgd_stepsize, h->x2.p, nullptr, nullptr));
-    DPGO_TRY(eval_at(h, h->x2.p, h->g2.p, h->S2.p, h->pb.p, dpgo::FLAG_NONE));
+    HIP_TRY(hipMemcpyAsync(h->use_a.p, en.data(), sizeof(int) * K, hipMemcpyHostToDevice, h->stream));
+    // X_in may alias X_out (in-place update): the candidate stays in x2 until the select
+    auto cs = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
+    const bool want = results != nullptr || P.verbose;
+    if (st && st->ref == X_in && !want) {  // one pass: X_out = x2 and |X_out - XPrev|^2
+      HIP_TRY(dpgo::launch_select(r, b, cs, h->x2.p, x1, h->use_a.p, x1, X_out));
+      return status_pass(h, X_out, *st, o, true);
+    }
+    HIP_TRY(dpgo::launch_select(r, b, cs, h->x2.p, x1, h->use_a.p, x1, X_out));
+    if (want) DPGO_TRY(finalize(h, dpgo::OP_REL_CHANGE, h->pa.p, 1, nullptr, 0));
+    if (st) DPGO_TRY(status_pass(h, X_out, *st, o, false));
+    if (!want) return DPGO_HIP_OK;
+    DPGO_TRY(eval_at(h, X_out, h->g2.p, h->S2.p, h->pb.p, dpgo::FLAG_NONE));
     DPGO_TRY(finalize(h, dpgo::OP_SUM, h->pb.p, 2, nullptr, 0));
     DPGO_TRY(download_sums(h));
-    HIP_TRY(hipMemcpyAsync(h->use_a.p, en.data(), sizeof(int) * K, hipMemcpyHostToDevice, h->stream));
-    auto cs = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
-    HIP_TRY(dpgo::launch_select(r, b, cs, h->x2.p, x1, h->use_a.p, x1, X_out));
-    DPGO_TRY(finalize(h, dpgo::OP_REL_CHANGE, h->pa.p, 1, nullptr, 0));
     DPGO_TRY(download_state(h));
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - t0).count();
     if (results) {
@@ -1083,7 +1210,7 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
     // ---- truncated CG (A.4)
     if (round > 0 || !fused_tcg) {
       if (!g_valid) {  // a retry Run restarts tCG from grad(x1), which EVAL_TCG did not store
-        DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_RUN));
+        DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_RUN, dpgo::MODE_EVAL_TCG, h->delta.p, pmode));
         g_valid = true;
       }
       if (exact) {  // delta = -P_X(g P^-1), partials <z, g>, |g|^2
@@ -1122,11 +1249,11 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
       }
       return DPGO_HIP_OK;
     };
-    // First step: when the previous call's first step stopped every agent (predict_boundary), only
-    // d_Hd is evaluated (MODE_QF: each edge once, no Hess[delta] vector).  A boundary / negative-
-    // curvature exit needs nothing more (eta = tau delta stays implicit, <eta, Heta> = tau^2 d_Hd);
-    // agents that take a CG step get Hess[delta] from a HESS pass over their tiles only.
-    const bool qf0 = h->predict_boundary && !exact && P.tr_max_inner > 0;
+    // First step: only d_Hd is evaluated (MODE_QF: each edge once, no Hess[delta] vector).  A
+    // boundary / negative-curvature exit needs nothing more (eta = tau delta stays implicit, <eta, Heta>
+    // = tau^2 d_Hd); agents that take a CG step get Hess[delta] from a HESS pass over their tiles only.
+    // Always the same formula for the first d_Hd, so an agent's result does not depend on the batch.
+    const bool qf0 = !exact && P.tr_max_inner > 0;
     // Single Run: the candidate, f(x2) and the rho test of the agents whose first step already ended
     // tCG are queued right behind the step test, before the host learns whether any agent continues
     // (those are retracted, evaluated and tested after their tCG: the *_EXPL launches below).
@@ -1166,11 +1293,12 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
       }
       if (!act) break;
       if (j == 0 && qf0) {
-        if (!g_valid)  // the CG-step agents' gradient (EVAL_TCG skipped storing it)
-          DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_TCG_CG));
+        if (!g_valid)  // the CG-step agents' gradient (EVAL_TCG skipped storing it; same pass again)
+          DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_TCG_CG, dpgo::MODE_EVAL_TCG, h->delta.p, pmode));
         auto cg = make_ctx(h, dpgo::FLAG_TCG_CG, h->pb.p);
-        HIP_TRY(dpgo::launch_spmm(r, b, dpgo::MODE_HESS, cg, qview(h), h->delta.p, nullptr, nullptr, x1, h->S.p,
-                                  h->Hdelta.p, nullptr));
+        DPGO_TRY(dpgo::spmm_launch(h, dpgo::MODE_HESS, cg,
+                                   dpgo::SpmmArgs{h->delta.p, nullptr, nullptr, x1, h->S.p, h->Hdelta.p, nullptr,
+                                                  nullptr, nullptr, dpgo::PRECON_NONE}));
         DPGO_TRY(launch_rest(0));
       }
       if (launched < P.tr_max_inner) {  // lookahead: iteration j+1 queued while j's update runs
@@ -1215,8 +1343,16 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
     HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(h->use_a.p), 1, K, h->stream));
     HIP_TRY(dpgo::launch_select(r, b, cs, x1, X_in, h->use_a.p, X_in, X_out));
   }
-  if (!results && !P.verbose) return DPGO_HIP_OK;  // no host round trip needed
-  DPGO_TRY(finalize(h, dpgo::OP_REL_CHANGE, h->pa.p, 1, nullptr, 0));
+  const bool want = results != nullptr || P.verbose;
+  // QuadraticOptimizer relativeChange against the input (the last select's partials, ref X_in)
+  if (want) DPGO_TRY(finalize(h, dpgo::OP_REL_CHANGE, h->pa.p, 1, nullptr, 0));
+  if (st) {
+    // the last select (FLAG_NONE over every tile, ref X_in) left |X_out - X_in|^2 in pa: reuse it
+    // when the status reference is X_in itself (an in-place update without acceleration)
+    const bool reuse = st->ref == X_in && !direct;
+    DPGO_TRY(status_pass(h, X_out, *st, o, reuse));
+  }
+  if (!want) return DPGO_HIP_OK;  // no host round trip needed
   DPGO_TRY(download_state(h));
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::high_resolution_clock::now() - t0).count();
   if (results) {
@@ -1234,6 +1370,21 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
   }
   return DPGO_HIP_OK;
 }
+
+int dpgo::eval_sums_dev(dpgo_hip_problem h, const double* X) {
+  DPGO_TRY(ready(h));
+  DPGO_TRY(ensure_work(h));
+  DPGO_TRY(eval_at(h, X, nullptr, nullptr, h->pa.p, dpgo::FLAG_NONE));
+  return finalize(h, dpgo::OP_SUM, h->pa.p, 3, nullptr, 0);
+}
+
+int dpgo::download_sums_public(dpgo_hip_problem h, std::vector<double>& out) {
+  DPGO_TRY(download_sums(h));
+  out = h->h_sums;
+  return DPGO_HIP_OK;
+}
+
+extern "C" {
 
 // ------------------------------------------------------------------ host-pointer variants
 namespace {

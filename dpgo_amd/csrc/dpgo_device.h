@@ -38,8 +38,21 @@ struct AgentState {
   int copy_pending;  // multi-iteration Run: accepted step still to be copied into x1
   int eta_implicit;  // tCG stopped at its first step on the boundary: eta = step delta, Heta = step Hdelta
                      // are not materialised (k_retract reads delta; g_eta / eta_Heta set by OP_TCG_STEP)
-  int pad2;
+  int ready;         // PGOAgentStatus::readyToTerminate of the last update (OP_STATUS)
+  double status_rel_change;  // PGOAgentStatus::relativeChange = |X - XPrev| / sqrt(n) (OP_STATUS)
+  // cumulative statistics since the handle was created (never reset; read by dpgo_hip_stats)
+  int st_calls;      // optimize calls in which the agent was enabled
+  int st_early;      // ... that returned at once (|grad| < tol, src/QuadraticOptimizer.cpp:68-70)
+  int st_runs;       // RTR Runs (radius-shrink retries included)
+  int st_tcg_iters;  // tCG inner iterations over all Runs
+  int st_status[5];  // tCG exits per TcgStatus over all Runs
+  int st_gave_up;    // updates that gave up after 12 rejected Runs
+  int st_cg_steps;   // tCG step tests that took a CG step (alpha)
+  int st_implicit;   // Runs whose tCG ended at its first step on the boundary (eta implicit)
+  int trace_n;       // per-iteration trace records written (FinalizeArgs::trace)
+  int pad3;
 };
+constexpr int kStatsInts = 12;  // st_calls .. st_implicit, contiguous
 
 // ---- DPP quad helpers -------------------------------------------------------------------
 template <int CTRL>

@@ -29,7 +29,20 @@ enum FinalizeOp {
   OP_RHO = 5,
   OP_REL_CHANGE = 6,
   OP_SUM = 7,
-  OP_EVAL_TCG_INIT = 8  // OP_EVAL_INIT then OP_TCG_INIT from one fused pass (f, |g|^2, <z,g>)
+  OP_EVAL_TCG_INIT = 8,  // OP_EVAL_INIT then OP_TCG_INIT from one fused pass (f, |g|^2, <z,g>)
+  OP_STATUS = 9          // PGOAgent status: relativeChange = sqrt(|X - XPrev|^2 / n), readyToTerminate
+};
+
+// Per-iteration trace (ROPTLIB ITERRESULT, src/QuadraticOptimizer.cpp:82-86): one record of
+// kTraceWidth doubles per tCG step test, tCG stopping test and rho test, per agent.
+constexpr int kTraceWidth = 16;
+enum TraceField {
+  TR_OP = 0,       // FinalizeOp that wrote the record (OP_TCG_STEP / OP_TCG_CHECK / OP_RHO)
+  TR_J = 1,        // tCG iteration index (0-based) / RTR outer iteration
+  TR_F1 = 2, TR_F2 = 3, TR_RHO = 4, TR_DELTA = 5,
+  TR_ALPHA = 6, TR_BETA = 7, TR_TAU = 8, TR_DHD = 9, TR_NORM_R = 10, TR_ZR = 11,
+  TR_STATUS = 12,  // tCG status when the record ends tCG / the Run, else -1
+  TR_ACCEPTED = 13, TR_NGF = 14, TR_RUN = 15
 };
 
 // Tile set + per-agent state for one launch.
@@ -74,6 +87,7 @@ struct QView {
 
 struct OptScalars {
   double tol, Delta0, Delta_max, theta, kappa;
+  double rel_tol, min_ratio;  // OP_STATUS: PGOAgentParameters relChangeTol, robustOptMinConvergenceRatio
   int min_inner, max_iter, single_run, pad;
 };
 
@@ -94,6 +108,9 @@ struct FinalizeArgs {
   int pub_kind;                 // 1: tcg_active, 2: run_active
   int agent_filter;             // 0: every agent; 1 / 2: only agents whose eta is / is not implicit
   int coherent;                 // read the partials with agent-scope loads (fused, SpmmArgs::fin_mode 2)
+  const double* conv_ratio;     // OP_STATUS: per-agent converged loop-closure ratio (nullptr = 1)
+  double* trace;                // per-iteration records [agent][trace_cap][kTraceWidth] (nullptr = off)
+  int trace_cap;
 };
 
 // SpMM modes that can run a fused finalize (SpmmArgs::fin_arrive); the others ignore it.
@@ -195,11 +212,18 @@ hipError_t launch_retract(int r, int b, const LaunchCtx& c, const double* X, con
 hipError_t launch_tangent(int r, int b, const LaunchCtx& c, const double* X, const double* V, double* out);
 hipError_t launch_precond(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
                           const double* V, double* out);
+// xcopy (optional): the X operand as read (PGOAgent::iterate's XPrev = X, src/PGOAgent.cpp:673)
 hipError_t launch_polar_vnext(int r, int b, const LaunchCtx& c, const double* X, double* V, const double* Yv,
-                              double gv, double sa, double sb, double* out);
+                              double gv, double sa, double sb, double* out, double* xcopy = nullptr);
 hipError_t launch_polar_comb(int r, int b, const LaunchCtx& c, const double* A, const double* Bv,
                              const double* ca, const double* cb, double* out, const double* Cv = nullptr,
-                             double sa = 1.0, double sb = 0.0, double* out2 = nullptr);
+                             double sa = 1.0, double sb = 0.0, double* out2 = nullptr, double* xcopy = nullptr);
+// PGOAgent::computeConvergedLoopClosureRatio (src/PGOAgent.cpp:1247-1289): per agent a, the share of
+// its loop closures idx[off[a] .. off[a+1]) whose weight w[] is exactly 1 or 0 (0/0 = NaN, as there)
+hipError_t launch_conv_ratio(int num_agents, const int* off, const int* idx, const double* w, double* ratio,
+                             hipStream_t stream);
+// partial |A - B|^2 per tile (no output vector)
+hipError_t launch_sqdiff(int r, int b, const LaunchCtx& c, const double* A, const double* Bv);
 hipError_t launch_select(int r, int b, const LaunchCtx& c, const double* A, const double* Bv, const int* use_a,
                          const double* ref, double* out);
 hipError_t launch_accept(int r, int b, const LaunchCtx& c, const double* x2, const double* g2, const double* S2,

@@ -523,8 +523,13 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
         double parts[3] = {own ? fpart : 0.0, own ? gpart : 0.0, own ? zr : 0.0};
         block_partials<3>(parts, c.partials, p.tile, args.fin_mode == 2);
       } else {
-        double parts[2] = {own ? fpart : 0.0, own ? gpart : 0.0};
-        block_partials<2>(parts, c.partials, p.tile, args.fin_mode == 2);
+        // third partial <G, X>: the central cost of a partitioned graph is sum_agents f - <G, X> / 2
+        // (each shared edge's cross term enters both endpoint agents' linear terms)
+        double gx = 0.0;
+#pragma unroll
+        for (int a = 0; a < R; ++a) gx = fma(gcol[a], xcol[a], gx);
+        double parts[3] = {own ? fpart : 0.0, own ? gpart : 0.0, own ? gx : 0.0};
+        block_partials<3>(parts, c.partials, p.tile, args.fin_mode == 2);
       }
     }
   } else if constexpr (MODE == MODE_CERT) {
@@ -839,7 +844,8 @@ __global__ __launch_bounds__(64) void k_polar_comb(LaunchCtx c, const double* __
                                                    const double* __restrict__ cb,
                                                    double* __restrict__ out,
                                                    const double* __restrict__ Cv, double sa,
-                                                   double sb, double* __restrict__ out2) {
+                                                   double sb, double* __restrict__ out2,
+                                                   double* __restrict__ xcopy) {
   constexpr int D = B - 1;
   constexpr int PW = R * B;
   constexpr int PS = PW + 1;
@@ -868,6 +874,11 @@ __global__ __launch_bounds__(64) void k_polar_comb(LaunchCtx c, const double* __
     double2 va[NV], vb[NV], vc[NV];
 #pragma unroll
     for (int i = 0; i < NV; ++i) va[i] = A2[t + 64 * i];
+    if (xcopy != nullptr) {  // XPrev = X (the A operand), written from the registers just loaded
+      double2* XC = reinterpret_cast<double2*>(xcopy + base);
+#pragma unroll
+      for (int i = 0; i < NV; ++i) XC[t + 64 * i] = va[i];
+    }
     if (Bv != nullptr) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) vb[i] = B2[t + 64 * i];
@@ -884,8 +895,11 @@ __global__ __launch_bounds__(64) void k_polar_comb(LaunchCtx c, const double* __
       dst[1] = comb(va[i].y, Bv ? vb[i].y : 0.0, Cv ? vc[i].y : 0.0);
     }
   } else {
-    for (int x = t; x < total; x += 64)
-      sm[(x / PW) * PS + x % PW] = comb(A[base + x], Bv ? Bv[base + x] : 0.0, Cv ? Cv[base + x] : 0.0);
+    for (int x = t; x < total; x += 64) {
+      const double av = A[base + x];
+      if (xcopy != nullptr) xcopy[base + x] = av;
+      sm[(x / PW) * PS + x % PW] = comb(av, Bv ? Bv[base + x] : 0.0, Cv ? Cv[base + x] : 0.0);
+    }
   }
   __syncthreads();
   if (t < count) {
@@ -938,7 +952,8 @@ __global__ __launch_bounds__(64) void k_polar_comb(LaunchCtx c, const double* __
 template <int R, int B>
 __global__ __launch_bounds__(64) void k_polar_vnext(LaunchCtx c, const double* __restrict__ X,
                                                     double* __restrict__ V, const double* __restrict__ Yv,
-                                                    double gv, double sa, double sb, double* __restrict__ out) {
+                                                    double gv, double sa, double sb, double* __restrict__ out,
+                                                    double* __restrict__ xcopy) {
   constexpr int D = B - 1;
   constexpr int PW = R * B;
   constexpr int PS = PW + 1;
@@ -976,6 +991,11 @@ __global__ __launch_bounds__(64) void k_polar_vnext(LaunchCtx c, const double* _
     double2 vx[NV], vv[NV], vy[NV];
 #pragma unroll
     for (int i = 0; i < NV; ++i) vx[i] = X2[t + 64 * i];
+    if (xcopy != nullptr) {
+      double2* XC = reinterpret_cast<double2*>(xcopy + base);
+#pragma unroll
+      for (int i = 0; i < NV; ++i) XC[t + 64 * i] = vx[i];
+    }
 #pragma unroll
     for (int i = 0; i < NV; ++i) vv[i] = V2[t + 64 * i];
 #pragma unroll
@@ -1011,8 +1031,10 @@ __global__ __launch_bounds__(64) void k_polar_vnext(LaunchCtx c, const double* _
       O2[t + 64 * i] = make_double2(src[0], src[1]);
     }
   } else {
-    for (int x = t; x < total; x += 64)
+    for (int x = t; x < total; x += 64) {
+      if (xcopy != nullptr) xcopy[base + x] = X[base + x];
       sm[(x / PW) * PS + x % PW] = V[base + x] + gv * (X[base + x] - Yv[base + x]);
+    }
     __syncthreads();
     project_span();
     __syncthreads();
@@ -1061,6 +1083,26 @@ __global__ __launch_bounds__(kThreads) void k_select(LaunchCtx c, const double* 
   block_partials<1>(parts, c.partials, p.tile);
 }
 
+// partial |A - B|^2 per tile (PGOAgent status relativeChange against XPrev, src/PGOAgent.cpp:707)
+template <int R, int B>
+__global__ __launch_bounds__(kThreads) void k_sqdiff(LaunchCtx c, const double* __restrict__ A,
+                                                     const double* __restrict__ Bv) {
+  const PoseLane p = pose_lane<B>(c);
+  if (tile_skipped(c, p.agent)) return;
+  const bool own = p.ok && p.k < B;
+  const long off = p.j * (R * B) + p.k * R;
+  double dd = 0.0;
+  if (own) {
+#pragma unroll
+    for (int a = 0; a < R; ++a) {
+      const double df = A[off + a] - Bv[off + a];
+      dd = fma(df, df, dd);
+    }
+  }
+  double parts[1] = {dd};
+  block_partials<1>(parts, c.partials, p.tile);
+}
+
 // accepted RTR step in a multi-iteration Run: x1 <- x2, g <- g2, S <- S2
 template <int R, int B>
 __global__ __launch_bounds__(kThreads) void k_accept(LaunchCtx c, const double* __restrict__ x2,
@@ -1088,6 +1130,28 @@ __global__ __launch_bounds__(kThreads) void k_accept(LaunchCtx c, const double* 
 // Per-agent finalize: reduce tile partials in a fixed order, run the scalar logic of the
 // RTR / tCG state machine (A.4) on device.
 // ------------------------------------------------------------------------------------------
+// Next per-iteration trace record of the agent (zeroed, status -1), or nullptr when tracing is off or
+// the agent's buffer is full (trace_n still counts, so the host sees the overflow).
+__device__ __forceinline__ double* trace_record(const FinalizeArgs& f, int agent, AgentState& s, int op) {
+  if (f.trace == nullptr) return nullptr;
+  const int i = s.trace_n++;
+  if (i >= f.trace_cap) return nullptr;
+  double* t = f.trace + (static_cast<long>(agent) * f.trace_cap + i) * kTraceWidth;
+#pragma unroll
+  for (int q = 0; q < kTraceWidth; ++q) t[q] = 0.0;
+  t[TR_OP] = op;
+  t[TR_STATUS] = -1.0;
+  return t;
+}
+
+// Cumulative statistics at the start of an optimize call (OP_EVAL_INIT / OP_EVAL_TCG_INIT).
+__device__ __forceinline__ void count_call(const FinalizeArgs& f, int agent, AgentState& s) {
+  const bool en = f.agent_enabled ? f.agent_enabled[agent] != 0 : true;
+  if (!en) return;
+  s.st_calls += 1;
+  if (!s.run_active) s.st_early += 1;
+}
+
 // The RTR / tCG scalar logic of one agent on its reduced partials tot[] (one thread).
 __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent, const double (&tot)[4],
                                                 AgentState& s) {
@@ -1105,6 +1169,7 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       s.Delta = o.Delta0;
       s.Delta_max = o.Delta_max;
       s.run_active = f.agent_enabled ? (f.agent_enabled[agent] != 0 && !(s.ngf < o.tol)) : !(s.ngf < o.tol);
+      count_call(f, agent, s);
       s.accepted = 0;
       s.runs = 0;
       s.outer_iters = 0;
@@ -1131,6 +1196,7 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       s.Delta = o.Delta0;
       s.Delta_max = o.Delta_max;
       s.run_active = f.agent_enabled ? (f.agent_enabled[agent] != 0 && !(s.ngf < o.tol)) : !(s.ngf < o.tol);
+      count_call(f, agent, s);
       s.accepted = 0;
       s.runs = 0;
       s.outer_iters = 0;
@@ -1183,6 +1249,14 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       const double D2 = s.Delta * s.Delta;
       s.alpha = alpha;
       s.tcg_iters += 1;
+      double* tr = trace_record(f, agent, s, OP_TCG_STEP);
+      if (tr) {
+        tr[TR_J] = s.tcg_iters - 1;
+        tr[TR_DHD] = d_Hd;
+        tr[TR_ALPHA] = alpha;
+        tr[TR_DELTA] = s.Delta;
+        tr[TR_RUN] = s.runs;
+      }
       if (d_Hd <= 0.0 || e_Pe_new >= D2) {
         const double tau = (-s.e_Pd + sqrt(s.e_Pd * s.e_Pd + s.d_Pd * (D2 - s.e_Pe))) / s.d_Pd;
         s.tau = tau;
@@ -1190,6 +1264,10 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
         s.tcg_mode = 1;
         s.tcg_status = d_Hd <= 0.0 ? TCG_NEGCURVTURE : TCG_EXCREGION;
         s.tcg_active = 0;
+        if (tr) {
+          tr[TR_TAU] = tau;
+          tr[TR_STATUS] = s.tcg_status;
+        }
         if (s.tcg_iters == 1) {
           // first step on the boundary (the common RBCD case): eta = tau delta and Heta = tau Hdelta
           // stay implicit.  delta = -z, so <g, eta> = -tau <z, g> and <eta, Heta> = tau^2 <delta, Hdelta>
@@ -1197,11 +1275,13 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
           s.eta_implicit = 1;
           s.g_eta = -tau * s.z_r;
           s.eta_Heta = tau * tau * d_Hd;
+          s.st_implicit += 1;
         }
       } else {
         s.e_Pe = e_Pe_new;
         s.step = alpha;
         s.tcg_mode = 0;
+        s.st_cg_steps += 1;
       }
       break;
     }
@@ -1210,13 +1290,24 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       const double norm_r = sqrt(tot[1]);
       const int j = s.tcg_iters - 1;
       const double r0t = pow(s.norm_r0, o.theta);
+      double* tr = trace_record(f, agent, s, OP_TCG_CHECK);
+      if (tr) {
+        tr[TR_J] = j;
+        tr[TR_NORM_R] = norm_r;
+        tr[TR_RUN] = s.runs;
+      }
       if (j >= o.min_inner && norm_r <= s.norm_r0 * fmin(r0t, o.kappa)) {
         s.tcg_status = o.kappa < r0t ? TCG_LCON : TCG_SCON;
         s.tcg_active = 0;
+        if (tr) tr[TR_STATUS] = s.tcg_status;
         break;
       }
       const double z_r_new = tot[0];
       const double beta = z_r_new / s.z_r;
+      if (tr) {
+        tr[TR_ZR] = z_r_new;
+        tr[TR_BETA] = beta;
+      }
       s.beta = beta;
       s.e_Pd = beta * (s.e_Pd + s.alpha * s.d_Pd);
       s.d_Pd = z_r_new + beta * beta * s.d_Pd;
@@ -1236,6 +1327,22 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       const double denom = -s.g_eta - 0.5 * s.eta_Heta;
       s.rho = (s.f1 - s.f2) / denom;
       s.accepted = s.rho > 0.1 ? 1 : 0;
+      double* tr = trace_record(f, agent, s, OP_RHO);
+      if (tr) {
+        tr[TR_J] = s.outer_iters;
+        tr[TR_F1] = s.f1;
+        tr[TR_F2] = s.f2;
+        tr[TR_RHO] = s.rho;
+        tr[TR_DELTA] = s.Delta;
+        tr[TR_ACCEPTED] = s.accepted;
+        tr[TR_NGF] = s.ngf;
+        tr[TR_STATUS] = s.tcg_status;
+        tr[TR_RUN] = s.runs;
+        tr[TR_ALPHA] = s.tcg_iters;  // inner iterations of this Run
+      }
+      s.st_runs += 1;
+      s.st_tcg_iters += s.tcg_iters;
+      if (s.tcg_status >= 0 && s.tcg_status < 5) s.st_status[s.tcg_status] += 1;
       if (s.rho < 0.25) {
         s.Delta = 0.25 * s.Delta;
       } else if (s.rho > 0.75 && (s.tcg_status == TCG_EXCREGION || s.tcg_status == TCG_NEGCURVTURE)) {
@@ -1251,6 +1358,7 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
         } else if (s.runs - 1 > 10) {
           s.gave_up = 1;
           s.run_active = 0;
+          s.st_gave_up += 1;
         } else {
           const double radius = s.Delta_max / 4.0;
           s.Delta = radius;
@@ -1267,6 +1375,13 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
     }
     case OP_REL_CHANGE: {
       s.rel_change = sqrt(tot[0] / static_cast<double>(f.agent_num_poses[agent]));
+      break;
+    }
+    case OP_STATUS: {  // PGOAgent::iterate status (src/PGOAgent.cpp:700-716), tot[0] = |X - XPrev|^2
+      const double rc = sqrt(tot[0] / static_cast<double>(f.agent_num_poses[agent]));
+      const double ratio = f.conv_ratio ? f.conv_ratio[agent] : 1.0;
+      s.status_rel_change = rc;
+      s.ready = (rc > o.rel_tol || ratio < o.min_ratio) ? 0 : 1;
       break;
     }
     case OP_SUM: {
@@ -1595,6 +1710,33 @@ __global__ __launch_bounds__(kThreads) void k_gnc_weights(GncEntries g, const do
   if (g.g_entry[e] >= 0) w_g[g.g_entry[e]] = w;
 }
 
+// One block per agent: converged (w == 1 or w == 0) over all loop closures of the agent.
+__global__ __launch_bounds__(kThreads) void k_conv_ratio(const int* __restrict__ off, const int* __restrict__ idx,
+                                                         const double* __restrict__ w, double* __restrict__ ratio) {
+  __shared__ int cnt[2];
+  const int a = blockIdx.x;
+  if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  int conv = 0;
+  for (int i = off[a] + threadIdx.x; i < off[a + 1]; i += kThreads) {
+    const double v = w[idx[i]];
+    conv += (v == 1.0 || v == 0.0) ? 1 : 0;
+  }
+  atomicAdd(&cnt[0], conv);  // integer sums: order-independent
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double total = static_cast<double>(off[a + 1] - off[a]);
+    ratio[a] = static_cast<double>(cnt[0]) / total;
+  }
+}
+
+hipError_t launch_conv_ratio(int num_agents, const int* off, const int* idx, const double* w, double* ratio,
+                             hipStream_t stream) {
+  if (num_agents == 0) return hipSuccess;
+  k_conv_ratio<<<num_agents, kThreads, 0, stream>>>(off, idx, w, ratio);
+  return hipGetLastError();
+}
+
 // w per slot (scatter of the edge-order weights) for the diagonal pass
 __global__ __launch_bounds__(kThreads) void k_weights_to_slots(int m, const int* __restrict__ slot_of_edge,
                                                                const double* __restrict__ w,
@@ -1900,16 +2042,23 @@ hipError_t launch_precond(int r, int b, const LaunchCtx& c, const double* X, con
 
 hipError_t launch_polar_comb(int r, int b, const LaunchCtx& c, const double* A, const double* Bv,
                              const double* ca, const double* cb, double* out, const double* Cv, double sa,
-                             double sb, double* out2) {
+                             double sb, double* out2, double* xcopy) {
   if (c.num_tiles == 0) return hipSuccess;
-  DPGO_DISPATCH(r, b, (k_polar_comb<R, B><<<c.num_tiles, 64, 0, c.stream>>>(c, A, Bv, ca, cb, out, Cv, sa, sb, out2)));
+  DPGO_DISPATCH(r, b, (k_polar_comb<R, B><<<c.num_tiles, 64, 0, c.stream>>>(c, A, Bv, ca, cb, out, Cv, sa, sb, out2,
+                                                                             xcopy)));
   return hipGetLastError();
 }
 
 hipError_t launch_polar_vnext(int r, int b, const LaunchCtx& c, const double* X, double* V, const double* Yv,
-                              double gv, double sa, double sb, double* out) {
+                              double gv, double sa, double sb, double* out, double* xcopy) {
   if (c.num_tiles == 0) return hipSuccess;
-  DPGO_DISPATCH(r, b, (k_polar_vnext<R, B><<<c.num_tiles, 64, 0, c.stream>>>(c, X, V, Yv, gv, sa, sb, out)));
+  DPGO_DISPATCH(r, b, (k_polar_vnext<R, B><<<c.num_tiles, 64, 0, c.stream>>>(c, X, V, Yv, gv, sa, sb, out, xcopy)));
+  return hipGetLastError();
+}
+
+hipError_t launch_sqdiff(int r, int b, const LaunchCtx& c, const double* A, const double* Bv) {
+  if (c.num_tiles == 0) return hipSuccess;
+  DPGO_DISPATCH(r, b, (k_sqdiff<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, A, Bv)));
   return hipGetLastError();
 }
 

@@ -132,6 +132,25 @@ struct dpgo_hip_problem_s {
   // (MODE_QF) and forms Hess[delta] only for agents that turn out to take a CG step
   bool predict_boundary = true;
   std::vector<double> h_sums;
+  // per-iteration trace (dpgo_hip_set_trace): [K][trace_cap][kTraceWidth] doubles
+  dpgo::DevBuf<double> trace;
+  int trace_cap = 0;
+  // in-step SpMM timing (dpgo_rbcd_set_kernel_timing): HIP events around every X.Q launch on the
+  // handle's stream, resolved per mode by take_spmm_times()
+  bool timing = false;
+  struct TimedLaunch {
+    int mode;
+    hipEvent_t a, b;
+  };
+  std::vector<TimedLaunch> timed;
+  std::vector<hipEvent_t> ev_pool;
+  ~dpgo_hip_problem_s() {
+    for (auto& t : timed) {
+      (void)hipEventDestroy(t.a);
+      (void)hipEventDestroy(t.b);
+    }
+    for (auto e : ev_pool) (void)hipEventDestroy(e);
+  }
 
   size_t vec_len() const { return static_cast<size_t>(N) * r * b; }
   size_t vec_bytes() const { return vec_len() * sizeof(double); }
@@ -144,4 +163,23 @@ namespace dpgo {
 LaunchCtx make_ctx(dpgo_hip_problem h, int flag_kind, double* partials);
 int problem_ready(dpgo_hip_problem h);
 int ensure_work_public(dpgo_hip_problem h);
+
+// PGOAgent status after an update (src/PGOAgent.cpp:700-716): relativeChange of X_out against ref
+// (XPrev), readyToTerminate with the converged loop-closure ratio per agent (nullptr = 1).
+struct StatusArgs {
+  const double* ref;
+  const double* conv_ratio;
+  double rel_tol, min_ratio;
+};
+// dpgo_hip_optimize_dev + the status pass (st may be null)
+int optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params, const double* X_in, double* X_out,
+                        const int* agent_enabled_host, dpgo_opt_result* results, const StatusArgs* st);
+// f / |grad|^2 / <G, X> per agent at X into the handle's sums (OP_SUM, nq 3): asynchronous
+int eval_sums_dev(dpgo_hip_problem h, const double* X);
+// copy the per-agent sums (4 per agent) to the host (synchronises)
+int download_sums_public(dpgo_hip_problem h, std::vector<double>& out);
+// X.Q launch with the handle's optional event timing
+int spmm_launch(dpgo_hip_problem h, int mode, const LaunchCtx& c, const SpmmArgs& a);
+// synchronise and add the elapsed ms / launch counts of the timed launches per SpmmMode (8 modes)
+int take_spmm_times(dpgo_hip_problem h, double* ms_per_mode, long long* launches_per_mode);
 }  // namespace dpgo

@@ -26,19 +26,42 @@ struct dpgo_rbcd_s {
   std::vector<long> own_pose_off;         // [owned + 1] pose offsets into owned buffers
   long Nown = 0;
   std::vector<int> own_global;            // owned buffer pose index -> global pose id
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;           // launch stream (the caller's after dpgo_rbcd_set_stream)
+  hipStream_t own_stream = nullptr;       // created and destroyed by the engine
   std::vector<dpgo_hip_problem> prob;     // per colour (nullptr if none owned)
   DevBuf<double> X, Y, V, Xprev;
-  // exchange
+  // exchange: the public poses' X only.  With Nesterov a receiver uses its neighbours' aux poses
+  // (constructGMatrix(neighborAuxPoseDict)), but those neighbours ran iterate(false) this iteration,
+  // so their Y equals their X: one copy serves both dictionaries.
   std::vector<long long> send_counts, recv_counts, send_off, recv_off;  // doubles
   long n_send_items = 0, n_recv_poses = 0;
-  DevBuf<int> pack_idx, unpack_x, unpack_y;
-  DevBuf<double> RX, RY;
+  DevBuf<int> pack_idx, unpack_x;
+  DevBuf<double> RX;   // received neighbour poses used by updates and reweighting
+  DevBuf<double> RXc;  // received neighbour poses of a central evaluation (kept apart from RX)
+  // status (PGOAgent::iterate, src/PGOAgent.cpp:700-716): per colour, each agent's loop closures (problem
+  // edge indices) and converged ratio (GNC_TLS only; otherwise 1)
+  struct LcList {
+    DevBuf<int> off, idx;
+    DevBuf<double> ratio;
+    bool valid = false;
+  };
+  std::vector<LcList*> lc;
+  // algorithmic-byte model inputs per colour per agent (dpgo_rbcd_bytes)
+  struct AgentSize {
+    double n, m_in, m_shared, gslots;
+  };
+  std::vector<std::vector<AgentSize>> asz;
+  double host_bytes = 0.0;  // per-iteration passes counted by the host (combination, G, exchange)
+  std::vector<long long> g_store_calls;  // per colour: optimize calls that stored grad(x1)
+  // in-step SpMM timing (dpgo_rbcd_set_kernel_timing)
+  double spmm_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long spmm_launches[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   // per colour G assembly tables
   struct GTab {
     DevBuf<int> slot_off, src, outgoing;
     DevBuf<double> R, t, kappa, tau, w;
     int nslots = 0;
+    long nent = 0;  // shared-edge entries
   };
   std::vector<GTab*> gt;
   // robust cost: per colour, the loop closures its agents reweight and the colour problem's weights
@@ -64,6 +87,7 @@ struct dpgo_rbcd_s {
       if (p) dpgo_hip_problem_destroy(p);
     for (auto* g : gt) delete g;
     for (auto* g : gnc) delete g;
+    for (auto* l : lc) delete l;
   }
   size_t rb() const { return static_cast<size_t>(r) * b; }
 };
@@ -81,28 +105,36 @@ double* color_ptr(dpgo_rbcd e, DevBuf<double>& buf, int c) {
   return buf.p + static_cast<size_t>(e->own_pose_off[e->color_off[c]]) * e->rb();
 }
 
+long color_first_pose(dpgo_rbcd e, int c) { return e->own_pose_off[e->color_off[c]]; }
+long color_num_poses(dpgo_rbcd e, int c) { return e->own_pose_off[e->color_off[c + 1]] - e->own_pose_off[e->color_off[c]]; }
+double pose_bytes(dpgo_rbcd e) { return 8.0 * static_cast<double>(e->rb()); }
+
 int polar(dpgo_rbcd e, int c, const double* A, const double* B, double ca, double cb, double* out,
-          const double* C = nullptr, double* out2 = nullptr) {
+          const double* C = nullptr, double* out2 = nullptr, double* xcopy = nullptr) {
   dpgo_hip_problem h = e->prob[c];
   if (!h) return DPGO_HIP_OK;
   // uniform Nesterov coefficients travel as kernel arguments
   auto ctx = make_ctx(h, FLAG_NONE, h->pa.p);
-  HIP_TRY(launch_polar_comb(e->r, e->b, ctx, A, B, nullptr, nullptr, out, C, ca, cb, out2));
+  HIP_TRY(launch_polar_comb(e->r, e->b, ctx, A, B, nullptr, nullptr, out, C, ca, cb, out2, xcopy));
+  e->host_bytes += pose_bytes(e) * static_cast<double>(color_num_poses(e, c)) *
+                   (1.0 + (B ? 1.0 : 0.0) + (C ? 1.0 : 0.0) + 1.0 + (out2 ? 1.0 : 0.0) + (xcopy ? 1.0 : 0.0));
   return DPGO_HIP_OK;
 }
 
 // out = project((1 - alpha) X + alpha V) for colour c, preceded by the colour's deferred updateV
-// V = project(V + gamma (X - Y)) in the same pass when one is pending
-int nesterov_comb(dpgo_rbcd e, int c, double* out) {
+// V = project(V + gamma (X - Y)) in the same pass when one is pending.  xcopy: XPrev = X (the selected
+// colour's status reference) written from the same loads.
+int nesterov_comb(dpgo_rbcd e, int c, double* out, double* xcopy = nullptr) {
   dpgo_hip_problem h = e->prob[c];
   if (!h) return DPGO_HIP_OK;
   double* Xc = color_ptr(e, e->X, c);
   double* Yc = color_ptr(e, e->Y, c);
   double* Vc = color_ptr(e, e->V, c);
-  if (!e->v_pending[c]) return polar(e, c, Xc, Vc, 1.0 - e->alpha, e->alpha, out);
+  if (!e->v_pending[c]) return polar(e, c, Xc, Vc, 1.0 - e->alpha, e->alpha, out, nullptr, nullptr, xcopy);
   e->v_pending[c] = 0;
   auto ctx = make_ctx(h, FLAG_NONE, h->pa.p);
-  HIP_TRY(launch_polar_vnext(e->r, e->b, ctx, Xc, Vc, Yc, e->v_gamma[c], 1.0 - e->alpha, e->alpha, out));
+  HIP_TRY(launch_polar_vnext(e->r, e->b, ctx, Xc, Vc, Yc, e->v_gamma[c], 1.0 - e->alpha, e->alpha, out, xcopy));
+  e->host_bytes += pose_bytes(e) * static_cast<double>(color_num_poses(e, c)) * (5.0 + (xcopy ? 1.0 : 0.0));
   return DPGO_HIP_OK;
 }
 
@@ -110,20 +142,23 @@ int copy_poses(dpgo_rbcd e, double* dst, const double* src, long first_pose, lon
   if (count <= 0) return DPGO_HIP_OK;
   HIP_TRY(hipMemcpyAsync(dst + first_pose * e->rb(), src + first_pose * e->rb(), sizeof(double) * count * e->rb(),
                          hipMemcpyDeviceToDevice, e->stream));
+  e->host_bytes += 2.0 * pose_bytes(e) * static_cast<double>(count);
   return DPGO_HIP_OK;
 }
 
-long color_first_pose(dpgo_rbcd e, int c) { return e->own_pose_off[e->color_off[c]]; }
-long color_num_poses(dpgo_rbcd e, int c) { return e->own_pose_off[e->color_off[c + 1]] - e->own_pose_off[e->color_off[c]]; }
-
-int assemble_G(dpgo_rbcd e, int c, bool aux) {
+// constructGMatrix (src/PGOAgent.cpp:783-859) for colour c from in-place neighbours (X) and received
+// ones (Rx).  In-place neighbours are never in colour c, so they ran iterate(false) this iteration
+// and their aux pose equals X (see dpgo_rbcd_pre_exchange): X serves both dictionaries.
+int assemble_G(dpgo_rbcd e, int c, const double* Rx) {
   dpgo_hip_problem h = e->prob[c];
   if (!h || e->gt[c]->nslots == 0) return DPGO_HIP_OK;
   auto* t = e->gt[c];
   GEdges ge{t->slot_off.p, t->src.p, t->outgoing.p, t->R.p, t->t.p, t->kappa.p, t->tau.p, t->w.p};
-  // in-place neighbours are never in colour c, so they ran iterate(false) this iteration and their
-  // aux pose equals X (see dpgo_rbcd_pre_exchange): X is read for both dictionaries
-  HIP_TRY(launch_assemble_G(e->r, e->b, ge, t->nslots, e->X.p, aux ? e->RY.p : e->RX.p, h->gblk.p, e->stream));
+  HIP_TRY(launch_assemble_G(e->r, e->b, ge, t->nslots, e->X.p, Rx, h->gblk.p, e->stream));
+  // per entry: neighbour pose + measurement (R, t, kappa, tau, w, src, outgoing); per slot: G block
+  const double d = e->d;
+  e->host_bytes += static_cast<double>(t->nent) * (pose_bytes(e) + 8.0 * (d * d + d + 3.0) + 8.0) +
+                   static_cast<double>(t->nslots) * (pose_bytes(e) + 4.0);
   return DPGO_HIP_OK;
 }
 
@@ -137,10 +172,19 @@ int reweight_color(dpgo_rbcd e, int c) {
                       g->R.p, g->t.p, g->kappa.p, g->tau.p};
   const RobustParams rp{e->P.robust_cost, e->mu, e->P.gnc_barc, e->P.huber_threshold, e->P.tls_threshold};
   HIP_TRY(launch_gnc_weights(e->r, e->b, ge, e->X.p, e->RX.p, rp, g->w_prob.p, e->gt[c]->w.p, e->stream));
-  return dpgo_hip_set_edge_weights_dev(h, g->w_prob.p);
+  DPGO_TRY(dpgo_hip_set_edge_weights_dev(h, g->w_prob.p));
+  if (e->P.robust_cost == DPGO_ROBUST_GNC_TLS) {  // computeConvergedLoopClosureRatio (:1247-1289)
+    auto* l = e->lc[c];
+    HIP_TRY(launch_conv_ratio(h->K, l->off.p, l->idx.p, g->w_prob.p, l->ratio.p, e->stream));
+    l->valid = true;
+  }
+  return DPGO_HIP_OK;
 }
 
-int optimize_color(dpgo_rbcd e, int c, const double* Xin, double* Xout, dpgo_opt_result* results) {
+// QuadraticOptimizer as PGOAgent::updateX configures it (src/PGOAgent.cpp:1131-1137), plus the agent
+// status against status_ref (XPrev) when the engine tracks it.
+int optimize_color(dpgo_rbcd e, int c, const double* Xin, double* Xout, dpgo_opt_result* results,
+                   const double* status_ref) {
   dpgo_hip_problem h = e->prob[c];
   if (!h) return DPGO_HIP_OK;
   dpgo_opt_params p;
@@ -151,7 +195,10 @@ int optimize_color(dpgo_rbcd e, int c, const double* Xin, double* Xout, dpgo_opt
   p.tr_max_inner = e->P.max_inner;
   p.tr_initial_radius = e->P.initial_radius;
   p.precon = e->P.precon;
-  DPGO_TRY(dpgo_hip_optimize_dev(h, &p, Xin, Xout, nullptr, results));
+  StatusArgs st{status_ref, e->lc[c]->valid ? e->lc[c]->ratio.p : nullptr, e->P.rel_change_tol,
+                e->P.min_convergence_ratio};
+  if (!h->predict_boundary) e->g_store_calls[c] += 1;  // EVAL_TCG stores grad(x1) (byte model)
+  DPGO_TRY(optimize_dev_status(h, &p, Xin, Xout, nullptr, results, status_ref ? &st : nullptr));
   e->agent_updates += h->K;
   return DPGO_HIP_OK;
 }
@@ -219,6 +266,9 @@ void dpgo_rbcd_default_params(dpgo_rbcd_params* p) {
   p->gnc_init_mu = 1e-4;
   p->huber_threshold = 3.0;
   p->tls_threshold = 10.0;
+  p->status = 1;
+  p->rel_change_tol = 5e-3;
+  p->min_convergence_ratio = 0.8;
 }
 
 int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, const int* agent_rank, int rank,
@@ -303,42 +353,38 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
   // ---- exchange plan: poses each peer needs from us / we need from each peer (sorted global ids)
   std::vector<std::set<int>> send_set, recv_set;
   exchange_plan(g, agent_of_pose, agent_rank, rank, world, send_set, recv_set);
-  const int mult = e->P.acceleration ? 2 : 1;
   const long long rbd = static_cast<long long>(e->rb());
   e->send_counts.assign(world, 0);
   e->recv_counts.assign(world, 0);
   e->send_off.assign(world + 1, 0);
   e->recv_off.assign(world + 1, 0);
-  std::vector<int> pack_idx, unpack_x, unpack_y;
+  std::vector<int> pack_idx, unpack_x;
   std::map<int, long> recv_slot;  // global pose -> recv pose index
   long rs = 0;
   for (int p = 0; p < world; ++p) {
     const long cnt_s = static_cast<long>(send_set[p].size()), cnt_r = static_cast<long>(recv_set[p].size());
-    e->send_counts[p] = cnt_s * rbd * mult;
-    e->recv_counts[p] = cnt_r * rbd * mult;
+    e->send_counts[p] = cnt_s * rbd;
+    e->recv_counts[p] = cnt_r * rbd;
     e->send_off[p + 1] = e->send_off[p] + e->send_counts[p];
     e->recv_off[p + 1] = e->recv_off[p] + e->recv_counts[p];
     for (int pose : send_set[p]) pack_idx.push_back(static_cast<int>(owned_index(pose)));
-    if (mult == 2)
-      for (int pose : send_set[p]) pack_idx.push_back(-1 - static_cast<int>(owned_index(pose)));
     const long base = e->recv_off[p] / rbd;  // recv segment start in poses
     long s = 0;
     for (int pose : recv_set[p]) {
       recv_slot[pose] = rs++;
       unpack_x.push_back(static_cast<int>(base + s));
-      if (mult == 2) unpack_y.push_back(static_cast<int>(base + cnt_r + s));
       ++s;
     }
   }
   e->n_send_items = static_cast<long>(pack_idx.size());
   e->n_recv_poses = rs;
-  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
+  if (hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(DPGO_HIP_EDEVICE, "stream create failed"));
+  e->stream = e->own_stream;
   int rc = upload_vec(e->pack_idx, pack_idx, e->stream);
   if (rc == DPGO_HIP_OK) rc = upload_vec(e->unpack_x, unpack_x, e->stream);
-  if (rc == DPGO_HIP_OK) rc = upload_vec(e->unpack_y, unpack_y, e->stream);
   if (rc != DPGO_HIP_OK) return bail(rc);
-  if (e->RX.ensure(std::max<long>(rs, 1) * e->rb()) != hipSuccess || e->RY.ensure(std::max<long>(rs, 1) * e->rb()) != hipSuccess ||
+  if (e->RX.ensure(std::max<long>(rs, 1) * e->rb()) != hipSuccess || e->RXc.ensure(std::max<long>(rs, 1) * e->rb()) != hipSuccess ||
       e->X.ensure(std::max<long>(e->Nown, 1) * e->rb()) != hipSuccess ||
       e->Y.ensure(std::max<long>(e->Nown, 1) * e->rb()) != hipSuccess ||
       e->V.ensure(std::max<long>(e->Nown, 1) * e->rb()) != hipSuccess ||
@@ -357,9 +403,14 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
   e->prob.assign(e->ncolors, nullptr);
   e->gt.assign(e->ncolors, nullptr);
   e->gnc.assign(e->ncolors, nullptr);
+  e->lc.assign(e->ncolors, nullptr);
+  e->asz.assign(e->ncolors, {});
+  e->g_store_calls.assign(e->ncolors, 0);
   for (int c = 0; c < e->ncolors; ++c) {
     e->gt[c] = new dpgo_rbcd_s::GTab();
     e->gnc[c] = new dpgo_rbcd_s::Gnc();
+    e->lc[c] = new dpgo_rbcd_s::LcList();
+    std::vector<int> lc_off{0}, lc_idx;  // every loop closure of each agent (converged ratio)
     const int a0 = e->color_off[c], a1 = e->color_off[c + 1];
     // loop closures this colour reweights (PGOAgent::updateLoopClosuresWeights): private ones that
     // are not odometry (local p2 != p1 + 1, as the partition's split), and shared ones whose other
@@ -374,7 +425,7 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
     rc = dpgo_hip_problem_create_batch(a1 - a0, counts.data(), d, e->r, &h);
     if (rc != DPGO_HIP_OK) return bail(rc);
     e->prob[c] = h;
-    dpgo_hip_problem_set_stream(h, e->stream);
+    h->stream = e->stream;
     std::vector<int> slot_off{0}, src, outgoing;
     std::vector<double> Rv, tv, kv, tauv, wv;
     for (int q = a0; q < a1; ++q) {
@@ -439,6 +490,20 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
         }
         slot_off.push_back(static_cast<int>(src.size()));
       }
+      dpgo_rbcd_s::AgentSize sz{static_cast<double>(agent_n[A]), 0.0, 0.0, static_cast<double>(gpose.size())};
+      for (size_t x = 0; x < agent_edges[q].size(); ++x) {
+        const size_t k = agent_edges[q][x];
+        const int i = g->p1[k], j = g->p2[k];
+        const bool own_i = agent_of_pose[i] == A, own_j = agent_of_pose[j] == A;
+        if (own_i && own_j)
+          sz.m_in += 1.0;
+        else
+          sz.m_shared += 1.0;
+        // loop closures (odometry = consecutive local indices, as the partition splits them)
+        if (!(own_i && own_j && local[j] == local[i] + 1)) lc_idx.push_back(static_cast<int>(prob_edges + static_cast<long>(x)));
+      }
+      e->asz[c].push_back(sz);
+      lc_off.push_back(static_cast<int>(lc_idx.size()));
       for (size_t x = 0; x < agent_edges[q].size(); ++x) {
         const size_t k = agent_edges[q][x];
         const int i = g->p1[k], j = g->p2[k];
@@ -473,6 +538,14 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
     if (rc != DPGO_HIP_OK) return bail(rc);
     auto* t = e->gt[c];
     t->nslots = static_cast<int>(slot_off.size()) - 1;
+    t->nent = static_cast<long>(src.size());
+    {
+      auto* l = e->lc[c];
+      rc = upload_vec(l->off, lc_off, e->stream);
+      if (rc == DPGO_HIP_OK) rc = upload_vec(l->idx, lc_idx, e->stream);
+      if (rc == DPGO_HIP_OK && l->ratio.ensure(a1 - a0) != hipSuccess) rc = fail(DPGO_HIP_ENOMEM, "ratio");
+      if (rc != DPGO_HIP_OK) return bail(rc);
+    }
     if (t->nslots != h->num_gslots) return bail(fail(DPGO_HIP_ESTATE, "G slot order mismatch"));
     rc = upload_vec(t->slot_off, slot_off, e->stream);
     if (rc == DPGO_HIP_OK) rc = upload_vec(t->src, src, e->stream);
@@ -502,19 +575,35 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
 
 int dpgo_rbcd_destroy(dpgo_rbcd e) {
   if (!e) return DPGO_HIP_OK;
-  hipStream_t s = e->stream;
-  if (s) (void)hipStreamSynchronize(s);
+  // drain the launch stream (possibly the caller's) and the engine's own; destroy only the own stream
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  hipStream_t own = e->own_stream;
+  if (own) (void)hipStreamSynchronize(own);
   delete e;
-  if (s) (void)hipStreamDestroy(s);
+  if (own) (void)hipStreamDestroy(own);
   return DPGO_HIP_OK;
 }
 
+namespace {
+void use_stream(dpgo_rbcd e, hipStream_t s) {
+  e->stream = s;
+  for (auto* h : e->prob)
+    if (h) h->stream = s;  // verbatim: a NULL stream is the HIP null stream here
+}
+}  // namespace
+
 int dpgo_rbcd_set_stream(dpgo_rbcd e, void* stream) {
   if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
-  if (!stream) return DPGO_HIP_OK;
-  e->stream = static_cast<hipStream_t>(stream);
-  for (auto* h : e->prob)
-    if (h) dpgo_hip_problem_set_stream(h, stream);
+  // work already queued on the previous stream completes before anything on the new one
+  if (e->stream != static_cast<hipStream_t>(stream)) HIP_TRY(hipStreamSynchronize(e->stream));
+  use_stream(e, static_cast<hipStream_t>(stream));
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_reset_stream(dpgo_rbcd e) {
+  if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
+  if (e->stream != e->own_stream) HIP_TRY(hipStreamSynchronize(e->stream));
+  use_stream(e, e->own_stream);
   return DPGO_HIP_OK;
 }
 
@@ -605,9 +694,10 @@ int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color) {
     }
   }
   const bool restart = restart_now(e);
-  // XPrev = X (:673) is only read by a restart (the relative-change status is not tracked here)
-  const long bytes = static_cast<long>(sizeof(double)) * e->Nown * static_cast<long>(e->rb());
-  if (restart && bytes) HIP_TRY(hipMemcpyAsync(e->Xprev.p, e->X.p, bytes, hipMemcpyDeviceToDevice, e->stream));
+  // XPrev = X (:673): every agent's on a restart iteration (restartNesterovAcceleration reads it);
+  // otherwise only the selected colour's, for its status (fused into its combination pass below;
+  // without acceleration the update's own select pass compares against the old X in place)
+  if (restart) DPGO_TRY(copy_poses(e, e->Xprev.p, e->X.p, 0, e->Nown));
   if (!e->P.acceleration) return DPGO_HIP_OK;
   const double N = static_cast<double>(e->K);
   e->gamma = (1.0 + std::sqrt(1.0 + 4.0 * N * N * e->gamma * e->gamma)) / (2.0 * N);  // updateGamma
@@ -617,7 +707,9 @@ int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color) {
     double* Xc = color_ptr(e, e->X, c);
     double* Yc = color_ptr(e, e->Y, c);
     if (c == color) {
-      DPGO_TRY(nesterov_comb(e, c, Yc));  // updateY (selected)
+      // updateY (selected); XPrev = X (:673) for the status, written from the same loads (a restart
+      // iteration already copied every X above)
+      DPGO_TRY(nesterov_comb(e, c, Yc, e->P.status && !restart ? color_ptr(e, e->Xprev, c) : nullptr));
       continue;
     }
     // non-selected agents, iterate(false): updateY, updateX(false, true): X = Y (one fused pass,
@@ -641,6 +733,7 @@ int dpgo_rbcd_pack(dpgo_rbcd e, double* send_dev) {
   // after dpgo_rbcd_pre_exchange (the others' entries are not read this iteration)
   HIP_TRY(launch_gather_poses(static_cast<int>(e->n_send_items), static_cast<int>(e->rb()), e->pack_idx.p, e->X.p,
                               e->X.p, send_dev, e->stream));
+  e->host_bytes += 2.0 * pose_bytes(e) * static_cast<double>(e->n_send_items);
   return DPGO_HIP_OK;
 }
 
@@ -651,9 +744,7 @@ int dpgo_rbcd_update(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_re
     if (!recv_dev) return fail(DPGO_HIP_EINVAL, "receive buffer required");
     HIP_TRY(launch_gather_poses(static_cast<int>(e->n_recv_poses), rbs, e->unpack_x.p, recv_dev, recv_dev, e->RX.p,
                                 e->stream));
-    if (e->P.acceleration)
-      HIP_TRY(launch_gather_poses(static_cast<int>(e->n_recv_poses), rbs, e->unpack_y.p, recv_dev, recv_dev, e->RY.p,
-                                  e->stream));
+    e->host_bytes += 2.0 * pose_bytes(e) * static_cast<double>(e->n_recv_poses);
   }
   const bool restart = restart_now(e);
   if (e->gnc_due) {
@@ -665,9 +756,11 @@ int dpgo_rbcd_update(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_re
   if (e->prob[color]) {
     double* Xc = color_ptr(e, e->X, color);
     double* Yc = color_ptr(e, e->Y, color);
+    double* Pc = color_ptr(e, e->Xprev, color);
+    const bool st = e->P.status != 0;
     if (e->P.acceleration) {
-      DPGO_TRY(assemble_G(e, color, true));  // constructGMatrix(neighborAuxPoseDict)
-      DPGO_TRY(optimize_color(e, color, Yc, Xc, results));
+      DPGO_TRY(assemble_G(e, color, e->RX.p));  // constructGMatrix(neighborAuxPoseDict)
+      DPGO_TRY(optimize_color(e, color, Yc, Xc, results, st && !restart ? Pc : nullptr));
       if (!restart) {
         // updateV: V = project(V + gamma (X - Y)).  Nothing reads this colour's V before its next
         // combination pass (the next dpgo_rbcd_pre_exchange), so it runs inside that pass
@@ -675,19 +768,150 @@ int dpgo_rbcd_update(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_re
         e->v_gamma[color] = e->gamma;
       } else {  // restartNesterovAcceleration(true) (:1040-1060); its V = X supersedes updateV
         DPGO_TRY(copy_poses(e, e->X.p, e->Xprev.p, color_first_pose(e, color), color_num_poses(e, color)));
-        DPGO_TRY(assemble_G(e, color, false));
-        DPGO_TRY(optimize_color(e, color, Xc, Xc, results));
+        DPGO_TRY(assemble_G(e, color, e->RX.p));  // constructGMatrix(neighborPoseDict): same poses
+        DPGO_TRY(optimize_color(e, color, Xc, Xc, results, st ? Pc : nullptr));
         DPGO_TRY(copy_poses(e, e->V.p, e->X.p, color_first_pose(e, color), color_num_poses(e, color)));
         DPGO_TRY(copy_poses(e, e->Y.p, e->X.p, color_first_pose(e, color), color_num_poses(e, color)));
       }
     } else {
-      DPGO_TRY(assemble_G(e, color, false));  // constructGMatrix(neighborPoseDict)
-      DPGO_TRY(optimize_color(e, color, Xc, Xc, results));
+      DPGO_TRY(assemble_G(e, color, e->RX.p));  // constructGMatrix(neighborPoseDict)
+      // in place: the update's final select compares the result against the old X (= XPrev)
+      DPGO_TRY(optimize_color(e, color, Xc, Xc, results, st ? Xc : nullptr));
     }
   }
   if (restart) {
     e->gamma = 0.0;
     e->alpha = 0.0;
+  }
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_central_eval(dpgo_rbcd e, const double* recv_dev, double* f_out, double* gradnorm_sq) {
+  if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
+  if (e->n_recv_poses > 0) {
+    if (!recv_dev) return fail(DPGO_HIP_EINVAL, "receive buffer required");
+    HIP_TRY(launch_gather_poses(static_cast<int>(e->n_recv_poses), static_cast<int>(e->rb()), e->unpack_x.p, recv_dev,
+                                recv_dev, e->RXc.p, e->stream));
+  }
+  // per colour: G from the current neighbour poses, then f / |P_X(XQ + G)|^2 / <G, X> per agent
+  for (int c = 0; c < e->ncolors; ++c) {
+    if (!e->prob[c]) continue;
+    DPGO_TRY(assemble_G(e, c, e->RXc.p));
+    DPGO_TRY(eval_sums_dev(e->prob[c], color_ptr(e, e->X, c)));
+  }
+  double f = 0.0;
+  if (gradnorm_sq)
+    for (int a = 0; a < e->K; ++a) gradnorm_sq[a] = 0.0;
+  for (int c = 0; c < e->ncolors; ++c) {
+    if (!e->prob[c]) continue;
+    std::vector<double> sums;
+    DPGO_TRY(download_sums_public(e->prob[c], sums));
+    for (int q = e->color_off[c]; q < e->color_off[c + 1]; ++q) {
+      const int a = q - e->color_off[c];
+      // central cost: each shared edge's cross term sits in both endpoint agents' <G, X>
+      f += sums[a * 4 + 0] - 0.5 * sums[a * 4 + 2];
+      if (gradnorm_sq) gradnorm_sq[e->owned[q]] = sums[a * 4 + 1];
+    }
+  }
+  if (f_out) *f_out = f;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_status(dpgo_rbcd e, double* rel_change, int* ready) {
+  if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
+  for (int c = 0; c < e->ncolors; ++c) {
+    dpgo_hip_problem h = e->prob[c];
+    if (!h) continue;
+    std::vector<AgentState> st(h->K);
+    HIP_TRY(hipMemcpyAsync(st.data(), h->state.p, sizeof(AgentState) * h->K, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    for (int q = e->color_off[c]; q < e->color_off[c + 1]; ++q) {
+      const AgentState& s = st[q - e->color_off[c]];
+      if (rel_change) rel_change[e->owned[q]] = s.status_rel_change;
+      if (ready) ready[e->owned[q]] = s.ready;
+    }
+  }
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_stats(dpgo_rbcd e, int* out) {
+  if (!e || !out) return fail(DPGO_HIP_EINVAL, "null argument");
+  for (int c = 0; c < e->ncolors; ++c) {
+    dpgo_hip_problem h = e->prob[c];
+    if (!h) continue;
+    std::vector<int> st(static_cast<size_t>(h->K) * kStatsInts);
+    DPGO_TRY(dpgo_hip_stats(h, st.data()));
+    for (int q = e->color_off[c]; q < e->color_off[c + 1]; ++q)
+      std::memcpy(out + static_cast<size_t>(e->owned[q]) * kStatsInts, &st[static_cast<size_t>(q - e->color_off[c]) * kStatsInts],
+                  sizeof(int) * kStatsInts);
+  }
+  return DPGO_HIP_OK;
+}
+
+// Algorithmic HBM bytes of everything the engine launched so far: the host-counted per-iteration
+// passes plus, per agent, each kernel's bytes times the number of launches that did work for the agent
+// (from the exact per-agent solver counters).  SURVEY 8(d)'s accounting: an X.Q pass over an agent
+// reads its Q as explicit b x b blocks (n + 2 m_in blocks of b^2 8 + 4 B, (n + 1) 4 B of row pointers)
+// and the pose vector once; a half pass (each edge once) reads n + m_in blocks.  P = r b 8 B per pose
+// vector, Minv / Q_jj packed (b (b + 1) / 2 doubles), S packed (d (d + 1) / 2 doubles).
+int dpgo_rbcd_bytes(dpgo_rbcd e, double* bytes, double* evaltcg_bytes_per_color) {
+  if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
+  const double P = pose_bytes(e), b = e->b, d = e->d;
+  const double blk = b * b * 8.0 + 4.0, DW = 8.0 * b * (b + 1) / 2, SW = 8.0 * d * (d + 1) / 2;
+  double total = e->host_bytes;
+  for (int c = 0; c < e->ncolors; ++c) {
+    dpgo_hip_problem h = e->prob[c];
+    if (evaltcg_bytes_per_color) evaltcg_bytes_per_color[c] = 0.0;
+    if (!h) continue;
+    std::vector<int> st(static_cast<size_t>(h->K) * kStatsInts);
+    DPGO_TRY(dpgo_hip_stats(h, st.data()));
+    double calls_all = 0.0;
+    for (int a = 0; a < h->K; ++a) {
+      const auto& z = e->asz[c][a];
+      const int* k = &st[static_cast<size_t>(a) * kStatsInts];
+      const double calls = k[0], runs = k[2], iters = k[3], lcon = k[6] + k[7], maxit = k[8], cg = k[10], impl = k[11];
+      const double bnd = k[4] + k[5];
+      calls_all = std::max(calls_all, calls);
+      const double full_in = (z.n + 2.0 * z.m_in) * blk + (z.n + 1.0) * 4.0 + z.n * P;
+      const double half_in = (z.n + z.m_in) * blk + (z.n + 1.0) * 4.0 + z.n * P;
+      const double gread = z.gslots * P + z.n * 4.0;
+      const double evaltcg = full_in + z.n * (SW + DW + P) + gread;  // + grad(x1) when stored (below)
+      if (evaltcg_bytes_per_color) evaltcg_bytes_per_color[c] += evaltcg;
+      total += calls * evaltcg;
+      total += runs * (half_in + z.n * SW);                           // QF first step test
+      total += (iters - runs + (runs - impl)) * (full_in + z.n * (P + SW + P));  // HESS
+      total += cg * z.n * (11.0 * P + DW) + (bnd - impl) * z.n * 6.0 * P;     // tCG updates
+      total += std::max(0.0, cg - lcon - maxit) * z.n * 3.0 * P;                 // tCG directions
+      total += runs * z.n * 3.0 * P + (runs - impl) * z.n * 2.0 * P;            // retraction
+      total += runs * (half_in + gread);                                          // f(x2)
+      if (e->P.status) total += calls * z.n * 2.0 * P;                            // status |X - XPrev|
+    }
+    // grad(x1) written by EVAL_TCG when stored (per handle, every agent)
+    double nposes = 0.0;
+    for (const auto& z : e->asz[c]) nposes += z.n;
+    total += static_cast<double>(e->g_store_calls[c]) * nposes * P;
+    (void)calls_all;
+  }
+  if (bytes) *bytes = total;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_set_kernel_timing(dpgo_rbcd e, int on) {
+  if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
+  for (auto* h : e->prob)
+    if (h) h->timing = on != 0;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_kernel_times(dpgo_rbcd e, double* ms_per_mode, long long* launches_per_mode) {
+  if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
+  for (auto* h : e->prob)
+    if (h) DPGO_TRY(take_spmm_times(h, e->spmm_ms, e->spmm_launches));
+  for (int m = 0; m < 8; ++m) {
+    if (ms_per_mode) ms_per_mode[m] = e->spmm_ms[m];
+    if (launches_per_mode) launches_per_mode[m] = e->spmm_launches[m];
+    e->spmm_ms[m] = 0.0;
+    e->spmm_launches[m] = 0;
   }
   return DPGO_HIP_OK;
 }

@@ -91,7 +91,18 @@ _SIGS = [
     ("dpgo_hip_spmm_bytes_bsr", [C.c_void_p], C.c_double),
     ("dpgo_hip_certify", [C.c_void_p, _dp, C.c_int, C.c_double, _dp, _dp, _ip, _dp], C.c_int),
     ("dpgo_hip_bench_hvp", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, _dp], C.c_int),
+    ("dpgo_hip_stats", [C.c_void_p, _ip], C.c_int),
+    ("dpgo_hip_set_trace", [C.c_void_p, C.c_int], C.c_int),
+    ("dpgo_hip_get_trace", [C.c_void_p, C.c_int, _dp, C.c_int, _ip], C.c_int),
+    ("dpgo_hip_build_id", [], C.c_char_p),
 ]
+STATS_INTS = 12
+STATS_FIELDS = ["calls", "early", "runs", "tcg_iters", "NEGCURVTURE", "EXCREGION", "LCON", "SCON", "MAXITER",
+                "gave_up", "cg_steps", "implicit"]
+TRACE_WIDTH = 16
+TRACE_FIELDS = ["op", "j", "f1", "f2", "rho", "Delta", "alpha", "beta", "tau", "d_Hd", "norm_r", "z_r", "status",
+                "accepted", "ngf", "run"]
+SPMM_MODES = ["XQ", "XQ_G", "EVAL", "HESS", "F", "EVAL_TCG", "CERT", "QF"]
 
 EXPORTED_SYMBOLS = [s[0] for s in _SIGS]
 
@@ -135,6 +146,11 @@ def _i32(a):
 
 def device_count() -> int:
     return int(lib().dpgo_hip_device_count())
+
+
+def build_id() -> str:
+    """Source hash compiled into the loaded libdpgo_hip.so (__graft_entry__.source_hash())."""
+    return lib().dpgo_hip_build_id().decode()
 
 
 def set_tuning(key: int, value: int):
@@ -348,6 +364,26 @@ class Problem:
     def synchronize(self):
         _check(lib().dpgo_hip_synchronize(self.h))
 
+    def stats(self):
+        """Cumulative solver counters per agent: list of dicts (STATS_FIELDS)."""
+        out = np.zeros(self.K * STATS_INTS, np.int32)
+        _check(lib().dpgo_hip_stats(self.h, out.ctypes.data_as(_ip)))
+        return [dict(zip(STATS_FIELDS, (int(v) for v in out[a * STATS_INTS:(a + 1) * STATS_INTS])))
+                for a in range(self.K)]
+
+    def set_trace(self, capacity):
+        _check(lib().dpgo_hip_set_trace(self.h, int(capacity)))
+        self._trace_cap = int(capacity)
+
+    def get_trace(self, agent=0):
+        """Per-iteration records of one agent: list of dicts (TRACE_FIELDS)."""
+        cap = getattr(self, "_trace_cap", 0)
+        buf = np.zeros(max(cap, 1) * TRACE_WIDTH)
+        n = C.c_int()
+        _check(lib().dpgo_hip_get_trace(self.h, int(agent), buf.ctypes.data_as(_dp), cap, C.byref(n)))
+        k = min(n.value, cap)
+        return [dict(zip(TRACE_FIELDS, buf[i * TRACE_WIDTH:(i + 1) * TRACE_WIDTH].tolist())) for i in range(k)]
+
 
 def tangent_project(X, V, d):
     r = X.shape[0]
@@ -387,7 +423,8 @@ class RbcdParams(C.Structure):
                 ("precon", C.c_int), ("algorithm", C.c_int), ("q_format", C.c_int),
                 ("robust_cost", C.c_int), ("robust_opt_inner_iters", C.c_int), ("gnc_max_iters", C.c_int),
                 ("gnc_barc", C.c_double), ("gnc_mu_step", C.c_double), ("gnc_init_mu", C.c_double),
-                ("huber_threshold", C.c_double), ("tls_threshold", C.c_double)]
+                ("huber_threshold", C.c_double), ("tls_threshold", C.c_double),
+                ("status", C.c_int), ("rel_change_tol", C.c_double), ("min_convergence_ratio", C.c_double)]
 
 
 _lp = C.POINTER(C.c_longlong)
@@ -422,6 +459,13 @@ _SIGS2 = [
     ("dpgo_rbcd_counters", [C.c_void_p, _lp, _lp], C.c_int),
     ("dpgo_rbcd_spmm_bytes", [C.c_void_p, C.c_int, _dp, _dp], C.c_int),
     ("dpgo_rbcd_bench_hvp", [C.c_void_p, C.c_int, C.c_int, _dp], C.c_int),
+    ("dpgo_rbcd_reset_stream", [C.c_void_p], C.c_int),
+    ("dpgo_rbcd_central_eval", [C.c_void_p, C.c_void_p, _dp, _dp], C.c_int),
+    ("dpgo_rbcd_status", [C.c_void_p, _dp, _ip], C.c_int),
+    ("dpgo_rbcd_stats", [C.c_void_p, _ip], C.c_int),
+    ("dpgo_rbcd_bytes", [C.c_void_p, _dp, _dp], C.c_int),
+    ("dpgo_rbcd_set_kernel_timing", [C.c_void_p, C.c_int], C.c_int),
+    ("dpgo_rbcd_kernel_times", [C.c_void_p, _dp, _lp], C.c_int),
 ]
 _SIGS.extend(_SIGS2)
 EXPORTED_SYMBOLS.extend(s[0] for s in _SIGS2)
@@ -609,7 +653,50 @@ class Rbcd:
     def get_X_into(self, Xflat):
         """Write owned poses into a global flat (device-layout) host array."""
         assert Xflat.dtype == np.float64 and Xflat.flags.c_contiguous
+        need = self.graph.n * (self.graph.d + 1) * self.params.r
+        if Xflat.size < need:
+            raise ValueError(f"X buffer holds {Xflat.size} doubles, the graph needs {need}")
         _check(lib().dpgo_rbcd_get_X(self.h, Xflat.ctypes.data_as(_dp)))
+
+    def reset_stream(self):
+        _check(lib().dpgo_rbcd_reset_stream(self.h))
+
+    def central_eval(self, recv_ptr=None):
+        """(this rank's central cost share, |RieGrad|^2 per agent [num_agents]) at the current X."""
+        f = C.c_double()
+        g = np.zeros(self.num_agents)
+        _check(lib().dpgo_rbcd_central_eval(self.h, C.c_void_p(recv_ptr or 0), C.byref(f), g.ctypes.data_as(_dp)))
+        return f.value, g
+
+    def status(self):
+        """(relativeChange[num_agents], readyToTerminate[num_agents]); NaN / -1 for other ranks' agents."""
+        rc = np.full(self.num_agents, np.nan)
+        rd = np.full(self.num_agents, -1, np.int32)
+        _check(lib().dpgo_rbcd_status(self.h, rc.ctypes.data_as(_dp), rd.ctypes.data_as(_ip)))
+        return rc, rd
+
+    def stats(self):
+        """Cumulative solver counters per agent: int array [num_agents, STATS_INTS] (zeros elsewhere)."""
+        out = np.zeros(self.num_agents * STATS_INTS, np.int32)
+        _check(lib().dpgo_rbcd_stats(self.h, out.ctypes.data_as(_ip)))
+        return out.reshape(self.num_agents, STATS_INTS)
+
+    def bytes(self):
+        """(cumulative algorithmic bytes of all launches, EVAL_TCG bytes per colour pass [num_colors])."""
+        b = C.c_double()
+        per = np.zeros(self.num_colors)
+        _check(lib().dpgo_rbcd_bytes(self.h, C.byref(b), per.ctypes.data_as(_dp)))
+        return b.value, per
+
+    def set_kernel_timing(self, on):
+        _check(lib().dpgo_rbcd_set_kernel_timing(self.h, int(bool(on))))
+
+    def kernel_times(self):
+        """{mode: (ms summed, launches)} of the timed in-step X.Q launches since the last call."""
+        ms = np.zeros(8)
+        n = np.zeros(8, np.int64)
+        _check(lib().dpgo_rbcd_kernel_times(self.h, ms.ctypes.data_as(_dp), n.ctypes.data_as(_lp)))
+        return {SPMM_MODES[m]: (float(ms[m]), int(n[m])) for m in range(8) if n[m] > 0}
 
     def pre_exchange(self, color):
         _check(lib().dpgo_rbcd_pre_exchange(self.h, int(color)))

@@ -186,6 +186,29 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
 /* Device buffer of the last tCG / RTR scalar state (for profiling / tests) */
 int dpgo_hip_synchronize(dpgo_hip_problem h);
 
+/* ---- solver statistics and per-iteration trace --------------------------------------------
+ * Cumulative per-agent counters since the handle was created, DPGO_STATS_INTS ints per agent:
+ * [optimize calls, calls that returned at once (|grad| < tol), RTR Runs, tCG inner iterations,
+ *  tCG exits NEGCURVTURE, EXCREGION, LCON, SCON, MAXITER, updates that gave up, tCG CG steps,
+ *  Runs whose tCG ended at its first step on the trust-region boundary]. */
+#define DPGO_STATS_INTS 12
+int dpgo_hip_stats(dpgo_hip_problem h, int* out /* [num_agents * DPGO_STATS_INTS] */);
+/* Per-iteration RTR / tCG trace (the reference prints it with ROPTLIB Debug = ITERRESULT when
+ * verbose, src/QuadraticOptimizer.cpp:82-86): after this call every tCG step test, tCG stopping
+ * test and rho test appends one record of DPGO_TRACE_WIDTH doubles per agent, up to `capacity`
+ * records per agent (0 turns tracing off).  Record fields (kernels.h TraceField): op (3 step test,
+ * 4 stopping test, 5 rho test), j, f1, f2, rho, Delta, alpha, beta, tau, <delta, H delta>, |r|,
+ * <z, r>, tCG status (-1 if none), accepted, |grad(x1)|, Run index. */
+#define DPGO_TRACE_WIDTH 16
+int dpgo_hip_set_trace(dpgo_hip_problem h, int capacity);
+/* Copies agent's records (at most max_records) into out; *count = records written since
+ * set_trace (may exceed capacity: the later ones were dropped). */
+int dpgo_hip_get_trace(dpgo_hip_problem h, int agent, double* out, int max_records, int* count);
+
+/* Source hash the library was compiled from (sha256 of the sources, hex; "unknown" if built
+ * without it): lets a caller check that a shipped binary matches the tree it runs with. */
+const char* dpgo_hip_build_id(void);
+
 /* ---- certification (not in the reference: parity is pinned against a sparse
  * eigensolver on the explicitly formed matrix) --------------------------------------------------
  * Smallest eigenvalue of the certificate matrix S(X) = Q - Lambda(X), Lambda = blockdiag of

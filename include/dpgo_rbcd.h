@@ -76,6 +76,11 @@ typedef struct {
   double gnc_init_mu;          /* 1e-4 */
   double huber_threshold;      /* 3 */
   double tls_threshold;        /* 10 */
+  /* PGOAgent status after every selected update (src/PGOAgent.cpp:700-716): relativeChange =
+   * |X - XPrev| / sqrt(n) and readyToTerminate, on the device (dpgo_rbcd_status) */
+  int status;                    /* 1 (the reference always computes it) */
+  double rel_change_tol;         /* 5e-3 (PGOAgentParameters::relChangeTol) */
+  double min_convergence_ratio;  /* 0.8 (robustOptMinConvergenceRatio, GNC_TLS only) */
 } dpgo_rbcd_params;
 
 /* RobustCostType (include/DPGO/DPGO_robust.h): weights need an edge-stream Q (q_format EDGES) */
@@ -96,7 +101,11 @@ int dpgo_rbcd_plan(dpgo_graph g, int num_agents, const int* agent_of_pose, const
 int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, const int* agent_rank,
                      int rank, int world, const dpgo_rbcd_params* p, dpgo_rbcd* out);
 int dpgo_rbcd_destroy(dpgo_rbcd e);
+/* Launch every engine operation on a caller-owned hipStream_t from now on (NULL = the HIP null
+ * stream); work queued on the previous stream is drained first.  The engine never destroys it. */
 int dpgo_rbcd_set_stream(dpgo_rbcd e, void* stream);
+/* Back to the engine's own (non-blocking) stream. */
+int dpgo_rbcd_reset_stream(dpgo_rbcd e);
 /* number of colour classes, agents owned by this rank, poses owned by this rank */
 int dpgo_rbcd_info(dpgo_rbcd e, int* num_colors, int* owned_agents, int* owned_poses,
                    int* owned_agents_per_color /* [num_colors] or NULL */);
@@ -109,7 +118,8 @@ int dpgo_rbcd_set_X(dpgo_rbcd e, const double* X_global);
 int dpgo_rbcd_get_X(dpgo_rbcd e, double* X_global);
 /* Phase 1 of iteration with selected colour c: every non-selected agent runs iterate(false). */
 int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color);
-/* Pack the public poses peers need (X, then Y when accelerated) into send_dev. */
+/* Pack the public poses peers need into send_dev (their X: with Nesterov the aux pose a receiver
+ * uses equals the sender's X, which ran iterate(false) this iteration). */
 int dpgo_rbcd_pack(dpgo_rbcd e, double* send_dev);
 /* Phase 2: selected agents of colour c update from the received neighbour poses. */
 int dpgo_rbcd_update(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_result* results);
@@ -123,6 +133,30 @@ int dpgo_rbcd_spmm_bytes(dpgo_rbcd e, int color, double* bsr_bytes, double* form
 int dpgo_rbcd_bench_hvp(dpgo_rbcd e, int color, int reps, double* ms);
 /* SpMM / HVP launches issued so far (for throughput accounting) */
 int dpgo_rbcd_counters(dpgo_rbcd e, long long* agent_updates, long long* iterations);
+
+/* Central evaluation (examples/MultiRobotExample.cpp:229-235): this rank's share of the whole-graph
+ * cost f(X) = 1/2 <X Q, X> (sum over ranks = the central cost; with robust costs the current weights)
+ * and, per owned agent, |RieGrad|^2 of its block (the greedy selection / stop test, :243-256).
+ * Call between iterations; recv_dev: the public poses of a dpgo_rbcd_pack + exchange done after the
+ * last update (required when world > 1).  gradnorm_sq[num_agents]: 0 for agents of other ranks.
+ * Synchronises. */
+int dpgo_rbcd_central_eval(dpgo_rbcd e, const double* recv_dev, double* f_out, double* gradnorm_sq);
+/* PGOAgentStatus of every owned agent's last selected update (src/PGOAgent.cpp:700-716):
+ * relativeChange and readyToTerminate, written at the agent's global index (others untouched).
+ * PGOAgent::shouldTerminate (:1007-1031) = every agent ready, gathered over ranks by the caller. */
+int dpgo_rbcd_status(dpgo_rbcd e, double* rel_change, int* ready);
+/* Cumulative solver counters per owned agent (DPGO_STATS_INTS ints at the agent's global index,
+ * layout of dpgo_hip_stats). */
+int dpgo_rbcd_stats(dpgo_rbcd e, int* out);
+/* Algorithmic HBM bytes of every kernel the engine launched so far (SURVEY 8(d) accounting over the
+ * exact per-agent launch counts) and, per colour, the bytes of one tCG-start evaluation pass
+ * (k_spmm MODE_EVAL_TCG) over the colour (evaltcg_bytes_per_color[num_colors], may be NULL). */
+int dpgo_rbcd_bytes(dpgo_rbcd e, double* bytes, double* evaltcg_bytes_per_color);
+/* HIP events around every in-step X.Q launch (on the launch stream) while on; dpgo_rbcd_kernel_times
+ * synchronises and returns, per SpMM mode (8: XQ, XQ_G, EVAL, HESS, F, EVAL_TCG, CERT, QF), the
+ * summed milliseconds and launch counts since the last call. */
+int dpgo_rbcd_set_kernel_timing(dpgo_rbcd e, int on);
+int dpgo_rbcd_kernel_times(dpgo_rbcd e, double* ms_per_mode, long long* launches_per_mode);
 
 #ifdef __cplusplus
 }

@@ -1096,8 +1096,19 @@ class Agent:
             success = self.update_X(do_opt, False, trace)
         if do_opt:
             self.status_relative_change = math.sqrt(float(np.sum((self.X - self.XPrev) ** 2)) / self.n)
-            ready = bool(success) and self.status_relative_change <= self.p.rel_change_tol
+            ready = bool(success) and not (self.status_relative_change > self.p.rel_change_tol)
+            if self.converged_loop_closure_ratio() < self.p.robust_opt_min_convergence_ratio:
+                ready = False
             self.ready_to_terminate = ready
+
+    def converged_loop_closure_ratio(self):
+        """computeConvergedLoopClosureRatio (:1247-1289): GNC_TLS only; loop closures whose weight is
+        exactly 1 or 0 over all private and shared loop closures (0/0 = NaN, as there)."""
+        if self.p.robust != "GNC_TLS":
+            return 1.0
+        w = np.concatenate([self.private_lc.weight, self.shared_lc.weight])
+        conv = float(np.sum((w == 1.0) | (w == 0.0)))
+        return conv / len(w) if len(w) else float("nan")
 
     def trajectory_local_frame(self):
         """:481-498"""
@@ -1249,7 +1260,7 @@ def greedy_colors(meas: Measurements, agent_of_pose, num_agents):
 
 def colour_rbcd(meas: Measurements, agent_of_pose, num_agents, X0, num_iters, r,
                 acceleration=False, robust="L2", precon=PRECON_BLOCK_JACOBI, trace=None,
-                robust_opt_inner_iters=30):
+                robust_opt_inner_iters=30, agents_out=None, algorithm="RTR"):
     """Colour-class RBCD schedule run with the PGOAgent restatement: at iteration t the agents of
     colour t mod C are selected; the others run iterate(false) first (their public X / aux Y are
     then delivered, as in examples/MultiRobotExample.cpp:181-213), then the selected agents run
@@ -1269,11 +1280,14 @@ def colour_rbcd(meas: Measurements, agent_of_pose, num_agents, X0, num_iters, r,
     agents = []
     for a in range(num_agents):
         ag = Agent(a, AgentParams(d, r, num_agents, acceleration=acceleration, robust=robust,
-                                  precon=precon, robust_opt_inner_iters=robust_opt_inner_iters))
+                                  precon=precon, robust_opt_inner_iters=robust_opt_inner_iters,
+                                  algorithm=algorithm))
         ag.set_pose_graph(*parts[a], n=int(counts[a]))
         cols = np.concatenate([np.arange(p * b, (p + 1) * b) for p in glob[a]])
         ag.set_X(X0[:, cols])
         agents.append(ag)
+    if agents_out is not None:
+        agents_out.extend(agents)
     colors = greedy_colors(meas, agent_of_pose, num_agents)
     C = max(colors) + 1
     for it in range(num_iters):

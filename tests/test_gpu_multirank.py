@@ -1,6 +1,11 @@
 """Multi-rank RBCD engine on the GPU: 2 processes (both on the one visible GPU) exchange public
-poses with all_to_all_single (gloo over host copies here; bench.py uses RCCL), and the result must
-equal the oracle's PGOAgent colour schedule."""
+poses with all_to_all_single (gloo over host copies here; bench.py uses RCCL).  The result must be
+bitwise the one-rank engine's (the per-agent arithmetic does not depend on how agents are batched or
+where neighbour poses come from) and match the oracle's PGOAgent colour schedule.
+
+The engine runs on the torch current stream (dpgo_rbcd_set_stream) and the exchange is issued on that
+same stream with no explicit device synchronisation between pack, exchange and update: stream order
+alone must make the halo consistent."""
 import os
 import socket
 
@@ -26,6 +31,10 @@ def _port():
     return p
 
 
+def _params(H, accel, robust):
+    return H.rbcd_params(r=R, acceleration=int(accel), robust_cost=H.ROBUST[robust], robust_opt_inner_iters=3)
+
+
 def _worker(rank, world, port, accel, robust, q):
     import sys
     sys.path.insert(0, ROOT)
@@ -37,33 +46,37 @@ def _worker(rank, world, port, accel, robust, q):
         g = H.Graph.grid3d(K, seed=5)
         aop = g.grid_partition(A)
         ranks = (np.arange(A ** 3) * world // A ** 3).astype(np.int32)
-        e = H.Rbcd(g, aop, ranks, rank, world, H.rbcd_params(r=R, acceleration=int(accel),
-                                                             robust_cost=H.ROBUST[robust], robust_opt_inner_iters=3))
+        e = H.Rbcd(g, aop, ranks, rank, world, _params(H, accel, robust))
         X0 = g.chain_init(R, O.lifting_matrix(3, R))
         e.set_X(X0)
         dev = torch.device("cuda", 0)
-        send = torch.zeros(max(int(e.send_counts.sum()), 1), dtype=torch.float64, device=dev)
-        recv = torch.zeros(max(int(e.recv_counts.sum()), 1), dtype=torch.float64, device=dev)
-        for it in range(ITERS):
-            c = it % e.num_colors
-            e.pre_exchange(c)
-            e.pack(send.data_ptr())
-            torch.cuda.synchronize()
-            hs, hr = send.cpu(), torch.empty_like(recv, device="cpu")
-            dist.all_to_all_single(hr, hs, [int(x) for x in e.recv_counts], [int(x) for x in e.send_counts])
-            recv.copy_(hr)
-            torch.cuda.synchronize()
-            e.update(c, recv.data_ptr())
+        s = torch.cuda.Stream(dev)
+        e.set_stream(s.cuda_stream)
+        with torch.cuda.stream(s):
+            send = torch.zeros(max(int(e.send_counts.sum()), 1), dtype=torch.float64, device=dev)
+            recv = torch.zeros(max(int(e.recv_counts.sum()), 1), dtype=torch.float64, device=dev)
+            rsplit = [int(x) for x in e.recv_counts]
+            ssplit = [int(x) for x in e.send_counts]
+            for it in range(ITERS):
+                c = it % e.num_colors
+                e.pre_exchange(c)
+                e.pack(send.data_ptr())
+                hs = send.cpu()  # D2H on the current stream: ordered after the pack
+                hr = torch.empty_like(recv, device="cpu")
+                dist.all_to_all_single(hr, hs, rsplit, ssplit)
+                recv.copy_(hr)  # H2D on the current stream: ordered before the update
+                e.update(c, recv.data_ptr())
         out = np.zeros(X0.size)
         e.get_X_into(out)
-        q.put((rank, out))
+        rc, rd = e.status()
+        q.put((rank, out, rc, rd))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("robust", ["L2", "GNC_TLS"])
 @pytest.mark.parametrize("accel", [False, True])
-def test_two_ranks_match_oracle(accel, robust):
+def test_two_ranks_bitwise_one_rank_and_oracle(accel, robust):
     """GNC_TLS: shared loop closures across the two ranks are reweighted by the lower-ID agent from
     the received neighbour poses (robust_opt_inner_iters = 3: reweightings at iterations 2 and 5)."""
     ctx = mp.get_context("spawn")
@@ -72,16 +85,32 @@ def test_two_ranks_match_oracle(accel, robust):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, accel, robust, q)) for r in range(2)]
     for p in procs:
         p.start()
-    outs = [q.get(timeout=240) for _ in range(2)]
+    outs = sorted([q.get(timeout=240) for _ in range(2)], key=lambda o: o[0])
     for p in procs:
         p.join(timeout=60)
     Xflat = outs[0][1] + outs[1][1]  # each rank wrote only its own poses into zeros
     from dpgo_amd import hip as H
     g = H.Graph.grid3d(K, seed=5)
+    aop = g.grid_partition(A)
+    X0 = g.chain_init(R, O.lifting_matrix(3, R))
+    # one rank, same schedule: bitwise the same poses and status
+    e1 = H.Rbcd(g, aop, np.zeros(A ** 3, np.int32), 0, 1, _params(H, accel, robust))
+    e1.set_X(X0)
+    for it in range(ITERS):
+        c = it % e1.num_colors
+        e1.pre_exchange(c)
+        e1.update(c, None)
+    X1 = np.zeros(X0.size)
+    e1.get_X_into(X1)
+    assert np.array_equal(Xflat, X1)
+    rc1, rd1 = e1.status()
+    ranks = (np.arange(A ** 3) * 2 // A ** 3)
+    for a in range(A ** 3):
+        rc, rd = outs[ranks[a]][2], outs[ranks[a]][3]
+        assert rc[a] == rc1[a] and rd[a] == rd1[a]
     a = g.arrays()
     meas = O.Measurements(3, np.zeros(g.m, np.int64), np.zeros(g.m, np.int64), a["p1"].astype(np.int64),
                           a["p2"].astype(np.int64), a["R"], a["t"], a["kappa"], a["tau"], np.ones(g.m), g.n)
-    X0 = g.chain_init(R, O.lifting_matrix(3, R))
-    Xo, _ = O.colour_rbcd(meas, g.grid_partition(A), A ** 3, X0, ITERS, R, acceleration=accel, robust=robust,
+    Xo, _ = O.colour_rbcd(meas, aop, A ** 3, X0, ITERS, R, acceleration=accel, robust=robust,
                           robust_opt_inner_iters=3)
     assert rel(H.from_dev_layout(Xflat, R), Xo) <= 1e-9

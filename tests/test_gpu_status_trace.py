@@ -1,0 +1,244 @@
+"""GPU parity of the per-iteration RTR trace, RGD, solver statistics, the engine's PGOAgent status and
+its central evaluation against the oracle (tests/ infrastructure only).
+
+References: ROPTLIB ITERRESULT trace (src/QuadraticOptimizer.cpp:82-86),
+QuadraticOptimizer::gradientDescent (src/QuadraticOptimizer.cpp:124-149), PGOAgent::iterate status
+(src/PGOAgent.cpp:700-716, 1247-1289), central evaluation (examples/MultiRobotExample.cpp:229-256)."""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import dpgo_oracle as O
+from tests._common import load_meas, random_point, rel
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hip():
+    from dpgo_amd import hip as H
+    assert H.device_count() >= 1
+    return H
+
+
+def _expected_records(trace):
+    """Oracle RTR trace -> the device's record sequence (tCG step test, tCG stopping test, rho test)."""
+    out = []
+    for outer in trace:
+        for t in outer["tcg"]:
+            st = dict(op=3, j=t["j"], d_Hd=t["d_Hd"], alpha=t["alpha"], Delta=outer["Delta"])
+            if "tau" in t:
+                st.update(tau=t["tau"], status=t["status"])
+            out.append(st)
+            if "norm_r" in t:
+                ck = dict(op=4, j=t["j"], norm_r=t["norm_r"])
+                if "status" in t:
+                    ck["status"] = t["status"]
+                else:
+                    ck.update(z_r=t["z_r"], beta=t["beta"])
+                out.append(ck)
+        out.append(dict(op=5, f1=outer["f1"], f2=outer["f2"], rho=outer["rho"], Delta=outer["Delta"],
+                        accepted=float(outer["accepted"]), ngf=outer["ngf"], status=outer["status"],
+                        alpha=outer["ninner"]))
+    return out
+
+
+def _close(a, b, tol):
+    return abs(a - b) <= tol * max(abs(b), 1e-300)
+
+
+@pytest.mark.parametrize("name,r,iters,tol,radius,inner", [
+    ("smallGrid3D", 5, 10, 1e-1, 10.0, 50),   # localPoseGraphOptimization (src/PGOAgent.cpp:975-984)
+    ("tinyGrid3D", 3, 10, 1e-1, 10.0, 50),
+    ("sphere2500", 3, 10, 1e-1, 10.0, 50),
+    ("smallGrid3D", 5, 1, 1e-2, 100.0, 10),   # updateX settings (:1131-1137)
+])
+@pytest.mark.parametrize("precon", ["bj", "exact"])
+def test_rtr_trace_matches_oracle(hip, name, r, iters, tol, radius, inner, precon):
+    """Every tCG step (d_Hd, alpha, tau, status), stopping test (|r|, <z, r>, beta, status) and rho test
+    (f1, f2, rho, Delta, accepted, |grad|, status, inner iterations) of the device RTR equals the
+    oracle's at 1e-10 relative (rho: cancellation-aware), in the same order."""
+    meas = load_meas(name)
+    d, n = meas.d, meas.num_poses
+    Q = O.connection_laplacian(meas, n)
+    P = O.QuadraticProblem(n, d, r)
+    P.set_Q(Q)
+    P.precon_mode = O.PRECON_BLOCK_JACOBI if precon == "bj" else O.PRECON_EXACT
+    X0 = O.lifting_matrix(d, r) @ O.chordal_initialization(d, n, meas)
+    trace = []
+    Xo, res = O.optimize(P, X0, O.OptParams(tr_iterations=iters, tr_tolerance=tol, tr_initial_radius=radius,
+                                            tr_max_inner=inner), trace)
+    H = hip.Problem(n, d, r)
+    H.set_Q_scipy(0, Q)
+    H.set_trace(4096)
+    p = hip.default_params(tr_iterations=iters, tr_tolerance=tol, tr_initial_radius=radius, tr_max_inner=inner,
+                           precon=hip.PRECON_BLOCK_JACOBI if precon == "bj" else hip.PRECON_EXACT)
+    Xh, rh = H.optimize(X0, p)
+    got = H.get_trace(0)
+    exp = _expected_records(trace)
+    assert len(exp) > 3
+    assert len(got) == len(exp)
+    for g, e in zip(got, exp):
+        assert int(g["op"]) == e["op"], (g, e)
+        for k, v in e.items():
+            if k in ("op",):
+                continue
+            if k in ("j", "status", "accepted"):
+                assert int(g[k]) == int(v), (k, g, e)
+            elif k == "rho":
+                # rho = (f1 - f2) / model decrease: the difference of two close costs loses digits
+                scale = 1e-10 + 1e-14 * abs(e["f1"]) / max(abs(e["f1"] - e["f2"]), 1e-300)
+                assert _close(g[k], v, scale), (k, g[k], v)
+            elif k == "alpha" and e["op"] == 5:
+                assert int(g[k]) == int(v)  # inner iterations of the Run
+            else:
+                assert _close(g[k], v, 1e-10), (k, g[k], v, e)
+    st = H.stats()[0]
+    runs = [t for t in trace]
+    assert st["calls"] == 1 and st["runs"] == len(runs)
+    assert st["tcg_iters"] == sum(t["ninner"] for t in runs)
+    for s, name_ in ((O.TCG_NEGCURVTURE, "NEGCURVTURE"), (O.TCG_EXCREGION, "EXCREGION"), (O.TCG_LCON, "LCON"),
+                     (O.TCG_SCON, "SCON"), (O.TCG_MAXITER, "MAXITER")):
+        assert st[name_] == sum(1 for t in runs if t["status"] == s)
+    assert rel(Xh, Xo) <= 1e-8
+
+
+@pytest.mark.parametrize("batched", [False, True])
+def test_rgd_matches_oracle(hip, batched):
+    """QuadraticOptimizer::gradientDescent (src/QuadraticOptimizer.cpp:124-149): one fixed-step (1e-3)
+    Riemannian gradient step with the QF retraction; X, fOpt, gradNormOpt and relativeChange."""
+    meas = load_meas("smallGrid3D")
+    d, r, n = 3, 5, meas.num_poses
+    Q = O.connection_laplacian(meas, n)
+    P = O.QuadraticProblem(n, d, r)
+    P.set_Q(Q)
+    Xs = [O.lifting_matrix(d, r) @ O.chordal_initialization(d, n, meas)]
+    if batched:
+        Xs += [random_point(r, d, n, 41), random_point(r, d, n, 42)]
+    H = hip.Problem(None, d, r, poses_per_agent=[n] * len(Xs))
+    for k in range(len(Xs)):
+        H.set_Q_scipy(k, Q)
+    p = hip.default_params(algorithm=hip.ALG_RGD, rgd_stepsize=1e-3)
+    Xh, rh = H.optimize(np.hstack(Xs), p)
+    b = d + 1
+    for k, X0 in enumerate(Xs):
+        Xo, ro = O.optimize(P, X0, O.OptParams(algorithm="RGD", rgd_stepsize=1e-3))
+        assert rel(Xh[:, k * n * b:(k + 1) * n * b], Xo) <= 1e-12
+        assert _close(rh[k]["fOpt"], ro["fOpt"], 1e-12)
+        assert _close(rh[k]["fInit"], ro["fInit"], 1e-12)
+        assert _close(rh[k]["gradNormOpt"], ro["gradNormOpt"], 1e-10)
+        assert _close(rh[k]["relativeChange"], ro["relativeChange"], 1e-10)
+
+
+def _grid_meas(hip, k, seed):
+    g = hip.Graph.grid3d(k, seed=seed)
+    a = g.arrays()
+    meas = O.Measurements(3, np.zeros(g.m, np.int64), np.zeros(g.m, np.int64), a["p1"].astype(np.int64),
+                          a["p2"].astype(np.int64), a["R"], a["t"], a["kappa"], a["tau"], np.ones(g.m), g.n)
+    return g, meas
+
+
+def _grid_outliers(hip, k, seed, frac, rng_seed):
+    g0 = hip.Graph.grid3d(k, seed=seed)
+    a = g0.arrays()
+    p1, p2 = a["p1"].astype(np.int64), a["p2"].astype(np.int64)
+    R, t = a["R"].copy(), a["t"].copy()
+    rng = np.random.default_rng(rng_seed)
+    lc = np.nonzero(np.abs(p2 - p1) != 1)[0]
+    bad = rng.choice(lc, size=max(1, int(frac * len(lc))), replace=False)
+    t[bad] += rng.normal(0.0, 5.0, size=(len(bad), 3))
+    g = hip.Graph.from_arrays(3, g0.n, p1, p2, R, t, a["kappa"], a["tau"])
+    meas = O.Measurements(3, np.zeros(len(p1), np.int64), np.zeros(len(p1), np.int64), p1, p2, R, t,
+                          a["kappa"], a["tau"], np.ones(len(p1)), g0.n)
+    return g, g0, meas
+
+
+@pytest.mark.parametrize("accel,robust,alg", [(False, "L2", "RTR"), (True, "L2", "RTR"), (True, "GNC_TLS", "RTR"),
+                                              (False, "L2", "RGD"), (True, "L2", "RGD")])
+def test_engine_status_and_counters_match_oracle(hip, accel, robust, alg):
+    """Per selected agent: PGOAgentStatus relativeChange = |X - XPrev| / sqrt(n) and readyToTerminate
+    (relChangeTol 5e-3; GNC_TLS: converged loop-closure ratio >= 0.8) after every iteration, and the
+    cumulative solver counters (Runs, tCG iterations and exits) over the run, against the oracle's
+    PGOAgent colour schedule (RGD: src/PGOAgent.cpp:1133, QuadraticOptimizer::gradientDescent)."""
+    k, A, r = 6, 2, 5
+    if robust == "L2":
+        g, meas = _grid_meas(hip, k, 3)
+        g0 = g
+    else:
+        g, g0, meas = _grid_outliers(hip, k, 3, 0.1, 7)
+    aop = g0.grid_partition(A)
+    X0 = g0.chain_init(r, O.lifting_matrix(3, r))
+    e = hip.Rbcd(g, aop, np.zeros(A ** 3, np.int32), 0, 1,
+                 hip.rbcd_params(r=r, acceleration=int(accel), robust_cost=hip.ROBUST[robust], robust_opt_inner_iters=3,
+                                 algorithm=hip.ALG_RTR if alg == "RTR" else hip.ALG_RGD))
+    e.set_X(X0)
+    iters = 7
+    agents, trace = [], []
+    Xo, colors = O.colour_rbcd(meas, aop, A ** 3, X0, iters, r, acceleration=accel, robust=robust,
+                               robust_opt_inner_iters=3, agents_out=agents, trace=trace, algorithm=alg)
+    # the oracle replays the schedule in one go; compare the final status of every agent (the status of
+    # its last selected iteration) and the counters accumulated over the whole run
+    for it in range(iters):
+        c = it % e.num_colors
+        e.pre_exchange(c)
+        e.update(c, None)
+    out = np.zeros(X0.size)
+    e.get_X_into(out)
+    assert rel(hip.from_dev_layout(out, r), Xo) <= 1e-9
+    rc, rd = e.status()
+    for a, ag in enumerate(agents):
+        assert _close(rc[a], ag.status_relative_change, 1e-8), (a, rc[a], ag.status_relative_change)
+        assert bool(rd[a]) == bool(ag.ready_to_terminate), a
+    st = e.stats()
+    # oracle per-agent counters from its trace: RTR outer records then (it, agent, result) per update
+    runs = np.zeros(A ** 3, int)
+    inner = np.zeros(A ** 3, int)
+    pending = []
+    for t in trace:
+        if isinstance(t, tuple):
+            a = t[1]
+            runs[a] += len(pending)
+            inner[a] += sum(p["ninner"] for p in pending)
+            pending = []
+        else:
+            pending.append(t)
+    if alg == "RTR":
+        assert list(st[:, 2]) == list(runs)
+        assert list(st[:, 3]) == list(inner)
+    assert list(st[:, 0]) == [sum(1 for t in trace if isinstance(t, tuple) and t[1] == a) for a in range(A ** 3)]
+    if robust == "GNC_TLS":
+        ratios = [ag.converged_loop_closure_ratio() for ag in agents]
+        assert min(ratios) < 1.0  # the reweighting decided some loop closures (ratio is exercised)
+
+
+def test_central_eval_matches_oracle(hip):
+    """Central cost and per-agent |RieGrad|^2 of the whole graph at the engine's X
+    (examples/MultiRobotExample.cpp:229-235, 243-256)."""
+    k, A, r = 6, 2, 5
+    g, meas = _grid_meas(hip, k, 4)
+    aop = g.grid_partition(A)
+    X0 = g.chain_init(r, O.lifting_matrix(3, r))
+    e = hip.Rbcd(g, aop, np.zeros(A ** 3, np.int32), 0, 1, hip.rbcd_params(r=r, acceleration=1))
+    e.set_X(X0)
+    for it in range(3):
+        e.pre_exchange(it % 2)
+        e.update(it % 2, None)
+    f, gn = e.central_eval()
+    out = np.zeros(X0.size)
+    e.get_X_into(out)
+    X = hip.from_dev_layout(out, r)
+    assert _close(f, O.central_cost(meas, X), 1e-11)
+    Qc = O.connection_laplacian(meas, g.n)
+    RG = O.tangent_project(X, np.asarray((Qc @ X.T).T), 3)
+    b = 4
+    for a in range(A ** 3):
+        cols = np.concatenate([np.arange(p * b, (p + 1) * b) for p in np.nonzero(aop == a)[0]])
+        assert _close(gn[a], float(np.sum(RG[:, cols] ** 2)), 1e-10)
+    # the evaluation changes nothing: continuing gives the oracle's trajectory
+    for it in range(3, 6):
+        e.pre_exchange(it % 2)
+        e.update(it % 2, None)
+    e.get_X_into(out)
+    Xo, _ = O.colour_rbcd(meas, aop, A ** 3, X0, 6, r, acceleration=True)
+    assert rel(hip.from_dev_layout(out, r), Xo) <= 1e-9

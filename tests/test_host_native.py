@@ -38,6 +38,15 @@ def test_library_exports_every_declared_symbol(H):
     assert set(H.EXPORTED_SYMBOLS) <= exported
 
 
+def test_library_built_from_this_tree(H):
+    """The loaded libdpgo_hip.so carries the sha256 of the sources it was compiled from; it must be
+    this tree's (a stale binary shipped beside newer sources fails here, on the CPU and on the box)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as G
+    assert H.build_id() == G.source_hash()
+
+
 def test_no_cpu_fallback_without_device(H):
     if H.device_count() > 0:
         pytest.skip("a GPU is visible")
