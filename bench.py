@@ -64,6 +64,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--init", default="chordal", choices=["chordal", "odometry"],
+                    help="initial X: chordalInitialization (examples/MultiRobotExample.cpp:158; PCG on the GPU) "
+                         "or the odometry chain")
     ap.add_argument("--burnin", type=int, default=0, help="untimed steps before the timed run's set_X")
     ap.add_argument("--k", type=int, default=100, help="grid side (k^3 poses)")
     ap.add_argument("--agents-per-axis", type=int, default=4)
@@ -111,7 +114,14 @@ def main():
     stream = torch.cuda.Stream(dev)
     eng.set_stream(stream.cuda_stream)
     YLift = H.lifting_matrix(3, args.r)
-    X0 = g.chain_init_dev_layout(args.r, YLift)
+    t_init = time.time()
+    init_info = {"kind": args.init}
+    if args.init == "chordal":
+        X0, it, rr = g.chordal_init_gpu(args.r, YLift, rtol=1e-10, max_iters=50000, dev_layout=True)
+        init_info.update(pcg_iterations=it, pcg_relres=rr)
+    else:
+        X0 = g.chain_init_dev_layout(args.r, YLift)
+    init_info["seconds"] = time.time() - t_init
     eng.set_X(X0)
     send = torch.empty(max(int(eng.send_counts.sum()), 1), dtype=torch.float64, device=dev)
     recv = torch.empty(max(int(eng.recv_counts.sum()), 1), dtype=torch.float64, device=dev)
@@ -251,7 +261,8 @@ def main():
         "config": {"workload": f"grid3d k={args.k} ({args.k ** 3} poses), r={args.r}, "
                                f"{num_agents} agents ({A}^3 sub-cubes), Nesterov={bool(args.accel)}, "
                                f"{args.robust} cost, colour schedule ({eng.num_colors} colours), "
-                               f"RTR 1x10 tCG, block-Jacobi precond, agent status on, burn-in {args.burnin} steps",
+                               f"RTR 1x10 tCG, block-Jacobi precond, agent status on, {args.init} init, "
+                               f"burn-in {args.burnin} steps",
                    "poses": g.n, "edges": g.m, "agents": num_agents, "parallelism": par},
         "rounds_per_s": args.steps / elapsed,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -287,6 +298,7 @@ def main():
         "central": {"f_start": f_start, "gradnorm_start": gn_start, "f_end": f_end, "gradnorm_end": gn_end,
                     "steps_between": args.warmup + args.steps},
         "setup_s": setup_s,
+        "init": init_info,
     }
     if X_start is not None:
         try:

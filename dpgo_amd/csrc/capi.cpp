@@ -62,6 +62,7 @@ dpgo::LaunchCtx make_ctx(dpgo_hip_problem h, int flag_kind, double* partials) {
   c.state = h->state.p;
   c.partials = partials;
   c.stream = h->stream;
+  c.round = 0;
   return c;
 }
 
@@ -755,7 +756,8 @@ int dpgo_hip_problem_create_batch(int num_agents, const int* poses_per_agent, in
   if (h->tile_agent.ensure(T) || h->tile_start.ensure(T) || h->tile_count.ensure(T) ||
       h->agent_tile_off.ensure(num_agents + 1) || h->agent_np.ensure(num_agents) ||
       h->enabled.ensure(num_agents) || h->use_a.ensure(num_agents) || h->pa.ensure(static_cast<size_t>(T) * dpgo::kPartialStride) ||
-      h->pb.ensure(static_cast<size_t>(T) * dpgo::kPartialStride) || h->sums.ensure(static_cast<size_t>(num_agents) * 4) ||
+      h->pb.ensure(static_cast<size_t>(T) * dpgo::kPartialStride) || h->pc.ensure(static_cast<size_t>(T) * dpgo::kPartialStride) ||
+      h->sums.ensure(static_cast<size_t>(num_agents) * 4) ||
       h->state.ensure(num_agents) || h->coef_a.ensure(num_agents) || h->coef_b.ensure(num_agents) ||
       h->arrive.ensure(num_agents))
     return cleanup(fail(DPGO_HIP_ENOMEM, "device allocation failed"));
@@ -1078,16 +1080,18 @@ int dpgo_hip_optimize_dev(dpgo_hip_problem h, const dpgo_opt_params* params, con
 namespace {
 // PGOAgent status pass (src/PGOAgent.cpp:700-716): |X_out - XPrev|^2 per agent, then OP_STATUS.
 // pa already holds |X_out - st->ref|^2 when `have_partials` (the final select compared against ref).
+// `partials`: |X_out - st.ref|^2 per tile already there (nullptr: computed here into pa)
 int status_pass(dpgo_hip_problem h, const double* X_out, const dpgo::StatusArgs& st, const dpgo::OptScalars& o0,
-                bool have_partials) {
-  if (!have_partials) {
+                const double* partials) {
+  if (!partials) {
     auto c = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
     HIP_TRY(dpgo::launch_sqdiff(h->r, h->b, c, X_out, st.ref));
+    partials = h->pa.p;
   }
   dpgo::OptScalars o = o0;
   o.rel_tol = st.rel_tol;
   o.min_ratio = st.min_ratio;
-  dpgo::FinalizeArgs f = make_fin(h, dpgo::OP_STATUS, h->pa.p, 1, nullptr, 0, &o);
+  dpgo::FinalizeArgs f = make_fin(h, dpgo::OP_STATUS, partials, 1, nullptr, 0, &o);
   f.conv_ratio = st.conv_ratio;
   HIP_TRY(dpgo::launch_finalize(f, h->K, h->stream));
   return DPGO_HIP_OK;
@@ -1166,11 +1170,11 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     const bool want = results != nullptr || P.verbose;
     if (st && st->ref == X_in && !want) {  // one pass: X_out = x2 and |X_out - XPrev|^2
       HIP_TRY(dpgo::launch_select(r, b, cs, h->x2.p, x1, h->use_a.p, x1, X_out));
-      return status_pass(h, X_out, *st, o, true);
+      return status_pass(h, X_out, *st, o, h->pa.p);
     }
     HIP_TRY(dpgo::launch_select(r, b, cs, h->x2.p, x1, h->use_a.p, x1, X_out));
     if (want) DPGO_TRY(finalize(h, dpgo::OP_REL_CHANGE, h->pa.p, 1, nullptr, 0));
-    if (st) DPGO_TRY(status_pass(h, X_out, *st, o, false));
+    if (st) DPGO_TRY(status_pass(h, X_out, *st, o, nullptr));
     if (!want) return DPGO_HIP_OK;
     DPGO_TRY(eval_at(h, X_out, h->g2.p, h->S2.p, h->pb.p, dpgo::FLAG_NONE));
     DPGO_TRY(finalize(h, dpgo::OP_SUM, h->pb.p, 2, nullptr, 0));
@@ -1321,9 +1325,11 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
       auto ca = make_ctx(h, dpgo::FLAG_NONE, nullptr);
       HIP_TRY(dpgo::launch_accept(r, b, ca, h->x2.p, h->g2.p, h->S2.p, h->x1.p, h->g.p, h->S.p));
     } else if (!direct) {
-      // speculative output: X_out = accepted ? x2 : X_in (repeated after a retry Run; agents that are
-      // done skip nothing here, rejected ones copy their unchanged input)
-      auto cs = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
+      // speculative output, queued before the host knows whether another Run follows: the agents whose
+      // outcome this Run decided write X_out = accepted ? x2 : X_in, once (X_out may alias X_in), and
+      // their |X_out - X_in|^2 partials into pc; agents that retry are written by a later Run
+      auto cs = make_ctx(h, dpgo::FLAG_DECIDED, h->pc.p);
+      cs.round = round;
       HIP_TRY(dpgo::launch_select(r, b, cs, h->x2.p, X_in, nullptr, X_in, X_out));
     } else {
       // x2 already sits in X_out: agents that did not move take X_in (queued before the retry
@@ -1338,19 +1344,19 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     }
   }
   // X_out: accepted candidate or the input (single Run), x1 (multi-iteration)
-  auto cs = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
+  auto cs = make_ctx(h, dpgo::FLAG_NONE, h->pc.p);
   if (!single) {
     HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(h->use_a.p), 1, K, h->stream));
     HIP_TRY(dpgo::launch_select(r, b, cs, x1, X_in, h->use_a.p, X_in, X_out));
   }
   const bool want = results != nullptr || P.verbose;
-  // QuadraticOptimizer relativeChange against the input (the last select's partials, ref X_in)
-  if (want) DPGO_TRY(finalize(h, dpgo::OP_REL_CHANGE, h->pa.p, 1, nullptr, 0));
+  // QuadraticOptimizer relativeChange against the input (the output select's partials, ref X_in)
+  if (want) DPGO_TRY(finalize(h, dpgo::OP_REL_CHANGE, h->pc.p, 1, nullptr, 0));
   if (st) {
-    // the last select (FLAG_NONE over every tile, ref X_in) left |X_out - X_in|^2 in pa: reuse it
-    // when the status reference is X_in itself (an in-place update without acceleration)
+    // the output select left |X_out - X_in|^2 in pc: reuse it when the status reference is X_in
+    // itself (an in-place update without acceleration)
     const bool reuse = st->ref == X_in && !direct;
-    DPGO_TRY(status_pass(h, X_out, *st, o, reuse));
+    DPGO_TRY(status_pass(h, X_out, *st, o, reuse ? h->pc.p : nullptr));
   }
   if (!want) return DPGO_HIP_OK;  // no host round trip needed
   DPGO_TRY(download_state(h));

@@ -450,6 +450,41 @@ int dpgo_graph_chordal_init(dpgo_graph g, int r, const double* YLift, double* X_
   return DPGO_HIP_OK;
 }
 
+int dpgo_chordal_initialization_gpu(int d, int n, int m, const int* p1, const int* p2, const double* R,
+                                    const double* t, const double* kappa, const double* tau, double rtol,
+                                    int max_iters, double* T_out, int* iters, double* relres) {
+  if ((d != 2 && d != 3) || n <= 0 || m < 0 || !T_out || (m > 0 && (!p1 || !p2 || !R || !t || !kappa || !tau)) ||
+      !(rtol > 0.0) || max_iters < 1)
+    return fail(DPGO_HIP_EINVAL, "bad chordal initialisation arguments");
+  for (int e = 0; e < m; ++e)
+    if (p1[e] < 0 || p1[e] >= n || p2[e] < 0 || p2[e] >= n || p1[e] == p2[e])
+      return fail(DPGO_HIP_EINVAL, "edge endpoint out of range");
+  if (usable_devices() == 0) return fail(DPGO_HIP_ENODEV, "no gfx950 device available (no CPU fallback)");
+  std::string err;
+  if (dpgo::chordal_initialization_gpu(d, n, m, p1, p2, R, t, kappa, tau, T_out, rtol, max_iters, iters, relres,
+                                       err) != 0)
+    return fail(DPGO_HIP_EDEVICE, err);
+  return DPGO_HIP_OK;
+}
+
+int dpgo_graph_chordal_init_gpu(dpgo_graph g, int r, const double* YLift, double rtol, int max_iters,
+                                double* X_out, int* iters, double* relres) {
+  if (!g || !YLift || !X_out) return fail(DPGO_HIP_EINVAL, "null argument");
+  const int d = g->d, b = d + 1, n = g->n;
+  std::vector<double> T(static_cast<size_t>(n) * d * b);
+  DPGO_TRY(dpgo_chordal_initialization_gpu(d, n, static_cast<int>(g->p1.size()), g->p1.data(), g->p2.data(),
+                                           g->R.data(), g->t.data(), g->kappa.data(), g->tau.data(), rtol, max_iters,
+                                           T.data(), iters, relres));
+  for (int p = 0; p < n; ++p)
+    for (int c = 0; c < b; ++c)
+      for (int a = 0; a < r; ++a) {
+        double acc = 0.0;
+        for (int u = 0; u < d; ++u) acc += YLift[u * r + a] * T[(static_cast<size_t>(p) * b + c) * d + u];
+        X_out[(static_cast<size_t>(p) * b + c) * r + a] = acc;
+      }
+  return DPGO_HIP_OK;
+}
+
 int dpgo_graph_chain_init(dpgo_graph g, int r, const double* YLift, double* X_out) {
   if (!g || !YLift || !X_out) return fail(DPGO_HIP_EINVAL, "null argument");
   const int d = g->d, b = d + 1, n = g->n;

@@ -37,5 +37,9 @@ void edge_blocks(int d, const double* R, const double* t, double kappa, double t
 // chordalInitialization (src/DPGO_utils.cpp:377-424), init.cpp: T_out d x (d+1) n column-major
 int chordal_initialization(int d, int n, int m, const int* p1, const int* p2, const double* R, const double* t,
                            const double* kappa, const double* tau, double* T_out, std::string& err);
+// same minimiser, both linear solves by Jacobi-PCG on the GPU (|r| <= rtol |b| per right-hand side)
+int chordal_initialization_gpu(int d, int n, int m, const int* p1, const int* p2, const double* R, const double* t,
+                               const double* kappa, const double* tau, double* T_out, double rtol, int max_iters,
+                               int* iters, double* relres, std::string& err);
 
 }  // namespace dpgo

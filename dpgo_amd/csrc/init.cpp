@@ -1,10 +1,12 @@
 // Chordal initialisation (chordalInitialization, src/DPGO_utils.cpp:377-424; used by
-// PGOAgent::localInitialization for the L2 cost, src/PGOAgent.cpp:947-962).  The reference solves the
-// two linear least-squares problems with SPQR; here their normal equations -- a d x d block
-// connection Laplacian for the rotations (R_0 = I fixed) and a scalar graph Laplacian for the
-// translations (t_0 = 0) -- are factorised by the host block Cholesky (chol.cpp).  Same unique
-// minimiser (connected graph); rotations are projected to SO(d) as projectToRotationGroup
-// (:478-492).  One-time host work, like the reference's.
+// PGOAgent::localInitialization for the L2 cost, src/PGOAgent.cpp:947-962, and by
+// examples/MultiRobotExample.cpp:158).  The reference solves the two linear least-squares problems
+// with SPQR; here their normal equations -- a d x d block connection Laplacian for the rotations
+// (R_0 = I fixed) and a scalar graph Laplacian for the translations (t_0 = 0) -- are solved either by
+// the host block Cholesky (chol.cpp, exact) or, for graphs whose factor would not fit (10^6-pose 3D
+// grids: the top separator alone is a dense 3*10^4 square), by Jacobi-preconditioned CG on the GPU to
+// a relative residual tolerance.  Same unique minimiser (connected graph); rotations are projected to
+// SO(d) as projectToRotationGroup (:478-492).
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -19,30 +21,96 @@ namespace dpgo {
 
 namespace {
 
-// symmetric block matrix as BSR (block (j, i) column-major) from a map of row-major blocks
-struct SymBlocks {
-  int n, b;
-  std::vector<std::map<int, std::vector<double>>> rows;
-  SymBlocks(int n_, int b_) : n(n_), b(b_), rows(n_) {}
-  double* at(int i, int j) {  // block (i, j), row-major
-    auto& blk = rows[i][j];
-    if (blk.empty()) blk.assign(static_cast<size_t>(b) * b, 0.0);
-    return blk.data();
+// Symmetric block-sparse system over free poses, rows sorted by column with duplicates merged:
+// block (j, col[k]) row-major bs x bs.  Assembled in O(entries) by counting, not by maps (the
+// device path runs 10^6-pose graphs).
+struct BlockSys {
+  int n = 0, bs = 0;
+  std::vector<int> rowptr, col;
+  std::vector<double> blk;
+};
+
+// Edge list of the system: per edge its two free rows (-1 = the fixed anchor) and per edge the blocks
+// Bii (row i), Bjj (row j), Bij (i, j) -- Bji = Bij^T.
+struct SysBuilder {
+  int n, bs;
+  std::vector<int> ei, ej;
+  std::vector<double> bii, bjj, bij;
+  SysBuilder(int n_, int bs_) : n(n_), bs(bs_) {}
+  void add(int i, int j, const double* Bii, const double* Bjj, const double* Bij) {
+    const int b2 = bs * bs;
+    ei.push_back(i);
+    ej.push_back(j);
+    bii.insert(bii.end(), Bii, Bii + b2);
+    bjj.insert(bjj.end(), Bjj, Bjj + b2);
+    bij.insert(bij.end(), Bij, Bij + b2);
   }
-  void to_bsr(std::vector<int>& rowptr, std::vector<int>& col, std::vector<double>& blocks) const {
-    rowptr.assign(n + 1, 0);
-    col.clear();
-    blocks.clear();
-    for (int j = 0; j < n; ++j) {
-      for (const auto& [i, blk] : rows[j]) {  // block (j, i) row-major -> column-major
-        col.push_back(i);
-        for (int v = 0; v < b; ++v)
-          for (int u = 0; u < b; ++u) blocks.push_back(blk[u * b + v]);
+  void build(BlockSys& S) const {
+    const int b2 = bs * bs;
+    const size_t m = ei.size();
+    S.n = n;
+    S.bs = bs;
+    std::vector<int> cnt(n + 1, 0);
+    for (int j = 0; j < n; ++j) cnt[j + 1] = 1;  // diagonal
+    for (size_t e = 0; e < m; ++e)
+      if (ei[e] >= 0 && ej[e] >= 0) {
+        ++cnt[ei[e] + 1];
+        ++cnt[ej[e] + 1];
       }
-      rowptr[j + 1] = static_cast<int>(col.size());
+    for (int j = 0; j < n; ++j) cnt[j + 1] += cnt[j];
+    std::vector<int> c(cnt[n]);
+    std::vector<double> b(static_cast<size_t>(cnt[n]) * b2, 0.0);
+    std::vector<int> fill(cnt.begin(), cnt.end() - 1);
+    for (int j = 0; j < n; ++j) c[fill[j]++] = j;
+    for (size_t e = 0; e < m; ++e) {
+      const int i = ei[e], j = ej[e];
+      if (i >= 0) {  // diagonal of row i: first entry of the row, summed in edge order
+        double* D = &b[static_cast<size_t>(cnt[i]) * b2];
+        for (int x = 0; x < b2; ++x) D[x] += bii[e * b2 + x];
+      }
+      if (j >= 0) {
+        double* D = &b[static_cast<size_t>(cnt[j]) * b2];
+        for (int x = 0; x < b2; ++x) D[x] += bjj[e * b2 + x];
+      }
+      if (i >= 0 && j >= 0) {
+        const int ki = fill[i]++, kj = fill[j]++;
+        c[ki] = j;
+        c[kj] = i;
+        for (int u = 0; u < bs; ++u)
+          for (int v = 0; v < bs; ++v) {
+            b[static_cast<size_t>(ki) * b2 + u * bs + v] = bij[e * b2 + u * bs + v];
+            b[static_cast<size_t>(kj) * b2 + v * bs + u] = bij[e * b2 + u * bs + v];
+          }
+      }
+    }
+    // sort each row by column and merge repeated (i, j) pairs (duplicate measurements)
+    S.rowptr.assign(n + 1, 0);
+    S.col.clear();
+    S.blk.clear();
+    S.col.reserve(c.size());
+    S.blk.reserve(b.size());
+    std::vector<int> idx;
+    for (int j = 0; j < n; ++j) {
+      idx.resize(cnt[j + 1] - cnt[j]);
+      for (size_t x = 0; x < idx.size(); ++x) idx[x] = cnt[j] + static_cast<int>(x);
+      std::stable_sort(idx.begin(), idx.end(), [&](int a, int bb) { return c[a] < c[bb]; });
+      for (size_t x = 0; x < idx.size(); ++x) {
+        const int k = idx[x];
+        if (!S.col.empty() && static_cast<int>(S.col.size()) > S.rowptr[j] && S.col.back() == c[k]) {
+          double* dst = &S.blk[S.blk.size() - b2];
+          for (int y = 0; y < b2; ++y) dst[y] += b[static_cast<size_t>(k) * b2 + y];
+        } else {
+          S.col.push_back(c[k]);
+          S.blk.insert(S.blk.end(), &b[static_cast<size_t>(k) * b2], &b[static_cast<size_t>(k) * b2] + b2);
+        }
+      }
+      S.rowptr[j + 1] = static_cast<int>(S.col.size());
     }
   }
 };
+
+// Direct solve with the host block Cholesky (blocks handed over column-major); rhs [row][bs][nr]
+int solve_direct(const BlockSys& S, int nr, std::vector<double>& rhs_x, std::string& err);
 
 // Solve (L L^T) x = rhs in place; rhs indexed by the ORIGINAL pose order, b values per pose.
 void chol_solve(const BlockCholesky& L, std::vector<double>& rhs) {
@@ -144,10 +212,156 @@ void project_rotation(int d, const double* M, double* out) {
     }
 }
 
-}  // namespace
+int solve_direct(const BlockSys& S, int nr, std::vector<double>& rhs_x, std::string& err) {
+  const int bs = S.bs, b2 = bs * bs, n = S.n;
+  std::vector<double> cm(S.blk.size());
+  for (size_t k = 0; k < S.col.size(); ++k)
+    for (int u = 0; u < bs; ++u)
+      for (int v = 0; v < bs; ++v) cm[k * b2 + v * bs + u] = S.blk[k * b2 + u * bs + v];
+  BlockCholesky L;
+  if (block_cholesky(n, bs, S.rowptr, S.col, cm, 0.0, 200u * 1000u * 1000u, L, err) != 0) return -1;
+  for (int a = 0; a < nr; ++a) {
+    std::vector<double> x(static_cast<size_t>(n) * bs);
+    for (int p = 0; p < n; ++p)
+      for (int v = 0; v < bs; ++v) x[static_cast<size_t>(p) * bs + v] = rhs_x[(static_cast<size_t>(p) * bs + v) * nr + a];
+    chol_solve(L, x);
+    for (int p = 0; p < n; ++p)
+      for (int v = 0; v < bs; ++v) rhs_x[(static_cast<size_t>(p) * bs + v) * nr + a] = x[static_cast<size_t>(p) * bs + v];
+  }
+  return 0;
+}
 
-int chordal_initialization(int d, int n, int m, const int* p1, const int* p2, const double* R, const double* t,
-                           const double* kappa, const double* tau, double* T_out, std::string& err) {
+// Jacobi-PCG on the device (one independent CG per right-hand side, advanced together): stops when
+// every right-hand side's |r| <= rtol |b| or after max_iters iterations.
+struct PcgReport {
+  int iters = 0;
+  double relres = 0.0;
+};
+
+int solve_pcg(const BlockSys& S, int nr, std::vector<double>& rhs_x, double rtol, int max_iters, PcgReport& rep,
+              std::string& err) {
+  const int bs = S.bs, b2 = bs * bs, n = S.n;
+  const size_t L = static_cast<size_t>(n) * bs * nr;
+  // block-Jacobi: inverse of each row's diagonal block (Gauss-Jordan, partial pivoting)
+  std::vector<double> minv(static_cast<size_t>(n) * b2, 0.0);
+  for (int j = 0; j < n; ++j) {
+    double A[3][6] = {{0}};
+    for (int k = S.rowptr[j]; k < S.rowptr[j + 1]; ++k)
+      if (S.col[k] == j)
+        for (int u = 0; u < bs; ++u)
+          for (int v = 0; v < bs; ++v) A[u][v] = S.blk[static_cast<size_t>(k) * b2 + u * bs + v];
+    for (int u = 0; u < bs; ++u) A[u][bs + u] = 1.0;
+    for (int c = 0; c < bs; ++c) {
+      int piv = c;
+      for (int u = c + 1; u < bs; ++u)
+        if (std::fabs(A[u][c]) > std::fabs(A[piv][c])) piv = u;
+      for (int v = 0; v < 2 * bs; ++v) std::swap(A[c][v], A[piv][v]);
+      if (A[c][c] == 0.0) {
+        err = "singular diagonal block (is the pose graph connected?)";
+        return -1;
+      }
+      const double inv = 1.0 / A[c][c];
+      for (int v = 0; v < 2 * bs; ++v) A[c][v] *= inv;
+      for (int u = 0; u < bs; ++u)
+        if (u != c) {
+          const double f = A[u][c];
+          for (int v = 0; v < 2 * bs; ++v) A[u][v] -= f * A[c][v];
+        }
+    }
+    for (int u = 0; u < bs; ++u)
+      for (int v = 0; v < bs; ++v) minv[static_cast<size_t>(j) * b2 + u * bs + v] = A[u][bs + v];
+  }
+  hipStream_t st = nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+    err = "stream create failed";
+    return -1;
+  }
+  struct StreamGuard {
+    hipStream_t s;
+    ~StreamGuard() {
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+    }
+  } guard{st};
+  DevBuf<int> drp, dcol;
+  DevBuf<double> dblk, dminv, x, r, z, pv, q, part;
+  const int P2 = kPcgBlocks * 2 * nr;
+  auto bad = [&](hipError_t e) {
+    if (e == hipSuccess) return false;
+    err = std::string("device: ") + hipGetErrorString(e);
+    return true;
+  };
+  if (bad(drp.ensure(n + 1)) || bad(dcol.ensure(S.col.size())) || bad(dblk.ensure(S.blk.size())) ||
+      bad(dminv.ensure(minv.size())) || bad(x.ensure(L)) || bad(r.ensure(L)) || bad(z.ensure(L)) ||
+      bad(pv.ensure(L)) || bad(q.ensure(L)) || bad(part.ensure(P2)))
+    return -1;
+  if (bad(hipMemcpyAsync(drp.p, S.rowptr.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice, st)) ||
+      bad(hipMemcpyAsync(dcol.p, S.col.data(), sizeof(int) * S.col.size(), hipMemcpyHostToDevice, st)) ||
+      bad(hipMemcpyAsync(dblk.p, S.blk.data(), sizeof(double) * S.blk.size(), hipMemcpyHostToDevice, st)) ||
+      bad(hipMemcpyAsync(dminv.p, minv.data(), sizeof(double) * minv.size(), hipMemcpyHostToDevice, st)) ||
+      bad(hipMemcpyAsync(r.p, rhs_x.data(), sizeof(double) * L, hipMemcpyHostToDevice, st)) ||
+      bad(hipMemsetAsync(x.p, 0, sizeof(double) * L, st)) || bad(hipMemsetAsync(q.p, 0, sizeof(double) * L, st)) ||
+      bad(hipMemsetAsync(pv.p, 0, sizeof(double) * L, st)))
+    return -1;
+  std::vector<double> hp(P2);
+  auto sums = [&](int q2, std::vector<double>& out) -> bool {  // fixed-order host sum of the partials
+    if (bad(hipMemcpyAsync(hp.data(), part.p, sizeof(double) * kPcgBlocks * q2, hipMemcpyDeviceToHost, st)) ||
+        bad(hipStreamSynchronize(st)))
+      return false;
+    out.assign(q2, 0.0);
+    for (int g = 0; g < kPcgBlocks; ++g)
+      for (int a = 0; a < q2; ++a) out[a] += hp[static_cast<size_t>(g) * q2 + a];
+    return true;
+  };
+  PcgCoef zero{{0.0, 0.0, 0.0}};
+  // x = 0, r = b: z = Minv r and <r, z>, |r|^2 (the update with alpha = 0); p = z
+  if (bad(launch_pcg_update(bs, nr, n, zero, pv.p, q.p, x.p, r.p, z.p, dminv.p, part.p, st))) return -1;
+  std::vector<double> s2, rz(nr), bn(nr);
+  if (!sums(2 * nr, s2)) return -1;
+  for (int a = 0; a < nr; ++a) {
+    rz[a] = s2[a];
+    bn[a] = std::sqrt(s2[nr + a]);
+  }
+  if (bad(launch_pcg_dir(bs, nr, n, zero, z.p, pv.p, st))) return -1;
+  rep.iters = 0;
+  rep.relres = 0.0;
+  for (int a = 0; a < nr; ++a) rep.relres = std::max(rep.relres, bn[a] > 0 ? 1.0 : 0.0);
+  while (rep.relres > rtol && rep.iters < max_iters) {
+    if (bad(launch_pcg_spmv(bs, nr, n, drp.p, dcol.p, dblk.p, pv.p, q.p, st)) ||
+        bad(launch_pcg_dot(bs, nr, n, pv.p, q.p, part.p, st)))
+      return -1;
+    std::vector<double> pq;
+    if (!sums(nr, pq)) return -1;
+    PcgCoef al = zero;
+    for (int a = 0; a < nr; ++a) al.v[a] = (bn[a] > 0 && pq[a] != 0.0) ? rz[a] / pq[a] : 0.0;
+    if (bad(launch_pcg_update(bs, nr, n, al, pv.p, q.p, x.p, r.p, z.p, dminv.p, part.p, st))) return -1;
+    if (!sums(2 * nr, s2)) return -1;
+    PcgCoef be = zero;
+    rep.relres = 0.0;
+    for (int a = 0; a < nr; ++a) {
+      if (bn[a] > 0) rep.relres = std::max(rep.relres, std::sqrt(s2[nr + a]) / bn[a]);
+      be.v[a] = (bn[a] > 0 && rz[a] != 0.0) ? s2[a] / rz[a] : 0.0;
+      rz[a] = s2[a];
+    }
+    ++rep.iters;
+    if (bad(launch_pcg_dir(bs, nr, n, be, z.p, pv.p, st))) return -1;
+  }
+  if (bad(hipMemcpyAsync(rhs_x.data(), x.p, sizeof(double) * L, hipMemcpyDeviceToHost, st)) || bad(hipStreamSynchronize(st)))
+    return -1;
+  if (!(rep.relres <= rtol)) {
+    err = "PCG did not reach the tolerance (relative residual " + std::to_string(rep.relres) + " after " +
+          std::to_string(rep.iters) + " iterations)";
+    return -1;
+  }
+  return 0;
+}
+
+// chordalInitialization with the linear solves done by `solver`: rotations (d x d block connection
+// Laplacian, d right-hand sides = the rows of R, R_0 = I) then translations (scalar Laplacian, d
+// right-hand sides, t_0 = 0), as the two SPQR solves of the reference (:377-476).
+template <typename Solver>
+int chordal_core(int d, int n, int m, const int* p1, const int* p2, const double* R, const double* t,
+                 const double* kappa, const double* tau, double* T_out, Solver&& solve, std::string& err) {
   if (n < 1) {
     err = "chordal initialisation: no poses";
     return -1;
@@ -156,60 +370,42 @@ int chordal_initialization(int d, int n, int m, const int* p1, const int* p2, co
   std::vector<double> Rch(static_cast<size_t>(n) * d2, 0.0);  // R_i row-major per pose
   for (int u = 0; u < d; ++u) Rch[u * d + u] = 1.0;
   if (nf > 0) {
-    // ---- rotations: min sum kappa |R_j - R_i R_ij|_F^2, R_0 = I; rows of R decouple into d
-    // right-hand sides of the d x d block connection Laplacian (free poses 1..n-1)
-    SymBlocks Q(nf, d);
-    std::vector<double> rhs(static_cast<size_t>(nf) * d * d, 0.0);  // [pose][u][row a]
+    // ---- rotations: min sum kappa |R_j - R_i R_ij|_F^2, R_0 = I; the rows of R decouple into d
+    // right-hand sides.  x A x^T form: A_ii += k R R^T, A_jj += k I, A_ij = -k R
+    SysBuilder B(nf, d);
+    std::vector<double> rhs(static_cast<size_t>(nf) * d * d, 0.0);  // [pose][v][row a]
+    double Bii[9], Bjj[9], Bij[9];
     for (int e = 0; e < m; ++e) {
       const int i = p1[e], j = p2[e];
       const double k = kappa[e];
       const double* Re = R + static_cast<size_t>(e) * d2;
-      // Q_ii += k R R^T, Q_jj += k I, Q_ij = -k R, Q_ji = -k R^T (x Q x^T with x = a row of R)
-      if (i > 0) {
-        double* B = Q.at(i - 1, i - 1);
-        for (int u = 0; u < d; ++u)
-          for (int v = 0; v < d; ++v) {
-            double s = 0;
-            for (int w = 0; w < d; ++w) s += Re[u * d + w] * Re[v * d + w];
-            B[u * d + v] += k * s;
-          }
-      }
-      if (j > 0) {
-        double* B = Q.at(j - 1, j - 1);
-        for (int u = 0; u < d; ++u) B[u * d + u] += k;
-      }
-      if (i > 0 && j > 0) {
-        double* Bij = Q.at(i - 1, j - 1);
-        double* Bji = Q.at(j - 1, i - 1);
-        for (int u = 0; u < d; ++u)
-          for (int v = 0; v < d; ++v) {
-            Bij[u * d + v] -= k * Re[u * d + v];
-            Bji[v * d + u] -= k * Re[u * d + v];
-          }
-      } else if (i == 0 && j > 0) {  // fixed x_0 = row a of I: rhs_j -= x_0 Q_0j = -k (row a of R)
+      for (int u = 0; u < d; ++u)
+        for (int v = 0; v < d; ++v) {
+          double s = 0;
+          for (int w = 0; w < d; ++w) s += Re[u * d + w] * Re[v * d + w];
+          Bii[u * d + v] = k * s;
+          Bjj[u * d + v] = u == v ? k : 0.0;
+          Bij[u * d + v] = -k * Re[u * d + v];
+        }
+      B.add(i - 1, j - 1, Bii, Bjj, Bij);
+      if (i == 0 && j > 0) {  // fixed x_0 = row a of I: rhs_j -= x_0 A_0j = k (row a of R)
         for (int a = 0; a < d; ++a)
           for (int v = 0; v < d; ++v) rhs[(static_cast<size_t>(j - 1) * d + v) * d + a] += k * Re[a * d + v];
-      } else if (j == 0 && i > 0) {  // rhs_i -= x_0 Q_0i, Q_0i = -k R^T  -> += k (R^T row a) = k R(:, a)
+      } else if (j == 0 && i > 0) {  // rhs_i -= x_0 A_0i, A_0i = -k R^T  -> += k R(:, a)
         for (int a = 0; a < d; ++a)
           for (int v = 0; v < d; ++v) rhs[(static_cast<size_t>(i - 1) * d + v) * d + a] += k * Re[v * d + a];
       }
     }
-    std::vector<int> rowptr, col;
-    std::vector<double> blocks;
-    Q.to_bsr(rowptr, col, blocks);
-    BlockCholesky L;
-    if (block_cholesky(nf, d, rowptr, col, blocks, 0.0, 200u * 1000u * 1000u, L, err) != 0) {
+    BlockSys S;
+    B.build(S);
+    if (solve(S, d, rhs, err) != 0) {
       err = "chordal initialisation (rotations): " + err + " (is the pose graph connected?)";
       return -1;
     }
-    for (int a = 0; a < d; ++a) {
-      std::vector<double> x(static_cast<size_t>(nf) * d);
-      for (int p = 0; p < nf; ++p)
-        for (int v = 0; v < d; ++v) x[static_cast<size_t>(p) * d + v] = rhs[(static_cast<size_t>(p) * d + v) * d + a];
-      chol_solve(L, x);
-      for (int p = 0; p < nf; ++p)
-        for (int v = 0; v < d; ++v) Rch[static_cast<size_t>(p + 1) * d2 + a * d + v] = x[static_cast<size_t>(p) * d + v];
-    }
+    for (int p = 1; p < n; ++p)
+      for (int a = 0; a < d; ++a)
+        for (int v = 0; v < d; ++v)
+          Rch[static_cast<size_t>(p) * d2 + a * d + v] = rhs[(static_cast<size_t>(p - 1) * d + v) * d + a];
     for (int p = 1; p < n; ++p) {
       double P[9];
       project_rotation(d, &Rch[static_cast<size_t>(p) * d2], P);
@@ -219,39 +415,28 @@ int chordal_initialization(int d, int n, int m, const int* p1, const int* p2, co
   // ---- translations (recoverTranslations): min sum tau |t_j - t_i - R_i t_ij|^2, t_0 = 0
   std::vector<double> tt(static_cast<size_t>(n) * d, 0.0);
   if (nf > 0) {
-    SymBlocks L1(nf, 1);
+    SysBuilder B(nf, 1);
     std::vector<double> rhs(static_cast<size_t>(nf) * d, 0.0);  // [pose][component]
     for (int e = 0; e < m; ++e) {
       const int i = p1[e], j = p2[e];
-      const double w = tau[e];
+      const double w = tau[e], mw = -w;
       double c[3] = {0, 0, 0};  // R_i t_ij
       for (int u = 0; u < d; ++u)
         for (int v = 0; v < d; ++v) c[u] += Rch[static_cast<size_t>(i) * d2 + u * d + v] * t[static_cast<size_t>(e) * d + v];
-      if (i > 0) *L1.at(i - 1, i - 1) += w;
-      if (j > 0) *L1.at(j - 1, j - 1) += w;
-      if (i > 0 && j > 0) {
-        *L1.at(i - 1, j - 1) -= w;
-        *L1.at(j - 1, i - 1) -= w;
-      }
+      B.add(i - 1, j - 1, &w, &w, &mw);
       for (int u = 0; u < d; ++u) {
         if (j > 0) rhs[static_cast<size_t>(j - 1) * d + u] += w * c[u];
         if (i > 0) rhs[static_cast<size_t>(i - 1) * d + u] -= w * c[u];
       }
     }
-    std::vector<int> rowptr, col;
-    std::vector<double> blocks;
-    L1.to_bsr(rowptr, col, blocks);
-    BlockCholesky L;
-    if (block_cholesky(nf, 1, rowptr, col, blocks, 0.0, 200u * 1000u * 1000u, L, err) != 0) {
+    BlockSys S;
+    B.build(S);
+    if (solve(S, d, rhs, err) != 0) {
       err = "chordal initialisation (translations): " + err + " (is the pose graph connected?)";
       return -1;
     }
-    for (int u = 0; u < d; ++u) {
-      std::vector<double> x(nf);
-      for (int p = 0; p < nf; ++p) x[p] = rhs[static_cast<size_t>(p) * d + u];
-      chol_solve(L, x);
-      for (int p = 0; p < nf; ++p) tt[static_cast<size_t>(p + 1) * d + u] = x[p];
-    }
+    for (int p = 0; p < nf; ++p)
+      for (int u = 0; u < d; ++u) tt[static_cast<size_t>(p + 1) * d + u] = rhs[static_cast<size_t>(p) * d + u];
   }
   // ---- T = [R_i | t_i] per pose, d x (d+1) n column-major
   const int b = d + 1;
@@ -261,6 +446,36 @@ int chordal_initialization(int d, int n, int m, const int* p1, const int* p2, co
         T_out[(static_cast<size_t>(p) * b + c) * d + u] =
             c < d ? Rch[static_cast<size_t>(p) * d2 + u * d + c] : tt[static_cast<size_t>(p) * d + u];
   return 0;
+}
+
+}  // namespace
+
+int chordal_initialization(int d, int n, int m, const int* p1, const int* p2, const double* R, const double* t,
+                           const double* kappa, const double* tau, double* T_out, std::string& err) {
+  return chordal_core(d, n, m, p1, p2, R, t, kappa, tau, T_out,
+                      [](const BlockSys& S, int nr, std::vector<double>& rx, std::string& e) {
+                        return solve_direct(S, nr, rx, e);
+                      },
+                      err);
+}
+
+int chordal_initialization_gpu(int d, int n, int m, const int* p1, const int* p2, const double* R, const double* t,
+                               const double* kappa, const double* tau, double* T_out, double rtol, int max_iters,
+                               int* iters, double* relres, std::string& err) {
+  int it_sum = 0;
+  double rr = 0.0;
+  const int rc = chordal_core(d, n, m, p1, p2, R, t, kappa, tau, T_out,
+                              [&](const BlockSys& S, int nr, std::vector<double>& rx, std::string& e) {
+                                PcgReport rep;
+                                const int r = solve_pcg(S, nr, rx, rtol, max_iters, rep, e);
+                                it_sum += rep.iters;
+                                rr = std::max(rr, rep.relres);
+                                return r;
+                              },
+                              err);
+  if (iters) *iters = it_sum;
+  if (relres) *relres = rr;
+  return rc;
 }
 
 }  // namespace dpgo

@@ -17,7 +17,8 @@ enum SpmmMode { MODE_XQ = 0, MODE_XQ_G = 1, MODE_EVAL = 2, MODE_HESS = 3, MODE_F
 // Per-agent tile gating: RUN skips agents out of the RTR Run, TCG those whose tCG stopped, TCG_MODE
 // those with no tCG step pending, MOVED those whose single-Run candidate was accepted.
 enum FlagKind { FLAG_NONE = 0, FLAG_RUN = 1, FLAG_TCG = 2, FLAG_TCG_MODE = 3, FLAG_MOVED = 4, FLAG_TCG_CG = 5,
-                FLAG_RUN_IMPL = 6, FLAG_RUN_EXPL = 7 };  // RUN_IMPL/EXPL: FLAG_RUN and eta (not) implicit
+                FLAG_RUN_IMPL = 6, FLAG_RUN_EXPL = 7,  // RUN_IMPL/EXPL: FLAG_RUN and eta (not) implicit
+                FLAG_DECIDED = 8 };  // only agents whose single-Run outcome was decided in Run `round`
 enum PreconMode { PRECON_EXACT = 0, PRECON_BLOCK_JACOBI = 1, PRECON_NONE = 2 };
 enum TcgStatus { TCG_NEGCURVTURE = 0, TCG_EXCREGION = 1, TCG_LCON = 2, TCG_SCON = 3, TCG_MAXITER = 4 };
 enum FinalizeOp {
@@ -55,6 +56,7 @@ struct LaunchCtx {
   AgentState* state;      // [num_agents] (may be null with FLAG_NONE)
   double* partials;       // [num_tiles * kPartialStride]
   hipStream_t stream;
+  int round;              // FLAG_DECIDED: the RTR Run index (0-based)
 };
 
 enum QFormat { QFMT_BSR = 0, QFMT_EDGES = 1 };
@@ -252,5 +254,25 @@ hipError_t launch_dot_multi(long len, const double* w, const double* basis, int 
 hipError_t launch_axpy_multi(long len, double* w, const double* basis, int k, const double* c, hipStream_t stream);
 hipError_t launch_scale(long len, const double* src, double s, double* dst, hipStream_t stream);
 hipError_t launch_bj_inverse_diag(int b, int n, const QView& q, double shift, double* Minv, hipStream_t stream);
+
+// ---- Jacobi-PCG on SPD block-sparse systems with several right-hand sides (GPU chordal
+// initialisation, init.cpp).  Vectors are [row][bs][nr]: row p holds bs x nr doubles (column a of
+// the block row is right-hand side a).  Blocks row-major bs x bs; minv: per row the inverse of the
+// diagonal block.  Reductions: fixed grid kPcgBlocks, partial[block][q] then summed on the host.
+constexpr int kPcgBlocks = 1024;
+struct PcgCoef {
+  double v[3];
+};
+// y = A x
+hipError_t launch_pcg_spmv(int bs, int nr, int n, const int* rowptr, const int* col, const double* blk,
+                           const double* x, double* y, hipStream_t stream);
+// partial[block * nr + a] = sum over the block's rows of <u_a, v_a>
+hipError_t launch_pcg_dot(int bs, int nr, int n, const double* u, const double* v, double* partial,
+                          hipStream_t stream);
+// x += alpha p, r -= alpha q, z = minv r; partial[block * 2 nr + a] = <r_a, z_a>, [.. + nr + a] = |r_a|^2
+hipError_t launch_pcg_update(int bs, int nr, int n, PcgCoef alpha, const double* p, const double* q, double* x,
+                             double* r, double* z, const double* minv, double* partial, hipStream_t stream);
+// p = z + beta p
+hipError_t launch_pcg_dir(int bs, int nr, int n, PcgCoef beta, const double* z, double* p, hipStream_t stream);
 
 }  // namespace dpgo

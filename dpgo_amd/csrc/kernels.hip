@@ -27,6 +27,8 @@ __device__ __forceinline__ bool tile_skipped(const LaunchCtx& c, int agent) {
   if (c.flag_kind == FLAG_TCG_CG) return s.tcg_mode != 0;
   if (c.flag_kind == FLAG_RUN_IMPL) return s.run_active == 0 || s.eta_implicit == 0;
   if (c.flag_kind == FLAG_RUN_EXPL) return s.run_active == 0 || s.eta_implicit != 0;
+  if (c.flag_kind == FLAG_DECIDED)  // accepted / gave up in Run `round`, or never ran (round 0)
+    return !(s.run_active == 0 && (s.runs == c.round + 1 || (c.round == 0 && s.runs == 0)));
   return false;
 }
 
@@ -2211,6 +2213,155 @@ hipError_t launch_bj_inverse_diag(int b, int n, const QView& q, double shift, do
     k_bj_inverse_diag<4><<<blocks, kThreads, 0, stream>>>(n, q, shift, Minv);
   else
     return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+// ---- Jacobi-PCG kernels (chordal initialisation on the device) --------------------------------
+template <int BS, int NR>
+__global__ __launch_bounds__(kThreads) void k_pcg_spmv(int n, const int* __restrict__ rowptr, const int* __restrict__ col,
+                                                       const double* __restrict__ blk, const double* __restrict__ x,
+                                                       double* __restrict__ y) {
+  const long p = static_cast<long>(blockIdx.x) * kThreads + threadIdx.x;
+  if (p >= n) return;
+  double acc[BS][NR];
+#pragma unroll
+  for (int u = 0; u < BS; ++u)
+#pragma unroll
+    for (int a = 0; a < NR; ++a) acc[u][a] = 0.0;
+  for (int k = rowptr[p]; k < rowptr[p + 1]; ++k) {
+    const double* B = blk + static_cast<long>(k) * (BS * BS);
+    const double* xv = x + static_cast<long>(col[k]) * (BS * NR);
+    double xl[BS][NR], bl[BS][BS];
+#pragma unroll
+    for (int v = 0; v < BS; ++v)
+#pragma unroll
+      for (int a = 0; a < NR; ++a) xl[v][a] = xv[v * NR + a];
+#pragma unroll
+    for (int u = 0; u < BS; ++u)
+#pragma unroll
+      for (int v = 0; v < BS; ++v) bl[u][v] = B[u * BS + v];
+#pragma unroll
+    for (int u = 0; u < BS; ++u)
+#pragma unroll
+      for (int v = 0; v < BS; ++v)
+#pragma unroll
+        for (int a = 0; a < NR; ++a) acc[u][a] = fma(bl[u][v], xl[v][a], acc[u][a]);
+  }
+  double* yv = y + p * (BS * NR);
+#pragma unroll
+  for (int u = 0; u < BS; ++u)
+#pragma unroll
+    for (int a = 0; a < NR; ++a) yv[u * NR + a] = acc[u][a];
+}
+
+// fixed-order block reduction of Q per-thread values into partial[blockIdx.x * Q + q]
+template <int Q>
+__device__ __forceinline__ void pcg_block_reduce(double (&v)[Q], double* __restrict__ partial) {
+  __shared__ double red[kThreads / 64][Q];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < Q; ++q) v[q] = wave_sum(v[q]);
+  if (lane == 0)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) red[wave][q] = v[q];
+  __syncthreads();
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) partial[blockIdx.x * Q + q] = ((red[0][q] + red[1][q]) + red[2][q]) + red[3][q];
+}
+
+template <int BS, int NR>
+__global__ __launch_bounds__(kThreads) void k_pcg_dot(int n, const double* __restrict__ u, const double* __restrict__ v,
+                                                      double* __restrict__ partial) {
+  double s[NR];
+#pragma unroll
+  for (int a = 0; a < NR; ++a) s[a] = 0.0;
+  for (long p = static_cast<long>(blockIdx.x) * kThreads + threadIdx.x; p < n; p += static_cast<long>(gridDim.x) * kThreads) {
+#pragma unroll
+    for (int w = 0; w < BS; ++w)
+#pragma unroll
+      for (int a = 0; a < NR; ++a) s[a] = fma(u[p * (BS * NR) + w * NR + a], v[p * (BS * NR) + w * NR + a], s[a]);
+  }
+  pcg_block_reduce<NR>(s, partial);
+}
+
+template <int BS, int NR>
+__global__ __launch_bounds__(kThreads) void k_pcg_update(int n, PcgCoef alpha, const double* __restrict__ pv,
+                                                         const double* __restrict__ qv, double* __restrict__ x,
+                                                         double* __restrict__ r, double* __restrict__ z,
+                                                         const double* __restrict__ minv, double* __restrict__ partial) {
+  double s[2 * NR];
+#pragma unroll
+  for (int a = 0; a < 2 * NR; ++a) s[a] = 0.0;
+  for (long p = static_cast<long>(blockIdx.x) * kThreads + threadIdx.x; p < n; p += static_cast<long>(gridDim.x) * kThreads) {
+    double rl[BS][NR];
+    const long o = p * (BS * NR);
+#pragma unroll
+    for (int w = 0; w < BS; ++w)
+#pragma unroll
+      for (int a = 0; a < NR; ++a) {
+        x[o + w * NR + a] = fma(alpha.v[a], pv[o + w * NR + a], x[o + w * NR + a]);
+        rl[w][a] = fma(-alpha.v[a], qv[o + w * NR + a], r[o + w * NR + a]);
+        r[o + w * NR + a] = rl[w][a];
+      }
+    const double* M = minv + p * (BS * BS);
+#pragma unroll
+    for (int u = 0; u < BS; ++u)
+#pragma unroll
+      for (int a = 0; a < NR; ++a) {
+        double zz = 0.0;
+#pragma unroll
+        for (int w = 0; w < BS; ++w) zz = fma(M[u * BS + w], rl[w][a], zz);
+        z[o + u * NR + a] = zz;
+        s[a] = fma(rl[u][a], zz, s[a]);
+        s[NR + a] = fma(rl[u][a], rl[u][a], s[NR + a]);
+      }
+  }
+  pcg_block_reduce<2 * NR>(s, partial);
+}
+
+template <int BS, int NR>
+__global__ __launch_bounds__(kThreads) void k_pcg_dir(int n, PcgCoef beta, const double* __restrict__ z,
+                                                      double* __restrict__ pv) {
+  for (long p = static_cast<long>(blockIdx.x) * kThreads + threadIdx.x; p < n; p += static_cast<long>(gridDim.x) * kThreads)
+#pragma unroll
+    for (int w = 0; w < BS; ++w)
+#pragma unroll
+      for (int a = 0; a < NR; ++a) pv[p * (BS * NR) + w * NR + a] = fma(beta.v[a], pv[p * (BS * NR) + w * NR + a], z[p * (BS * NR) + w * NR + a]);
+}
+
+#define DPGO_PCG_DISPATCH(BS_, NR_, CALL)                                   \
+  switch ((BS_) * 8 + (NR_)) {                                              \
+    case 1 * 8 + 2: { constexpr int BS = 1, NR = 2; CALL; break; }          \
+    case 1 * 8 + 3: { constexpr int BS = 1, NR = 3; CALL; break; }          \
+    case 2 * 8 + 2: { constexpr int BS = 2, NR = 2; CALL; break; }          \
+    case 3 * 8 + 3: { constexpr int BS = 3, NR = 3; CALL; break; }          \
+    default: return hipErrorInvalidValue;                                   \
+  }
+
+hipError_t launch_pcg_spmv(int bs, int nr, int n, const int* rowptr, const int* col, const double* blk,
+                           const double* x, double* y, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const int grid = (n + kThreads - 1) / kThreads;
+  DPGO_PCG_DISPATCH(bs, nr, (k_pcg_spmv<BS, NR><<<grid, kThreads, 0, stream>>>(n, rowptr, col, blk, x, y)));
+  return hipGetLastError();
+}
+
+hipError_t launch_pcg_dot(int bs, int nr, int n, const double* u, const double* v, double* partial,
+                          hipStream_t stream) {
+  DPGO_PCG_DISPATCH(bs, nr, (k_pcg_dot<BS, NR><<<kPcgBlocks, kThreads, 0, stream>>>(n, u, v, partial)));
+  return hipGetLastError();
+}
+
+hipError_t launch_pcg_update(int bs, int nr, int n, PcgCoef alpha, const double* p, const double* q, double* x,
+                             double* r, double* z, const double* minv, double* partial, hipStream_t stream) {
+  DPGO_PCG_DISPATCH(bs, nr, (k_pcg_update<BS, NR><<<kPcgBlocks, kThreads, 0, stream>>>(n, alpha, p, q, x, r, z, minv,
+                                                                                       partial)));
+  return hipGetLastError();
+}
+
+hipError_t launch_pcg_dir(int bs, int nr, int n, PcgCoef beta, const double* z, double* p, hipStream_t stream) {
+  DPGO_PCG_DISPATCH(bs, nr, (k_pcg_dir<BS, NR><<<kPcgBlocks, kThreads, 0, stream>>>(n, beta, z, p)));
   return hipGetLastError();
 }
 

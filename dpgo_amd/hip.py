@@ -441,6 +441,9 @@ _SIGS2 = [
     ("dpgo_graph_chordal_init", [C.c_void_p, C.c_int, _dp, _dp], C.c_int),
     ("dpgo_chordal_initialization", [C.c_int, C.c_int, C.c_int, _ip, _ip, _dp, _dp, _dp, _dp, _dp], C.c_int),
     ("dpgo_graph_grid_partition", [C.c_void_p, C.c_int, _ip], C.c_int),
+    ("dpgo_chordal_initialization_gpu", [C.c_int, C.c_int, C.c_int, _ip, _ip, _dp, _dp, _dp, _dp, C.c_double,
+                                         C.c_int, _dp, _ip, _dp], C.c_int),
+    ("dpgo_graph_chordal_init_gpu", [C.c_void_p, C.c_int, _dp, C.c_double, C.c_int, _dp, _ip, _dp], C.c_int),
     ("dpgo_rbcd_default_params", [C.POINTER(RbcdParams)], None),
     ("dpgo_rbcd_plan", [C.c_void_p, C.c_int, _ip, _ip, C.c_int, C.c_int, _lp, _lp, _ip, _ip], C.c_int),
     ("dpgo_rbcd_create", [C.c_void_p, C.c_int, _ip, _ip, C.c_int, C.c_int, C.POINTER(RbcdParams),
@@ -549,6 +552,15 @@ class Graph:
         _check(lib().dpgo_graph_chordal_init(self.h, r, Yp, out.ctypes.data_as(_dp)))
         return from_dev_layout(out, r)
 
+    def chordal_init_gpu(self, r, YLift, rtol=1e-12, max_iters=20000, dev_layout=False):
+        """chordalInitialization by Jacobi-PCG on the GPU; returns (X, PCG iterations, relative residual)."""
+        Y, Yp = _f64(np.asarray(YLift, dtype=np.float64).T.ravel())
+        out = np.empty(self.n * (self.d + 1) * r)
+        it, rr = C.c_int(), C.c_double()
+        _check(lib().dpgo_graph_chordal_init_gpu(self.h, r, Yp, float(rtol), int(max_iters), out.ctypes.data_as(_dp),
+                                                 C.byref(it), C.byref(rr)))
+        return (out if dev_layout else from_dev_layout(out, r)), it.value, rr.value
+
     def chain_init_dev_layout(self, r, YLift):
         Y, Yp = _f64(np.asarray(YLift, dtype=np.float64).T.ravel())
         out = np.empty(self.n * (self.d + 1) * r)
@@ -572,6 +584,21 @@ def chordal_initialization(d, n, p1, p2, R, t, kappa, tau):
     out = np.empty(d * (d + 1) * n)
     _check(lib().dpgo_chordal_initialization(d, int(n), len(a1), a1p, a2p, Rp, tp, kp, tap, out.ctypes.data_as(_dp)))
     return from_dev_layout(out, d)
+
+
+def chordal_initialization_gpu(d, n, p1, p2, R, t, kappa, tau, rtol=1e-12, max_iters=20000):
+    """chordalInitialization with both solves by Jacobi-PCG on the GPU: (T, iterations, rel. residual)."""
+    a1, a1p = _i32(p1)
+    a2, a2p = _i32(p2)
+    Rr, Rp = _f64(np.asarray(R).reshape(-1))
+    tt, tp = _f64(np.asarray(t).reshape(-1))
+    kk, kp = _f64(kappa)
+    ta, tap = _f64(tau)
+    out = np.empty(d * (d + 1) * n)
+    it, rr = C.c_int(), C.c_double()
+    _check(lib().dpgo_chordal_initialization_gpu(d, int(n), len(a1), a1p, a2p, Rp, tp, kp, tap, float(rtol),
+                                                 int(max_iters), out.ctypes.data_as(_dp), C.byref(it), C.byref(rr)))
+    return from_dev_layout(out, d), it.value, rr.value
 
 
 def exchange_plan(graph: "Graph", agent_of_pose, agent_rank, rank, world):

@@ -53,6 +53,15 @@ int dpgo_chordal_initialization(int d, int n, int m, const int* p1, const int* p
                                 const double* t, const double* kappa, const double* tau, double* T_out);
 /* X = YLift * chordal T for a graph handle (r x (d+1) n, column-major). */
 int dpgo_graph_chordal_init(dpgo_graph g, int r, const double* YLift_colmajor, double* X_out);
+/* chordalInitialization with both linear solves by Jacobi-preconditioned CG on the GPU (for graphs
+ * whose direct factor is too large: a 10^6-pose 3D grid): each right-hand side to |r| <= rtol |b|
+ * (DPGO_HIP_EDEVICE if max_iters is not enough).  iters: PCG iterations of both solves; relres: the
+ * largest final relative residual.  Same system assembly and projections as the host version. */
+int dpgo_chordal_initialization_gpu(int d, int n, int m, const int* p1, const int* p2, const double* R,
+                                    const double* t, const double* kappa, const double* tau, double rtol,
+                                    int max_iters, double* T_out, int* iters, double* relres);
+int dpgo_graph_chordal_init_gpu(dpgo_graph g, int r, const double* YLift_colmajor, double rtol, int max_iters,
+                                double* X_out, int* iters, double* relres);
 /* Grid graphs: agent = sub-cube (x/s, y/s, z/s), s = k / A; id = ax + A (ay + A az). */
 int dpgo_graph_grid_partition(dpgo_graph g, int agents_per_axis, int* agent_of_pose);
 

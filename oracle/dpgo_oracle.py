@@ -1306,7 +1306,7 @@ def colour_rbcd(meas: Measurements, agent_of_pose, num_agents, X0, num_iters, r,
                     ag.update_neighbor_poses(other.id, other.shared_pose_dict(True), aux=True)
         for ag in agents:
             if colors[ag.id] == c:
-                ag.iterate(True)
+                ag.iterate(True, trace)  # RTR outer records of the update, then (it, agent, result)
                 if trace is not None:
                     trace.append((it, ag.id, ag.last_result))
     X = np.zeros_like(X0)

@@ -79,7 +79,20 @@ def test_rtr_trace_matches_oracle(hip, name, r, iters, tol, radius, inner, preco
     exp = _expected_records(trace)
     assert len(exp) > 3
     assert len(got) == len(exp)
+    # Tolerance: 1e-10 relative with block-Jacobi; 1e-7 with the exact factor, whose single
+    # applications already agree with the oracle's sparse LU only to ~1e-10 (cond(Q + 0.1 I) eps).
+    # Quantities that shrink inside one tCG (d_Hd, alpha, |r|, <z, r>, beta, tau) are measured against
+    # their largest magnitude in that tCG: their terms cancel, so their rounding floor is set by it.
+    # rho = (f1 - f2) / model decrease: f1 - f2 loses the digits |f1| / |f1 - f2|.
+    tol = 1e-10 if precon == "bj" else 1e-7
+    scale, run_id = {}, None
     for g, e in zip(got, exp):
+        if e["op"] == 5 or run_id != g["run"]:
+            run_id = g["run"]
+            scale = {}
+        for k in ("d_Hd", "alpha", "norm_r", "z_r", "beta", "tau"):
+            if k in e and not (k == "alpha" and e["op"] == 5):
+                scale[k] = max(scale.get(k, 0.0), abs(e[k]))
         assert int(g["op"]) == e["op"], (g, e)
         for k, v in e.items():
             if k in ("op",):
@@ -87,13 +100,14 @@ def test_rtr_trace_matches_oracle(hip, name, r, iters, tol, radius, inner, preco
             if k in ("j", "status", "accepted"):
                 assert int(g[k]) == int(v), (k, g, e)
             elif k == "rho":
-                # rho = (f1 - f2) / model decrease: the difference of two close costs loses digits
-                scale = 1e-10 + 1e-14 * abs(e["f1"]) / max(abs(e["f1"] - e["f2"]), 1e-300)
-                assert _close(g[k], v, scale), (k, g[k], v)
+                rt = 10 * tol + 1e-13 * abs(e["f1"]) / max(abs(e["f1"] - e["f2"]), 1e-300)
+                assert _close(g[k], v, rt), (k, g[k], v)
             elif k == "alpha" and e["op"] == 5:
                 assert int(g[k]) == int(v)  # inner iterations of the Run
+            elif k in scale:
+                assert abs(g[k] - v) <= tol * max(scale[k], 1e-300), (k, g[k], v, e)
             else:
-                assert _close(g[k], v, 1e-10), (k, g[k], v, e)
+                assert _close(g[k], v, tol), (k, g[k], v, e)
     st = H.stats()[0]
     runs = [t for t in trace]
     assert st["calls"] == 1 and st["runs"] == len(runs)
@@ -155,7 +169,7 @@ def _grid_outliers(hip, k, seed, frac, rng_seed):
 
 
 @pytest.mark.parametrize("accel,robust,alg", [(False, "L2", "RTR"), (True, "L2", "RTR"), (True, "GNC_TLS", "RTR"),
-                                              (False, "L2", "RGD"), (True, "L2", "RGD")])
+                                              (False, "GNC_TLS", "RTR"), (False, "L2", "RGD"), (True, "L2", "RGD")])
 def test_engine_status_and_counters_match_oracle(hip, accel, robust, alg):
     """Per selected agent: PGOAgentStatus relativeChange = |X - XPrev| / sqrt(n) and readyToTerminate
     (relChangeTol 5e-3; GNC_TLS: converged loop-closure ratio >= 0.8) after every iteration, and the
