@@ -485,6 +485,30 @@ int dpgo_graph_chordal_init_gpu(dpgo_graph g, int r, const double* YLift, double
   return DPGO_HIP_OK;
 }
 
+int dpgo_graph_distributed_init(dpgo_graph g, int num_agents, const int* agent_of_pose, int r, const double* YLift,
+                                int use_gpu, double rtol, int max_iters, double* X_out, int* iters, double* relres) {
+  if (!g || !YLift || !X_out || !agent_of_pose || num_agents <= 0) return fail(DPGO_HIP_EINVAL, "null argument");
+  const int d = g->d, b = d + 1, n = g->n;
+  for (int i = 0; i < n; ++i)
+    if (agent_of_pose[i] < 0 || agent_of_pose[i] >= num_agents) return fail(DPGO_HIP_EINVAL, "agent_of_pose out of range");
+  if (use_gpu && usable_devices() == 0) return fail(DPGO_HIP_ENODEV, "no gfx950 device available (no CPU fallback)");
+  if (use_gpu && (!(rtol > 0.0) || max_iters < 1)) return fail(DPGO_HIP_EINVAL, "bad PCG tolerance");
+  std::vector<double> T(static_cast<size_t>(n) * d * b);
+  std::string err;
+  if (dpgo::distributed_initialization(d, n, static_cast<int>(g->p1.size()), g->p1.data(), g->p2.data(), g->R.data(),
+                                       g->t.data(), g->kappa.data(), g->tau.data(), agent_of_pose, num_agents,
+                                       use_gpu != 0, rtol, max_iters, T.data(), iters, relres, err) != 0)
+    return fail(use_gpu ? DPGO_HIP_EDEVICE : DPGO_HIP_EINVAL, err);
+  for (int p = 0; p < n; ++p)
+    for (int c = 0; c < b; ++c)
+      for (int a = 0; a < r; ++a) {
+        double acc = 0.0;
+        for (int u = 0; u < d; ++u) acc += YLift[u * r + a] * T[(static_cast<size_t>(p) * b + c) * d + u];
+        X_out[(static_cast<size_t>(p) * b + c) * r + a] = acc;
+      }
+  return DPGO_HIP_OK;
+}
+
 int dpgo_graph_chain_init(dpgo_graph g, int r, const double* YLift, double* X_out) {
   if (!g || !YLift || !X_out) return fail(DPGO_HIP_EINVAL, "null argument");
   const int d = g->d, b = d + 1, n = g->n;

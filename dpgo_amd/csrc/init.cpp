@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstring>
 #include <map>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -356,27 +357,35 @@ int solve_pcg(const BlockSys& S, int nr, std::vector<double>& rhs_x, double rtol
   return 0;
 }
 
-// chordalInitialization with the linear solves done by `solver`: rotations (d x d block connection
-// Laplacian, d right-hand sides = the rows of R, R_0 = I) then translations (scalar Laplacian, d
-// right-hand sides, t_0 = 0), as the two SPQR solves of the reference (:377-476).
+// chordalInitialization with the linear solves done by `solve`: rotations (d x d block connection
+// Laplacian, d right-hand sides = the rows of R) then translations (scalar Laplacian, d right-hand
+// sides), as the two SPQR solves of the reference (:377-476).  The poses flagged in `anchor` are held
+// at R = I, t = 0 (the reference: pose 0 only); each connected component needs one.
 template <typename Solver>
 int chordal_core(int d, int n, int m, const int* p1, const int* p2, const double* R, const double* t,
-                 const double* kappa, const double* tau, double* T_out, Solver&& solve, std::string& err) {
+                 const double* kappa, const double* tau, const std::vector<char>& anchor, double* T_out,
+                 Solver&& solve, std::string& err) {
   if (n < 1) {
     err = "chordal initialisation: no poses";
     return -1;
   }
-  const int d2 = d * d, nf = n - 1;
+  const int d2 = d * d;
+  std::vector<int> row(n, -1);
+  int nf = 0;
+  for (int p = 0; p < n; ++p)
+    if (!anchor[p]) row[p] = nf++;
   std::vector<double> Rch(static_cast<size_t>(n) * d2, 0.0);  // R_i row-major per pose
-  for (int u = 0; u < d; ++u) Rch[u * d + u] = 1.0;
+  for (int p = 0; p < n; ++p)
+    for (int u = 0; u < d; ++u) Rch[static_cast<size_t>(p) * d2 + u * d + u] = 1.0;
   if (nf > 0) {
-    // ---- rotations: min sum kappa |R_j - R_i R_ij|_F^2, R_0 = I; the rows of R decouple into d
-    // right-hand sides.  x A x^T form: A_ii += k R R^T, A_jj += k I, A_ij = -k R
+    // ---- rotations: min sum kappa |R_j - R_i R_ij|_F^2; the rows of R decouple into d right-hand
+    // sides.  x A x^T form: A_ii += k R R^T, A_jj += k I, A_ij = -k R
     SysBuilder B(nf, d);
-    std::vector<double> rhs(static_cast<size_t>(nf) * d * d, 0.0);  // [pose][v][row a]
+    std::vector<double> rhs(static_cast<size_t>(nf) * d * d, 0.0);  // [row][v][row a of R]
     double Bii[9], Bjj[9], Bij[9];
     for (int e = 0; e < m; ++e) {
-      const int i = p1[e], j = p2[e];
+      const int i = p1[e], j = p2[e], ri = row[i], rj = row[j];
+      if (ri < 0 && rj < 0) continue;
       const double k = kappa[e];
       const double* Re = R + static_cast<size_t>(e) * d2;
       for (int u = 0; u < d; ++u)
@@ -387,13 +396,13 @@ int chordal_core(int d, int n, int m, const int* p1, const int* p2, const double
           Bjj[u * d + v] = u == v ? k : 0.0;
           Bij[u * d + v] = -k * Re[u * d + v];
         }
-      B.add(i - 1, j - 1, Bii, Bjj, Bij);
-      if (i == 0 && j > 0) {  // fixed x_0 = row a of I: rhs_j -= x_0 A_0j = k (row a of R)
+      B.add(ri, rj, Bii, Bjj, Bij);
+      if (ri < 0) {  // fixed x_i = row a of I: rhs_j -= x_i A_ij = k (row a of R)
         for (int a = 0; a < d; ++a)
-          for (int v = 0; v < d; ++v) rhs[(static_cast<size_t>(j - 1) * d + v) * d + a] += k * Re[a * d + v];
-      } else if (j == 0 && i > 0) {  // rhs_i -= x_0 A_0i, A_0i = -k R^T  -> += k R(:, a)
+          for (int v = 0; v < d; ++v) rhs[(static_cast<size_t>(rj) * d + v) * d + a] += k * Re[a * d + v];
+      } else if (rj < 0) {  // rhs_i -= x_j A_ji, A_ji = -k R^T  -> += k R(:, a)
         for (int a = 0; a < d; ++a)
-          for (int v = 0; v < d; ++v) rhs[(static_cast<size_t>(i - 1) * d + v) * d + a] += k * Re[v * d + a];
+          for (int v = 0; v < d; ++v) rhs[(static_cast<size_t>(ri) * d + v) * d + a] += k * Re[v * d + a];
       }
     }
     BlockSys S;
@@ -402,31 +411,31 @@ int chordal_core(int d, int n, int m, const int* p1, const int* p2, const double
       err = "chordal initialisation (rotations): " + err + " (is the pose graph connected?)";
       return -1;
     }
-    for (int p = 1; p < n; ++p)
+    for (int p = 0; p < n; ++p) {
+      if (row[p] < 0) continue;
+      double M[9], P[9];
       for (int a = 0; a < d; ++a)
-        for (int v = 0; v < d; ++v)
-          Rch[static_cast<size_t>(p) * d2 + a * d + v] = rhs[(static_cast<size_t>(p - 1) * d + v) * d + a];
-    for (int p = 1; p < n; ++p) {
-      double P[9];
-      project_rotation(d, &Rch[static_cast<size_t>(p) * d2], P);
+        for (int v = 0; v < d; ++v) M[a * d + v] = rhs[(static_cast<size_t>(row[p]) * d + v) * d + a];
+      project_rotation(d, M, P);
       std::memcpy(&Rch[static_cast<size_t>(p) * d2], P, sizeof(double) * d2);
     }
   }
-  // ---- translations (recoverTranslations): min sum tau |t_j - t_i - R_i t_ij|^2, t_0 = 0
+  // ---- translations (recoverTranslations): min sum tau |t_j - t_i - R_i t_ij|^2, anchors t = 0
   std::vector<double> tt(static_cast<size_t>(n) * d, 0.0);
   if (nf > 0) {
     SysBuilder B(nf, 1);
-    std::vector<double> rhs(static_cast<size_t>(nf) * d, 0.0);  // [pose][component]
+    std::vector<double> rhs(static_cast<size_t>(nf) * d, 0.0);  // [row][component]
     for (int e = 0; e < m; ++e) {
-      const int i = p1[e], j = p2[e];
+      const int i = p1[e], j = p2[e], ri = row[i], rj = row[j];
+      if (ri < 0 && rj < 0) continue;
       const double w = tau[e], mw = -w;
       double c[3] = {0, 0, 0};  // R_i t_ij
       for (int u = 0; u < d; ++u)
         for (int v = 0; v < d; ++v) c[u] += Rch[static_cast<size_t>(i) * d2 + u * d + v] * t[static_cast<size_t>(e) * d + v];
-      B.add(i - 1, j - 1, &w, &w, &mw);
+      B.add(ri, rj, &w, &w, &mw);
       for (int u = 0; u < d; ++u) {
-        if (j > 0) rhs[static_cast<size_t>(j - 1) * d + u] += w * c[u];
-        if (i > 0) rhs[static_cast<size_t>(i - 1) * d + u] -= w * c[u];
+        if (rj >= 0) rhs[static_cast<size_t>(rj) * d + u] += w * c[u];
+        if (ri >= 0) rhs[static_cast<size_t>(ri) * d + u] -= w * c[u];
       }
     }
     BlockSys S;
@@ -435,8 +444,9 @@ int chordal_core(int d, int n, int m, const int* p1, const int* p2, const double
       err = "chordal initialisation (translations): " + err + " (is the pose graph connected?)";
       return -1;
     }
-    for (int p = 0; p < nf; ++p)
-      for (int u = 0; u < d; ++u) tt[static_cast<size_t>(p + 1) * d + u] = rhs[static_cast<size_t>(p) * d + u];
+    for (int p = 0; p < n; ++p)
+      if (row[p] >= 0)
+        for (int u = 0; u < d; ++u) tt[static_cast<size_t>(p) * d + u] = rhs[static_cast<size_t>(row[p]) * d + u];
   }
   // ---- T = [R_i | t_i] per pose, d x (d+1) n column-major
   const int b = d + 1;
@@ -448,11 +458,42 @@ int chordal_core(int d, int n, int m, const int* p1, const int* p2, const double
   return 0;
 }
 
+// Breadth-first eccentricity centre of the pose set `verts` (edges restricted to it): the middle of
+// a longest BFS path found by two sweeps (exact on trees, within one hop of the centre on grids).
+int bfs_centre(const std::vector<std::vector<int>>& adj, const std::vector<int>& verts, const std::vector<int>& agent_of,
+               int a, std::vector<int>& dist, std::vector<int>& par) {
+  auto sweep = [&](int s) {
+    std::vector<int> q{s};
+    dist[s] = 0;
+    par[s] = -1;
+    int last = s;
+    for (size_t h = 0; h < q.size(); ++h) {
+      const int v = q[h];
+      last = v;
+      for (int u : adj[v])
+        if (agent_of[u] == a && dist[u] < 0) {
+          dist[u] = dist[v] + 1;
+          par[u] = v;
+          q.push_back(u);
+        }
+    }
+    for (int v : q) dist[v] = -1;
+    return last;
+  };
+  const int x = sweep(verts[0]);
+  const int y = sweep(x);  // par[] now describes BFS tree from x; path y -> x
+  std::vector<int> path;
+  for (int v = y; v >= 0; v = par[v]) path.push_back(v);
+  return path[path.size() / 2];
+}
+
 }  // namespace
 
 int chordal_initialization(int d, int n, int m, const int* p1, const int* p2, const double* R, const double* t,
                            const double* kappa, const double* tau, double* T_out, std::string& err) {
-  return chordal_core(d, n, m, p1, p2, R, t, kappa, tau, T_out,
+  std::vector<char> anchor(std::max(n, 1), 0);
+  anchor[0] = 1;  // R_0 = I, t_0 = 0 (:389, :458)
+  return chordal_core(d, n, m, p1, p2, R, t, kappa, tau, anchor, T_out,
                       [](const BlockSys& S, int nr, std::vector<double>& rx, std::string& e) {
                         return solve_direct(S, nr, rx, e);
                       },
@@ -464,7 +505,9 @@ int chordal_initialization_gpu(int d, int n, int m, const int* p1, const int* p2
                                int* iters, double* relres, std::string& err) {
   int it_sum = 0;
   double rr = 0.0;
-  const int rc = chordal_core(d, n, m, p1, p2, R, t, kappa, tau, T_out,
+  std::vector<char> anchor(std::max(n, 1), 0);
+  anchor[0] = 1;
+  const int rc = chordal_core(d, n, m, p1, p2, R, t, kappa, tau, anchor, T_out,
                               [&](const BlockSys& S, int nr, std::vector<double>& rx, std::string& e) {
                                 PcgReport rep;
                                 const int r = solve_pcg(S, nr, rx, rtol, max_iters, rep, e);
@@ -476,6 +519,178 @@ int chordal_initialization_gpu(int d, int n, int m, const int* p1, const int* p2
   if (iters) *iters = it_sum;
   if (relres) *relres = rr;
   return rc;
+}
+
+int distributed_initialization(int d, int n, int m, const int* p1, const int* p2, const double* R, const double* t,
+                               const double* kappa, const double* tau, const int* agent_of, int num_agents, bool gpu,
+                               double rtol, int max_iters, double* T_out, int* iters, double* relres,
+                               std::string& err) {
+  const int d2 = d * d, b = d + 1;
+  // ---- PGOAgent::localInitialization: chordal on every agent's private graph (all agents in one
+  // block-diagonal system; one anchor per agent, at the agent's BFS centre)
+  std::vector<int> q1, q2;
+  std::vector<double> qR, qt, qk, qtau;
+  std::vector<std::vector<int>> adj(n);
+  std::vector<std::vector<int>> verts(num_agents);
+  for (int p = 0; p < n; ++p) verts[agent_of[p]].push_back(p);
+  for (int e = 0; e < m; ++e) {
+    const int i = p1[e], j = p2[e];
+    if (agent_of[i] != agent_of[j]) continue;
+    q1.push_back(i);
+    q2.push_back(j);
+    qR.insert(qR.end(), R + static_cast<size_t>(e) * d2, R + static_cast<size_t>(e + 1) * d2);
+    qt.insert(qt.end(), t + static_cast<size_t>(e) * d, t + static_cast<size_t>(e + 1) * d);
+    qk.push_back(kappa[e]);
+    qtau.push_back(tau[e]);
+    adj[i].push_back(j);
+    adj[j].push_back(i);
+  }
+  std::vector<char> anchor(n, 0);
+  {
+    std::vector<int> dist(n, -1), par(n, -1);
+    for (int a = 0; a < num_agents; ++a) {
+      if (verts[a].empty()) {
+        err = "agent without poses";
+        return -1;
+      }
+      anchor[bfs_centre(adj, verts[a], std::vector<int>(agent_of, agent_of + n), a, dist, par)] = 1;
+    }
+  }
+  std::vector<double> Tl(static_cast<size_t>(n) * d * b);
+  int it_sum = 0;
+  double rr = 0.0;
+  auto direct = [](const BlockSys& S, int nr, std::vector<double>& rx, std::string& e) {
+    return solve_direct(S, nr, rx, e);
+  };
+  auto pcg = [&](const BlockSys& S, int nr, std::vector<double>& rx, std::string& e) {
+    PcgReport rep;
+    const int r = solve_pcg(S, nr, rx, rtol, max_iters, rep, e);
+    it_sum += rep.iters;
+    rr = std::max(rr, rep.relres);
+    return r;
+  };
+  const int mq = static_cast<int>(q1.size());
+  const int rc = gpu ? chordal_core(d, n, mq, q1.data(), q2.data(), qR.data(), qt.data(), qk.data(), qtau.data(),
+                                    anchor, Tl.data(), pcg, err)
+                     : chordal_core(d, n, mq, q1.data(), q2.data(), qR.data(), qt.data(), qk.data(), qtau.data(),
+                                    anchor, Tl.data(), direct, err);
+  if (iters) *iters = it_sum;
+  if (relres) *relres = rr;
+  if (rc != 0) return rc;
+  auto Rl = [&](int p, int u, int c) { return Tl[(static_cast<size_t>(p) * b + c) * d + u]; };  // R_loc(u, c)
+  auto tl = [&](int p, int u) { return Tl[(static_cast<size_t>(p) * b + d) * d + u]; };
+  // ---- initializeInGlobalFrame: agents join the frame of the agent holding pose 0 in breadth-first
+  // order over the agent graph; each takes the L2 average, over its shared loop closures with agents
+  // already in the frame, of the frame transform every closure implies (rotations: chordal mean
+  // projected to SO(d); translations: tau-weighted mean).  The reference averages robustly (GNC-TLS,
+  // robustSinglePoseAveraging); on outlier-free data the two coincide.
+  std::vector<std::vector<int>> shared(num_agents);
+  std::vector<std::set<int>> nbr(num_agents);
+  for (int e = 0; e < m; ++e) {
+    const int ai = agent_of[p1[e]], aj = agent_of[p2[e]];
+    if (ai == aj) continue;
+    shared[ai].push_back(e);
+    shared[aj].push_back(e);
+    nbr[ai].insert(aj);
+    nbr[aj].insert(ai);
+  }
+  std::vector<double> FR(static_cast<size_t>(num_agents) * d2, 0.0), Ft(static_cast<size_t>(num_agents) * d, 0.0);
+  std::vector<char> done(num_agents, 0);
+  std::vector<int> order{agent_of[0]};
+  done[agent_of[0]] = 1;
+  for (int u = 0; u < d; ++u) FR[static_cast<size_t>(agent_of[0]) * d2 + u * d + u] = 1.0;
+  // world pose of a pose of an aligned agent
+  auto world = [&](int p, double* Rw, double* tw) {
+    const int a = agent_of[p];
+    const double* F = &FR[static_cast<size_t>(a) * d2];
+    for (int u = 0; u < d; ++u) {
+      for (int c = 0; c < d; ++c) {
+        double s = 0.0;
+        for (int w = 0; w < d; ++w) s += F[u * d + w] * Rl(p, w, c);
+        Rw[u * d + c] = s;
+      }
+      double s = Ft[static_cast<size_t>(a) * d + u];
+      for (int w = 0; w < d; ++w) s += F[u * d + w] * tl(p, w);
+      tw[u] = s;
+    }
+  };
+  for (size_t h = 0; h < order.size(); ++h) {
+    for (int A : nbr[order[h]]) {
+      if (done[A]) continue;
+      // closures of A to agents already in the frame: implied world pose of A's endpoint
+      struct Est {
+        int p;
+        double Rw[9], tw[3], w, wk;
+      };
+      std::vector<Est> est;
+      for (int e : shared[A]) {
+        const int i = p1[e], j = p2[e];
+        const bool a_is_j = agent_of[j] == A;
+        const int other = a_is_j ? i : j;
+        if (!done[agent_of[other]]) continue;
+        double Ro[9], to[3];
+        world(other, Ro, to);
+        const double* Re = R + static_cast<size_t>(e) * d2;
+        const double* te = t + static_cast<size_t>(e) * d;
+        Est x;
+        x.p = a_is_j ? j : i;
+        x.w = tau[e];
+        x.wk = kappa[e];
+        for (int u = 0; u < d; ++u)
+          for (int c = 0; c < d; ++c) {
+            double s = 0.0;
+            for (int w = 0; w < d; ++w) s += a_is_j ? Ro[u * d + w] * Re[w * d + c] : Ro[u * d + w] * Re[c * d + w];
+            x.Rw[u * d + c] = s;  // T_j = T_i T_e, or T_i = T_j T_e^-1
+          }
+        for (int u = 0; u < d; ++u) {
+          double s = 0.0;
+          for (int w = 0; w < d; ++w) s += (a_is_j ? Ro[u * d + w] : x.Rw[u * d + w]) * te[w];
+          x.tw[u] = a_is_j ? to[u] + s : to[u] - s;
+        }
+        est.push_back(x);
+      }
+      if (est.empty()) continue;
+      // rotation: chordal mean of Rw R_loc^T (kappa-weighted) projected to SO(d)
+      double M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+      for (const auto& x : est) {
+        const double k = x.wk;
+        for (int u = 0; u < d; ++u)
+          for (int c = 0; c < d; ++c) {
+            double s = 0.0;
+            for (int w = 0; w < d; ++w) s += x.Rw[u * d + w] * Rl(x.p, c, w);
+            M[u * d + c] += k * s;
+          }
+      }
+      double* F = &FR[static_cast<size_t>(A) * d2];
+      project_rotation(d, M, F);
+      double tsum[3] = {0, 0, 0}, wsum = 0.0;
+      for (const auto& x : est) {
+        for (int u = 0; u < d; ++u) {
+          double s = 0.0;
+          for (int w = 0; w < d; ++w) s += F[u * d + w] * tl(x.p, w);
+          tsum[u] += x.w * (x.tw[u] - s);
+        }
+        wsum += x.w;
+      }
+      for (int u = 0; u < d; ++u) Ft[static_cast<size_t>(A) * d + u] = tsum[u] / wsum;
+      done[A] = 1;
+      order.push_back(A);
+    }
+  }
+  for (int a = 0; a < num_agents; ++a)
+    if (!done[a]) {
+      err = "agent graph is not connected (an agent shares no loop closure with the others)";
+      return -1;
+    }
+  for (int p = 0; p < n; ++p) {
+    double Rw[9], tw[3];
+    world(p, Rw, tw);
+    for (int u = 0; u < d; ++u) {
+      for (int c = 0; c < d; ++c) T_out[(static_cast<size_t>(p) * b + c) * d + u] = Rw[u * d + c];
+      T_out[(static_cast<size_t>(p) * b + d) * d + u] = tw[u];
+    }
+  }
+  return 0;
 }
 
 }  // namespace dpgo

@@ -896,6 +896,21 @@ int dpgo_rbcd_bytes(dpgo_rbcd e, double* bytes, double* evaltcg_bytes_per_color)
   return DPGO_HIP_OK;
 }
 
+int dpgo_rbcd_set_trace(dpgo_rbcd e, int capacity) {
+  if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
+  for (auto* h : e->prob)
+    if (h) DPGO_TRY(dpgo_hip_set_trace(h, capacity));
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_get_trace(dpgo_rbcd e, int agent, double* out, int max_records, int* count) {
+  if (!e || agent < 0 || agent >= e->K) return fail(DPGO_HIP_EINVAL, "bad agent");
+  for (int c = 0; c < e->ncolors; ++c)
+    for (int q = e->color_off[c]; q < e->color_off[c + 1]; ++q)
+      if (e->owned[q] == agent) return dpgo_hip_get_trace(e->prob[c], q - e->color_off[c], out, max_records, count);
+  return fail(DPGO_HIP_EINVAL, "agent not owned by this rank");
+}
+
 int dpgo_rbcd_set_kernel_timing(dpgo_rbcd e, int on) {
   if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
   for (auto* h : e->prob)

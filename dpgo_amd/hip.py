@@ -444,6 +444,8 @@ _SIGS2 = [
     ("dpgo_chordal_initialization_gpu", [C.c_int, C.c_int, C.c_int, _ip, _ip, _dp, _dp, _dp, _dp, C.c_double,
                                          C.c_int, _dp, _ip, _dp], C.c_int),
     ("dpgo_graph_chordal_init_gpu", [C.c_void_p, C.c_int, _dp, C.c_double, C.c_int, _dp, _ip, _dp], C.c_int),
+    ("dpgo_graph_distributed_init", [C.c_void_p, C.c_int, _ip, C.c_int, _dp, C.c_int, C.c_double, C.c_int, _dp, _ip,
+                                     _dp], C.c_int),
     ("dpgo_rbcd_default_params", [C.POINTER(RbcdParams)], None),
     ("dpgo_rbcd_plan", [C.c_void_p, C.c_int, _ip, _ip, C.c_int, C.c_int, _lp, _lp, _ip, _ip], C.c_int),
     ("dpgo_rbcd_create", [C.c_void_p, C.c_int, _ip, _ip, C.c_int, C.c_int, C.POINTER(RbcdParams),
@@ -468,6 +470,8 @@ _SIGS2 = [
     ("dpgo_rbcd_stats", [C.c_void_p, _ip], C.c_int),
     ("dpgo_rbcd_bytes", [C.c_void_p, _dp, _dp], C.c_int),
     ("dpgo_rbcd_set_kernel_timing", [C.c_void_p, C.c_int], C.c_int),
+    ("dpgo_rbcd_set_trace", [C.c_void_p, C.c_int], C.c_int),
+    ("dpgo_rbcd_get_trace", [C.c_void_p, C.c_int, _dp, C.c_int, _ip], C.c_int),
     ("dpgo_rbcd_kernel_times", [C.c_void_p, _dp, _lp], C.c_int),
 ]
 _SIGS.extend(_SIGS2)
@@ -559,6 +563,17 @@ class Graph:
         it, rr = C.c_int(), C.c_double()
         _check(lib().dpgo_graph_chordal_init_gpu(self.h, r, Yp, float(rtol), int(max_iters), out.ctypes.data_as(_dp),
                                                  C.byref(it), C.byref(rr)))
+        return (out if dev_layout else from_dev_layout(out, r)), it.value, rr.value
+
+    def distributed_init(self, agent_of_pose, r, YLift, gpu=True, rtol=1e-12, max_iters=20000, dev_layout=False):
+        """Per-agent chordal (localInitialization) + breadth-first frame alignment (initializeInGlobalFrame);
+        returns (X, PCG iterations, relative residual)."""
+        aop, ap = _i32(agent_of_pose)
+        Y, Yp = _f64(np.asarray(YLift, dtype=np.float64).T.ravel())
+        out = np.empty(self.n * (self.d + 1) * r)
+        it, rr = C.c_int(), C.c_double()
+        _check(lib().dpgo_graph_distributed_init(self.h, int(aop.max()) + 1, ap, r, Yp, int(bool(gpu)), float(rtol),
+                                                 int(max_iters), out.ctypes.data_as(_dp), C.byref(it), C.byref(rr)))
         return (out if dev_layout else from_dev_layout(out, r)), it.value, rr.value
 
     def chain_init_dev_layout(self, r, YLift):
@@ -714,6 +729,19 @@ class Rbcd:
         per = np.zeros(self.num_colors)
         _check(lib().dpgo_rbcd_bytes(self.h, C.byref(b), per.ctypes.data_as(_dp)))
         return b.value, per
+
+    def set_trace(self, capacity):
+        _check(lib().dpgo_rbcd_set_trace(self.h, int(capacity)))
+        self._trace_cap = int(capacity)
+
+    def get_trace(self, agent):
+        """Per-iteration records of one owned agent's updates: list of dicts (TRACE_FIELDS)."""
+        cap = getattr(self, "_trace_cap", 0)
+        buf = np.zeros(max(cap, 1) * TRACE_WIDTH)
+        n = C.c_int()
+        _check(lib().dpgo_rbcd_get_trace(self.h, int(agent), buf.ctypes.data_as(_dp), cap, C.byref(n)))
+        return [dict(zip(TRACE_FIELDS, buf[i * TRACE_WIDTH:(i + 1) * TRACE_WIDTH].tolist()))
+                for i in range(min(n.value, cap))]
 
     def set_kernel_timing(self, on):
         _check(lib().dpgo_rbcd_set_kernel_timing(self.h, int(bool(on))))

@@ -62,6 +62,17 @@ int dpgo_chordal_initialization_gpu(int d, int n, int m, const int* p1, const in
                                     int max_iters, double* T_out, int* iters, double* relres);
 int dpgo_graph_chordal_init_gpu(dpgo_graph g, int r, const double* YLift_colmajor, double rtol, int max_iters,
                                 double* X_out, int* iters, double* relres);
+/* The multi-robot initialisation: PGOAgent::localInitialization on every agent (chordal on its private
+ * graph, src/PGOAgent.cpp:947-962; anchored at the agent's breadth-first centre pose instead of its
+ * first pose -- the unconstrained rotation relaxation shrinks with graph distance from the anchor)
+ * then initializeInGlobalFrame (:369-432): agents join the frame of the agent holding pose 0 in
+ * breadth-first order, each by the L2 average over its shared loop closures with agents already in
+ * the frame (the reference averages with GNC-TLS; identical on outlier-free data).  use_gpu: the
+ * block-diagonal chordal systems by Jacobi-PCG on the device (rtol, max_iters), else host Cholesky.
+ * X_out = YLift * T (r x (d+1) n, column-major). */
+int dpgo_graph_distributed_init(dpgo_graph g, int num_agents, const int* agent_of_pose, int r,
+                                const double* YLift_colmajor, int use_gpu, double rtol, int max_iters, double* X_out,
+                                int* iters, double* relres);
 /* Grid graphs: agent = sub-cube (x/s, y/s, z/s), s = k / A; id = ax + A (ay + A az). */
 int dpgo_graph_grid_partition(dpgo_graph g, int agents_per_axis, int* agent_of_pose);
 
@@ -165,6 +176,10 @@ int dpgo_rbcd_bytes(dpgo_rbcd e, double* bytes, double* evaltcg_bytes_per_color)
  * synchronises and returns, per SpMM mode (8: XQ, XQ_G, EVAL, HESS, F, EVAL_TCG, CERT, QF), the
  * summed milliseconds and launch counts since the last call. */
 int dpgo_rbcd_set_kernel_timing(dpgo_rbcd e, int on);
+/* Per-iteration RTR / tCG trace of every owned agent's updates (dpgo_hip_set_trace / _get_trace
+ * records, per agent at its global index). */
+int dpgo_rbcd_set_trace(dpgo_rbcd e, int capacity);
+int dpgo_rbcd_get_trace(dpgo_rbcd e, int agent, double* out, int max_records, int* count);
 int dpgo_rbcd_kernel_times(dpgo_rbcd e, double* ms_per_mode, long long* launches_per_mode);
 
 #ifdef __cplusplus

@@ -797,6 +797,122 @@ def chordal_initialization(d, n, meas: Measurements):
     return T
 
 
+def _bfs_centre(adj, start, member):
+    """Middle of a longest breadth-first path found by two sweeps (restates init.cpp's bfs_centre:
+    the same visiting order, so the same pose)."""
+    def sweep(s):
+        dist = {s: 0}
+        par = {s: -1}
+        q = [s]
+        h = 0
+        last = s
+        while h < len(q):
+            v = q[h]
+            h += 1
+            last = v
+            for u in adj[v]:
+                if member[u] and u not in dist:
+                    dist[u] = dist[v] + 1
+                    par[u] = v
+                    q.append(u)
+        return last, par
+    x, _ = sweep(start)
+    y, par = sweep(x)
+    path = []
+    v = y
+    while v >= 0:
+        path.append(v)
+        v = par[v]
+    return path[len(path) // 2]
+
+
+def distributed_initialization(meas: Measurements, agent_of_pose, num_agents):
+    """PGOAgent::localInitialization on every agent (chordalInitialization of its private graph,
+    src/PGOAgent.cpp:947-962, src/DPGO_utils.cpp:377-476) anchored at the agent's breadth-first centre,
+    then initializeInGlobalFrame (:369-432) with an L2 frame average over the shared loop closures,
+    agents joining in breadth-first order from the agent holding pose 0.  Returns T (d x (d+1) n)."""
+    d = meas.d
+    b = d + 1
+    n = len(agent_of_pose)
+    aop = np.asarray(agent_of_pose)
+    adj = [[] for _ in range(n)]
+    priv = [e for e in range(meas.m) if aop[meas.p1[e]] == aop[meas.p2[e]]]
+    for e in priv:
+        i, j = int(meas.p1[e]), int(meas.p2[e])
+        adj[i].append(j)
+        adj[j].append(i)
+    T = np.zeros((d, n * b))
+    for a in range(num_agents):
+        verts = np.nonzero(aop == a)[0]
+        member = aop == a
+        c = _bfs_centre(adj, int(verts[0]), member)
+        # relabel: anchor first, then the agent's other poses in ascending order
+        order = [c] + [int(v) for v in verts if v != c]
+        loc = {v: k for k, v in enumerate(order)}
+        es = [e for e in priv if aop[meas.p1[e]] == a]
+        sub = meas.subset(np.array(es, dtype=np.int64))
+        sub.p1 = np.array([loc[int(v)] for v in meas.p1[es]], dtype=np.int64)
+        sub.p2 = np.array([loc[int(v)] for v in meas.p2[es]], dtype=np.int64)
+        Ta = chordal_initialization(d, len(order), sub)
+        for k, v in enumerate(order):
+            T[:, v * b:(v + 1) * b] = Ta[:, k * b:(k + 1) * b]
+    shared = [[] for _ in range(num_agents)]
+    nbr = [set() for _ in range(num_agents)]
+    for e in range(meas.m):
+        ai, aj = int(aop[meas.p1[e]]), int(aop[meas.p2[e]])
+        if ai != aj:
+            shared[ai].append(e)
+            shared[aj].append(e)
+            nbr[ai].add(aj)
+            nbr[aj].add(ai)
+    FR = np.zeros((num_agents, d, d))
+    Ft = np.zeros((num_agents, d))
+    done = np.zeros(num_agents, bool)
+    root = int(aop[0])
+    FR[root] = np.eye(d)
+    done[root] = True
+    order = [root]
+
+    def world(p):
+        a = aop[p]
+        return FR[a] @ T[:, p * b:p * b + d], FR[a] @ T[:, p * b + d] + Ft[a]
+
+    h = 0
+    while h < len(order):
+        for A in sorted(nbr[order[h]]):
+            if done[A]:
+                continue
+            est = []
+            for e in shared[A]:
+                i, j = int(meas.p1[e]), int(meas.p2[e])
+                a_is_j = aop[j] == A
+                other = i if a_is_j else j
+                if not done[aop[other]]:
+                    continue
+                Ro, to = world(other)
+                if a_is_j:
+                    Rw = Ro @ meas.R[e]
+                    tw = to + Ro @ meas.t[e]
+                else:
+                    Rw = Ro @ meas.R[e].T
+                    tw = to - Rw @ meas.t[e]
+                est.append((j if a_is_j else i, Rw, tw, meas.kappa[e], meas.tau[e]))
+            if not est:
+                continue
+            M = sum(k * (Rw @ T[:, p * b:p * b + d].T) for p, Rw, tw, k, w in est)
+            FR[A] = project_to_rotation(M)
+            Ft[A] = sum(w * (tw - FR[A] @ T[:, p * b + d]) for p, Rw, tw, k, w in est) / sum(e_[4] for e_ in est)
+            done[A] = True
+            order.append(A)
+        h += 1
+    out = np.zeros_like(T)
+    for p in range(n):
+        Rw, tw = world(p)
+        out[:, p * b:p * b + d] = Rw
+        out[:, p * b + d] = tw
+    return out
+
+
 def lifting_matrix(d, r, seed=2):
     """Repo-defined YLift: Q factor of a seeded Gaussian r x d (SplitMix64)."""
     rng = SplitMix64(seed)

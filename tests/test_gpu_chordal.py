@@ -56,3 +56,36 @@ def test_gpu_chordal_reports_nonconvergence(hip):
     with pytest.raises(hip.DPGOHipError, match="PCG did not reach"):
         hip.chordal_initialization_gpu(meas.d, meas.num_poses, meas.p1, meas.p2, meas.R, meas.t, meas.kappa,
                                        meas.tau, rtol=1e-14, max_iters=3)
+
+
+@pytest.mark.parametrize("name,agents", [("smallGrid3D", 5), ("city10000", 8)])
+def test_gpu_distributed_init_matches_host_and_oracle(hip, name, agents):
+    """Per-agent chordal (one block-diagonal PCG on the device) + frame alignment vs the host Cholesky
+    path and the oracle restatement (PGOAgent::localInitialization + initializeInGlobalFrame)."""
+    meas = load_meas(name)
+    d, n, r = meas.d, meas.num_poses, 5
+    aop = np.minimum(np.arange(n) // (n // agents), agents - 1).astype(np.int32)
+    g = hip.Graph.from_arrays(d, n, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau)
+    YL = O.lifting_matrix(d, r)
+    Xg, iters, rr = g.distributed_init(aop, r, YL, gpu=True, rtol=1e-12)
+    Xh, _, _ = g.distributed_init(aop, r, YL, gpu=False)
+    assert rr <= 1e-12 and iters > 0
+    assert rel(Xg, Xh) <= 1e-8
+    assert rel(Xg, YL @ O.distributed_initialization(meas, aop, agents)) <= 1e-8
+
+
+def test_gpu_distributed_init_grid_cubes(hip):
+    """BASELINE's partition (cube agents) on a 24^3 grid: PCG vs host; far better than odometry."""
+    g = hip.Graph.grid3d(24, seed=2)
+    aop = g.grid_partition(4)
+    r = 5
+    YL = O.lifting_matrix(3, r)
+    Xg, _, _ = g.distributed_init(aop, r, YL, gpu=True, rtol=1e-12)
+    Xh, _, _ = g.distributed_init(aop, r, YL, gpu=False)
+    assert rel(Xg, Xh) <= 1e-8
+    e = hip.Rbcd(g, aop, np.zeros(64, np.int32), 0, 1, hip.rbcd_params(r=r))
+    e.set_X(hip.to_dev_layout(Xg))
+    f_dist, _ = e.central_eval()
+    e.set_X(g.chain_init_dev_layout(r, YL))
+    f_chain, _ = e.central_eval()
+    assert f_dist < 1e-3 * f_chain

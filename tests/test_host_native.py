@@ -162,3 +162,21 @@ def test_cpp_host_cases():
     assert p.returncode == 0, out[-3000:]
     for name in ["Chi2Inv", "RobustSingleRotationAveraging", "RobustSinglePoseAveraging", "Construction"]:
         assert f"[PASS] {name}" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("name,agents", [("smallGrid3D", 5), ("input_INTEL_g2o", 4), ("city10000", 8)])
+def test_distributed_initialization_matches_oracle(H, name, agents):
+    """PGOAgent::localInitialization per agent + initializeInGlobalFrame (host Cholesky path) vs the
+    oracle's restatement: contiguous agents as examples/MultiRobotExample.cpp:73-90."""
+    from oracle import dpgo_oracle as O
+    from tests._common import load_meas, rel
+    meas = load_meas(name)
+    d, n, r = meas.d, meas.num_poses, 5
+    aop = np.minimum(np.arange(n) // (n // agents), agents - 1).astype(np.int32)
+    g = H.Graph.from_arrays(d, n, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau)
+    YL = O.lifting_matrix(d, r)
+    X, _, _ = g.distributed_init(aop, r, YL, gpu=False)
+    To = O.distributed_initialization(meas, aop, agents)
+    assert rel(X, YL @ To) <= 1e-8
+    # the init is a good start: far below the odometry chain's cost
+    assert O.central_cost(meas, YL @ To) < O.central_cost(meas, YL @ O.chain_initialization(d, n, meas))
