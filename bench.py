@@ -8,8 +8,11 @@ One *step* = one sweep over both colours = every agent updated once (64 agent up
 RTR(1 outer, 10 tCG) solve as PGOAgent::updateX configures it, plus the agent status) plus the
 public-pose exchange.
 
-The timed region starts from the odometry initialisation after `--burnin` untimed steps (the iterate
-then re-enters set_X, i.e. PGOAgent::setX: Nesterov restarts from it), then `--warmup` untimed steps.
+Initial X (`--init`): the multi-robot initialisation (every agent's local chordal initialisation aligned
+into one frame over the shared loop closures, PCG on the GPU).  `--burnin` untimed steps then bring the
+solve into its converging phase, where every update's truncated CG runs its 10 iterations (the RTR
+inner loop: Hessian-vector products, preconditioner, CG recurrences); the iterate re-enters set_X
+(PGOAgent::setX: Nesterov restarts from it), then `--warmup` untimed steps and the timed steps.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
@@ -71,7 +74,9 @@ def main():
                          "whole graph (examples/MultiRobotExample.cpp:158; its unconstrained rotation relaxation "
                          "shrinks below fp64 resolution far from the anchor on a 10^6-pose noisy grid); odometry "
                          "= the odometry chain")
-    ap.add_argument("--burnin", type=int, default=0, help="untimed steps before the timed run's set_X")
+    ap.add_argument("--burnin", type=int, default=300,
+                    help="untimed steps from the initialisation before the timed run's set_X: from the distributed "
+                         "init, ~200 steps bring every agent into the regime where tCG runs its 10 iterations")
     ap.add_argument("--k", type=int, default=100, help="grid side (k^3 poses)")
     ap.add_argument("--agents-per-axis", type=int, default=4)
     ap.add_argument("--r", type=int, default=5)

@@ -1258,6 +1258,8 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
         tr[TR_ALPHA] = alpha;
         tr[TR_DELTA] = s.Delta;
         tr[TR_RUN] = s.runs;
+        tr[TR_ZR] = s.z_r;           // <z, r> the step uses
+        tr[TR_NORM_R] = s.norm_r0;   // |r_0| of this tCG
       }
       if (d_Hd <= 0.0 || e_Pe_new >= D2) {
         const double tau = (-s.e_Pd + sqrt(s.e_Pd * s.e_Pd + s.d_Pd * (D2 - s.e_Pe))) / s.d_Pd;
