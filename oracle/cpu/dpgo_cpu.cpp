@@ -8,11 +8,14 @@
 //   LiftedSEManifold project (one-sided Jacobi)  src/manifold/LiftedSEManifold.cpp:34-45
 // Only bench.py's cpu_baseline leg and tests/ use it (via oracle/cpu_port.py): it is the
 // timed host-core baseline ("kind": "port") beside the GPU path, never part of the product.
+#include <omp.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstring>
 #include <map>
+#include <set>
 #include <vector>
 
 namespace {
@@ -216,8 +219,17 @@ void precond(const Agent& A, const double* X, const double* V, double* Z) {
   }
 }
 
+// tCG / RTR counters of one optimize call (the layout of dpgo_hip_stats' first ten ints)
+struct OptStats {
+  int calls = 0, early = 0, runs = 0, tcg_iters = 0, status[5] = {0, 0, 0, 0, 0}, gave_up = 0;
+};
+
 // QuadraticOptimizer::optimize with RTR, 1 outer iteration, radius-shrink retries
-double optimize(const Agent& A, const double* Xin, double* Xout, int max_inner, double radius, double tol, Work& w) {
+double optimize(const Agent& A, const double* Xin, double* Xout, int max_inner, double radius, double tol, Work& w,
+                OptStats* stats = nullptr) {
+  OptStats dummy;
+  OptStats& st = stats ? *stats : dummy;
+  st.calls += 1;
   const size_t L = A.L();
   const int r = A.r, d = A.d, rb = r * A.b;
   std::memcpy(w.x1.data(), Xin, sizeof(double) * L);
@@ -226,6 +238,7 @@ double optimize(const Agent& A, const double* Xin, double* Xout, int max_inner, 
   const double ngf = std::sqrt(ng2);
   if (ngf < tol) {
     std::memcpy(Xout, Xin, sizeof(double) * L);
+    st.early += 1;
     return f1;
   }
   for (int run = 0; run < 12; ++run) {
@@ -236,7 +249,7 @@ double optimize(const Agent& A, const double* Xin, double* Xout, int max_inner, 
     precond(A, w.x1.data(), w.rv.data(), w.z.data());
     double z_r = dot(w.z, w.rv), d_Pd = z_r, e_Pe = 0, e_Pd = 0;
     const double nr0 = std::sqrt(dot(w.rv, w.rv));
-    int status = 4;
+    int status = 4, inner = max_inner;
     for (size_t i = 0; i < L; ++i) w.delta[i] = -w.z[i];
     for (int j = 0; j < max_inner; ++j) {
       hess(A, w.x1.data(), w.S.data(), w.delta.data(), w.Hd.data());
@@ -250,6 +263,7 @@ double optimize(const Agent& A, const double* Xin, double* Xout, int max_inner, 
           w.Heta[i] += tau * w.Hd[i];
         }
         status = dHd <= 0 ? 0 : 1;
+        inner = j + 1;
         break;
       }
       e_Pe = ePe_new;
@@ -260,7 +274,8 @@ double optimize(const Agent& A, const double* Xin, double* Xout, int max_inner, 
       }
       const double nr = std::sqrt(dot(w.rv, w.rv));
       if (nr <= nr0 * std::min(nr0, 0.1)) {
-        status = 2;
+        status = 0.1 < nr0 ? 2 : 3;  // LCON / SCON (kappa < |r0|^theta)
+        inner = j + 1;
         break;
       }
       precond(A, w.x1.data(), w.rv.data(), w.z.data());
@@ -271,7 +286,9 @@ double optimize(const Agent& A, const double* Xin, double* Xout, int max_inner, 
       d_Pd = zr_new + beta * beta * d_Pd;
       z_r = zr_new;
     }
-    (void)status;
+    st.runs += 1;
+    st.tcg_iters += inner;
+    st.status[status] += 1;
     for (int j = 0; j < A.n; ++j) {
       for (int e = 0; e < rb; ++e) w.x2[j * rb + e] = w.x1[j * rb + e] + w.eta[j * rb + e];
       qf_pose(r, d, &w.x2[static_cast<size_t>(j) * rb]);
@@ -285,6 +302,7 @@ double optimize(const Agent& A, const double* Xin, double* Xout, int max_inner, 
     }
     radius /= 4.0;
   }
+  st.gave_up += 1;
   std::memcpy(Xout, Xin, sizeof(double) * L);
   return f1;
 }
@@ -445,5 +463,358 @@ double dpgo_cpu_time_agent_step(int d, int r, int m, const int* p1, const int* p
   if (f_out) *f_out = f;
   return sec / reps;
 }
+
+}  // extern "C"
+
+// =============================================================================================
+// Multi-agent colour-schedule RBCD on the host: the CPU restatement of the engine's schedule
+// (oracle.colour_rbcd, PGOAgent::iterate src/PGOAgent.cpp:642-718 for every agent, L2 cost,
+// block-Jacobi), single-threaded or OpenMP over the agents of a colour class.  Baseline and
+// full-scale parity infrastructure only.
+// =============================================================================================
+namespace {
+
+struct SharedEdge {
+  int own;        // agent-local pose
+  long nbr;       // global neighbour pose
+  int outgoing;   // the agent owns p1
+  double T[4][4], Om[4];
+};
+
+struct CpuAgent {
+  Agent A;
+  std::vector<long> poses;  // global ids, local order
+  std::vector<SharedEdge> shared;
+  OptStats st;
+  double status_rel = 0.0;
+  int ready = 0;
+};
+
+struct CpuEngine {
+  int d = 0, r = 0, b = 0, K = 0, C = 0, accel = 0, restart = 30;
+  long n = 0;
+  std::vector<int> color;
+  std::vector<CpuAgent> ag;
+  std::vector<double> X, Y, V, XP;  // global, r b doubles per pose
+  double gamma = 0.0, alpha = 0.0;
+  long iteration = 0;
+  std::vector<Work> work;  // per thread
+  size_t rb() const { return static_cast<size_t>(r) * b; }
+};
+
+void build_agent(int d, int r, int m, const int* p1, const int* p2, const double* R, const double* t, const double* kappa,
+                 const double* tau, const int* agent_of, const std::vector<int>& local, int a,
+                 const std::vector<int>& edges, CpuAgent& out) {
+  const int b = d + 1, bb = b * b, rb = r * b;
+  Agent& A = out.A;
+  A.d = d;
+  A.r = r;
+  A.b = b;
+  A.n = static_cast<int>(out.poses.size());
+  struct Trip {
+    int i, j;
+    double blk[16];
+  };
+  std::vector<Trip> trips;
+  trips.reserve(edges.size() * 3 + A.n);
+  for (int j = 0; j < A.n; ++j) {
+    Trip tz{j, j, {0}};
+    trips.push_back(tz);
+  }
+  for (int e : edges) {
+    const int i = p1[e], j = p2[e];
+    const bool oi = agent_of[i] == a, oj = agent_of[j] == a;
+    double T[4][4], Om[4];
+    edge_T(d, &R[static_cast<size_t>(e) * d * d], &t[static_cast<size_t>(e) * d], T);
+    for (int u = 0; u < d; ++u) Om[u] = kappa[e];
+    Om[d] = tau[e];
+    Trip ii{local[i], local[i], {0}}, jj{local[j], local[j], {0}}, ij{local[i], local[j], {0}}, ji{local[j], local[i], {0}};
+    for (int u = 0; u < b; ++u)
+      for (int v = 0; v < b; ++v) {
+        double s = 0;
+        for (int q = 0; q < b; ++q) s += T[u][q] * Om[q] * T[v][q];
+        ii.blk[v * b + u] = s;  // column-major blocks (block (j, i) col-major = Q_ij row-major)
+        jj.blk[v * b + u] = u == v ? Om[u] : 0.0;
+        ij.blk[v * b + u] = -T[u][v] * Om[v];
+        ji.blk[v * b + u] = -Om[u] * T[v][u];
+      }
+    if (oi && oj) {
+      trips.push_back(ii);
+      trips.push_back(jj);
+      trips.push_back(ij);
+      trips.push_back(ji);
+    } else {
+      SharedEdge se;
+      se.outgoing = oi ? 1 : 0;
+      se.own = oi ? local[i] : local[j];
+      se.nbr = oi ? j : i;
+      std::memcpy(se.T, T, sizeof(T));
+      std::memcpy(se.Om, Om, sizeof(Om));
+      out.shared.push_back(se);
+      trips.push_back(oi ? ii : jj);
+    }
+  }
+  std::stable_sort(trips.begin(), trips.end(), [](const Trip& x, const Trip& y) { return x.i != y.i ? x.i < y.i : x.j < y.j; });
+  A.rowptr.assign(A.n + 1, 0);
+  A.col.clear();
+  A.blk.clear();
+  for (size_t k = 0; k < trips.size(); ++k) {
+    const Trip& tr = trips[k];
+    if (k > 0 && trips[k - 1].i == tr.i && trips[k - 1].j == tr.j) {  // same block: accumulate
+      double* dst = &A.blk[A.blk.size() - bb];
+      for (int x = 0; x < bb; ++x) dst[x] += tr.blk[x];
+    } else {
+      A.col.push_back(tr.j);
+      A.blk.insert(A.blk.end(), tr.blk, tr.blk + bb);
+    }
+    A.rowptr[tr.i + 1] = static_cast<int>(A.col.size());
+  }
+  // block-Jacobi inverses (Gauss-Jordan) of the diagonal blocks + 0.1 I
+  A.minv.assign(static_cast<size_t>(A.n) * bb, 0.0);
+  for (int j = 0; j < A.n; ++j) {
+    double M[4][8] = {{0}};
+    for (int k = A.rowptr[j]; k < A.rowptr[j + 1]; ++k)
+      if (A.col[k] == j)
+        for (int u = 0; u < b; ++u)
+          for (int v = 0; v < b; ++v) M[u][v] = A.blk[static_cast<size_t>(k) * bb + v * b + u];
+    for (int u = 0; u < b; ++u) {
+      M[u][u] += 0.1;
+      M[u][b + u] = 1.0;
+    }
+    for (int c = 0; c < b; ++c) {
+      int piv = c;
+      for (int u = c + 1; u < b; ++u)
+        if (std::fabs(M[u][c]) > std::fabs(M[piv][c])) piv = u;
+      for (int v = 0; v < 2 * b; ++v) std::swap(M[c][v], M[piv][v]);
+      const double inv = 1.0 / M[c][c];
+      for (int v = 0; v < 2 * b; ++v) M[c][v] *= inv;
+      for (int u = 0; u < b; ++u)
+        if (u != c) {
+          const double f = M[u][c];
+          for (int v = 0; v < 2 * b; ++v) M[u][v] -= f * M[c][v];
+        }
+    }
+    for (int u = 0; u < b; ++u)
+      for (int v = 0; v < b; ++v) A.minv[static_cast<size_t>(j) * bb + u * b + v] = M[u][b + v];
+  }
+  // G slots: the public poses (fixed structure)
+  A.gslot.assign(A.n, -1);
+  for (const auto& se : out.shared)
+    if (A.gslot[se.own] < 0) {
+      A.gslot[se.own] = static_cast<int>(A.gpose.size());
+      A.gpose.push_back(se.own);
+    }
+  A.gblk.assign(A.gpose.size() * rb, 0.0);
+}
+
+// constructGMatrix (:783-859) from the neighbours' current global poses
+void assemble_G(CpuAgent& c, const std::vector<double>& Xg, int r, int b) {
+  const int rb = r * b;
+  std::fill(c.A.gblk.begin(), c.A.gblk.end(), 0.0);
+  for (const auto& se : c.shared) {
+    double* gv = &c.A.gblk[static_cast<size_t>(c.A.gslot[se.own]) * rb];
+    const double* Xn = &Xg[static_cast<size_t>(se.nbr) * rb];
+    for (int cc = 0; cc < b; ++cc)
+      for (int a = 0; a < r; ++a) {
+        double s = 0;
+        for (int u = 0; u < b; ++u) s += Xn[u * r + a] * (se.outgoing ? se.Om[u] * se.T[cc][u] : se.T[u][cc] * se.Om[cc]);
+        gv[cc * r + a] -= s;
+      }
+  }
+}
+
+void gather(const CpuAgent& c, const std::vector<double>& G, std::vector<double>& out, size_t rb) {
+  out.resize(c.poses.size() * rb);
+  for (size_t q = 0; q < c.poses.size(); ++q)
+    std::memcpy(&out[q * rb], &G[static_cast<size_t>(c.poses[q]) * rb], sizeof(double) * rb);
+}
+
+void scatter(const CpuAgent& c, const std::vector<double>& in, std::vector<double>& G, size_t rb) {
+  for (size_t q = 0; q < c.poses.size(); ++q)
+    std::memcpy(&G[static_cast<size_t>(c.poses[q]) * rb], &in[q * rb], sizeof(double) * rb);
+}
+
+void project_all(std::vector<double>& M, int r, int d, size_t rb) {
+  for (size_t q = 0; q < M.size() / rb; ++q) polar_pose(r, d, &M[q * rb]);
+}
+
+// PGOAgent::iterate for agent a (selected or not) on the global state; gamma / alpha already updated
+void iterate_agent(CpuEngine& E, int a, bool selected, bool restart, Work& w) {
+  CpuAgent& c = E.ag[a];
+  const size_t rb = E.rb();
+  if (selected && w.x1.size() != c.A.L()) w.init(c.A.L(), static_cast<size_t>(c.A.n) * E.d * E.d);
+  std::vector<double> X, Y, V, XP;
+  gather(c, E.X, X, rb);
+  XP = X;  // XPrev = X (:673)
+  if (E.accel) {
+    gather(c, E.V, V, rb);
+    Y.resize(X.size());
+    for (size_t i = 0; i < X.size(); ++i) Y[i] = (1.0 - E.alpha) * X[i] + E.alpha * V[i];  // updateY
+    project_all(Y, E.r, E.d, rb);
+    if (selected) {
+      assemble_G(c, E.X, E.r, E.b);  // neighbours' aux poses = their X after iterate(false)
+      optimize(c.A, Y.data(), X.data(), 10, 100.0, 1e-2, w, &c.st);
+    } else {
+      X = Y;  // updateX(false, true)
+    }
+    for (size_t i = 0; i < X.size(); ++i) V[i] = V[i] + E.gamma * (X[i] - Y[i]);  // updateV
+    project_all(V, E.r, E.d, rb);
+    if (restart) {  // restartNesterovAcceleration (:1040-1060)
+      X = XP;
+      if (selected) {
+        assemble_G(c, E.X, E.r, E.b);
+        optimize(c.A, X.data(), X.data(), 10, 100.0, 1e-2, w, &c.st);
+      }
+      V = X;
+      Y = X;
+    }
+    scatter(c, V, E.V, rb);
+    scatter(c, Y, E.Y, rb);
+  } else if (selected) {
+    assemble_G(c, E.X, E.r, E.b);
+    optimize(c.A, X.data(), X.data(), 10, 100.0, 1e-2, w, &c.st);
+  }
+  if (selected) {  // status (:700-716)
+    double s = 0.0;
+    for (size_t i = 0; i < X.size(); ++i) s += (X[i] - XP[i]) * (X[i] - XP[i]);
+    c.status_rel = std::sqrt(s / static_cast<double>(c.poses.size()));
+    c.ready = c.status_rel <= 5e-3 ? 1 : 0;
+  }
+  scatter(c, X, E.X, rb);
+}
+
+}  // namespace
+
+extern "C" {
+
+void* dpgo_cpu_rbcd_create(int d, int r, int m, const int* p1, const int* p2, const double* R, const double* t,
+                           const double* kappa, const double* tau, long n, const int* agent_of_pose, int num_agents,
+                           int accel, int restart_interval) {
+  auto* E = new CpuEngine();
+  E->d = d;
+  E->r = r;
+  E->b = d + 1;
+  E->n = n;
+  E->K = num_agents;
+  E->accel = accel;
+  E->restart = restart_interval;
+  std::vector<int> local(n);
+  E->ag.resize(num_agents);
+  for (long i = 0; i < n; ++i) {
+    const int a = agent_of_pose[i];
+    local[i] = static_cast<int>(E->ag[a].poses.size());
+    E->ag[a].poses.push_back(i);
+  }
+  std::vector<std::vector<int>> edges(num_agents);
+  std::vector<std::set<int>> adj(num_agents);
+  for (int e = 0; e < m; ++e) {
+    const int a1 = agent_of_pose[p1[e]], a2 = agent_of_pose[p2[e]];
+    edges[a1].push_back(e);
+    if (a2 != a1) {
+      edges[a2].push_back(e);
+      adj[a1].insert(a2);
+      adj[a2].insert(a1);
+    }
+  }
+  // greedy colouring in agent-id order (the engine's and oracle.greedy_colors')
+  E->color.assign(num_agents, -1);
+  for (int a = 0; a < num_agents; ++a) {
+    std::set<int> used;
+    for (int nb : adj[a])
+      if (E->color[nb] >= 0) used.insert(E->color[nb]);
+    int c = 0;
+    while (used.count(c)) ++c;
+    E->color[a] = c;
+    E->C = std::max(E->C, c + 1);
+  }
+#pragma omp parallel for schedule(dynamic)
+  for (int a = 0; a < num_agents; ++a)
+    build_agent(d, r, m, p1, p2, R, t, kappa, tau, agent_of_pose, local, a, edges[a], E->ag[a]);
+  const size_t L = static_cast<size_t>(n) * E->rb();
+  E->X.assign(L, 0.0);
+  E->Y.assign(L, 0.0);
+  E->V.assign(L, 0.0);
+  E->work.resize(std::max(1, omp_get_max_threads()));
+  return E;
+}
+
+void dpgo_cpu_rbcd_destroy(void* h) { delete static_cast<CpuEngine*>(h); }
+
+// PGOAgent::setX for every agent: X, and Nesterov restarted (V = Y = X, gamma = alpha = 0)
+void dpgo_cpu_rbcd_set_X(void* h, const double* Xg) {
+  auto* E = static_cast<CpuEngine*>(h);
+  std::memcpy(E->X.data(), Xg, sizeof(double) * E->X.size());
+  E->Y = E->X;
+  E->V = E->X;
+  E->gamma = E->alpha = 0.0;
+  E->iteration = 0;
+}
+
+void dpgo_cpu_rbcd_get_X(void* h, double* Xg) {
+  auto* E = static_cast<CpuEngine*>(h);
+  std::memcpy(Xg, E->X.data(), sizeof(double) * E->X.size());
+}
+
+// One colour iteration (colour = iteration mod C) with `threads` OpenMP threads over each phase's
+// agents.  upd_sec (optional, [num_agents]): wall seconds of each selected agent's iterate(true).
+// timed_serial > 0: the first timed_serial selected agents run one after another on one thread
+// (each timed alone), the rest in parallel.  Returns the iteration's wall seconds.
+double dpgo_cpu_rbcd_iterate(void* h, int threads, double* upd_sec, int timed_serial) {
+  auto* E = static_cast<CpuEngine*>(h);
+  const auto t0 = std::chrono::steady_clock::now();
+  const int c = static_cast<int>(E->iteration % E->C);
+  E->iteration += 1;
+  const bool restart = E->accel && ((E->iteration + 1) % E->restart == 0);
+  if (E->accel) {
+    const double N = E->K;
+    E->gamma = (1 + std::sqrt(1 + 4 * N * N * E->gamma * E->gamma)) / (2 * N);
+    E->alpha = 1 / (E->gamma * N);
+  }
+  std::vector<int> sel, oth;
+  for (int a = 0; a < E->K; ++a) (E->color[a] == c ? sel : oth).push_back(a);
+  const int T = std::max(1, std::min(threads, static_cast<int>(E->work.size())));
+#pragma omp parallel for num_threads(T) schedule(dynamic)
+  for (int q = 0; q < static_cast<int>(oth.size()); ++q) iterate_agent(*E, oth[q], false, restart, E->work[omp_get_thread_num()]);
+  const int ns = std::min<int>(std::max(timed_serial, 0), static_cast<int>(sel.size()));
+  for (int q = 0; q < ns; ++q) {
+    const auto u0 = std::chrono::steady_clock::now();
+    iterate_agent(*E, sel[q], true, restart, E->work[0]);
+    if (upd_sec) upd_sec[sel[q]] = std::chrono::duration<double>(std::chrono::steady_clock::now() - u0).count();
+  }
+#pragma omp parallel for num_threads(T) schedule(dynamic)
+  for (int q = ns; q < static_cast<int>(sel.size()); ++q) {
+    const auto u0 = std::chrono::steady_clock::now();
+    iterate_agent(*E, sel[q], true, restart, E->work[omp_get_thread_num()]);
+    if (upd_sec) upd_sec[sel[q]] = std::chrono::duration<double>(std::chrono::steady_clock::now() - u0).count();
+  }
+  if (restart) E->gamma = E->alpha = 0.0;
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// per agent: calls, early, runs, tcg_iters, status[5], gave_up (dpgo_hip_stats' first ten)
+void dpgo_cpu_rbcd_stats(void* h, int* out) {
+  auto* E = static_cast<CpuEngine*>(h);
+  for (int a = 0; a < E->K; ++a) {
+    const OptStats& s = E->ag[a].st;
+    int* o = out + a * 10;
+    o[0] = s.calls;
+    o[1] = s.early;
+    o[2] = s.runs;
+    o[3] = s.tcg_iters;
+    for (int k = 0; k < 5; ++k) o[4 + k] = s.status[k];
+    o[9] = s.gave_up;
+  }
+}
+
+void dpgo_cpu_rbcd_status(void* h, double* rel, int* ready) {
+  auto* E = static_cast<CpuEngine*>(h);
+  for (int a = 0; a < E->K; ++a) {
+    rel[a] = E->ag[a].status_rel;
+    ready[a] = E->ag[a].ready;
+  }
+}
+
+int dpgo_cpu_rbcd_color(void* h, int agent) { return static_cast<CpuEngine*>(h)->color[agent]; }
+int dpgo_cpu_max_threads(void) { return omp_get_max_threads(); }
 
 }  // extern "C"

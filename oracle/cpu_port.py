@@ -68,3 +68,78 @@ def baseline(graph, agent_of_pose, X_dev_layout, r, accel, num_agents, sample_up
                       f"interior agent {agent} ({npose} poses) on 1 host thread; a full step over all "
                       f"{num_agents} agents would take {num_agents * sec:.2f} s on this core",
             "seconds_per_agent_update": sec, "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
+
+
+# ---- multi-agent colour schedule on the host (dpgo_cpu_rbcd_*) -------------------------------
+class CpuRbcd:
+    """The engine's colour-class RBCD schedule restated on the host (L2, block-Jacobi, Nesterov with
+    restart), OpenMP over the agents of a colour class.  TEST / BASELINE INFRASTRUCTURE."""
+
+    def __init__(self, d, r, arrays, n, agent_of_pose, num_agents, accel, restart_interval=30):
+        L = lib()
+        dp, ip, vp = C.POINTER(C.c_double), C.POINTER(C.c_int), C.c_void_p
+        if not hasattr(L, "_rbcd_bound"):
+            L.dpgo_cpu_rbcd_create.argtypes = [C.c_int, C.c_int, C.c_int, ip, ip, dp, dp, dp, dp, C.c_long, ip, C.c_int,
+                                               C.c_int, C.c_int]
+            L.dpgo_cpu_rbcd_create.restype = vp
+            L.dpgo_cpu_rbcd_destroy.argtypes = [vp]
+            L.dpgo_cpu_rbcd_set_X.argtypes = [vp, dp]
+            L.dpgo_cpu_rbcd_get_X.argtypes = [vp, dp]
+            L.dpgo_cpu_rbcd_iterate.argtypes = [vp, C.c_int, dp, C.c_int]
+            L.dpgo_cpu_rbcd_iterate.restype = C.c_double
+            L.dpgo_cpu_rbcd_stats.argtypes = [vp, ip]
+            L.dpgo_cpu_rbcd_status.argtypes = [vp, dp, ip]
+            L.dpgo_cpu_rbcd_color.argtypes = [vp, C.c_int]
+            L.dpgo_cpu_max_threads.restype = C.c_int
+            L._rbcd_bound = True
+        self._keep = [np.ascontiguousarray(arrays["p1"], np.int32), np.ascontiguousarray(arrays["p2"], np.int32),
+                      np.ascontiguousarray(arrays["R"], np.float64).ravel(),
+                      np.ascontiguousarray(arrays["t"], np.float64).ravel(),
+                      np.ascontiguousarray(arrays["kappa"], np.float64), np.ascontiguousarray(arrays["tau"], np.float64),
+                      np.ascontiguousarray(agent_of_pose, np.int32)]
+        p1, p2, R, t, k, ta, aop = self._keep
+        self.n, self.r, self.d, self.K = int(n), r, d, int(num_agents)
+        self.h = L.dpgo_cpu_rbcd_create(d, r, len(p1), p1.ctypes.data_as(ip), p2.ctypes.data_as(ip),
+                                        R.ctypes.data_as(dp), t.ctypes.data_as(dp), k.ctypes.data_as(dp),
+                                        ta.ctypes.data_as(dp), int(n), aop.ctypes.data_as(ip), int(num_agents),
+                                        int(accel), int(restart_interval))
+        self.colors = [L.dpgo_cpu_rbcd_color(self.h, a) for a in range(self.K)]
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().dpgo_cpu_rbcd_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def set_X(self, X_dev_layout):
+        x = np.ascontiguousarray(X_dev_layout, np.float64)
+        lib().dpgo_cpu_rbcd_set_X(self.h, x.ctypes.data_as(C.POINTER(C.c_double)))
+
+    def get_X(self):
+        x = np.empty(self.n * (self.d + 1) * self.r)
+        lib().dpgo_cpu_rbcd_get_X(self.h, x.ctypes.data_as(C.POINTER(C.c_double)))
+        return x
+
+    def iterate(self, threads=1, timed_serial=0):
+        """One colour iteration; returns (wall seconds, per-agent update seconds (nan = not selected))."""
+        sec = np.full(self.K, np.nan)
+        w = lib().dpgo_cpu_rbcd_iterate(self.h, int(threads), sec.ctypes.data_as(C.POINTER(C.c_double)),
+                                        int(timed_serial))
+        return w, sec
+
+    def stats(self):
+        out = np.zeros(self.K * 10, np.int32)
+        lib().dpgo_cpu_rbcd_stats(self.h, out.ctypes.data_as(C.POINTER(C.c_int)))
+        return out.reshape(self.K, 10)
+
+    def status(self):
+        rc = np.zeros(self.K)
+        rd = np.zeros(self.K, np.int32)
+        lib().dpgo_cpu_rbcd_status(self.h, rc.ctypes.data_as(C.POINTER(C.c_double)), rd.ctypes.data_as(C.POINTER(C.c_int)))
+        return rc, rd
+
+
+def max_threads():
+    return int(lib().dpgo_cpu_max_threads())

@@ -180,3 +180,39 @@ def test_distributed_initialization_matches_oracle(H, name, agents):
     assert rel(X, YL @ To) <= 1e-8
     # the init is a good start: far below the odometry chain's cost
     assert O.central_cost(meas, YL @ To) < O.central_cost(meas, YL @ O.chain_initialization(d, n, meas))
+
+
+@pytest.mark.parametrize("accel", [False, True])
+def test_cpu_engine_matches_oracle_colour_schedule(accel):
+    """oracle/cpu's multi-agent colour schedule (the like-for-like CPU baseline, OpenMP over a colour's
+    agents) vs the numpy PGOAgent restatement, through a Nesterov restart (iteration 29)."""
+    from oracle import cpu_port
+    k, A, r = 6, 2, 5
+    g = O.grid3d(k, seed=3)
+    s = k // A
+    aop = np.array([(c[0] // s) + A * ((c[1] // s) + A * (c[2] // s)) for c in g.extra["coords"]], np.int32)
+    X0 = O.lifting_matrix(3, r) @ O.chain_initialization(3, g.num_poses, g)
+    arrays = dict(p1=g.p1, p2=g.p2, R=g.R, t=g.t, kappa=g.kappa, tau=g.tau)
+    E = cpu_port.CpuRbcd(3, r, arrays, g.num_poses, aop, A ** 3, accel)
+    E.set_X(O.to_dev(X0))
+    iters = 31
+    for _ in range(iters):
+        E.iterate(threads=4)
+    agents, trace = [], []
+    Xo, cols = O.colour_rbcd(g, aop, A ** 3, X0, iters, r, acceleration=accel, agents_out=agents, trace=trace)
+    assert E.colors == cols
+    assert rel(O.from_dev(E.get_X(), r), Xo) <= 1e-10
+    rc, rd = E.status()
+    for a, ag in enumerate(agents):
+        assert abs(rc[a] - ag.status_relative_change) <= 1e-9 * ag.status_relative_change
+        assert bool(rd[a]) == bool(ag.ready_to_terminate)
+    st = E.stats()
+    runs = np.zeros(A ** 3, int)
+    pending = []
+    for t in trace:
+        if isinstance(t, tuple):
+            runs[t[1]] += len(pending)
+            pending = []
+        else:
+            pending.append(t)
+    assert list(st[:, 2]) == list(runs)
