@@ -143,3 +143,40 @@ class CpuRbcd:
 
 def max_threads():
     return int(lib().dpgo_cpu_max_threads())
+
+
+def engine_baseline(graph, agent_of_pose, X_start, r, accel, num_agents, warmup=3, rounds=20):
+    """The like-for-like host baseline: oracle/cpu runs the engine's colour schedule from the GPU's
+    timed-region start X (fresh Nesterov, as after set_X), with the reference's preconditioner
+    replaced by block-Jacobi on both sides (CHOLMOD is absent).  Protocol: warm-up 3, then
+    the median over 20 rounds.
+      single thread: a round = one agent update (iterate(true)) of the first colour, each timed alone;
+      all cores:     a round = one colour iteration (every agent, OpenMP over the selected ones).
+    Returns (result dict, the CPU's X after its iterations, its per-agent counters, iterations run)."""
+    arrays = graph.arrays()
+    E = CpuRbcd(graph.d, r, arrays, graph.n, agent_of_pose, num_agents, accel)
+    E.set_X(X_start)
+    T = max_threads()
+    per_colour = min(sum(1 for c in E.colors if c == 0), sum(1 for c in E.colors if c == 1) or 10 ** 9)
+    ns = min(warmup + rounds, per_colour)
+    _, sec = E.iterate(threads=T, timed_serial=ns)  # iteration 0: ns updates serially, the rest in parallel
+    serial = [sec[a] for a in range(num_agents) if E.colors[a] == 0 and not np.isnan(sec[a])][:ns]
+    one = float(np.median(serial[warmup:])) if len(serial) > warmup else float("nan")
+    walls, sel_counts = [], []
+    for it in range(1, 1 + warmup + rounds):
+        w, s = E.iterate(threads=T)
+        walls.append(w)
+        sel_counts.append(int(np.sum(~np.isnan(s))))
+    med = float(np.median(walls[warmup:]))
+    upd = float(np.median(sel_counts[warmup:]))
+    res = {"value": upd / med, "unit": "RBCD agent-updates/s", "cores": T, "kind": "port",
+           "sample": (f"oracle/cpu colour-schedule RBCD (L2, Nesterov={bool(accel)}, block-Jacobi on both sides: "
+                      f"CHOLMOD absent) from the GPU timed region's start X; all cores: median of {rounds} colour "
+                      f"iterations ({upd:.0f} agent updates each, OpenMP over them) after {warmup} warm-up; "
+                      f"one core: median of {max(len(serial) - warmup, 0)} single agent updates after {warmup}"),
+           "seconds_per_iteration_all_cores": med,
+           "single_thread": {"value": 1.0 / one if one > 0 else None, "seconds_per_agent_update": one,
+                             "cores": 1},
+           "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
+    iters = 1 + warmup + rounds
+    return res, E.get_X(), E.stats(), iters
