@@ -84,6 +84,9 @@ def main():
     ap.add_argument("--spmm-reps", type=int, default=20)
     ap.add_argument("--kernel-timing", type=int, default=1, help="HIP events around in-step X.Q launches")
     ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--pmc-calib-mb", type=int, default=0,
+                    help="tools/pmc_step.py: one device copy of this many MiB before the timed region (a launch of "
+                         "known read/write bytes for the FETCH_SIZE calibration)")
     ap.add_argument("--robust", default="L2", choices=["L2", "GNC_TLS", "TLS", "Huber", "GM", "L1"],
                     help="robust cost (L2: throughput setting; GNC_TLS: the reference default, "
                          "reweighting every 30 iterations on the device)")
@@ -191,8 +194,11 @@ def main():
         f_start, gn_start = central()
         for _ in range(args.warmup):
             step()
+        if args.pmc_calib_mb:
+            cx = torch.ones(args.pmc_calib_mb * (1 << 17), dtype=torch.float64, device=dev)
+            torch.empty_like(cx).copy_(cx)
         st0 = eng.stats().copy()
-        b0, evaltcg_bytes = eng.bytes()
+        b0, _ = eng.bytes()
         eng.kernel_times()  # drop anything recorded so far
         eng.set_kernel_timing(args.kernel_timing)
         sync()
@@ -226,22 +232,31 @@ def main():
            "first_step_boundary_runs": tot["implicit"], "runs": tot["runs"], "updates": tot["calls"],
            "gave_up": tot["gave_up"]}
 
-    # ---- roofline: the in-step X.Q launches timed with HIP events on the engine stream
-    per_mode = {m: {"ms_total": v[0], "launches": v[1], "avg_ms": v[0] / max(v[1], 1)} for m, v in ktimes.items()}
+    # ---- roofline: the in-step X.Q launches timed with HIP events on the engine stream; bytes per launch =
+    # the SURVEY 8d model over every agent of the colour (both colours' launches averaged)
+    mb = [eng.mode_bytes(c) for c in range(eng.num_colors)]
     step_ms = 1e3 * elapsed / args.steps
-    ev = per_mode.get("EVAL_TCG")
-    ev_bytes = float(np.mean(evaltcg_bytes)) if len(evaltcg_bytes) else 0.0
-    achieved = ev_bytes / (ev["avg_ms"] * 1e-3) / 1e9 if ev and ev["avg_ms"] > 0 else 0.0
+    traffic = measured_traffic()
+    per_mode = {}
+    for m, v in ktimes.items():
+        avg = v[0] / max(v[1], 1)
+        byt = float(np.mean([x.get(m, 0.0) for x in mb]))
+        e = {"ms_total": v[0], "launches": v[1], "avg_ms": avg, "algorithmic_bytes_per_launch": byt,
+             "GBps": byt / (avg * 1e-3) / 1e9 if avg > 0 else 0.0}
+        e["frac"] = e["GBps"] / HBM_PEAK_GBS
+        tb = (traffic or {}).get("kernels", {}).get(m, {}).get("traffic_bytes_per_launch")
+        if tb:
+            e["traffic_bytes_per_launch"] = tb
+            e["traffic_GBps"] = tb / (avg * 1e-3) / 1e9
+        per_mode[m] = e
     dominant = max(per_mode, key=lambda m: per_mode[m]["ms_total"]) if per_mode else None
+    dm = per_mode.get(dominant, {})
     step_bytes = (b1 - b0) / args.steps
     if world > 1:
         tb = torch.tensor([step_bytes], dtype=torch.float64, device="cpu" if one_device else dev)
         dist.all_reduce(tb)
         step_bytes = float(tb.item())
-    traffic = measured_traffic()
-    ev_traffic = None
-    if traffic and "kernels" in traffic:
-        ev_traffic = traffic["kernels"].get("EVAL_TCG", {}).get("traffic_bytes_per_launch")
+    spmm_ms_step = sum(v["ms_total"] for v in per_mode.values()) / args.steps
 
     # ---- the standalone X.Q SpMM over one colour class (the metric's "X.Q SpMM HBM GB/s")
     fmt_bytes, spmm_ms = eng.bench_spmm(0, args.spmm_reps)
@@ -276,20 +291,21 @@ def main():
                                f"burn-in {args.burnin} steps",
                    "poses": g.n, "edges": g.m, "agents": num_agents, "parallelism": par},
         "rounds_per_s": args.steps / elapsed,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": ev_traffic,
-                     "kernel": "k_spmm<5,4,MODE_EVAL_TCG,edge-stream> (in-step: f, grad, S, tCG start; every agent "
-                               "of a colour per launch)",
-                     "algorithmic_bytes_per_launch": ev_bytes,
-                     "algorithmic_bytes_definition": "SURVEY 8d: Q as b x b blocks (n + 2 m_in)(b^2 8 + 4) + (n+1) 4 "
-                                                     "+ X 160 n + S 48 n + Minv 80 n + delta 160 n + G 160 per slot",
-                     "avg_launch_ms": ev["avg_ms"] if ev else None,
-                     "launches_timed": ev["launches"] if ev else 0,
-                     "traffic_frac": (ev_traffic / (ev["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS)
-                     if (ev_traffic and ev) else None,
-                     "dominant_in_step_kernel": dominant,
+        "roofline": {"bound": "hbm", "achieved": dm.get("GBps", 0.0), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": dm.get("frac", 0.0),
+                     "traffic": dm.get("traffic_bytes_per_launch"),
+                     "kernel": f"k_spmm<5,4,MODE_{dominant},edge-stream>: the in-step kernel with the most time "
+                               "(every agent of a colour per launch)",
+                     "algorithmic_bytes_per_launch": dm.get("algorithmic_bytes_per_launch"),
+                     "algorithmic_bytes_definition": "SURVEY 8d per agent: Q as b x b blocks (n + 2 m_in)(b^2 8 + 4) "
+                                                     "+ (n+1) 4 + pose vector 160 n, + per mode: HESS eta 160 n + S "
+                                                     "48 n + out 160 n; EVAL_TCG S 48 n + Minv 80 n + out 160 n + G; "
+                                                     "QF half pass + S; F half pass + G (dpgo_rbcd_mode_bytes)",
+                     "avg_launch_ms": dm.get("avg_ms"),
+                     "launches_timed": dm.get("launches", 0),
+                     "traffic_frac": (dm["traffic_GBps"] / HBM_PEAK_GBS) if "traffic_GBps" in dm else None,
                      "in_step_spmm": per_mode,
+                     "spmm_ms_per_step": spmm_ms_step,
                      "step_level": {"algorithmic_bytes_per_step": step_bytes,
                                     "GBps": step_bytes / (step_ms * 1e-3) / 1e9,
                                     "frac": step_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -301,7 +317,8 @@ def main():
                     "GBps": bsr_bytes / (spmm_ms * 1e-3) / 1e9 if spmm_ms > 0 else 0.0,
                     "frac": bsr_bytes / (spmm_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if spmm_ms > 0 else 0.0,
                     "format_bytes_per_launch": fmt_bytes,
-                    "traffic_bytes_per_launch": traffic.get("traffic_bytes_per_launch") if traffic else None},
+                    "traffic_bytes_per_launch": (traffic or {}).get("kernels", {}).get("XQ", {}).get(
+                        "traffic_bytes_per_launch")},
         "hvp": {"per_s": 1e3 / hvp_ms if hvp_ms > 0 else 0.0, "avg_launch_ms": hvp_ms,
                 "agents": int(eng.agents_per_color[0]),
                 "what": "Riemannian HVP (EucHessianEta + EucHvToHv, tangent-projected) over colour class 0"},

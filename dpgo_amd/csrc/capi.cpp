@@ -510,7 +510,7 @@ int sync_g(dpgo_hip_problem h) {
 
 int ensure_work(dpgo_hip_problem h) {
   const size_t L = h->vec_len(), SL = h->s_len();
-  DevBuf<double>* vecs[] = {&h->x1, &h->x2, &h->g, &h->g2, &h->eta, &h->Heta, &h->rv,
+  DevBuf<double>* vecs[] = {&h->x1, &h->x2, &h->g, &h->g2, &h->eta, &h->rv,
                             &h->z,  &h->delta, &h->Hdelta, &h->tA, &h->tB};
   for (auto* v : vecs) HIP_TRY(v->ensure(L));
   HIP_TRY(h->S.ensure(SL));
@@ -1241,12 +1241,12 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     auto launch_rest = [&](int j) -> int {
       auto cu = make_ctx(h, dpgo::FLAG_TCG_MODE, h->pb.p);
       HIP_TRY(dpgo::launch_tcg_update(r, b, cu, x1, h->minv.p, pmode, h->delta.p, h->Hdelta.p, h->eta.p,
-                                      h->Heta.p, j == 0 ? h->g.p : h->rv.p, h->rv.p, h->z.p, j == 0 ? 1 : 0));
+                                      j == 0 ? h->g.p : h->rv.p, h->rv.p, h->z.p, j == 0 ? 1 : 0));
       if (exact)  // z = Prec(r) with the factor; replaces the identity z and its partials
         DPGO_TRY(exact_precond(h, h->rv.p, h->z.p, nullptr, x1, h->rv.p, h->pb.p, dpgo::FLAG_TCG_MODE));
       const int tag = next_tag(h);
       tags.push_back(tag);
-      DPGO_TRY(finalize(h, dpgo::OP_TCG_CHECK, h->pb.p, 2, nullptr, 0, &o, nullptr, 1, tag));
+      DPGO_TRY(finalize(h, dpgo::OP_TCG_CHECK, h->pb.p, 3, nullptr, 0, &o, nullptr, 1, tag));
       if (j + 1 < P.tr_max_inner) {  // the last direction update is never used
         auto cd = make_ctx(h, dpgo::FLAG_TCG, nullptr);
         HIP_TRY(dpgo::launch_tcg_dir(r, b, cd, h->z.p, h->delta.p));
@@ -1264,7 +1264,7 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     const bool spec = qf0 && single;
     auto launch_candidate = [&](int run_flag, int filter) -> int {
       auto cr = make_ctx(h, run_flag, h->pa.p);
-      HIP_TRY(dpgo::launch_retract(r, b, cr, x1, h->eta.p, 1.0, x2, h->g.p, h->Heta.p, h->delta.p));
+      HIP_TRY(dpgo::launch_retract(r, b, cr, x1, h->eta.p, 1.0, x2, h->g.p, nullptr, h->delta.p));
       // single Run: only f(x2) and |grad(x2)| are consumed (fOpt / gradNormOpt), |grad(x2)| only as a
       // statistic
       const int rtag = next_tag(h);

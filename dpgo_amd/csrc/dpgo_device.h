@@ -25,7 +25,8 @@ struct AgentState {
   double Delta, Delta_max;        // trust-region radius
   double e_Pe, e_Pd, d_Pd, z_r;   // tCG recurrences
   double norm_r0, alpha, tau, beta, step;
-  double g_eta, eta_Heta, rho, rel_change;
+  double g_eta, eta_Heta, rho, rel_change;  // eta_Heta: carried through tCG as a scalar (OP_TCG_CHECK)
+  double d_Hd;                              // <delta, Hdelta> of the last step test
   int tcg_active;   // tCG still iterating
   int tcg_mode;     // update kernel: 0 CG step (alpha), 1 boundary step (tau) + stop, 2 idle
   int tcg_status;   // 0 NEGCURVTURE 1 EXCREGION 2 LCON 3 SCON 4 MAXITER, -1 none
@@ -36,8 +37,8 @@ struct AgentState {
   int outer_iters;  // accepted + rejected outer iterations
   int gave_up;      // too many rejections -> returns the input
   int copy_pending;  // multi-iteration Run: accepted step still to be copied into x1
-  int eta_implicit;  // tCG stopped at its first step on the boundary: eta = step delta, Heta = step Hdelta
-                     // are not materialised (k_retract reads delta; g_eta / eta_Heta set by OP_TCG_STEP)
+  int eta_implicit;  // tCG stopped at its first step on the boundary: eta = step delta is not
+                     // materialised (k_retract reads delta; g_eta / eta_Heta set by OP_TCG_STEP)
   int ready;         // PGOAgentStatus::readyToTerminate of the last update (OP_STATUS)
   double status_rel_change;  // PGOAgentStatus::relativeChange = |X - XPrev| / sqrt(n) (OP_STATUS)
   // cumulative statistics since the handle was created (never reset; read by dpgo_hip_stats)

@@ -206,7 +206,7 @@ inline hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const 
 hipError_t launch_tcg_init(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
                            const double* g, double* delta);
 hipError_t launch_tcg_update(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
-                             const double* delta, const double* Hdelta, double* eta, double* Heta,
+                             const double* delta, const double* Hdelta, double* eta,
                              const double* r_in, double* rv, double* z, int first);
 hipError_t launch_tcg_dir(int r, int b, const LaunchCtx& c, const double* z, double* delta);
 hipError_t launch_retract(int r, int b, const LaunchCtx& c, const double* X, const double* V, double scale,

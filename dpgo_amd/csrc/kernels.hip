@@ -665,63 +665,64 @@ __global__ __launch_bounds__(kThreads) void k_tcg_init(LaunchCtx c, const double
   block_partials<2>(parts, c.partials, p.tile);
 }
 
-// tCG step (A.4 steps 1-3, 5 first half): eta += s delta; Heta += s Hdelta; for a CG step
-// (mode 0) also r += alpha Hdelta and z = Prec(r) with partials <z,r>, |r|^2.
+// tCG step (A.4 steps 1-3, 5 first half): eta += s delta; for a CG step (mode 0) also r += alpha Hdelta
+// and z = Prec(r) with partials <z,r>, |r|^2.  Heta is never formed: the third partial <eta_old, Hdelta>
+// lets OP_TCG_CHECK carry <eta, Heta> as a scalar, <eta + s delta, H(eta + s delta)> = <eta, Heta>
+// + s (2 <eta, Hdelta> + s <delta, Hdelta>) (H self-adjoint on the tangent space), which is all the rho
+// test reads of it (src/QuadraticOptimizer.cpp via ROPTLIB RTRNewton).
 template <int R, int B>
 __global__ __launch_bounds__(kThreads) void k_tcg_update(LaunchCtx c, const double* __restrict__ X,
                                                          const double* __restrict__ Minv, int pmode,
                                                          const double* __restrict__ delta,
                                                          const double* __restrict__ Hdelta,
-                                                         double* __restrict__ eta, double* __restrict__ Heta,
-                                                         const double* r_in, double* r, double* __restrict__ z,
-                                                         int first) {
+                                                         double* __restrict__ eta, const double* r_in, double* r,
+                                                         double* __restrict__ z, int first) {
   const PoseLane p = pose_lane<B>(c);
   if (tile_skipped(c, p.agent)) return;  // FLAG_TCG_MODE: skips mode 2
   const AgentState& st = c.state[p.agent];
-  if (st.eta_implicit) return;  // first-step boundary exit: eta / Heta stay implicit (k_retract)
+  if (st.eta_implicit) return;  // first-step boundary exit: eta stays implicit (k_retract)
   const int mode = st.tcg_mode;
   const double step = st.step;
   const bool own = p.ok && p.k < B;
   const long off = p.j * (R * B) + p.k * R;
-  double dcol[R], hcol[R], ecol[R], hecol[R];
+  double dcol[R], hcol[R], ecol[R];
   load_col<R, B>(delta, p.j, p.k, p.ok, dcol);
   load_col<R, B>(Hdelta, p.j, p.k, p.ok, hcol);
-  if (first) {  // eta = Heta = 0 at the start of tCG
+  double eh = 0.0;
+  if (first) {  // eta = 0 at the start of tCG
 #pragma unroll
-    for (int a = 0; a < R; ++a) ecol[a] = hecol[a] = 0.0;
+    for (int a = 0; a < R; ++a) ecol[a] = 0.0;
   } else {
     load_col<R, B>(eta, p.j, p.k, p.ok, ecol);
-    load_col<R, B>(Heta, p.j, p.k, p.ok, hecol);
+#pragma unroll
+    for (int a = 0; a < R; ++a) eh = fma(ecol[a], hcol[a], eh);
   }
 #pragma unroll
-  for (int a = 0; a < R; ++a) {
-    ecol[a] = fma(step, dcol[a], ecol[a]);
-    hecol[a] = fma(step, hcol[a], hecol[a]);
-  }
+  for (int a = 0; a < R; ++a) ecol[a] = fma(step, dcol[a], ecol[a]);
   store_vec<R>(eta, off, own, ecol);
-  store_vec<R>(Heta, off, own, hecol);
-  if (mode != 0) return;  // boundary step: tCG stops, r/z untouched (uniform per agent)
-  double rcol[R], xcol[R];
-  load_col<R, B>(r_in, p.j, p.k, p.ok, rcol);  // r_in = grad on the first step
-  load_col<R, B>(X, p.j, p.k, p.ok, xcol);
-#pragma unroll
-  for (int a = 0; a < R; ++a) rcol[a] = fma(step, hcol[a], rcol[a]);
-  double Rf[R][B], Xf[R][B], Zf[R][B];
-  quad_gather<R, B>(rcol, Rf);
-  quad_gather<R, B>(xcol, Xf);
-  precond_pose<R, B>(Xf, Minv, p.j, p.ok, pmode, Rf, Zf);
-  double zc[R];
-  select_col<R, B>(Zf, p.k, zc);
   double zr = 0.0, rr = 0.0;
+  if (mode == 0) {  // a boundary step ends tCG: r / z untouched (uniform per agent)
+    double rcol[R], xcol[R];
+    load_col<R, B>(r_in, p.j, p.k, p.ok, rcol);  // r_in = grad on the first step
+    load_col<R, B>(X, p.j, p.k, p.ok, xcol);
 #pragma unroll
-  for (int a = 0; a < R; ++a) {
-    zr = fma(zc[a], rcol[a], zr);
-    rr = fma(rcol[a], rcol[a], rr);
+    for (int a = 0; a < R; ++a) rcol[a] = fma(step, hcol[a], rcol[a]);
+    double Rf[R][B], Xf[R][B], Zf[R][B];
+    quad_gather<R, B>(rcol, Rf);
+    quad_gather<R, B>(xcol, Xf);
+    precond_pose<R, B>(Xf, Minv, p.j, p.ok, pmode, Rf, Zf);
+    double zc[R];
+    select_col<R, B>(Zf, p.k, zc);
+#pragma unroll
+    for (int a = 0; a < R; ++a) {
+      zr = fma(zc[a], rcol[a], zr);
+      rr = fma(rcol[a], rcol[a], rr);
+    }
+    store_vec<R>(r, off, own, rcol);
+    store_vec<R>(z, off, own, zc);
   }
-  store_vec<R>(r, off, own, rcol);
-  store_vec<R>(z, off, own, zc);
-  double parts[2] = {own ? zr : 0.0, own ? rr : 0.0};
-  block_partials<2>(parts, c.partials, p.tile);
+  double parts[3] = {own ? zr : 0.0, own ? rr : 0.0, own ? eh : 0.0};
+  block_partials<3>(parts, c.partials, p.tile);
 }
 
 // delta = -z + beta delta for agents whose tCG continues (A.4 step 5)
@@ -738,9 +739,10 @@ __global__ __launch_bounds__(kThreads) void k_tcg_dir(LaunchCtx c, const double*
   for (int a = 0; a < R; ++a) delta[off + a] = fma(beta, delta[off + a], -z[off + a]);
 }
 
-// x2 = R_x1(scale * eta) (QF retraction, A.2) with partials <g,eta>, <eta,Heta>.  For agents whose
-// eta is implicit (AgentState::eta_implicit) and delta_impl is given, eta = step delta is formed here
-// (the same fma the update kernel would have stored) and the dots come from OP_TCG_STEP instead.
+// x2 = R_x1(scale * eta) (QF retraction, A.2) with partials <g,eta> and, when HV is given, <eta,HV>
+// (the tCG carries <eta, Heta> as a scalar and passes none).  For agents whose eta is implicit
+// (AgentState::eta_implicit) and delta_impl is given, eta = step delta is formed here (the same fma the
+// update kernel would have stored) and the dots come from OP_TCG_STEP instead.
 template <int R, int B>
 __global__ __launch_bounds__(kThreads) void k_retract(LaunchCtx c, const double* __restrict__ X,
                                                       const double* __restrict__ V, double scale,
@@ -776,13 +778,15 @@ __global__ __launch_bounds__(kThreads) void k_retract(LaunchCtx c, const double*
   if (g != nullptr) {
     double ge = 0.0, eh = 0.0;
     if (!impl) {
-      double gcol[R], hcol[R];
+      double gcol[R];
       load_col<R, B>(g, p.j, p.k, p.ok, gcol);
-      load_col<R, B>(HV, p.j, p.k, p.ok, hcol);
 #pragma unroll
-      for (int a = 0; a < R; ++a) {
-        ge = fma(gcol[a], vcol[a], ge);
-        eh = fma(vcol[a], hcol[a], eh);
+      for (int a = 0; a < R; ++a) ge = fma(gcol[a], vcol[a], ge);
+      if (HV != nullptr) {
+        double hcol[R];
+        load_col<R, B>(HV, p.j, p.k, p.ok, hcol);
+#pragma unroll
+        for (int a = 0; a < R; ++a) eh = fma(vcol[a], hcol[a], eh);
       }
     }
     double parts[2] = {own ? ge : 0.0, own ? eh : 0.0};
@@ -1219,6 +1223,7 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       s.norm_r0 = sqrt(tot[1]);
       s.tcg_active = 1;
       s.tcg_status = TCG_MAXITER;
+      s.eta_Heta = 0.0;
       break;
     }
     case OP_TCG_INIT: {
@@ -1238,6 +1243,7 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       s.tcg_mode = 2;
       s.tcg_status = TCG_MAXITER;
       s.tcg_iters = 0;
+      s.eta_Heta = 0.0;
       break;
     }
     case OP_TCG_STEP: {  // after k_spmm<HESS>: tot[0] = <delta, H delta>
@@ -1246,6 +1252,7 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
         break;
       }
       const double d_Hd = tot[0];
+      s.d_Hd = d_Hd;
       const double alpha = s.z_r / d_Hd;
       const double e_Pe_new = s.e_Pe + 2.0 * alpha * s.e_Pd + alpha * alpha * s.d_Pd;
       const double D2 = s.Delta * s.Delta;
@@ -1289,7 +1296,9 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       }
       break;
     }
-    case OP_TCG_CHECK: {  // after k_tcg_update: tot[0] = <z,r>, tot[1] = |r|^2
+    case OP_TCG_CHECK: {  // after k_tcg_update: tot[0] = <z,r>, tot[1] = |r|^2, tot[2] = <eta_old, Hdelta>
+      if (s.tcg_mode == 2 || s.eta_implicit) break;
+      s.eta_Heta += s.step * (2.0 * tot[2] + s.step * s.d_Hd);  // <eta, Heta> after eta += step delta
       if (s.tcg_mode != 0) break;
       const double norm_r = sqrt(tot[1]);
       const int j = s.tcg_iters - 1;
@@ -1318,14 +1327,11 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       s.z_r = z_r_new;
       break;
     }
-    case OP_RHO: {  // pa: <g,eta>, <eta,Heta> ; pb: f(x2), |grad(x2)|^2
+    case OP_RHO: {  // pa: <g,eta> ; pb: f(x2), |grad(x2)|^2 (<eta,Heta> carried by OP_TCG_CHECK)
       if (!s.run_active) break;
       s.tcg_active = 0;
       s.tcg_mode = 2;
-      if (!s.eta_implicit) {
-        s.g_eta = tot[0];
-        s.eta_Heta = tot[1];
-      }
+      if (!s.eta_implicit) s.g_eta = tot[0];
       s.f2 = tot[2];
       s.ngf2 = sqrt(tot[3]);
       const double denom = -s.g_eta - 0.5 * s.eta_Heta;
@@ -2010,10 +2016,10 @@ hipError_t launch_tcg_init(int r, int b, const LaunchCtx& c, const double* X, co
 }
 
 hipError_t launch_tcg_update(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
-                             const double* delta, const double* Hdelta, double* eta, double* Heta,
+                             const double* delta, const double* Hdelta, double* eta,
                              const double* r_in, double* rv, double* z, int first) {
   if (c.num_tiles == 0) return hipSuccess;
-  DPGO_DISPATCH(r, b, (k_tcg_update<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, Minv, pmode, delta, Hdelta, eta, Heta, r_in, rv, z, first)));
+  DPGO_DISPATCH(r, b, (k_tcg_update<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, Minv, pmode, delta, Hdelta, eta, r_in, rv, z, first)));
   return hipGetLastError();
 }
 

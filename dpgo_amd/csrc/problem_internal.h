@@ -114,7 +114,7 @@ struct dpgo_hip_problem_s {
   long chol_blocks = 0;
 
   // work
-  dpgo::DevBuf<double> x1, x2, g, g2, S, S2, eta, Heta, rv, z, delta, Hdelta, tA, tB;
+  dpgo::DevBuf<double> x1, x2, g, g2, S, S2, eta, rv, z, delta, Hdelta, tA, tB;
   dpgo::DevBuf<double> pa, pb, sums, coef_a, coef_b;
   // |X_out - X_in|^2 partials of the single-Run output select: each tile written once, in the Run
   // its agent's outcome was decided (an in-place X_in is overwritten by then)

@@ -880,9 +880,11 @@ int dpgo_rbcd_bytes(dpgo_rbcd e, double* bytes, double* evaltcg_bytes_per_color)
       total += calls * evaltcg;
       total += runs * (half_in + z.n * SW);                           // QF first step test
       total += (iters - runs + (runs - impl)) * (full_in + z.n * (P + SW + P));  // HESS
-      total += cg * z.n * (11.0 * P + DW) + (bnd - impl) * z.n * 6.0 * P;     // tCG updates
+      // tCG updates: a CG step reads delta, Hdelta, eta, r, X, Minv and writes eta, r, z; a boundary step
+      // reads delta, Hdelta, eta and writes eta (the first step of a tCG reads no eta)
+      total += cg * z.n * (8.0 * P + DW) - runs * z.n * P + (bnd - impl) * z.n * 4.0 * P;
       total += std::max(0.0, cg - lcon - maxit) * z.n * 3.0 * P;                 // tCG directions
-      total += runs * z.n * 3.0 * P + (runs - impl) * z.n * 2.0 * P;            // retraction
+      total += runs * z.n * 3.0 * P + (runs - impl) * z.n * 1.0 * P;            // retraction (+ g)
       total += runs * (half_in + gread);                                          // f(x2)
       if (e->P.status) total += calls * z.n * 2.0 * P;                            // status |X - XPrev|
     }
@@ -893,6 +895,25 @@ int dpgo_rbcd_bytes(dpgo_rbcd e, double* bytes, double* evaltcg_bytes_per_color)
     (void)calls_all;
   }
   if (bytes) *bytes = total;
+  return DPGO_HIP_OK;
+}
+
+// Algorithmic bytes of ONE X.Q launch per SpMM mode over every agent of a colour (the same per-agent
+// terms as dpgo_rbcd_bytes): the per-launch figure the in-step roofline divides by the launch time.
+int dpgo_rbcd_mode_bytes(dpgo_rbcd e, int color, double* out) {
+  if (!e || !out || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
+  const double P = pose_bytes(e), b = e->b, d = e->d;
+  const double blk = b * b * 8.0 + 4.0, DW = 8.0 * b * (b + 1) / 2, SW = 8.0 * d * (d + 1) / 2;
+  for (int m = 0; m < 8; ++m) out[m] = 0.0;
+  for (const auto& z : e->asz[color]) {
+    const double full_in = (z.n + 2.0 * z.m_in) * blk + (z.n + 1.0) * 4.0 + z.n * P;
+    const double half_in = (z.n + z.m_in) * blk + (z.n + 1.0) * 4.0 + z.n * P;
+    const double gread = z.gslots * P + z.n * 4.0;
+    out[MODE_EVAL_TCG] += full_in + z.n * (SW + DW + P) + gread;
+    out[MODE_HESS] += full_in + z.n * (P + SW + P);
+    out[MODE_QF] += half_in + z.n * SW;
+    out[MODE_F] += half_in + gread;
+  }
   return DPGO_HIP_OK;
 }
 

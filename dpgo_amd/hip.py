@@ -469,6 +469,7 @@ _SIGS2 = [
     ("dpgo_rbcd_status", [C.c_void_p, _dp, _ip], C.c_int),
     ("dpgo_rbcd_stats", [C.c_void_p, _ip], C.c_int),
     ("dpgo_rbcd_bytes", [C.c_void_p, _dp, _dp], C.c_int),
+    ("dpgo_rbcd_mode_bytes", [C.c_void_p, C.c_int, _dp], C.c_int),
     ("dpgo_rbcd_set_kernel_timing", [C.c_void_p, C.c_int], C.c_int),
     ("dpgo_rbcd_set_trace", [C.c_void_p, C.c_int], C.c_int),
     ("dpgo_rbcd_get_trace", [C.c_void_p, C.c_int, _dp, C.c_int, _ip], C.c_int),
@@ -729,6 +730,12 @@ class Rbcd:
         per = np.zeros(self.num_colors)
         _check(lib().dpgo_rbcd_bytes(self.h, C.byref(b), per.ctypes.data_as(_dp)))
         return b.value, per
+
+    def mode_bytes(self, color):
+        """{SpMM mode: algorithmic bytes of one launch over every agent of the colour}."""
+        out = np.zeros(8)
+        _check(lib().dpgo_rbcd_mode_bytes(self.h, int(color), out.ctypes.data_as(_dp)))
+        return {SPMM_MODES[m]: float(out[m]) for m in range(8) if out[m] > 0}
 
     def set_trace(self, capacity):
         _check(lib().dpgo_rbcd_set_trace(self.h, int(capacity)))

@@ -172,6 +172,9 @@ int dpgo_rbcd_stats(dpgo_rbcd e, int* out);
  * exact per-agent launch counts) and, per colour, the bytes of one tCG-start evaluation pass
  * (k_spmm MODE_EVAL_TCG) over the colour (evaltcg_bytes_per_color[num_colors], may be NULL). */
 int dpgo_rbcd_bytes(dpgo_rbcd e, double* bytes, double* evaltcg_bytes_per_color);
+/* Algorithmic bytes of one X.Q launch over every agent of `color`, per SpMM mode (out[8], indexed as
+ * dpgo_rbcd_kernel_times; 0 for modes the engine does not launch in a step). */
+int dpgo_rbcd_mode_bytes(dpgo_rbcd e, int color, double* out);
 /* HIP events around every in-step X.Q launch (on the launch stream) while on; dpgo_rbcd_kernel_times
  * synchronises and returns, per SpMM mode (8: XQ, XQ_G, EVAL, HESS, F, EVAL_TCG, CERT, QF), the
  * summed milliseconds and launch counts since the last call. */
