@@ -186,7 +186,7 @@ struct RobustParams {
 };
 
 // Runtime-selectable kernel variants (A/B tuning in one process; see tools/spmm_ab.py).
-enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_COUNT = 4 };
+enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH = 2, TUNE_COUNT = 4 };
 // variant of the edge-stream SpMM used unless TUNE_EDGE_VARIANT overrides it (bit 0: XCD-aware
 // tile remap; v >> 1: minimum waves per SIMD the register allocation must allow, none/4/5/6)
 constexpr int kEdgeDefaultVariant = 1;

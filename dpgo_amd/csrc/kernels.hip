@@ -328,10 +328,12 @@ __device__ __forceinline__ void spmm_accumulate_edges(const QView& q, const doub
 constexpr int var_unr(int v) { return v == 2 || v == 5 ? 2 : (v == 3 || v == 4) ? 4 : 1; }
 constexpr bool var_nt(int v) { return v == 1; }  // default-policy loads measured faster (tools/spmm_ab.py)
 constexpr bool var_xcd(int v) { return v == 4 || v == 5 || v == 6; }
-// edge-stream variants: bit 0 = XCD-aware tile remap, v >> 1 = register budget (minimum waves per
-// SIMD requested from the compiler: 0 -> none, 1 -> 4, 2 -> 5, 3 -> 6)
+// edge-stream variants: bit 0 = XCD-aware tile remap, bits 1-2 = register budget (minimum waves per
+// SIMD requested from the compiler: 0 -> none, 1 -> 4, 2 -> 5, 3 -> 6), bit 3 = the epilogue's own-pose
+// operands (X, S, Minv, G slot) loaded before the edge loop, their latency hidden behind it
 constexpr bool evar_xcd(int v) { return (v & 1) != 0; }
-constexpr int evar_waves(int v) { return (v >> 1) == 0 ? 1 : 3 + (v >> 1); }
+constexpr int evar_waves(int v) { return ((v >> 1) & 3) == 0 ? 1 : 3 + ((v >> 1) & 3); }
+constexpr bool evar_pre(int v) { return (v & 8) != 0; }
 
 
 __device__ void finalize_agent(const FinalizeArgs& f, int agent);
@@ -378,6 +380,27 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
   if (tile_skipped(c, p.agent)) {
     if constexpr (spmm_fusable(MODE)) spmm_arrive(args, p.agent);
     return;
+  }
+
+  // epilogue operands issued ahead of the edge loop (edge-stream variant bit 3)
+  constexpr bool PRE = FMT == QFMT_EDGES && evar_pre(VAR);
+  constexpr bool PRE_S = PRE && (MODE == MODE_HESS || MODE == MODE_QF || MODE == MODE_CERT);
+  constexpr bool PRE_X = PRE && MODE == MODE_HESS;
+  constexpr bool PRE_M = PRE && MODE == MODE_EVAL_TCG;
+  double pre_x[R], pre_s[s_width(D)], pre_m[B];
+  int pre_slot = -1;
+  if constexpr (PRE_X) load_col<R, B>(X, p.j, p.k, p.ok, pre_x);
+  if constexpr (PRE_S) {
+#pragma unroll
+    for (int q = 0; q < s_width(D); ++q) pre_s[q] = p.ok ? S_in[p.j * s_width(D) + q] : 0.0;
+  }
+  if constexpr (PRE_M) {
+    if (args.pmode != PRECON_NONE) {
+#pragma unroll
+      for (int u = 0; u < B; ++u)
+        pre_m[u] = p.ok ? args.Minv[p.j * diag_width(B - 1) + minv_index<B>(u, p.k < B ? p.k : 0)] : 0.0;
+    }
+    if (p.ok && p.k < B && gidx != nullptr) pre_slot = gidx[p.j];
   }
 
   double acc[R][B];
@@ -456,7 +479,7 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
 #pragma unroll
     for (int a = 0; a < R; ++a) gcol[a] = 0.0;
     if (own && gidx != nullptr) {
-      const int slot = gidx[p.j];
+      const int slot = PRE_M ? pre_slot : gidx[p.j];
       if (slot >= 0) {
 #pragma unroll
         for (int a = 0; a < R; ++a) gcol[a] = gblk[static_cast<long>(slot) * (R * B) + p.k * R + a];
@@ -502,7 +525,8 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
           double mk[B];  // column k of Minv (row-major b x b)
 #pragma unroll
           for (int u = 0; u < B; ++u)
-            mk[u] = p.ok ? args.Minv[p.j * diag_width(B - 1) + minv_index<B>(u, p.k < B ? p.k : 0)] : 0.0;
+            mk[u] = PRE_M ? pre_m[u]
+                          : (p.ok ? args.Minv[p.j * diag_width(B - 1) + minv_index<B>(u, p.k < B ? p.k : 0)] : 0.0);
           double zq[R];
 #pragma unroll
           for (int a = 0; a < R; ++a) {
@@ -543,7 +567,8 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
 #pragma unroll
     for (int u = 0; u < D; ++u)
 #pragma unroll
-      for (int v = 0; v < D; ++v) S[u][v] = p.ok ? S_in[p.j * s_width(D) + sym_index<D>(u, v)] : 0.0;
+      for (int v = 0; v < D; ++v)
+        S[u][v] = PRE_S ? pre_s[sym_index<D>(u, v)] : (p.ok ? S_in[p.j * s_width(D) + sym_index<D>(u, v)] : 0.0);
     double Vf[R][D], hc[R];
     quad_gather_y<R, D>(vcol, Vf);
     sub_y_times_col<R, D>(Vf, S, p.k, qc, hc);
@@ -558,7 +583,8 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
 #pragma unroll
     for (int u = 0; u < D; ++u)
 #pragma unroll
-      for (int v = 0; v < D; ++v) S[u][v] = p.ok ? S_in[p.j * s_width(D) + sym_index<D>(u, v)] : 0.0;
+      for (int v = 0; v < D; ++v)
+        S[u][v] = PRE_S ? pre_s[sym_index<D>(u, v)] : (p.ok ? S_in[p.j * s_width(D) + sym_index<D>(u, v)] : 0.0);
     double Vf[R][D], w[R], hc[R];
     quad_gather_y<R, D>(vcol, Vf);
     constexpr double kq = FMT == QFMT_EDGES ? 2.0 : 1.0;
@@ -574,12 +600,18 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     double vcol[R], xcol[R];
 #pragma unroll
     for (int a = 0; a < R; ++a) vcol[a] = xin[a];
-    load_col<R, B>(X, p.j, p.k, p.ok, xcol);
+    if constexpr (PRE_X) {
+#pragma unroll
+      for (int a = 0; a < R; ++a) xcol[a] = pre_x[a];
+    } else {
+      load_col<R, B>(X, p.j, p.k, p.ok, xcol);
+    }
     double S[D][D];
 #pragma unroll
     for (int u = 0; u < D; ++u)
 #pragma unroll
-      for (int v = 0; v < D; ++v) S[u][v] = p.ok ? S_in[p.j * s_width(D) + sym_index<D>(u, v)] : 0.0;
+      for (int v = 0; v < D; ++v)
+        S[u][v] = PRE_S ? pre_s[sym_index<D>(u, v)] : (p.ok ? S_in[p.j * s_width(D) + sym_index<D>(u, v)] : 0.0);
     double Vf[R][D], Xf[R][D];
     quad_gather_y<R, D>(vcol, Vf);
     quad_gather_y<R, D>(xcol, Xf);
@@ -1945,7 +1977,7 @@ __global__ __launch_bounds__(kThreads) void k_assemble_G(GEdges e, int nslots, c
     default: return hipErrorInvalidValue;                  \
   }
 
-int g_tuning[TUNE_COUNT] = {0, -1, 0, 0};
+int g_tuning[TUNE_COUNT] = {0, -1, 1, 0};
 
 bool supported_rb(int r, int b) {
   if (b == 3) return r >= 2 && r <= 8;
@@ -1977,6 +2009,12 @@ hipError_t spmm_variant54(int var, dim3 grid, const LaunchCtx& c, const QView& q
 template <int MODE>
 hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const SpmmArgs& a) {
   if (q.fmt == QFMT_EDGES) {
+    constexpr bool kPreMode = MODE == MODE_HESS || MODE == MODE_QF || MODE == MODE_EVAL_TCG;
+    if (kPreMode && r == 5 && b == 4 && g_tuning[TUNE_EPI_PREFETCH] > 0 && g_tuning[TUNE_EDGE_VARIANT] < 0)
+    {
+      k_spmm<5, 4, MODE, kEdgeDefaultVariant | 8, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+      return hipSuccess;
+    }
     const int var = g_tuning[TUNE_EDGE_VARIANT] < 0 ? kEdgeDefaultVariant : g_tuning[TUNE_EDGE_VARIANT];
     if (MODE == MODE_XQ && r == 5 && b == 4 && var != kEdgeDefaultVariant)
       return spmm_variant54<QFMT_EDGES>(var, grid, c, q, a);

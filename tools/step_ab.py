@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""A/B timing of a tuning key over the bench workload in the CG regime (1M-pose grid, 64 agents,
+distributed init + burn-in): alternating rounds of `--steps` RBCD steps per value, plus the standalone
+Riemannian HVP over colour 0.  Prints one JSON line per round and a summary (median ms/step per value).
+
+  python tools/step_ab.py --key 2 --values 0 1 [--rounds 3 --steps 20 --burnin 300]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--key", type=int, required=True)
+    ap.add_argument("--values", type=int, nargs="+", required=True)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--burnin", type=int, default=300)
+    ap.add_argument("--k", type=int, default=100)
+    a = ap.parse_args()
+    import torch
+    from dpgo_amd import hip as H
+    dev = torch.device("cuda", 0)
+    g = H.Graph.grid3d(a.k, seed=0)
+    aop = g.grid_partition(4)
+    eng = H.Rbcd(g, aop, np.zeros(64, np.int32), 0, 1, H.rbcd_params(r=5, acceleration=1))
+    s = torch.cuda.Stream(dev)
+    eng.set_stream(s.cuda_stream)
+    X0, _, _ = g.distributed_init(aop, 5, H.lifting_matrix(3, 5), gpu=True, rtol=1e-12, max_iters=50000,
+                                  dev_layout=True)
+    eng.set_X(X0)
+
+    def step():
+        for c in range(eng.num_colors):
+            eng.pre_exchange(c)
+            eng.update(c, None)
+
+    with torch.cuda.stream(s):
+        for _ in range(a.burnin):
+            step()
+        Xb = np.zeros(X0.size)
+        eng.get_X_into(Xb)
+        res = {v: [] for v in a.values}
+        hvp = {v: [] for v in a.values}
+        fin = {}
+        for rnd in range(a.rounds):
+            for v in a.values:
+                H.set_tuning(a.key, v)
+                eng.set_X(Xb)
+                step()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(a.steps):
+                    step()
+                torch.cuda.synchronize()
+                ms = 1e3 * (time.perf_counter() - t0) / a.steps
+                f, _ = eng.central_eval()
+                hv = eng.bench_hvp(0, 20)
+                res[v].append(ms)
+                hvp[v].append(hv)
+                fin.setdefault(v, f)
+                print(json.dumps({"round": rnd, "value": v, "ms_per_step": ms, "hvp_ms": hv, "f": f}), flush=True)
+    print(json.dumps({"key": a.key, "median_ms_per_step": {v: float(np.median(res[v])) for v in a.values},
+                      "median_hvp_ms": {v: float(np.median(hvp[v])) for v in a.values},
+                      "f_after": fin}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
