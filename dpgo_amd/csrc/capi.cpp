@@ -1226,6 +1226,9 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
       DPGO_TRY(finalize(h, dpgo::OP_TCG_INIT, h->pa.p, 2, nullptr, 0, &o));
     }
     std::vector<int> tags, step_tags;
+    // Consumer-side finalize (TUNE_FUSE_TCG): the step test's scalar logic runs in the update kernel's
+    // prologue and the stopping test's in the direction update's, three launches per tCG iteration.
+    const bool fuse_tcg = dpgo::g_tuning[dpgo::TUNE_FUSE_TCG] > 0 && !exact;
     // iteration j's step test: Hdelta = Hess[delta] and d_Hd = <delta, Hdelta>, or (qf) d_Hd alone
     auto launch_step = [&](bool qf) -> int {
       auto ch = make_ctx(h, dpgo::FLAG_TCG, h->pa.p);
@@ -1235,21 +1238,29 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
       step_tags.push_back(stag);
       const dpgo::SpmmArgs sa{h->delta.p, nullptr, nullptr, x1, h->S.p, qf ? nullptr : h->Hdelta.p, nullptr,
                               nullptr, nullptr, dpgo::PRECON_NONE};
+      if (fuse_tcg && !qf) return dpgo::spmm_launch(h, dpgo::MODE_HESS, ch, sa);  // decided by the update
       return spmm_then_finalize(h, qf ? dpgo::MODE_QF : dpgo::MODE_HESS, ch, sa,
                                 make_fin(h, dpgo::OP_TCG_STEP, h->pa.p, 1, nullptr, 0, &o, nullptr, 1, stag));
     };
-    auto launch_rest = [&](int j) -> int {
+    // the first step after a QF step test was decided by the QF pass's finalize
+    auto launch_rest = [&](int j, bool step_decided) -> int {
       auto cu = make_ctx(h, dpgo::FLAG_TCG_MODE, h->pb.p);
+      const bool fs = fuse_tcg && !step_decided;
+      const dpgo::FinalizeArgs fstep =
+          make_fin(h, dpgo::OP_TCG_STEP, h->pa.p, 1, nullptr, 0, &o, nullptr, 1, step_tags[j]);
       HIP_TRY(dpgo::launch_tcg_update(r, b, cu, x1, h->minv.p, pmode, h->delta.p, h->Hdelta.p, h->eta.p,
-                                      j == 0 ? h->g.p : h->rv.p, h->rv.p, h->z.p, j == 0 ? 1 : 0));
+                                      j == 0 ? h->g.p : h->rv.p, h->rv.p, h->z.p, j == 0 ? 1 : 0,
+                                      fs ? &fstep : nullptr, h->arrive.p));
       if (exact)  // z = Prec(r) with the factor; replaces the identity z and its partials
         DPGO_TRY(exact_precond(h, h->rv.p, h->z.p, nullptr, x1, h->rv.p, h->pb.p, dpgo::FLAG_TCG_MODE));
       const int tag = next_tag(h);
       tags.push_back(tag);
-      DPGO_TRY(finalize(h, dpgo::OP_TCG_CHECK, h->pb.p, 3, nullptr, 0, &o, nullptr, 1, tag));
-      if (j + 1 < P.tr_max_inner) {  // the last direction update is never used
+      const dpgo::FinalizeArgs fcheck = make_fin(h, dpgo::OP_TCG_CHECK, h->pb.p, 3, nullptr, 0, &o, nullptr, 1, tag);
+      const bool dir = j + 1 < P.tr_max_inner;  // the last direction update is never used
+      if (!(fuse_tcg && dir)) HIP_TRY(dpgo::launch_finalize(fcheck, h->K, h->stream));
+      if (dir) {
         auto cd = make_ctx(h, dpgo::FLAG_TCG, nullptr);
-        HIP_TRY(dpgo::launch_tcg_dir(r, b, cd, h->z.p, h->delta.p));
+        HIP_TRY(dpgo::launch_tcg_dir(r, b, cd, h->z.p, h->delta.p, fuse_tcg ? &fcheck : nullptr, h->arrive.p));
       }
       return DPGO_HIP_OK;
     };
@@ -1285,7 +1296,7 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
         rtag = launch_candidate(dpgo::FLAG_RUN_IMPL, 1);
         if (rtag < 0) return rtag;
       }
-      if (!qf0) DPGO_TRY(launch_rest(0));
+      if (!qf0) DPGO_TRY(launch_rest(0, false));
       launched = 1;
     }
     for (int j = 0; j < P.tr_max_inner; ++j) {
@@ -1303,11 +1314,11 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
         DPGO_TRY(dpgo::spmm_launch(h, dpgo::MODE_HESS, cg,
                                    dpgo::SpmmArgs{h->delta.p, nullptr, nullptr, x1, h->S.p, h->Hdelta.p, nullptr,
                                                   nullptr, nullptr, dpgo::PRECON_NONE}));
-        DPGO_TRY(launch_rest(0));
+        DPGO_TRY(launch_rest(0, true));
       }
       if (launched < P.tr_max_inner) {  // lookahead: iteration j+1 queued while j's update runs
         DPGO_TRY(launch_step(false));
-        DPGO_TRY(launch_rest(launched));
+        DPGO_TRY(launch_rest(launched, false));
         ++launched;
       }
       DPGO_TRY(wait_published(h, tags[j], &act));  // after the stopping test of iteration j

@@ -186,7 +186,7 @@ struct RobustParams {
 };
 
 // Runtime-selectable kernel variants (A/B tuning in one process; see tools/spmm_ab.py).
-enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH = 2, TUNE_COUNT = 4 };
+enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH = 2, TUNE_FUSE_TCG = 3, TUNE_COUNT = 4 };
 // variant of the edge-stream SpMM used unless TUNE_EDGE_VARIANT overrides it (bit 0: XCD-aware
 // tile remap; v >> 1: minimum waves per SIMD the register allocation must allow, none/4/5/6)
 constexpr int kEdgeDefaultVariant = 1;
@@ -207,8 +207,12 @@ hipError_t launch_tcg_init(int r, int b, const LaunchCtx& c, const double* X, co
                            const double* g, double* delta);
 hipError_t launch_tcg_update(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
                              const double* delta, const double* Hdelta, double* eta,
-                             const double* r_in, double* rv, double* z, int first);
-hipError_t launch_tcg_dir(int r, int b, const LaunchCtx& c, const double* z, double* delta);
+                             const double* r_in, double* rv, double* z, int first,
+                             const FinalizeArgs* fin = nullptr, int* arrive = nullptr);
+// fin / arrive: the consumer-side finalize (OP_TCG_STEP in the update, OP_TCG_CHECK in the direction
+// update) instead of a separate k_finalize launch; null = read the decision from the state.
+hipError_t launch_tcg_dir(int r, int b, const LaunchCtx& c, const double* z, double* delta,
+                          const FinalizeArgs* fin = nullptr, int* arrive = nullptr);
 hipError_t launch_retract(int r, int b, const LaunchCtx& c, const double* X, const double* V, double scale,
                           double* out, const double* g, const double* HV, const double* delta_impl = nullptr);
 hipError_t launch_tangent(int r, int b, const LaunchCtx& c, const double* X, const double* V, double* out);

@@ -337,6 +337,9 @@ constexpr bool evar_pre(int v) { return (v & 8) != 0; }
 
 
 __device__ void finalize_agent(const FinalizeArgs& f, int agent);
+template <int NQ>
+__device__ void prologue_finalize(const FinalizeArgs& f, int agent, int* arrive, AgentState& sh);
+__device__ void finalize_arrive(const FinalizeArgs& f, int agent, int* arrive, const AgentState& sh);
 
 // Fused finalize (SpmmArgs::fin_arrive): every block of the launch arrives once per agent tile, after
 // its partial is written (release: fence, then the count); the block that completes its agent's
@@ -702,33 +705,58 @@ __global__ __launch_bounds__(kThreads) void k_tcg_init(LaunchCtx c, const double
 // lets OP_TCG_CHECK carry <eta, Heta> as a scalar, <eta + s delta, H(eta + s delta)> = <eta, Heta>
 // + s (2 <eta, Hdelta> + s <delta, Hdelta>) (H self-adjoint on the tangent space), which is all the rho
 // test reads of it (src/QuadraticOptimizer.cpp via ROPTLIB RTRNewton).
-template <int R, int B>
+template <int R, int B, bool FUSED>
 __global__ __launch_bounds__(kThreads) void k_tcg_update(LaunchCtx c, const double* __restrict__ X,
                                                          const double* __restrict__ Minv, int pmode,
                                                          const double* __restrict__ delta,
                                                          const double* __restrict__ Hdelta,
                                                          double* __restrict__ eta, const double* r_in, double* r,
-                                                         double* __restrict__ z, int first) {
+                                                         double* __restrict__ z, int first, FinalizeArgs fin,
+                                                         int* arrive) {
   const PoseLane p = pose_lane<B>(c);
-  if (tile_skipped(c, p.agent)) return;  // FLAG_TCG_MODE: skips mode 2
-  const AgentState& st = c.state[p.agent];
-  if (st.eta_implicit) return;  // first-step boundary exit: eta stays implicit (k_retract)
-  const int mode = st.tcg_mode;
-  const double step = st.step;
   const bool own = p.ok && p.k < B;
   const long off = p.j * (R * B) + p.k * R;
+  int mode;
+  double step;
   double dcol[R], hcol[R], ecol[R];
-  load_col<R, B>(delta, p.j, p.k, p.ok, dcol);
-  load_col<R, B>(Hdelta, p.j, p.k, p.ok, hcol);
-  double eh = 0.0;
-  if (first) {  // eta = 0 at the start of tCG
+  __shared__ AgentState sh;  // FUSED: this block's copy of the agent's state after the step test
+  if constexpr (FUSED) {
+    // The step test (OP_TCG_STEP on the HESS partials) runs here instead of a k_finalize launch.  Only
+    // an agent still in tCG can take a step: its operands are requested before the test so their
+    // latency overlaps it.
+    const bool pre = fin.state[p.agent].tcg_active != 0;
 #pragma unroll
-    for (int a = 0; a < R; ++a) ecol[a] = 0.0;
+    for (int a = 0; a < R; ++a) dcol[a] = hcol[a] = ecol[a] = 0.0;
+    if (pre) {
+      load_col<R, B>(delta, p.j, p.k, p.ok, dcol);
+      load_col<R, B>(Hdelta, p.j, p.k, p.ok, hcol);
+      if (!first) load_col<R, B>(eta, p.j, p.k, p.ok, ecol);
+    }
+    prologue_finalize<1>(fin, p.agent, arrive, sh);
+    if (sh.tcg_mode == 2 || sh.eta_implicit) {
+      finalize_arrive(fin, p.agent, arrive, sh);
+      return;
+    }
+    mode = sh.tcg_mode;
+    step = sh.step;
   } else {
-    load_col<R, B>(eta, p.j, p.k, p.ok, ecol);
+    if (tile_skipped(c, p.agent)) return;  // FLAG_TCG_MODE: skips mode 2
+    const AgentState& st = c.state[p.agent];
+    if (st.eta_implicit) return;  // first-step boundary exit: eta stays implicit (k_retract)
+    mode = st.tcg_mode;
+    step = st.step;
+    load_col<R, B>(delta, p.j, p.k, p.ok, dcol);
+    load_col<R, B>(Hdelta, p.j, p.k, p.ok, hcol);
+    if (first) {  // eta = 0 at the start of tCG
 #pragma unroll
-    for (int a = 0; a < R; ++a) eh = fma(ecol[a], hcol[a], eh);
+      for (int a = 0; a < R; ++a) ecol[a] = 0.0;
+    } else {
+      load_col<R, B>(eta, p.j, p.k, p.ok, ecol);
+    }
   }
+  double eh = 0.0;  // <eta_old, Hdelta> (eta_old = 0 on the first step)
+#pragma unroll
+  for (int a = 0; a < R; ++a) eh = fma(ecol[a], hcol[a], eh);
 #pragma unroll
   for (int a = 0; a < R; ++a) ecol[a] = fma(step, dcol[a], ecol[a]);
   store_vec<R>(eta, off, own, ecol);
@@ -755,20 +783,42 @@ __global__ __launch_bounds__(kThreads) void k_tcg_update(LaunchCtx c, const doub
   }
   double parts[3] = {own ? zr : 0.0, own ? rr : 0.0, own ? eh : 0.0};
   block_partials<3>(parts, c.partials, p.tile);
+  if constexpr (FUSED) finalize_arrive(fin, p.agent, arrive, sh);
 }
 
-// delta = -z + beta delta for agents whose tCG continues (A.4 step 5)
-template <int R, int B>
+// delta = -z + beta delta for agents whose tCG continues (A.4 step 5).  FUSED: the stopping test and
+// beta (OP_TCG_CHECK on the update's partials) run here instead of a k_finalize launch.
+template <int R, int B, bool FUSED>
 __global__ __launch_bounds__(kThreads) void k_tcg_dir(LaunchCtx c, const double* __restrict__ z,
-                                                      double* __restrict__ delta) {
+                                                      double* __restrict__ delta, FinalizeArgs fin, int* arrive) {
   const PoseLane p = pose_lane<B>(c);
-  if (tile_skipped(c, p.agent)) return;  // FLAG_TCG
-  const double beta = c.state[p.agent].beta;
   const bool own = p.ok && p.k < B;
-  if (!own) return;
   const long off = p.j * (R * B) + p.k * R;
+  if constexpr (FUSED) {
+    __shared__ AgentState sh;
+    const bool pre = own && fin.state[p.agent].tcg_active != 0;  // only a CG step can continue
+    double zc[R], dc[R];
+    if (pre) {
 #pragma unroll
-  for (int a = 0; a < R; ++a) delta[off + a] = fma(beta, delta[off + a], -z[off + a]);
+      for (int a = 0; a < R; ++a) {
+        zc[a] = z[off + a];
+        dc[a] = delta[off + a];
+      }
+    }
+    prologue_finalize<3>(fin, p.agent, arrive, sh);
+    if (pre && sh.tcg_active) {
+      const double beta = sh.beta;
+#pragma unroll
+      for (int a = 0; a < R; ++a) delta[off + a] = fma(beta, dc[a], -zc[a]);
+    }
+    finalize_arrive(fin, p.agent, arrive, sh);
+  } else {
+    if (tile_skipped(c, p.agent)) return;  // FLAG_TCG
+    const double beta = c.state[p.agent].beta;
+    if (!own) return;
+#pragma unroll
+    for (int a = 0; a < R; ++a) delta[off + a] = fma(beta, delta[off + a], -z[off + a]);
+  }
 }
 
 // x2 = R_x1(scale * eta) (QF retraction, A.2) with partials <g,eta> and, when HV is given, <eta,HV>
@@ -1384,7 +1434,9 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       }
       s.st_runs += 1;
       s.st_tcg_iters += s.tcg_iters;
-      if (s.tcg_status >= 0 && s.tcg_status < 5) s.st_status[s.tcg_status] += 1;
+#pragma unroll
+      for (int q = 0; q < 5; ++q)  // static indices: the state stays in registers
+        if (s.tcg_status == q) s.st_status[q] += 1;
       if (s.rho < 0.25) {
         s.Delta = 0.25 * s.Delta;
       } else if (s.rho > 0.75 && (s.tcg_status == TCG_EXCREGION || s.tcg_status == TCG_NEGCURVTURE)) {
@@ -1519,13 +1571,91 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
     tot[q] = v;
   }
   if (l != 0) return;
-  finalize_scalar(f, agent, tot, sh_state);
+  // the scalar logic runs on a register copy: a chain of dependent LDS accesses costs microseconds
+  AgentState st = sh_state;
+  finalize_scalar(f, agent, tot, st);
   double* dst = reinterpret_cast<double*>(&f.state[agent]);
-  const double* srcw = reinterpret_cast<const double*>(&sh_state);
+  const double* srcw = reinterpret_cast<const double*>(&st);
 #pragma unroll
   for (int w = 0; w < kStateWords; ++w) dst[w] = srcw[w];
 }
 
+
+// Consumer-side finalize: the scalar logic of a k_finalize launch run in the prologue of the kernel
+// that consumes its decision (k_tcg_update: OP_TCG_STEP, k_tcg_dir: OP_TCG_CHECK), so a tCG iteration
+// is three launches instead of five.  Every block of the agent restates k_finalize's reduction of the
+// agent's tile partials (same per-thread serial sums, same tree: bitwise the same totals) and its
+// scalar logic on a private LDS copy of the agent's state, so every block takes the same decision.
+// The block that arrives last on the agent's counter writes the copy back and publishes the status
+// word.  A block reads the global state and partials only before its first barrier (their values are
+// in LDS by then) and arrives after it, so the write-back races with no reader of this launch.
+template <int NQ>
+__device__ void prologue_finalize(const FinalizeArgs& f, int agent, int* arrive, AgentState& sh) {
+  (void)arrive;
+  constexpr int kStateWords = static_cast<int>(sizeof(AgentState) / sizeof(double));
+  __shared__ double red[NQ][kThreads];
+  const int t0 = f.agent_tile_off[agent], t1 = f.agent_tile_off[agent + 1];
+  if (threadIdx.x < kStateWords)
+    reinterpret_cast<double*>(&sh)[threadIdx.x] = reinterpret_cast<const double*>(&f.state[agent])[threadIdx.x];
+  double acc[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) acc[q] = 0.0;
+  for (int t = t0 + threadIdx.x; t < t1; t += kThreads) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const double* src = q < f.nq_a ? f.pa : f.pb;
+      const int qq = q < f.nq_a ? q : q - f.nq_a;
+      acc[q] += src[t * kPartialStride + qq];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) red[q][threadIdx.x] = acc[q];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int l = threadIdx.x;
+    double tot[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      double v = (red[q][l] + red[q][l + 128]) + (red[q][l + 64] + red[q][l + 192]);
+#pragma unroll
+      for (int w = 32; w > 0; w >>= 1) v += __shfl_down(v, w, 64);
+      tot[q] = v;
+    }
+    if (l == 0) {
+      FinalizeArgs g = f;
+      g.pub = nullptr;  // published once, by the last block (finalize_arrive)
+      AgentState st = sh;  // register copy (see k_finalize)
+      finalize_scalar(g, agent, tot, st);
+      sh = st;
+    }
+  }
+  __syncthreads();
+}
+
+// Second half of the consumer-side finalize, at the end of the block (every block of the agent calls
+// it exactly once, skipped or not): the last block to arrive writes the state copy back and
+// publishes.  Arriving last means every other block of the agent has finished, so all of this
+// launch's reads of the agent's global state are done.
+__device__ void finalize_arrive(const FinalizeArgs& f, int agent, int* arrive, const AgentState& sh) {
+  constexpr int kStateWords = static_cast<int>(sizeof(AgentState) / sizeof(double));
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int n = f.agent_tile_off[agent + 1] - f.agent_tile_off[agent];
+    const int old = atomicAdd(&arrive[agent], 1);
+    s_last = old == n - 1 ? 1 : 0;
+    if (s_last) atomicExch(&arrive[agent], 0);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x < kStateWords)
+    reinterpret_cast<double*>(&f.state[agent])[threadIdx.x] = reinterpret_cast<const double*>(&sh)[threadIdx.x];
+  if (threadIdx.x == 0 && f.pub != nullptr) {
+    const int flag = f.pub_kind == 1 ? sh.tcg_active : sh.run_active;
+    __hip_atomic_store(&f.pub[agent], (f.pub_tag << 1) | (flag ? 1 : 0), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
 
 // --- block-Jacobi inverse of (Q_jj + shift I), computed on device from Q's diagonal blocks ---
 // In place on A = [M | I] (B x 2B): Gauss-Jordan with partial pivoting (SPD, so pivoting is a
@@ -2055,15 +2185,25 @@ hipError_t launch_tcg_init(int r, int b, const LaunchCtx& c, const double* X, co
 
 hipError_t launch_tcg_update(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
                              const double* delta, const double* Hdelta, double* eta,
-                             const double* r_in, double* rv, double* z, int first) {
+                             const double* r_in, double* rv, double* z, int first, const FinalizeArgs* fin,
+                             int* arrive) {
   if (c.num_tiles == 0) return hipSuccess;
-  DPGO_DISPATCH(r, b, (k_tcg_update<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, Minv, pmode, delta, Hdelta, eta, r_in, rv, z, first)));
+  if (fin != nullptr) {
+    DPGO_DISPATCH(r, b, (k_tcg_update<R, B, true><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, Minv, pmode, delta, Hdelta, eta, r_in, rv, z, first, *fin, arrive)));
+  } else {
+    DPGO_DISPATCH(r, b, (k_tcg_update<R, B, false><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, Minv, pmode, delta, Hdelta, eta, r_in, rv, z, first, FinalizeArgs{}, nullptr)));
+  }
   return hipGetLastError();
 }
 
-hipError_t launch_tcg_dir(int r, int b, const LaunchCtx& c, const double* z, double* delta) {
+hipError_t launch_tcg_dir(int r, int b, const LaunchCtx& c, const double* z, double* delta, const FinalizeArgs* fin,
+                          int* arrive) {
   if (c.num_tiles == 0) return hipSuccess;
-  DPGO_DISPATCH(r, b, (k_tcg_dir<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, z, delta)));
+  if (fin != nullptr) {
+    DPGO_DISPATCH(r, b, (k_tcg_dir<R, B, true><<<c.num_tiles, kThreads, 0, c.stream>>>(c, z, delta, *fin, arrive)));
+  } else {
+    DPGO_DISPATCH(r, b, (k_tcg_dir<R, B, false><<<c.num_tiles, kThreads, 0, c.stream>>>(c, z, delta, FinalizeArgs{}, nullptr)));
+  }
   return hipGetLastError();
 }
 

@@ -268,3 +268,28 @@ def test_central_eval_matches_oracle(hip):
     e.get_X_into(out)
     Xo, _ = O.colour_rbcd(meas, aop, A ** 3, X0, 6, r, acceleration=True)
     assert rel(hip.from_dev_layout(out, r), Xo) <= 1e-9
+
+
+def test_consumer_side_finalize_bitwise(hip):
+    """The tCG loop with the step / stopping tests run in the consuming kernels' prologues (tuning key
+    TUNE_FUSE_TCG, measured slower and off by default) gives bitwise the engine's default result."""
+    g = hip.Graph.grid3d(12, seed=5)
+    aop = g.grid_partition(2)
+    X0, _, _ = g.distributed_init(aop, 5, hip.lifting_matrix(3, 5), gpu=True, rtol=1e-12, dev_layout=True)
+    out = []
+    for fuse in (0, 1):
+        hip.set_tuning(3, fuse)
+        try:
+            e = hip.Rbcd(g, aop, np.zeros(8, np.int32), 0, 1, hip.rbcd_params(r=5, acceleration=1))
+            e.set_X(X0)
+            for it in range(40):
+                e.pre_exchange(it % e.num_colors)
+                e.update(it % e.num_colors, None)
+            X = np.zeros(X0.size)
+            e.get_X_into(X)
+            out.append((X, e.stats().copy()))
+        finally:
+            hip.set_tuning(3, 0)
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1])
+    assert out[0][1][:, 10].sum() > 0  # CG steps were taken
