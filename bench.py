@@ -84,6 +84,9 @@ def main():
     ap.add_argument("--spmm-reps", type=int, default=20)
     ap.add_argument("--kernel-timing", type=int, default=1, help="HIP events around in-step X.Q launches")
     ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--certify-iters", type=int, default=0,
+                    help="> 0: certified gap of the final iterate over the whole graph (dpgo_graph_certify: Lanczos "
+                         "steps on lambda_min of the central certificate matrix, SE(d) rounding, both costs)")
     ap.add_argument("--pmc-calib-mb", type=int, default=0,
                     help="tools/pmc_step.py: one device copy of this many MiB before the timed region (a launch of "
                          "known read/write bytes for the FETCH_SIZE calibration)")
@@ -355,6 +358,20 @@ def main():
             out["speedup_vs_cpu_all_cores"] = value / cb["value"]
         except Exception as exc:  # reported, never silently replaced
             out["cpu_baseline"] = {"error": repr(exc)}
+    if args.certify_iters > 0:
+        with torch.cuda.stream(stream):
+            Xc = np.zeros(X0.size)
+            eng.get_X_into(Xc)
+        if world > 1:
+            tx = torch.from_numpy(Xc) if one_device else torch.from_numpy(Xc).to(dev)
+            dist.all_reduce(tx)
+            Xc = tx.cpu().numpy()
+        if rank == 0:
+            t_c = time.time()
+            c = g.certify(Xc, args.r, max_iters=args.certify_iters, tol=1e-10)
+            c["seconds"] = time.time() - t_c
+            c["certified"] = bool(c["lambda_min"] >= -1e-6 * abs(c["f_relax"]) / max(g.n, 1))
+            out["certificate"] = c
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -564,3 +564,65 @@ int dpgo_graph_grid_partition(dpgo_graph g, int A, int* agent_of_pose) {
 }
 
 }  // extern "C"
+
+// Certified optimality gap of an iterate of the whole graph (the reference has no
+// certification, so it is pinned against the oracle's explicit matrices).  X: r x (d+1) n,
+// column-major (the reference layout; dpgo_rbcd_get_X's layout).  One single-agent edge-stream handle
+// holds the central Q (unit weights); lambda_min(S(X)) by dpgo_hip_certify; f_relax = f(X); the
+// rounding follows PGOAgent::getTrajectoryInLocalFrame (src/PGOAgent.cpp:481-498): T = Y_0^T X,
+// every rotation block projected to SO(d), translations relative to pose 0; f_rounded = f(T) (T
+// lifted by zero rows, which leaves the quadratic form unchanged).  When lambda_min >= -eps the
+// relaxation is solved globally and f_relax <= f* <= f_rounded: f_rounded - f_relax bounds the
+// rounded trajectory's suboptimality.
+int dpgo_graph_certify(dpgo_graph g, int r, const double* X, int max_iters, double tol, double* lambda_min,
+                       double* residual, int* iters, double* f_relax, double* f_rounded, double* T_rounded,
+                       double* eigvec) {
+  if (!g || !X || !lambda_min || r < g->d) return fail(DPGO_HIP_EINVAL, "bad certification arguments");
+  const int d = g->d, b = d + 1, n = g->n, m = static_cast<int>(g->p1.size());
+  dpgo_hip_problem h = nullptr;
+  DPGO_TRY(dpgo_hip_problem_create(n, d, r, &h));
+  struct Guard {
+    dpgo_hip_problem h;
+    ~Guard() { dpgo_hip_problem_destroy(h); }
+  } guard{h};
+  const std::vector<double> w(static_cast<size_t>(m), 1.0);
+  DPGO_TRY(dpgo_hip_set_Q_edges(h, 0, m, g->p1.data(), g->p2.data(), g->R.data(), g->t.data(), g->kappa.data(),
+                                g->tau.data(), w.data()));
+  double res = 0.0;
+  int it = 0;
+  DPGO_TRY(dpgo_hip_certify(h, X, max_iters, tol, lambda_min, &res, &it, eigvec));
+  if (residual) *residual = res;
+  if (iters) *iters = it;
+  double fx = 0.0;
+  DPGO_TRY(dpgo_hip_f(h, X, &fx));
+  if (f_relax) *f_relax = fx;
+  // rounding: T = Y_0^T X (Y_0 = rows 0..r-1, columns 0..d-1 of X)
+  std::vector<double> T(static_cast<size_t>(n) * b * d);
+  for (int p = 0; p < n; ++p)
+    for (int c = 0; c < b; ++c)
+      for (int u = 0; u < d; ++u) {
+        double acc = 0.0;
+        for (int a = 0; a < r; ++a) acc += X[static_cast<size_t>(u) * r + a] * X[(static_cast<size_t>(p) * b + c) * r + a];
+        T[(static_cast<size_t>(p) * b + c) * d + u] = acc;
+      }
+  double t0[3] = {0.0, 0.0, 0.0};
+  for (int u = 0; u < d; ++u) t0[u] = T[static_cast<size_t>(d) * d + u];
+  std::vector<double> XT(static_cast<size_t>(n) * b * r, 0.0);
+  for (int p = 0; p < n; ++p) {
+    double M[9], Rp[9];
+    for (int u = 0; u < d; ++u)
+      for (int c = 0; c < d; ++c) M[u * d + c] = T[(static_cast<size_t>(p) * b + c) * d + u];
+    dpgo::project_to_rotation(d, M, Rp);
+    for (int u = 0; u < d; ++u) {
+      for (int c = 0; c < d; ++c) T[(static_cast<size_t>(p) * b + c) * d + u] = Rp[u * d + c];
+      T[(static_cast<size_t>(p) * b + d) * d + u] -= t0[u];
+    }
+    for (int c = 0; c < b; ++c)
+      for (int u = 0; u < d; ++u) XT[(static_cast<size_t>(p) * b + c) * r + u] = T[(static_cast<size_t>(p) * b + c) * d + u];
+  }
+  double fr = 0.0;
+  DPGO_TRY(dpgo_hip_f(h, XT.data(), &fr));
+  if (f_rounded) *f_rounded = fr;
+  if (T_rounded) std::memcpy(T_rounded, T.data(), sizeof(double) * T.size());
+  return DPGO_HIP_OK;
+}

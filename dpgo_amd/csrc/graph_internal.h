@@ -43,6 +43,9 @@ int chordal_initialization_gpu(int d, int n, int m, const int* p1, const int* p2
                                int* iters, double* relres, std::string& err);
 // PGOAgent::localInitialization (chordal per agent on its private graph, anchored at the agent's BFS
 // centre) + initializeInGlobalFrame (breadth-first L2 alignment over shared loop closures)
+// projectToRotationGroup of a d x d row-major matrix (init.cpp)
+void project_to_rotation(int d, const double* M, double* out);
+
 int distributed_initialization(int d, int n, int m, const int* p1, const int* p2, const double* R, const double* t,
                                const double* kappa, const double* tau, const int* agent_of, int num_agents, bool gpu,
                                double rtol, int max_iters, double* T_out, int* iters, double* relres,

@@ -693,4 +693,6 @@ int distributed_initialization(int d, int n, int m, const int* p1, const int* p2
   return 0;
 }
 
+void project_to_rotation(int d, const double* M, double* out) { project_rotation(d, M, out); }
+
 }  // namespace dpgo

@@ -441,6 +441,8 @@ _SIGS2 = [
     ("dpgo_graph_chordal_init", [C.c_void_p, C.c_int, _dp, _dp], C.c_int),
     ("dpgo_chordal_initialization", [C.c_int, C.c_int, C.c_int, _ip, _ip, _dp, _dp, _dp, _dp, _dp], C.c_int),
     ("dpgo_graph_grid_partition", [C.c_void_p, C.c_int, _ip], C.c_int),
+    ("dpgo_graph_certify", [C.c_void_p, C.c_int, _dp, C.c_int, C.c_double, _dp, _dp, _ip, _dp, _dp, _dp, _dp],
+     C.c_int),
     ("dpgo_chordal_initialization_gpu", [C.c_int, C.c_int, C.c_int, _ip, _ip, _dp, _dp, _dp, _dp, C.c_double,
                                          C.c_int, _dp, _ip, _dp], C.c_int),
     ("dpgo_graph_chordal_init_gpu", [C.c_void_p, C.c_int, _dp, C.c_double, C.c_int, _dp, _ip, _dp], C.c_int),
@@ -581,6 +583,30 @@ class Graph:
         Y, Yp = _f64(np.asarray(YLift, dtype=np.float64).T.ravel())
         out = np.empty(self.n * (self.d + 1) * r)
         _check(lib().dpgo_graph_chain_init(self.h, r, Yp, out.ctypes.data_as(_dp)))
+        return out
+
+    def certify(self, X, r, max_iters=300, tol=1e-8, want_rounded=False, want_vector=False):
+        """Certified optimality gap of X (flat r x (d+1) n column-major buffer, or the r x (d+1) n
+        matrix) for the whole graph: dict(lambda_min, residual, iters, f_relax, f_rounded, gap, rel_gap
+        [, T_rounded d x (d+1) n])."""
+        X = np.asarray(X, dtype=np.float64)
+        flat = np.ascontiguousarray(X.T).ravel() if X.ndim == 2 else np.ascontiguousarray(X).ravel()
+        if flat.size != r * (self.d + 1) * self.n:
+            raise DPGOHipError("X has the wrong size")
+        lam, res, fx, fr = C.c_double(), C.c_double(), C.c_double(), C.c_double()
+        it = C.c_int()
+        T = np.empty(self.d * (self.d + 1) * self.n) if want_rounded else None
+        V = np.empty(flat.size) if want_vector else None
+        _check(lib().dpgo_graph_certify(self.h, int(r), flat.ctypes.data_as(_dp), int(max_iters), float(tol),
+                                        C.byref(lam), C.byref(res), C.byref(it), C.byref(fx), C.byref(fr),
+                                        T.ctypes.data_as(_dp) if T is not None else None,
+                                        V.ctypes.data_as(_dp) if V is not None else None))
+        out = dict(lambda_min=lam.value, residual=res.value, iters=it.value, f_relax=fx.value, f_rounded=fr.value,
+                   gap=fr.value - fx.value, rel_gap=(fr.value - fx.value) / fx.value if fx.value else float("nan"))
+        if T is not None:
+            out["T_rounded"] = from_dev_layout(T, self.d)
+        if V is not None:
+            out["eigvec"] = V.reshape(-1, r).T if V.ndim == 1 else V  # r x (d+1) n
         return out
 
     def grid_partition(self, agents_per_axis):

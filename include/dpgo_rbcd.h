@@ -74,6 +74,16 @@ int dpgo_graph_distributed_init(dpgo_graph g, int num_agents, const int* agent_o
                                 const double* YLift_colmajor, int use_gpu, double rtol, int max_iters, double* X_out,
                                 int* iters, double* relres);
 /* Grid graphs: agent = sub-cube (x/s, y/s, z/s), s = k / A; id = ax + A (ay + A az). */
+/* Certified optimality gap of an iterate X (r x (d+1) n, column-major, e.g. the engine's
+ * dpgo_rbcd_get_X gathered over ranks) for the whole graph's central Q (unit weights): lambda_min of
+ * the certificate matrix S(X) = Q - Lambda(X) (dpgo_hip_certify), f_relax = f(X), and f_rounded =
+ * f of X rounded to SE(d) as PGOAgent::getTrajectoryInLocalFrame does (src/PGOAgent.cpp:481-498;
+ * T_rounded: d x (d+1) n, optional; eigvec: the Ritz vector of lambda_min, r x (d+1) n, optional).
+ * lambda_min >= -eps certifies f_relax <= f* <= f_rounded.
+ * Not in the reference (parity-unpinned against it; pinned against the oracle's explicit S). */
+int dpgo_graph_certify(dpgo_graph g, int r, const double* X, int max_iters, double tol, double* lambda_min,
+                       double* residual, int* iters, double* f_relax, double* f_rounded, double* T_rounded,
+                       double* eigvec);
 int dpgo_graph_grid_partition(dpgo_graph g, int agents_per_axis, int* agent_of_pose);
 
 /* ---- RBCD engine ----------------------------------------------------------------------------*/

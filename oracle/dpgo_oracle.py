@@ -539,6 +539,18 @@ def certificate_matrix(Q, X, d):
     return (Q - sp.block_diag(list(L), format="csr")).tocsr()
 
 
+def round_to_se(X, d):
+    """PGOAgent::getTrajectoryInLocalFrame (src/PGOAgent.cpp:481-498): T = Y_0^T X, every rotation
+    block projected to SO(d), translations relative to pose 0 (d x (d+1) n)."""
+    b = d + 1
+    T = X[:, :d].T @ X
+    t0 = T[:, d].copy()
+    for i in range(X.shape[1] // b):
+        T[:, i * b:i * b + d] = project_to_rotation(T[:, i * b:i * b + d])
+        T[:, i * b + d] -= t0
+    return T
+
+
 def certificate_min_eig(S):
     """lambda_min of the certificate matrix (dense below 3000 rows, else ARPACK 'SA')."""
     if S.shape[0] <= 3000:

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from oracle import dpgo_oracle as O
-from tests._common import load_meas, random_point
+from tests._common import load_meas, random_point, rel
 
 pytestmark = pytest.mark.gpu
 
@@ -77,3 +77,69 @@ def test_certificate_rejects_batched(hip):
     H = hip.Problem(None, 3, 3, poses_per_agent=[4, 4])
     with pytest.raises(Exception):
         H.certify(np.zeros((3, 32)))
+
+
+@pytest.mark.parametrize("name,agents,iters", [("smallGrid3D", 5, 400), ("city10000", 8, 300)])
+def test_graph_certify_engine_iterate(hip, name, agents, iters):
+    """Certified gap of the multi-agent engine's iterate over the whole graph (dpgo_graph_certify):
+    f(X), the SE(d) rounding (PGOAgent::getTrajectoryInLocalFrame) and its cost against the oracle;
+    lambda_min as an eigenvalue of the oracle's explicit S (Ritz residual; exact value below 3000
+    rows)."""
+    meas = load_meas(name)
+    d, n, r = meas.d, meas.num_poses, 5
+    aop = np.minimum(np.arange(n) // (n // agents), agents - 1).astype(np.int32)
+    g = hip.Graph.from_arrays(d, n, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau)
+    X0, _, _ = g.distributed_init(aop, r, O.lifting_matrix(d, r), gpu=True, rtol=1e-12, dev_layout=True)
+    e = hip.Rbcd(g, aop, np.zeros(agents, np.int32), 0, 1, hip.rbcd_params(r=r, acceleration=1))
+    e.set_X(X0)
+    gn = None
+    for it in range(iters):
+        e.pre_exchange(it % e.num_colors)
+        e.update(it % e.num_colors, None)
+        if it % 100 == 99:
+            _, gsq = e.central_eval()
+            gn = float(np.sqrt(np.sum(gsq)))
+            if gn < 1e-7:
+                break
+    Xd = np.zeros(X0.size)
+    e.get_X_into(Xd)
+    c = g.certify(Xd, r, max_iters=1500 if n < 1000 else 400, tol=1e-10, want_rounded=True, want_vector=True)
+    X = hip.from_dev_layout(Xd, r)
+    Q = O.connection_laplacian(meas, n)
+    assert abs(c["f_relax"] - O.central_cost(meas, X)) <= 1e-12 * abs(c["f_relax"])
+    T = O.round_to_se(X, d)
+    assert rel(c["T_rounded"], T) <= 1e-10
+    assert abs(c["f_rounded"] - O.central_cost(meas, T)) <= 1e-10 * abs(c["f_rounded"])
+    S = O.certificate_matrix(Q, X, d)
+    lam_bound = float(abs(S).sum(axis=1).max())  # >= |lambda|max (Gershgorin)
+    v = c["eigvec"]
+    assert abs(np.linalg.norm(v) - 1.0) <= 1e-8
+    # lambda_min lies within the Ritz residual of an eigenvalue of S; the reported residual is the true one
+    res = np.linalg.norm(np.asarray((S @ v.T).T) - c["lambda_min"] * v)
+    assert abs(res - c["residual"]) <= 1e-3 * res + 1e-9 * lam_bound, (res, c["residual"])
+    assert res <= 1e-3 * lam_bound
+    if S.shape[0] <= 3000:
+        lam_o = float(np.linalg.eigvalsh(S.toarray())[0])
+        assert abs(c["lambda_min"] - lam_o) <= 1e-6 * lam_bound
+
+
+@pytest.mark.parametrize("name", ["smallGrid3D", "tinyGrid3D"])
+def test_graph_certify_certified_gap(hip, name):
+    """At the relaxation's global optimum (RTR from chordal initialisation) the central certificate
+    holds and f_rounded - f(X) >= 0 is a certified suboptimality bound of the SE(d) rounding."""
+    meas = load_meas(name)
+    d, n, r = meas.d, meas.num_poses, 5
+    Q = O.connection_laplacian(meas, n)
+    X0 = O.lifting_matrix(d, r) @ O.chordal_initialization(d, n, meas)
+    H = hip.Problem(n, d, r)
+    H.set_Q_scipy(0, Q)
+    Xo, _ = H.optimize(X0, hip.default_params(tr_iterations=100, tr_tolerance=1e-10, tr_max_inner=200,
+                                              precon=hip.PRECON_EXACT))
+    g = hip.Graph.from_arrays(d, n, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau)
+    c = g.certify(Xo, r, max_iters=1500, tol=1e-10)
+    S = O.certificate_matrix(Q, Xo, d)
+    lam_bound = float(abs(S).sum(axis=1).max())
+    assert abs(c["lambda_min"] - float(np.linalg.eigvalsh(S.toarray())[0])) <= 1e-6 * lam_bound
+    assert c["lambda_min"] >= -1e-6 * lam_bound
+    assert c["gap"] >= -1e-9 * abs(c["f_relax"])
+    assert abs(c["f_rounded"] - O.central_cost(meas, O.round_to_se(Xo, d))) <= 1e-10 * abs(c["f_rounded"])
