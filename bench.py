@@ -83,6 +83,9 @@ def main():
     ap.add_argument("--accel", type=int, default=1)
     ap.add_argument("--spmm-reps", type=int, default=20)
     ap.add_argument("--kernel-timing", type=int, default=1, help="HIP events around in-step X.Q launches")
+    ap.add_argument("--exchange", default="torch", choices=["torch", "native"],
+                    help="N > 1 halo exchange: torch.distributed all_to_all_single (RCCL), or the library's own "
+                         "RCCL group send/recv (dpgo_rbcd_comm_init / dpgo_rbcd_exchange)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--certify-iters", type=int, default=0,
                     help="> 0: certified gap of the final iterate over the whole graph (dpgo_graph_certify: Lanczos "
@@ -146,9 +149,17 @@ def main():
     out_splits = [int(x) for x in eng.recv_counts]
     setup_s = time.time() - t_setup
 
+    native = args.exchange == "native" and world > 1
+    if native:
+        uid = [H.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(uid[0])
+
     def exchange():
         if world == 1:
             return None
+        if native:
+            return eng.exchange()
         eng.pack(send.data_ptr())
         if one_device:
             recv_h = torch.empty(recv.shape, dtype=recv.dtype)
@@ -272,6 +283,8 @@ def main():
         par = "1 GPU, all 64 agents on it (no exchange)"
     elif one_device:
         par = f"{world} ranks on ONE device (rehearsal), halo all_to_all over gloo through host copies"
+    elif native:
+        par = f"agents over {world} GPUs (2x2x2 super-cubes), halo by the library's RCCL group send/recv over xGMI"
     else:
         par = f"agents over {world} GPUs (2x2x2 super-cubes), halo all_to_all_single over RCCL/xGMI"
     out = {

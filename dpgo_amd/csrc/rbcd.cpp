@@ -13,6 +13,12 @@
 #include <set>
 #include <vector>
 
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <mutex>
+#include <string>
+
 #include "graph_internal.h"
 
 using namespace dpgo;
@@ -81,8 +87,14 @@ struct dpgo_rbcd_s {
   std::vector<double> v_gamma;
   long iteration = 0;
   long long agent_updates = 0;
+  // native exchange (dpgo_rbcd_comm_init / dpgo_rbcd_exchange): RCCL communicator over the ranks and
+  // engine-owned send / receive buffers in the all_to_all layout (peer-major, send_off / recv_off)
+  ncclComm_t comm = nullptr;
+  bool own_comm = false;
+  DevBuf<double> xsend, xrecv;
 
-  ~dpgo_rbcd_s() {
+  ~dpgo_rbcd_s();
+  void release() {
     for (auto* p : prob)
       if (p) dpgo_hip_problem_destroy(p);
     for (auto* g : gt) delete g;
@@ -992,3 +1004,134 @@ int dpgo_rbcd_counters(dpgo_rbcd e, long long* agent_updates, long long* iterati
 }
 
 }  // extern "C"
+
+// ---- native halo exchange over RCCL (examples/MultiRobotExample.cpp:188-213: every agent sends its
+// public poses to its neighbours before the selected agents update) ---------------------------------
+// RCCL is resolved at run time: the copy already in the process when there is one (the loader matches
+// its soname, so a caller that created the communicator and this library use the same instance),
+// otherwise the system librccl.  Nothing here links RCCL, so the library loads without it.
+namespace {
+struct RcclApi {
+  void* lib = nullptr;
+  std::string err;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommCount)(const ncclComm_t, int*) = nullptr;
+  ncclResult_t (*CommUserRank)(const ncclComm_t, int*) = nullptr;
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+RcclApi& rccl() {
+  static RcclApi api;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    api.lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL | RTLD_NOLOAD);
+    if (!api.lib) api.lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!api.lib) api.lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!api.lib) {
+      const char* e = dlerror();
+      api.err = e ? e : "librccl.so.1 not found";
+      return;
+    }
+#define DPGO_RCCL_SYM(f) api.f = reinterpret_cast<decltype(api.f)>(dlsym(api.lib, "nccl" #f))
+    DPGO_RCCL_SYM(GetUniqueId);
+    DPGO_RCCL_SYM(CommInitRank);
+    DPGO_RCCL_SYM(CommDestroy);
+    DPGO_RCCL_SYM(CommCount);
+    DPGO_RCCL_SYM(CommUserRank);
+    DPGO_RCCL_SYM(Send);
+    DPGO_RCCL_SYM(Recv);
+    DPGO_RCCL_SYM(GroupStart);
+    DPGO_RCCL_SYM(GroupEnd);
+    DPGO_RCCL_SYM(GetErrorString);
+#undef DPGO_RCCL_SYM
+    if (!api.GetUniqueId || !api.CommInitRank || !api.CommDestroy || !api.CommCount || !api.CommUserRank ||
+        !api.Send || !api.Recv || !api.GroupStart || !api.GroupEnd || !api.GetErrorString) {
+      api.err = "librccl.so.1 lacks a required entry point";
+      api.lib = nullptr;
+    }
+  });
+  return api;
+}
+
+int rccl_check(ncclResult_t r, const char* what) {
+  if (r == ncclSuccess) return DPGO_HIP_OK;
+  return fail(DPGO_HIP_EDEVICE, std::string(what) + ": " + rccl().GetErrorString(r));
+}
+
+int rccl_ready() {
+  if (!rccl().lib) return fail(DPGO_HIP_EDEVICE, "RCCL unavailable: " + rccl().err);
+  return DPGO_HIP_OK;
+}
+}  // namespace
+
+dpgo_rbcd_s::~dpgo_rbcd_s() {
+  if (comm && own_comm && rccl().lib) (void)rccl().CommDestroy(comm);
+  release();
+}
+
+int dpgo_rccl_unique_id(void* id_out) {
+  if (!id_out) return fail(DPGO_HIP_EINVAL, "null argument");
+  DPGO_TRY(rccl_ready());
+  ncclUniqueId id;
+  DPGO_TRY(rccl_check(rccl().GetUniqueId(&id), "ncclGetUniqueId"));
+  std::memcpy(id_out, &id, sizeof(id));
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_comm_init(dpgo_rbcd e, const void* id) {
+  if (!e || !id) return fail(DPGO_HIP_EINVAL, "null argument");
+  if (e->comm) return fail(DPGO_HIP_ESTATE, "engine already has a communicator");
+  DPGO_TRY(rccl_ready());
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  ncclComm_t c = nullptr;
+  DPGO_TRY(rccl_check(rccl().CommInitRank(&c, e->world, uid, e->rank), "ncclCommInitRank"));
+  e->comm = c;
+  e->own_comm = true;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_comm_attach(dpgo_rbcd e, void* comm) {
+  if (!e || !comm) return fail(DPGO_HIP_EINVAL, "null argument");
+  if (e->comm) return fail(DPGO_HIP_ESTATE, "engine already has a communicator");
+  DPGO_TRY(rccl_ready());
+  int count = 0, me = -1;
+  DPGO_TRY(rccl_check(rccl().CommCount(static_cast<ncclComm_t>(comm), &count), "ncclCommCount"));
+  DPGO_TRY(rccl_check(rccl().CommUserRank(static_cast<ncclComm_t>(comm), &me), "ncclCommUserRank"));
+  if (count != e->world || me != e->rank) return fail(DPGO_HIP_EINVAL, "communicator does not match the engine's ranks");
+  e->comm = static_cast<ncclComm_t>(comm);
+  e->own_comm = false;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_exchange(dpgo_rbcd e, const double** recv_dev) {
+  if (!e || !recv_dev) return fail(DPGO_HIP_EINVAL, "null argument");
+  if (e->world > 1 && !e->comm) return fail(DPGO_HIP_ESTATE, "no communicator (dpgo_rbcd_comm_init / _attach)");
+  HIP_TRY(e->xsend.ensure(std::max<long long>(e->send_off[e->world], 1)));
+  HIP_TRY(e->xrecv.ensure(std::max<long long>(e->recv_off[e->world], 1)));
+  DPGO_TRY(dpgo_rbcd_pack(e, e->xsend.p));
+  if (e->world > 1) {
+    // one group: every peer's send and receive, on the engine stream (stream order = halo order)
+    DPGO_TRY(rccl_check(rccl().GroupStart(), "ncclGroupStart"));
+    int rc = DPGO_HIP_OK;
+    for (int p = 0; p < e->world && rc == DPGO_HIP_OK; ++p) {
+      if (e->send_counts[p] > 0)
+        rc = rccl_check(rccl().Send(e->xsend.p + e->send_off[p], static_cast<size_t>(e->send_counts[p]), ncclFloat64, p,
+                                    e->comm, e->stream), "ncclSend");
+      if (rc == DPGO_HIP_OK && e->recv_counts[p] > 0)
+        rc = rccl_check(rccl().Recv(e->xrecv.p + e->recv_off[p], static_cast<size_t>(e->recv_counts[p]), ncclFloat64,
+                                    p, e->comm, e->stream), "ncclRecv");
+    }
+    const int rc_end = rccl_check(rccl().GroupEnd(), "ncclGroupEnd");
+    DPGO_TRY(rc);
+    DPGO_TRY(rc_end);
+  }
+  *recv_dev = e->xrecv.p;
+  return DPGO_HIP_OK;
+}

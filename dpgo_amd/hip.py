@@ -153,6 +153,13 @@ def build_id() -> str:
     return lib().dpgo_hip_build_id().decode()
 
 
+def rccl_unique_id() -> bytes:
+    """ncclGetUniqueId through the library's RCCL (128 opaque bytes)."""
+    buf = C.create_string_buffer(128)
+    _check(lib().dpgo_rccl_unique_id(buf))
+    return buf.raw
+
+
 def set_tuning(key: int, value: int):
     _check(lib().dpgo_hip_set_tuning(int(key), int(value)))
 
@@ -472,6 +479,10 @@ _SIGS2 = [
     ("dpgo_rbcd_stats", [C.c_void_p, _ip], C.c_int),
     ("dpgo_rbcd_bytes", [C.c_void_p, _dp, _dp], C.c_int),
     ("dpgo_rbcd_mode_bytes", [C.c_void_p, C.c_int, _dp], C.c_int),
+    ("dpgo_rccl_unique_id", [C.c_void_p], C.c_int),
+    ("dpgo_rbcd_comm_init", [C.c_void_p, C.c_void_p], C.c_int),
+    ("dpgo_rbcd_comm_attach", [C.c_void_p, C.c_void_p], C.c_int),
+    ("dpgo_rbcd_exchange", [C.c_void_p, C.POINTER(C.c_void_p)], C.c_int),
     ("dpgo_rbcd_set_kernel_timing", [C.c_void_p, C.c_int], C.c_int),
     ("dpgo_rbcd_set_trace", [C.c_void_p, C.c_int], C.c_int),
     ("dpgo_rbcd_get_trace", [C.c_void_p, C.c_int, _dp, C.c_int, _ip], C.c_int),
@@ -756,6 +767,19 @@ class Rbcd:
         per = np.zeros(self.num_colors)
         _check(lib().dpgo_rbcd_bytes(self.h, C.byref(b), per.ctypes.data_as(_dp)))
         return b.value, per
+
+    def comm_init(self, uid: bytes):
+        """Create the engine's RCCL communicator (collective over the engine's ranks); uid from
+        rccl_unique_id() on one rank, shared by the caller."""
+        buf = C.create_string_buffer(bytes(uid), 128)
+        _check(lib().dpgo_rbcd_comm_init(self.h, buf))
+
+    def exchange(self):
+        """Pack + RCCL send/recv of the public poses (after pre_exchange); returns the device pointer of
+        the engine-owned receive buffer for update()."""
+        p = C.c_void_p()
+        _check(lib().dpgo_rbcd_exchange(self.h, C.byref(p)))
+        return p.value
 
     def mode_bytes(self, color):
         """{SpMM mode: algorithmic bytes of one launch over every agent of the colour}."""

@@ -182,6 +182,20 @@ int dpgo_rbcd_stats(dpgo_rbcd e, int* out);
  * exact per-agent launch counts) and, per colour, the bytes of one tCG-start evaluation pass
  * (k_spmm MODE_EVAL_TCG) over the colour (evaltcg_bytes_per_color[num_colors], may be NULL). */
 int dpgo_rbcd_bytes(dpgo_rbcd e, double* bytes, double* evaltcg_bytes_per_color);
+/* ---- native halo exchange (examples/MultiRobotExample.cpp:188-213) -------------------
+ * RCCL point-to-point over the ranks of the engine, without torch: dpgo_rccl_unique_id on one rank
+ * (DPGO_RCCL_ID_BYTES opaque bytes, broadcast by the caller out of band), dpgo_rbcd_comm_init on every
+ * rank (collective; the engine owns and destroys the communicator), or dpgo_rbcd_comm_attach of a
+ * caller-owned ncclComm_t of the same RCCL instance (its size / rank must equal world / rank).  Per
+ * iteration, after dpgo_rbcd_pre_exchange: dpgo_rbcd_exchange packs the public poses and posts one
+ * ncclGroupStart / per-peer ncclSend + ncclRecv / ncclGroupEnd on the engine stream; *recv_dev is the
+ * engine-owned receive buffer to pass to dpgo_rbcd_update.  RCCL is resolved at run time (the copy
+ * already loaded in the process, else the system librccl.so.1); DPGO_HIP_EDEVICE if absent. */
+#define DPGO_RCCL_ID_BYTES 128
+int dpgo_rccl_unique_id(void* id_out);
+int dpgo_rbcd_comm_init(dpgo_rbcd e, const void* id);
+int dpgo_rbcd_comm_attach(dpgo_rbcd e, void* comm);
+int dpgo_rbcd_exchange(dpgo_rbcd e, const double** recv_dev);
 /* Algorithmic bytes of one X.Q launch over every agent of `color`, per SpMM mode (out[8], indexed as
  * dpgo_rbcd_kernel_times; 0 for modes the engine does not launch in a step). */
 int dpgo_rbcd_mode_bytes(dpgo_rbcd e, int color, double* out);
