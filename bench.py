@@ -226,6 +226,11 @@ def main():
         st1 = eng.stats().copy()
         b1, _ = eng.bytes()
         f_end, gn_end = central()
+    ready, owned = eng.ready_votes()
+    if world > 1:
+        tv = torch.tensor([ready, owned], dtype=torch.int64, device="cpu" if one_device else dev)
+        dist.all_reduce(tv)
+        ready, owned = (int(v) for v in tv.cpu().numpy())
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if one_device else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -340,7 +345,8 @@ def main():
                 "what": "Riemannian HVP (EucHessianEta + EucHvToHv, tangent-projected) over colour class 0"},
         "tcg": tcg,
         "central": {"f_start": f_start, "gradnorm_start": gn_start, "f_end": f_end, "gradnorm_end": gn_end,
-                    "steps_between": args.warmup + args.steps},
+                    "steps_between": args.warmup + args.steps,
+                    "agents_ready_to_terminate": ready, "agents": owned, "should_terminate": ready == owned},
         "setup_s": setup_s,
         "init": init_info,
     }

@@ -755,6 +755,14 @@ class Rbcd:
         _check(lib().dpgo_rbcd_status(self.h, rc.ctypes.data_as(_dp), rd.ctypes.data_as(_ip)))
         return rc, rd
 
+    def ready_votes(self):
+        """This rank's share of PGOAgent::shouldTerminate (src/PGOAgent.cpp:1007-1031): (owned agents
+        ready to terminate, owned agents).  Every agent of the team is ready iff the sums over ranks are
+        equal (the caller all-reduces them); the maxNumIters cap is the caller's loop bound."""
+        _, rd = self.status()
+        mine = rd >= 0
+        return int(np.sum(rd[mine] == 1)), int(np.sum(mine))
+
     def stats(self):
         """Cumulative solver counters per agent: int array [num_agents, STATS_INTS] (zeros elsewhere)."""
         out = np.zeros(self.num_agents * STATS_INTS, np.int32)
