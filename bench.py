@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 METRIC = "RBCD iters/sec + X·Q SpMM HBM GB/s, 1M-pose synth grid r=5, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 STATS = ["calls", "early", "runs", "tcg_iters", "NEGCURVTURE", "EXCREGION", "LCON", "SCON", "MAXITER",
-         "gave_up", "cg_steps", "implicit"]
+         "gave_up", "cg_steps", "implicit", "first_full"]
 
 
 def measured_traffic():

@@ -110,7 +110,7 @@ int dpgo::take_spmm_times(dpgo_hip_problem h, double* ms, long long* launches) {
     HIP_TRY(hipEventSynchronize(t.b));
     float v = 0.f;
     HIP_TRY(hipEventElapsedTime(&v, t.a, t.b));
-    if (t.mode >= 0 && t.mode < 8) {
+    if (t.mode >= 0 && t.mode < dpgo::kSpmmModes) {
       ms[t.mode] += v;
       launches[t.mode] += 1;
     }
@@ -1229,18 +1229,22 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     // Consumer-side finalize (TUNE_FUSE_TCG): the step test's scalar logic runs in the update kernel's
     // prologue and the stopping test's in the direction update's, three launches per tCG iteration.
     const bool fuse_tcg = dpgo::g_tuning[dpgo::TUNE_FUSE_TCG] > 0 && !exact;
-    // iteration j's step test: Hdelta = Hess[delta] and d_Hd = <delta, Hdelta>, or (qf) d_Hd alone
-    auto launch_step = [&](bool qf) -> int {
+    // iteration j's step test: Hdelta = Hess[delta] and d_Hd = <delta, Hdelta> (MODE_HESS); for the
+    // first step d_Hd by the each-edge-once formula, alone (MODE_QF) or with Hdelta stored (MODE_HESS_QF)
+    auto launch_step = [&](int mode) -> int {
       auto ch = make_ctx(h, dpgo::FLAG_TCG, h->pa.p);
       // the step test publishes too: when it already stopped every agent (a boundary or
       // negative-curvature step, the common RBCD case) the host launches no further iteration
       const int stag = next_tag(h);
       step_tags.push_back(stag);
+      const bool qf = mode == dpgo::MODE_QF;
       const dpgo::SpmmArgs sa{h->delta.p, nullptr, nullptr, x1, h->S.p, qf ? nullptr : h->Hdelta.p, nullptr,
                               nullptr, nullptr, dpgo::PRECON_NONE};
-      if (fuse_tcg && !qf) return dpgo::spmm_launch(h, dpgo::MODE_HESS, ch, sa);  // decided by the update
-      return spmm_then_finalize(h, qf ? dpgo::MODE_QF : dpgo::MODE_HESS, ch, sa,
-                                make_fin(h, dpgo::OP_TCG_STEP, h->pa.p, 1, nullptr, 0, &o, nullptr, 1, stag));
+      if (fuse_tcg && mode == dpgo::MODE_HESS) return dpgo::spmm_launch(h, mode, ch, sa);  // decided by the update
+      dpgo::OptScalars os = o;
+      os.first_full = mode == dpgo::MODE_HESS_QF ? 1 : 0;
+      return spmm_then_finalize(h, mode, ch, sa,
+                                make_fin(h, dpgo::OP_TCG_STEP, h->pa.p, 1, nullptr, 0, &os, nullptr, 1, stag));
     };
     // the first step after a QF step test was decided by the QF pass's finalize
     auto launch_rest = [&](int j, bool step_decided) -> int {
@@ -1269,10 +1273,15 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     // = tau^2 d_Hd); agents that take a CG step get Hess[delta] from a HESS pass over their tiles only.
     // Always the same formula for the first d_Hd, so an agent's result does not depend on the batch.
     const bool qf0 = !exact && P.tr_max_inner > 0;
-    // Single Run: the candidate, f(x2) and the rho test of the agents whose first step already ended
-    // tCG are queued right behind the step test, before the host learns whether any agent continues
-    // (those are retracted, evaluated and tested after their tCG: the *_EXPL launches below).
-    const bool spec = qf0 && single;
+    // When the previous call took CG steps the first step test is the full pass (MODE_HESS_QF): same
+    // d_Hd, and Hess[delta] is there for the agents that continue (no second pass over them).
+    const int first_kind = dpgo::g_tuning[dpgo::TUNE_FIRST_STEP];
+    const bool full0 = qf0 && (first_kind == 2 || (first_kind == 0 && !h->predict_boundary));
+    // Single Run, first steps predicted on the boundary: the candidate, f(x2) and the rho test of the
+    // agents whose first step already ended tCG are queued right behind the step test, before the host
+    // learns whether any agent continues (those are retracted, evaluated and tested after their tCG:
+    // the *_EXPL launches below).
+    const bool spec = qf0 && single && !full0;
     auto launch_candidate = [&](int run_flag, int filter) -> int {
       auto cr = make_ctx(h, run_flag, h->pa.p);
       HIP_TRY(dpgo::launch_retract(r, b, cr, x1, h->eta.p, 1.0, x2, h->g.p, nullptr, h->delta.p));
@@ -1291,7 +1300,7 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     int launched = 0, rtag = 0;
     bool cg_agents = !qf0;  // some agent may still be in tCG after the first step test
     if (P.tr_max_inner > 0) {
-      DPGO_TRY(launch_step(qf0));
+      DPGO_TRY(launch_step(full0 ? dpgo::MODE_HESS_QF : qf0 ? dpgo::MODE_QF : dpgo::MODE_HESS));
       if (spec) {
         rtag = launch_candidate(dpgo::FLAG_RUN_IMPL, 1);
         if (rtag < 0) return rtag;
@@ -1310,14 +1319,16 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
       if (j == 0 && qf0) {
         if (!g_valid)  // the CG-step agents' gradient (EVAL_TCG skipped storing it; same pass again)
           DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_TCG_CG, dpgo::MODE_EVAL_TCG, h->delta.p, pmode));
-        auto cg = make_ctx(h, dpgo::FLAG_TCG_CG, h->pb.p);
-        DPGO_TRY(dpgo::spmm_launch(h, dpgo::MODE_HESS, cg,
-                                   dpgo::SpmmArgs{h->delta.p, nullptr, nullptr, x1, h->S.p, h->Hdelta.p, nullptr,
-                                                  nullptr, nullptr, dpgo::PRECON_NONE}));
+        if (!full0) {  // Hess[delta] of the agents taking a CG step (the QF pass did not form it)
+          auto cg = make_ctx(h, dpgo::FLAG_TCG_CG, h->pb.p);
+          DPGO_TRY(dpgo::spmm_launch(h, dpgo::MODE_HESS, cg,
+                                     dpgo::SpmmArgs{h->delta.p, nullptr, nullptr, x1, h->S.p, h->Hdelta.p, nullptr,
+                                                    nullptr, nullptr, dpgo::PRECON_NONE}));
+        }
         DPGO_TRY(launch_rest(0, true));
       }
       if (launched < P.tr_max_inner) {  // lookahead: iteration j+1 queued while j's update runs
-        DPGO_TRY(launch_step(false));
+        DPGO_TRY(launch_step(dpgo::MODE_HESS));
         DPGO_TRY(launch_rest(launched, false));
         ++launched;
       }

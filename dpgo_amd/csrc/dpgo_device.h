@@ -50,10 +50,10 @@ struct AgentState {
   int st_gave_up;    // updates that gave up after 12 rejected Runs
   int st_cg_steps;   // tCG step tests that took a CG step (alpha)
   int st_implicit;   // Runs whose tCG ended at its first step on the boundary (eta implicit)
+  int st_first_full; // Runs whose first step test was the full pass (MODE_HESS_QF, Hess[delta] stored)
   int trace_n;       // per-iteration trace records written (FinalizeArgs::trace)
-  int pad3;
 };
-constexpr int kStatsInts = 12;  // st_calls .. st_implicit, contiguous
+constexpr int kStatsInts = 13;  // st_calls .. st_first_full, contiguous
 
 // ---- DPP quad helpers -------------------------------------------------------------------
 template <int CTRL>

@@ -13,7 +13,8 @@ constexpr int kPartialStride = 4;  // doubles of partial sums per tile
 // partial <z, g>)
 // CERT: V (Q - Lambda(X)) = VQ - [V_Y S | 0] (the certificate matrix, no projection)
 enum SpmmMode { MODE_XQ = 0, MODE_XQ_G = 1, MODE_EVAL = 2, MODE_HESS = 3, MODE_F = 4, MODE_EVAL_TCG = 5, MODE_CERT = 6,
-                MODE_QF = 7 };
+                MODE_QF = 7, MODE_HESS_QF = 8 };
+constexpr int kSpmmModes = 9;
 // Per-agent tile gating: RUN skips agents out of the RTR Run, TCG those whose tCG stopped, TCG_MODE
 // those with no tCG step pending, MOVED those whose single-Run candidate was accepted.
 enum FlagKind { FLAG_NONE = 0, FLAG_RUN = 1, FLAG_TCG = 2, FLAG_TCG_MODE = 3, FLAG_MOVED = 4, FLAG_TCG_CG = 5,
@@ -90,7 +91,8 @@ struct QView {
 struct OptScalars {
   double tol, Delta0, Delta_max, theta, kappa;
   double rel_tol, min_ratio;  // OP_STATUS: PGOAgentParameters relChangeTol, robustOptMinConvergenceRatio
-  int min_inner, max_iter, single_run, pad;
+  int min_inner, max_iter, single_run;
+  int first_full;  // OP_TCG_STEP of a first step measured by MODE_HESS_QF (statistics only)
 };
 
 struct FinalizeArgs {
@@ -117,7 +119,8 @@ struct FinalizeArgs {
 
 // SpMM modes that can run a fused finalize (SpmmArgs::fin_arrive); the others ignore it.
 __host__ __device__ constexpr bool spmm_fusable(int mode) {
-  return mode == MODE_EVAL || mode == MODE_EVAL_TCG || mode == MODE_F || mode == MODE_QF || mode == MODE_HESS;
+  return mode == MODE_EVAL || mode == MODE_EVAL_TCG || mode == MODE_F || mode == MODE_QF || mode == MODE_HESS ||
+         mode == MODE_HESS_QF;
 }
 
 // Operands of one SpMM launch (unused ones may be null).
@@ -186,7 +189,9 @@ struct RobustParams {
 };
 
 // Runtime-selectable kernel variants (A/B tuning in one process; see tools/spmm_ab.py).
-enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH = 2, TUNE_FUSE_TCG = 3, TUNE_COUNT = 4 };
+enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH = 2, TUNE_FUSE_TCG = 3,
+               TUNE_FIRST_STEP = 4,  // 0: predicted from the previous call, 1: always MODE_QF, 2: always MODE_HESS_QF
+               TUNE_COUNT = 8 };
 // variant of the edge-stream SpMM used unless TUNE_EDGE_VARIANT overrides it (bit 0: XCD-aware
 // tile remap; v >> 1: minimum waves per SIMD the register allocation must allow, none/4/5/6)
 constexpr int kEdgeDefaultVariant = 1;

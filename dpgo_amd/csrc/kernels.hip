@@ -274,7 +274,9 @@ __device__ __forceinline__ void edge_loop(const QView& q, const double* __restri
 // all staged in LDS, the last entries of j's ascending list) are accumulated and the diagonal term
 // enters with weight 1/2; then f_j = <X_j, acc_j> + <G_j, X_j>.  No second-visit record loads and
 // half the neighbour gathers.
-template <int R, int B, bool STAGED, bool HALF = false>
+// NODIAG (the first-step quadratic form, MODE_QF / MODE_HESS_QF): the half sum without the diagonal
+// term (added after the quad reduction, qf_first_step_dhd); the lane-3 mirror of a d = 2 quad is zeroed.
+template <int R, int B, bool STAGED, bool HALF = false, bool NODIAG = false>
 __device__ __forceinline__ void spmm_accumulate_edges(const QView& q, const double* __restrict__ in, long j,
                                                       int k, int beg, int end, const int2* s_inc, int i0,
                                                       const double* s_rec, int e0, double (&acc)[R][B],
@@ -316,12 +318,152 @@ __device__ __forceinline__ void spmm_accumulate_edges(const QView& q, const doub
   const bool act = k < B;
 #pragma unroll
   for (int a = 0; a < R; ++a) xown[a] = act ? xj[a] : 0.0;  // column k of in_j (load_col), for the epilogues
+  if constexpr (NODIAG) {
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int c = 0; c < B; ++c) acc[a][c] = act ? acc[a][c] : 0.0;
+    return;
+  }
 #pragma unroll
   for (int a = 0; a < R; ++a) xj[a] = HALF ? 0.5 * xj[a] : xj[a];
 #pragma unroll
   for (int a = 0; a < R; ++a)
 #pragma unroll
     for (int c = 0; c < B; ++c) acc[a][c] = act ? fma(xj[a], dk[c], acc[a][c]) : 0.0;
+}
+
+// Row kc of the pose's packed symmetric diagonal block Q_jj (static indices only).
+template <int B>
+__device__ __forceinline__ void diag_row(const QView& q, long j, int kc, double (&dk)[B]) {
+  constexpr int DW = diag_width(B - 1);
+  const double* dj = q.diag + j * DW;
+#pragma unroll
+  for (int c = 0; c < B; ++c) {
+    int o = sym_index<B>(0, c);
+    if (kc == 1) o = sym_index<B>(1, c);
+    if (kc == 2) o = sym_index<B>(2, c);
+    if (B > 3 && kc == 3) o = sym_index<B>(B > 3 ? 3 : 0, c);
+    dk[c] = dj[o];
+  }
+}
+
+// edge_loop accumulating every incidence into acc and into a second accumulator (the same stage
+// consumed twice: bitwise each accumulator's own edge_loop)
+template <int R, int B, bool INC_LDS, bool REC_LDS>
+__device__ __forceinline__ void edge_loop_dual(const QView& q, const double* __restrict__ in, int kc, int z0, int z1,
+                                               const int2* s_inc, int i0, const double* s_rec, int e0,
+                                               double (&acc)[R][B], double (&acc2)[R][B]) {
+  constexpr int RW = edge_rec_width(B - 1);
+  for (int z = z0; z < z1; ++z) {
+    int2 ie;
+    if constexpr (INC_LDS)
+      ie = s_inc[z - i0];
+    else
+      ie = q.inc[z];
+    const bool outg = (ie.x & 1) != 0;
+    const int off = outg ? kc : 4 * kc;
+    const int stride = outg ? 4 : 1;
+    const double* mr;
+    if constexpr (REC_LDS)
+      mr = s_rec + ((ie.x >> 1) - e0) * RW + off;
+    else
+      mr = q.rec + static_cast<long>(ie.x >> 1) * RW + off;
+    double m[B], x[R];
+#pragma unroll
+    for (int c = 0; c < B; ++c) m[c] = mr[c * stride];
+    const double* xk = in + static_cast<long>(ie.y) * (R * B) + kc * R;
+#pragma unroll
+    for (int a = 0; a < R; ++a) x[a] = xk[a];
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int c = 0; c < B; ++c) {
+        acc[a][c] = fma(-x[a], m[c], acc[a][c]);
+        acc2[a][c] = fma(-x[a], m[c], acc2[a][c]);
+      }
+  }
+}
+
+// MODE_HESS_QF accumulation: the full block row of V.Q, bitwise MODE_HESS's (same incidences in the same
+// order), and on the way the first-visit half sum the MODE_QF pass forms (the pose's own first visits,
+// ids >= rec_first[j], the tail of its list, from zero in the same order: bitwise that pass's sum),
+// reduce-scattered into qch.
+template <int R, int B, bool STAGED>
+__device__ __forceinline__ void spmm_accumulate_edges_dual(const QView& q, const double* __restrict__ in, long j,
+                                                           int k, int beg, int end, const int2* s_inc, int i0,
+                                                           const double* s_rec, int e0, double (&acc)[R][B],
+                                                           double (&xown)[R], double (&qch)[R]) {
+  const int kc = k < B ? k : 0;
+  const bool act = k < B;
+  const int rf = q.rec_first[j];
+  double half[R][B];
+#pragma unroll
+  for (int a = 0; a < R; ++a)
+#pragma unroll
+    for (int c = 0; c < B; ++c) half[a][c] = 0.0;
+  int midh = end;
+  if constexpr (STAGED) {
+    int mid = beg;  // as spmm_accumulate_edges: second visits (ids below the tile's range) first
+    while (mid < end && (s_inc[mid - i0].x >> 1) < e0) ++mid;
+    while (midh > mid && (s_inc[midh - 1 - i0].x >> 1) >= rf) --midh;
+    edge_loop<R, B, true, false>(q, in, kc, beg, mid, s_inc, i0, s_rec, e0, acc);
+    edge_loop<R, B, true, true>(q, in, kc, mid, midh, s_inc, i0, s_rec, e0, acc);
+    edge_loop_dual<R, B, true, true>(q, in, kc, midh, end, s_inc, i0, s_rec, e0, acc, half);
+  } else {
+    while (midh > beg && (q.inc[midh - 1].x >> 1) >= rf) --midh;
+    edge_loop<R, B, false, false>(q, in, kc, beg, midh, s_inc, i0, s_rec, e0, acc);
+    edge_loop_dual<R, B, false, false>(q, in, kc, midh, end, s_inc, i0, s_rec, e0, acc, half);
+  }
+#pragma unroll
+  for (int a = 0; a < R; ++a)
+#pragma unroll
+    for (int c = 0; c < B; ++c) half[a][c] = act ? half[a][c] : 0.0;
+  quad_reduce_scatter<R, B>(half, k, qch);
+  double xj[R], dk[B];
+  const double* pj = in + j * (R * B) + kc * R;
+#pragma unroll
+  for (int a = 0; a < R; ++a) xj[a] = pj[a];
+  diag_row<B>(q, j, kc, dk);
+#pragma unroll
+  for (int a = 0; a < R; ++a) xown[a] = act ? xj[a] : 0.0;
+#pragma unroll
+  for (int a = 0; a < R; ++a)
+#pragma unroll
+    for (int c = 0; c < B; ++c) acc[a][c] = act ? fma(xj[a], dk[c], acc[a][c]) : 0.0;
+}
+
+// The first tCG step's d_Hd = <V, Hess[V]> = <V, VQ> - <V_Y, V_Y S> (A.3; P_X self-adjoint on tangent V)
+// from the first-visit half sum: <V, VQ> = sum_j <V_j, 2 h_j + V_j Q_jj>, h_j = sum over j's first
+// visits.  One formula for MODE_QF and MODE_HESS_QF, so an agent's first step does not depend on
+// which of the two its batch ran.
+template <int R, int B>
+__device__ __forceinline__ double qf_first_step_dhd(const QView& q, long j, int k, bool ok, const double (&vcol)[R],
+                                                    const double (&qch)[R], const double (&S)[B - 1][B - 1]) {
+  constexpr int D = B - 1;
+  const int kc = k < B ? k : 0;
+  double dk[B];
+  if (ok) {
+    diag_row<B>(q, j, kc, dk);
+  } else {
+#pragma unroll
+    for (int c = 0; c < B; ++c) dk[c] = 0.0;
+  }
+  double Vf[R][B], Vy[R][D], w[R], hc[R];
+  quad_gather<R, B>(vcol, Vf);
+  quad_gather_y<R, D>(vcol, Vy);
+#pragma unroll
+  for (int a = 0; a < R; ++a) {
+    double dg = 0.0;  // column k of V_j Q_jj
+#pragma unroll
+    for (int u = 0; u < B; ++u) dg = fma(Vf[a][u], dk[u], dg);
+    w[a] = fma(2.0, qch[a], dg);
+  }
+  sub_y_times_col<R, D>(Vy, S, k, w, hc);
+  double dpart = 0.0;
+#pragma unroll
+  for (int a = 0; a < R; ++a) dpart = fma(vcol[a], hc[a], dpart);
+  return dpart;
 }
 
 // SpMM variants: neighbours per step, non-temporal block loads, XCD tile remap
@@ -387,8 +529,8 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
 
   // epilogue operands issued ahead of the edge loop (edge-stream variant bit 3)
   constexpr bool PRE = FMT == QFMT_EDGES && evar_pre(VAR);
-  constexpr bool PRE_S = PRE && (MODE == MODE_HESS || MODE == MODE_QF || MODE == MODE_CERT);
-  constexpr bool PRE_X = PRE && MODE == MODE_HESS;
+  constexpr bool PRE_S = PRE && (MODE == MODE_HESS || MODE == MODE_HESS_QF || MODE == MODE_QF || MODE == MODE_CERT);
+  constexpr bool PRE_X = PRE && (MODE == MODE_HESS || MODE == MODE_HESS_QF);
   constexpr bool PRE_M = PRE && MODE == MODE_EVAL_TCG;
   double pre_x[R], pre_s[s_width(D)], pre_m[B];
   int pre_slot = -1;
@@ -416,6 +558,9 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
   double xin[R];
 #pragma unroll
   for (int a = 0; a < R; ++a) xin[a] = 0.0;
+  double qch[R];  // MODE_HESS_QF (edge stream): column k of the first-visit half sum
+#pragma unroll
+  for (int a = 0; a < R; ++a) qch[a] = 0.0;
   if constexpr (FMT == QFMT_EDGES) {
     // The half (each-edge-once) passes read only the tile's first-visit records, each exactly once and
     // as whole 128-byte lines per pose quad: they skip the LDS stage (less LDS, more resident waves).
@@ -439,14 +584,23 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
       for (int x = threadIdx.x; x < ne * (RW / 2); x += kThreads) s_rec2[x] = src[x];
     }
     if constexpr (STAGE) __syncthreads();
+    constexpr bool NODIAG = MODE == MODE_QF;
     if (p.ok) {
       const double* s_rec = reinterpret_cast<const double*>(s_rec2);
-      if (staged)
-        spmm_accumulate_edges<R, B, true, HALF>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc, i0,
-                                                s_rec, e0, acc, xin);
-      else
-        spmm_accumulate_edges<R, B, false, HALF>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc, i0,
-                                                 s_rec, e0, acc, xin);
+      if constexpr (MODE == MODE_HESS_QF) {
+        if (staged)
+          spmm_accumulate_edges_dual<R, B, true>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc, i0,
+                                                 s_rec, e0, acc, xin, qch);
+        else
+          spmm_accumulate_edges_dual<R, B, false>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc, i0,
+                                                  s_rec, e0, acc, xin, qch);
+      } else if (staged) {
+        spmm_accumulate_edges<R, B, true, HALF, NODIAG>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc,
+                                                        i0, s_rec, e0, acc, xin);
+      } else {
+        spmm_accumulate_edges<R, B, false, HALF, NODIAG>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc,
+                                                         i0, s_rec, e0, acc, xin);
+      }
     }
   } else {
     if (p.ok && p.k < B) spmm_accumulate<R, B, var_unr(VAR), var_nt(VAR)>(q, in, p.j, p.k, acc);
@@ -588,18 +742,20 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
 #pragma unroll
       for (int v = 0; v < D; ++v)
         S[u][v] = PRE_S ? pre_s[sym_index<D>(u, v)] : (p.ok ? S_in[p.j * s_width(D) + sym_index<D>(u, v)] : 0.0);
-    double Vf[R][D], w[R], hc[R];
-    quad_gather_y<R, D>(vcol, Vf);
-    constexpr double kq = FMT == QFMT_EDGES ? 2.0 : 1.0;
-#pragma unroll
-    for (int a = 0; a < R; ++a) w[a] = kq * qc[a];
-    sub_y_times_col<R, D>(Vf, S, p.k, w, hc);
     double dpart = 0.0;
+    if constexpr (FMT == QFMT_EDGES) {
+      // qc: the first-visit half sum without the diagonal (NODIAG)
+      dpart = qf_first_step_dhd<R, B>(q, p.j, p.k, p.ok, vcol, qc, S);
+    } else {  // BSR: the full row, <V, VQ> = sum_j <V_j, (VQ)_j>
+      double Vf[R][D], hc[R];
+      quad_gather_y<R, D>(vcol, Vf);
+      sub_y_times_col<R, D>(Vf, S, p.k, qc, hc);
 #pragma unroll
-    for (int a = 0; a < R; ++a) dpart = fma(vcol[a], hc[a], dpart);
+      for (int a = 0; a < R; ++a) dpart = fma(vcol[a], hc[a], dpart);
+    }
     double parts[1] = {own ? dpart : 0.0};
     block_partials<1>(parts, c.partials, p.tile, args.fin_mode == 2);
-  } else if constexpr (MODE == MODE_HESS) {
+  } else if constexpr (MODE == MODE_HESS || MODE == MODE_HESS_QF) {
     double vcol[R], xcol[R];
 #pragma unroll
     for (int a = 0; a < R; ++a) vcol[a] = xin[a];
@@ -624,8 +780,15 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     sym_ytm_cols<R, D>(Xf, h1, S2);
     sub_y_times_col<R, D>(Xf, S2, p.k, h1, hc);  // tangent projection at X
     double dpart = 0.0;
+    if constexpr (MODE == MODE_HESS) {
 #pragma unroll
-    for (int a = 0; a < R; ++a) dpart = fma(vcol[a], hc[a], dpart);
+      for (int a = 0; a < R; ++a) dpart = fma(vcol[a], hc[a], dpart);
+    } else if constexpr (FMT == QFMT_EDGES) {  // the first step's d_Hd by the MODE_QF formula
+      dpart = qf_first_step_dhd<R, B>(q, p.j, p.k, p.ok, vcol, qch, S);
+    } else {  // BSR MODE_QF's: <V, h1>, h1 = VQ - V_Y S
+#pragma unroll
+      for (int a = 0; a < R; ++a) dpart = fma(vcol[a], h1[a], dpart);
+    }
     store_vec<R>(out, off, own, hc);
     double parts[1] = {own ? dpart : 0.0};
     block_partials<1>(parts, c.partials, p.tile, args.fin_mode == 2);
@@ -1340,6 +1503,7 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       const double D2 = s.Delta * s.Delta;
       s.alpha = alpha;
       s.tcg_iters += 1;
+      if (s.tcg_iters == 1 && o.first_full) s.st_first_full += 1;
       double* tr = trace_record(f, agent, s, OP_TCG_STEP);
       if (tr) {
         tr[TR_J] = s.tcg_iters - 1;
@@ -2107,7 +2271,7 @@ __global__ __launch_bounds__(kThreads) void k_assemble_G(GEdges e, int nslots, c
     default: return hipErrorInvalidValue;                  \
   }
 
-int g_tuning[TUNE_COUNT] = {0, -1, 1, 0};
+int g_tuning[TUNE_COUNT] = {0, -1, 1, 0, 0, 0, 0, 0};
 
 bool supported_rb(int r, int b) {
   if (b == 3) return r >= 2 && r <= 8;
@@ -2139,7 +2303,7 @@ hipError_t spmm_variant54(int var, dim3 grid, const LaunchCtx& c, const QView& q
 template <int MODE>
 hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const SpmmArgs& a) {
   if (q.fmt == QFMT_EDGES) {
-    constexpr bool kPreMode = MODE == MODE_HESS || MODE == MODE_QF || MODE == MODE_EVAL_TCG;
+    constexpr bool kPreMode = MODE == MODE_HESS || MODE == MODE_HESS_QF || MODE == MODE_QF || MODE == MODE_EVAL_TCG;
     if (kPreMode && r == 5 && b == 4 && g_tuning[TUNE_EPI_PREFETCH] > 0 && g_tuning[TUNE_EDGE_VARIANT] < 0)
     {
       k_spmm<5, 4, MODE, kEdgeDefaultVariant | 8, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
@@ -2170,6 +2334,7 @@ hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const QView& 
     case MODE_EVAL_TCG: e = spmm_mode<MODE_EVAL_TCG>(r, b, grid, c, q, a); break;
     case MODE_CERT: e = spmm_mode<MODE_CERT>(r, b, grid, c, q, a); break;
     case MODE_QF: e = spmm_mode<MODE_QF>(r, b, grid, c, q, a); break;
+    case MODE_HESS_QF: e = spmm_mode<MODE_HESS_QF>(r, b, grid, c, q, a); break;
     default: break;
   }
   if (e != hipSuccess) return e;

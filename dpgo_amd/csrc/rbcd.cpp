@@ -60,8 +60,8 @@ struct dpgo_rbcd_s {
   double host_bytes = 0.0;  // per-iteration passes counted by the host (combination, G, exchange)
   std::vector<long long> g_store_calls;  // per colour: optimize calls that stored grad(x1)
   // in-step SpMM timing (dpgo_rbcd_set_kernel_timing)
-  double spmm_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  long long spmm_launches[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  double spmm_ms[kSpmmModes] = {};
+  long long spmm_launches[kSpmmModes] = {};
   // per colour G assembly tables
   struct GTab {
     DevBuf<int> slot_off, src, outgoing;
@@ -881,7 +881,8 @@ int dpgo_rbcd_bytes(dpgo_rbcd e, double* bytes, double* evaltcg_bytes_per_color)
     for (int a = 0; a < h->K; ++a) {
       const auto& z = e->asz[c][a];
       const int* k = &st[static_cast<size_t>(a) * kStatsInts];
-      const double calls = k[0], runs = k[2], iters = k[3], lcon = k[6] + k[7], maxit = k[8], cg = k[10], impl = k[11];
+      const double calls = k[0], runs = k[2], iters = k[3], lcon = k[6] + k[7], maxit = k[8], cg = k[10], impl = k[11],
+                   full = k[12];
       const double bnd = k[4] + k[5];
       calls_all = std::max(calls_all, calls);
       const double full_in = (z.n + 2.0 * z.m_in) * blk + (z.n + 1.0) * 4.0 + z.n * P;
@@ -890,8 +891,10 @@ int dpgo_rbcd_bytes(dpgo_rbcd e, double* bytes, double* evaltcg_bytes_per_color)
       const double evaltcg = full_in + z.n * (SW + DW + P) + gread;  // + grad(x1) when stored (below)
       if (evaltcg_bytes_per_color) evaltcg_bytes_per_color[c] += evaltcg;
       total += calls * evaltcg;
-      total += runs * (half_in + z.n * SW);                           // QF first step test
-      total += (iters - runs + (runs - impl)) * (full_in + z.n * (P + SW + P));  // HESS
+      // first step test: the each-edge-once pass (QF), or the full pass storing Hess[delta] (HESS_QF,
+      // counted as taken by agents that continue with CG steps)
+      total += (runs - full) * (half_in + z.n * SW) + full * (full_in + z.n * (P + SW + P));
+      total += (iters - runs + std::max(0.0, runs - impl - full)) * (full_in + z.n * (P + SW + P));  // HESS
       // tCG updates: a CG step reads delta, Hdelta, eta, r, X, Minv and writes eta, r, z; a boundary step
       // reads delta, Hdelta, eta and writes eta (the first step of a tCG reads no eta)
       total += cg * z.n * (8.0 * P + DW) - runs * z.n * P + (bnd - impl) * z.n * 4.0 * P;
@@ -916,13 +919,14 @@ int dpgo_rbcd_mode_bytes(dpgo_rbcd e, int color, double* out) {
   if (!e || !out || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
   const double P = pose_bytes(e), b = e->b, d = e->d;
   const double blk = b * b * 8.0 + 4.0, DW = 8.0 * b * (b + 1) / 2, SW = 8.0 * d * (d + 1) / 2;
-  for (int m = 0; m < 8; ++m) out[m] = 0.0;
+  for (int m = 0; m < kSpmmModes; ++m) out[m] = 0.0;
   for (const auto& z : e->asz[color]) {
     const double full_in = (z.n + 2.0 * z.m_in) * blk + (z.n + 1.0) * 4.0 + z.n * P;
     const double half_in = (z.n + z.m_in) * blk + (z.n + 1.0) * 4.0 + z.n * P;
     const double gread = z.gslots * P + z.n * 4.0;
     out[MODE_EVAL_TCG] += full_in + z.n * (SW + DW + P) + gread;
     out[MODE_HESS] += full_in + z.n * (P + SW + P);
+    out[MODE_HESS_QF] += full_in + z.n * (P + SW + P);
     out[MODE_QF] += half_in + z.n * SW;
     out[MODE_F] += half_in + gread;
   }
@@ -955,7 +959,7 @@ int dpgo_rbcd_kernel_times(dpgo_rbcd e, double* ms_per_mode, long long* launches
   if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
   for (auto* h : e->prob)
     if (h) DPGO_TRY(take_spmm_times(h, e->spmm_ms, e->spmm_launches));
-  for (int m = 0; m < 8; ++m) {
+  for (int m = 0; m < kSpmmModes; ++m) {
     if (ms_per_mode) ms_per_mode[m] = e->spmm_ms[m];
     if (launches_per_mode) launches_per_mode[m] = e->spmm_launches[m];
     e->spmm_ms[m] = 0.0;

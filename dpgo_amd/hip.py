@@ -96,13 +96,13 @@ _SIGS = [
     ("dpgo_hip_get_trace", [C.c_void_p, C.c_int, _dp, C.c_int, _ip], C.c_int),
     ("dpgo_hip_build_id", [], C.c_char_p),
 ]
-STATS_INTS = 12
+STATS_INTS = 13
 STATS_FIELDS = ["calls", "early", "runs", "tcg_iters", "NEGCURVTURE", "EXCREGION", "LCON", "SCON", "MAXITER",
-                "gave_up", "cg_steps", "implicit"]
+                "gave_up", "cg_steps", "implicit", "first_full"]
 TRACE_WIDTH = 16
 TRACE_FIELDS = ["op", "j", "f1", "f2", "rho", "Delta", "alpha", "beta", "tau", "d_Hd", "norm_r", "z_r", "status",
                 "accepted", "ngf", "run"]
-SPMM_MODES = ["XQ", "XQ_G", "EVAL", "HESS", "F", "EVAL_TCG", "CERT", "QF"]
+SPMM_MODES = ["XQ", "XQ_G", "EVAL", "HESS", "F", "EVAL_TCG", "CERT", "QF", "HESS_QF"]
 
 EXPORTED_SYMBOLS = [s[0] for s in _SIGS]
 
@@ -791,9 +791,9 @@ class Rbcd:
 
     def mode_bytes(self, color):
         """{SpMM mode: algorithmic bytes of one launch over every agent of the colour}."""
-        out = np.zeros(8)
+        out = np.zeros(len(SPMM_MODES))
         _check(lib().dpgo_rbcd_mode_bytes(self.h, int(color), out.ctypes.data_as(_dp)))
-        return {SPMM_MODES[m]: float(out[m]) for m in range(8) if out[m] > 0}
+        return {SPMM_MODES[m]: float(out[m]) for m in range(len(SPMM_MODES)) if out[m] > 0}
 
     def set_trace(self, capacity):
         _check(lib().dpgo_rbcd_set_trace(self.h, int(capacity)))
@@ -813,10 +813,10 @@ class Rbcd:
 
     def kernel_times(self):
         """{mode: (ms summed, launches)} of the timed in-step X.Q launches since the last call."""
-        ms = np.zeros(8)
-        n = np.zeros(8, np.int64)
+        ms = np.zeros(len(SPMM_MODES))
+        n = np.zeros(len(SPMM_MODES), np.int64)
         _check(lib().dpgo_rbcd_kernel_times(self.h, ms.ctypes.data_as(_dp), n.ctypes.data_as(_lp)))
-        return {SPMM_MODES[m]: (float(ms[m]), int(n[m])) for m in range(8) if n[m] > 0}
+        return {SPMM_MODES[m]: (float(ms[m]), int(n[m])) for m in range(len(SPMM_MODES)) if n[m] > 0}
 
     def pre_exchange(self, color):
         _check(lib().dpgo_rbcd_pre_exchange(self.h, int(color)))

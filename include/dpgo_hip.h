@@ -190,8 +190,9 @@ int dpgo_hip_synchronize(dpgo_hip_problem h);
  * Cumulative per-agent counters since the handle was created, DPGO_STATS_INTS ints per agent:
  * [optimize calls, calls that returned at once (|grad| < tol), RTR Runs, tCG inner iterations,
  *  tCG exits NEGCURVTURE, EXCREGION, LCON, SCON, MAXITER, updates that gave up, tCG CG steps,
- *  Runs whose tCG ended at its first step on the trust-region boundary]. */
-#define DPGO_STATS_INTS 12
+ *  Runs whose tCG ended at its first step on the trust-region boundary, Runs whose first step test
+ *  was the full pass that also stores Hess[delta] (chosen when the previous call took CG steps)]. */
+#define DPGO_STATS_INTS 13
 int dpgo_hip_stats(dpgo_hip_problem h, int* out /* [num_agents * DPGO_STATS_INTS] */);
 /* Per-iteration RTR / tCG trace (the reference prints it with ROPTLIB Debug = ITERRESULT when
  * verbose, src/QuadraticOptimizer.cpp:82-86): after this call every tCG step test, tCG stopping

@@ -196,11 +196,13 @@ int dpgo_rccl_unique_id(void* id_out);
 int dpgo_rbcd_comm_init(dpgo_rbcd e, const void* id);
 int dpgo_rbcd_comm_attach(dpgo_rbcd e, void* comm);
 int dpgo_rbcd_exchange(dpgo_rbcd e, const double** recv_dev);
-/* Algorithmic bytes of one X.Q launch over every agent of `color`, per SpMM mode (out[8], indexed as
+/* SpMM modes of the per-mode arrays: XQ, XQ_G, EVAL, HESS, F, EVAL_TCG, CERT, QF, HESS_QF */
+#define DPGO_SPMM_MODES 9
+/* Algorithmic bytes of one X.Q launch over every agent of `color`, per SpMM mode (out[DPGO_SPMM_MODES], indexed as
  * dpgo_rbcd_kernel_times; 0 for modes the engine does not launch in a step). */
 int dpgo_rbcd_mode_bytes(dpgo_rbcd e, int color, double* out);
 /* HIP events around every in-step X.Q launch (on the launch stream) while on; dpgo_rbcd_kernel_times
- * synchronises and returns, per SpMM mode (8: XQ, XQ_G, EVAL, HESS, F, EVAL_TCG, CERT, QF), the
+ * synchronises and returns, per SpMM mode (DPGO_SPMM_MODES entries, order above), the
  * summed milliseconds and launch counts since the last call. */
 int dpgo_rbcd_set_kernel_timing(dpgo_rbcd e, int on);
 /* Per-iteration RTR / tCG trace of every owned agent's updates (dpgo_hip_set_trace / _get_trace

@@ -106,7 +106,7 @@ def test_graph_certify_engine_iterate(hip, name, agents, iters):
     c = g.certify(Xd, r, max_iters=1500 if n < 1000 else 400, tol=1e-10, want_rounded=True, want_vector=True)
     X = hip.from_dev_layout(Xd, r)
     Q = O.connection_laplacian(meas, n)
-    assert abs(c["f_relax"] - O.central_cost(meas, X)) <= 1e-12 * abs(c["f_relax"])
+    assert abs(c["f_relax"] - O.central_cost(meas, X)) <= 1e-11 * abs(c["f_relax"])  # f: a sum of cancelling terms
     T = O.round_to_se(X, d)
     assert rel(c["T_rounded"], T) <= 1e-10
     assert abs(c["f_rounded"] - O.central_cost(meas, T)) <= 1e-10 * abs(c["f_rounded"])

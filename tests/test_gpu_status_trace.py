@@ -293,3 +293,34 @@ def test_consumer_side_finalize_bitwise(hip):
     assert np.array_equal(out[0][0], out[1][0])
     assert np.array_equal(out[0][1], out[1][1])
     assert out[0][1][:, 10].sum() > 0  # CG steps were taken
+
+
+def test_first_step_kind_bitwise(hip):
+    """The first tCG step's d_Hd is one formula whether the batch ran the each-edge-once pass (MODE_QF)
+    or the full pass that also stores Hess[delta] (MODE_HESS_QF, chosen when the previous call took CG
+    steps): forcing either kind gives bitwise the same iterates, traces and counters (tuning key 4)."""
+    g = hip.Graph.grid3d(12, seed=5)
+    aop = g.grid_partition(2)
+    X0, _, _ = g.distributed_init(aop, 5, hip.lifting_matrix(3, 5), gpu=True, rtol=1e-12, dev_layout=True)
+    out = []
+    for kind in (1, 2, 0):
+        hip.set_tuning(4, kind)
+        try:
+            e = hip.Rbcd(g, aop, np.zeros(8, np.int32), 0, 1, hip.rbcd_params(r=5, acceleration=1))
+            e.set_trace(512)
+            e.set_X(X0)
+            for it in range(40):
+                e.pre_exchange(it % e.num_colors)
+                e.update(it % e.num_colors, None)
+            X = np.zeros(X0.size)
+            e.get_X_into(X)
+            tr = np.array([[rec[k] for k in hip.TRACE_FIELDS] for rec in e.get_trace(3)])
+            out.append((X, e.stats().copy(), tr))
+        finally:
+            hip.set_tuning(4, 0)
+    for other in out[1:]:
+        assert np.array_equal(out[0][0], other[0])
+        assert np.array_equal(out[0][1][:, :12], other[1][:, :12])
+        assert np.array_equal(out[0][2], other[2], equal_nan=True)
+    assert out[1][1][:, 12].sum() > 0 and out[0][1][:, 12].sum() == 0
+    assert out[0][1][:, 10].sum() > 0  # CG steps were taken
