@@ -348,14 +348,18 @@ __device__ __forceinline__ void diag_row(const QView& q, long j, int kc, double 
   }
 }
 
-// edge_loop accumulating every incidence into acc and into a second accumulator (the same stage
-// consumed twice: bitwise each accumulator's own edge_loop)
+// edge_loop accumulating every incidence into acc and into a second accumulator (the same ping-pong
+// stages consumed twice: bitwise each accumulator's own edge_loop)
 template <int R, int B, bool INC_LDS, bool REC_LDS>
 __device__ __forceinline__ void edge_loop_dual(const QView& q, const double* __restrict__ in, int kc, int z0, int z1,
                                                const int2* s_inc, int i0, const double* s_rec, int e0,
                                                double (&acc)[R][B], double (&acc2)[R][B]) {
   constexpr int RW = edge_rec_width(B - 1);
-  for (int z = z0; z < z1; ++z) {
+  struct Stage {
+    double m[B];
+    double x[R];
+  };
+  auto fetch = [&](int z, Stage& st) {
     int2 ie;
     if constexpr (INC_LDS)
       ie = s_inc[z - i0];
@@ -369,19 +373,30 @@ __device__ __forceinline__ void edge_loop_dual(const QView& q, const double* __r
       mr = s_rec + ((ie.x >> 1) - e0) * RW + off;
     else
       mr = q.rec + static_cast<long>(ie.x >> 1) * RW + off;
-    double m[B], x[R];
 #pragma unroll
-    for (int c = 0; c < B; ++c) m[c] = mr[c * stride];
+    for (int c = 0; c < B; ++c) st.m[c] = mr[c * stride];
     const double* xk = in + static_cast<long>(ie.y) * (R * B) + kc * R;
 #pragma unroll
-    for (int a = 0; a < R; ++a) x[a] = xk[a];
+    for (int a = 0; a < R; ++a) st.x[a] = xk[a];
+  };
+  auto consume = [&](const Stage& st) {
 #pragma unroll
     for (int a = 0; a < R; ++a)
 #pragma unroll
       for (int c = 0; c < B; ++c) {
-        acc[a][c] = fma(-x[a], m[c], acc[a][c]);
-        acc2[a][c] = fma(-x[a], m[c], acc2[a][c]);
+        acc[a][c] = fma(-st.x[a], st.m[c], acc[a][c]);
+        acc2[a][c] = fma(-st.x[a], st.m[c], acc2[a][c]);
       }
+  };
+  if (z0 >= z1) return;
+  Stage sa, sb;
+  fetch(z0, sa);
+  for (int nz = z0; nz < z1; nz += 2) {
+    fetch(min(nz + 1, z1 - 1), sb);
+    consume(sa);
+    if (nz + 1 >= z1) break;
+    fetch(min(nz + 2, z1 - 1), sa);
+    consume(sb);
   }
 }
 
