@@ -348,93 +348,51 @@ __device__ __forceinline__ void diag_row(const QView& q, long j, int kc, double 
   }
 }
 
-// edge_loop accumulating every incidence into acc and into a second accumulator (the same ping-pong
-// stages consumed twice: bitwise each accumulator's own edge_loop)
-template <int R, int B, bool INC_LDS, bool REC_LDS>
-__device__ __forceinline__ void edge_loop_dual(const QView& q, const double* __restrict__ in, int kc, int z0, int z1,
-                                               const int2* s_inc, int i0, const double* s_rec, int e0,
-                                               double (&acc)[R][B], double (&acc2)[R][B]) {
-  constexpr int RW = edge_rec_width(B - 1);
-  struct Stage {
-    double m[B];
-    double x[R];
-  };
-  auto fetch = [&](int z, Stage& st) {
-    int2 ie;
-    if constexpr (INC_LDS)
-      ie = s_inc[z - i0];
-    else
-      ie = q.inc[z];
-    const bool outg = (ie.x & 1) != 0;
-    const int off = outg ? kc : 4 * kc;
-    const int stride = outg ? 4 : 1;
-    const double* mr;
-    if constexpr (REC_LDS)
-      mr = s_rec + ((ie.x >> 1) - e0) * RW + off;
-    else
-      mr = q.rec + static_cast<long>(ie.x >> 1) * RW + off;
-#pragma unroll
-    for (int c = 0; c < B; ++c) st.m[c] = mr[c * stride];
-    const double* xk = in + static_cast<long>(ie.y) * (R * B) + kc * R;
-#pragma unroll
-    for (int a = 0; a < R; ++a) st.x[a] = xk[a];
-  };
-  auto consume = [&](const Stage& st) {
+// column k of the quad-reduced running sum (the lane-3 mirror of a d = 2 quad masked out; for d = 3
+// every lane is active and acc is reduced in place, no copy held across the edge loop)
+template <int R, int B>
+__device__ __forceinline__ void snapshot_half(const double (&acc)[R][B], int k, bool act, double (&qch)[R]) {
+  if constexpr (B == 4) {
+    (void)act;
+    quad_reduce_scatter<R, B>(acc, k, qch);
+  } else {
+    double half[R][B];
 #pragma unroll
     for (int a = 0; a < R; ++a)
 #pragma unroll
-      for (int c = 0; c < B; ++c) {
-        acc[a][c] = fma(-st.x[a], st.m[c], acc[a][c]);
-        acc2[a][c] = fma(-st.x[a], st.m[c], acc2[a][c]);
-      }
-  };
-  if (z0 >= z1) return;
-  Stage sa, sb;
-  fetch(z0, sa);
-  for (int nz = z0; nz < z1; nz += 2) {
-    fetch(min(nz + 1, z1 - 1), sb);
-    consume(sa);
-    if (nz + 1 >= z1) break;
-    fetch(min(nz + 2, z1 - 1), sa);
-    consume(sb);
+      for (int c = 0; c < B; ++c) half[a][c] = act ? acc[a][c] : 0.0;
+    quad_reduce_scatter<R, B>(half, k, qch);
   }
 }
 
-// MODE_HESS_QF accumulation: the full block row of V.Q, bitwise MODE_HESS's (same incidences in the same
-// order), and on the way the first-visit half sum the MODE_QF pass forms (the pose's own first visits,
-// ids >= rec_first[j], the tail of its list, from zero in the same order: bitwise that pass's sum),
-// reduce-scattered into qch.
-template <int R, int B, bool STAGED>
-__device__ __forceinline__ void spmm_accumulate_edges_dual(const QView& q, const double* __restrict__ in, long j,
-                                                           int k, int beg, int end, const int2* s_inc, int i0,
-                                                           const double* s_rec, int e0, double (&acc)[R][B],
-                                                           double (&xown)[R], double (&qch)[R]) {
+// MODE_HESS / MODE_HESS_QF accumulation of a block row of V.Q: the pose's own first visits (ids >=
+// rec_first[j], the tail of its ascending list) first and from zero -- exactly the sum the MODE_QF pass
+// forms -- then the other incidences, then the diagonal.  SNAP (MODE_HESS_QF): that first-visit sum
+// is reduce-scattered into qch on the way (bitwise the QF pass's), so one pass gives Hess[V] and the
+// first step's d_Hd; MODE_HESS runs the same order, so both passes give bitwise the same Hess[V].
+template <int R, int B, bool STAGED, bool SNAP>
+__device__ __forceinline__ void spmm_accumulate_edges_hq(const QView& q, const double* __restrict__ in, long j,
+                                                         int k, int beg, int end, const int2* s_inc, int i0,
+                                                         const double* s_rec, int e0, double (&acc)[R][B],
+                                                         double (&xown)[R], double (&qch)[R]) {
   const int kc = k < B ? k : 0;
   const bool act = k < B;
   const int rf = q.rec_first[j];
-  double half[R][B];
-#pragma unroll
-  for (int a = 0; a < R; ++a)
-#pragma unroll
-    for (int c = 0; c < B; ++c) half[a][c] = 0.0;
   int midh = end;
   if constexpr (STAGED) {
-    int mid = beg;  // as spmm_accumulate_edges: second visits (ids below the tile's range) first
+    int mid = beg;  // second visits (ids below the tile's range) | first visits of earlier poses of the tile
     while (mid < end && (s_inc[mid - i0].x >> 1) < e0) ++mid;
     while (midh > mid && (s_inc[midh - 1 - i0].x >> 1) >= rf) --midh;
+    edge_loop<R, B, true, true>(q, in, kc, midh, end, s_inc, i0, s_rec, e0, acc);
+    if constexpr (SNAP) snapshot_half<R, B>(acc, k, act, qch);
     edge_loop<R, B, true, false>(q, in, kc, beg, mid, s_inc, i0, s_rec, e0, acc);
     edge_loop<R, B, true, true>(q, in, kc, mid, midh, s_inc, i0, s_rec, e0, acc);
-    edge_loop_dual<R, B, true, true>(q, in, kc, midh, end, s_inc, i0, s_rec, e0, acc, half);
   } else {
     while (midh > beg && (q.inc[midh - 1].x >> 1) >= rf) --midh;
+    edge_loop<R, B, false, false>(q, in, kc, midh, end, s_inc, i0, s_rec, e0, acc);
+    if constexpr (SNAP) snapshot_half<R, B>(acc, k, act, qch);
     edge_loop<R, B, false, false>(q, in, kc, beg, midh, s_inc, i0, s_rec, e0, acc);
-    edge_loop_dual<R, B, false, false>(q, in, kc, midh, end, s_inc, i0, s_rec, e0, acc, half);
   }
-#pragma unroll
-  for (int a = 0; a < R; ++a)
-#pragma unroll
-    for (int c = 0; c < B; ++c) half[a][c] = act ? half[a][c] : 0.0;
-  quad_reduce_scatter<R, B>(half, k, qch);
   double xj[R], dk[B];
   const double* pj = in + j * (R * B) + kc * R;
 #pragma unroll
@@ -602,13 +560,14 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     constexpr bool NODIAG = MODE == MODE_QF;
     if (p.ok) {
       const double* s_rec = reinterpret_cast<const double*>(s_rec2);
-      if constexpr (MODE == MODE_HESS_QF) {
+      if constexpr (MODE == MODE_HESS || MODE == MODE_HESS_QF) {
+        constexpr bool SNAP = MODE == MODE_HESS_QF;
         if (staged)
-          spmm_accumulate_edges_dual<R, B, true>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc, i0,
-                                                 s_rec, e0, acc, xin, qch);
+          spmm_accumulate_edges_hq<R, B, true, SNAP>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc,
+                                                     i0, s_rec, e0, acc, xin, qch);
         else
-          spmm_accumulate_edges_dual<R, B, false>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc, i0,
-                                                  s_rec, e0, acc, xin, qch);
+          spmm_accumulate_edges_hq<R, B, false, SNAP>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc,
+                                                      i0, s_rec, e0, acc, xin, qch);
       } else if (staged) {
         spmm_accumulate_edges<R, B, true, HALF, NODIAG>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc,
                                                         i0, s_rec, e0, acc, xin);
@@ -786,6 +745,9 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
 #pragma unroll
       for (int v = 0; v < D; ++v)
         S[u][v] = PRE_S ? pre_s[sym_index<D>(u, v)] : (p.ok ? S_in[p.j * s_width(D) + sym_index<D>(u, v)] : 0.0);
+    double dpart = 0.0;
+    if constexpr (MODE == MODE_HESS_QF && FMT == QFMT_EDGES)  // the first step's d_Hd by the MODE_QF formula
+      dpart = qf_first_step_dhd<R, B>(q, p.j, p.k, p.ok, vcol, qch, S);  // (first: its temporaries die here)
     double Vf[R][D], Xf[R][D];
     quad_gather_y<R, D>(vcol, Vf);
     quad_gather_y<R, D>(xcol, Xf);
@@ -794,13 +756,10 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     double S2[D][D];
     sym_ytm_cols<R, D>(Xf, h1, S2);
     sub_y_times_col<R, D>(Xf, S2, p.k, h1, hc);  // tangent projection at X
-    double dpart = 0.0;
     if constexpr (MODE == MODE_HESS) {
 #pragma unroll
       for (int a = 0; a < R; ++a) dpart = fma(vcol[a], hc[a], dpart);
-    } else if constexpr (FMT == QFMT_EDGES) {  // the first step's d_Hd by the MODE_QF formula
-      dpart = qf_first_step_dhd<R, B>(q, p.j, p.k, p.ok, vcol, qch, S);
-    } else {  // BSR MODE_QF's: <V, h1>, h1 = VQ - V_Y S
+    } else if constexpr (FMT != QFMT_EDGES) {  // BSR MODE_QF's: <V, h1>, h1 = VQ - V_Y S
 #pragma unroll
       for (int a = 0; a < R; ++a) dpart = fma(vcol[a], h1[a], dpart);
     }
