@@ -93,6 +93,9 @@ def main():
     ap.add_argument("--pmc-calib-mb", type=int, default=0,
                     help="tools/pmc_step.py: one device copy of this many MiB before the timed region (a launch of "
                          "known read/write bytes for the FETCH_SIZE calibration)")
+    ap.add_argument("--precon", default="block_jacobi", choices=["block_jacobi", "exact"],
+                    help="block_jacobi: per-pose (Q_jj + 0.1 I)^-1 (throughput setting, CPU baseline too); exact: the "
+                         "reference's factor of Q + 0.1 I (host Cholesky per agent, GPU triangular solves)")
     ap.add_argument("--robust", default="L2", choices=["L2", "GNC_TLS", "TLS", "Huber", "GM", "L1"],
                     help="robust cost (L2: throughput setting; GNC_TLS: the reference default, "
                          "reweighting every 30 iterations on the device)")
@@ -125,7 +128,8 @@ def main():
     aop = g.grid_partition(A)
     num_agents = A ** 3
     agent_rank = super_cube_ranks(A, world)
-    params = H.rbcd_params(r=args.r, acceleration=args.accel, robust_cost=H.ROBUST[args.robust])
+    params = H.rbcd_params(r=args.r, acceleration=args.accel, robust_cost=H.ROBUST[args.robust],
+                           precon=H.PRECON_EXACT if args.precon == "exact" else H.PRECON_BLOCK_JACOBI)
     eng = H.Rbcd(g, aop, agent_rank, rank, world, params)
     # every engine launch and the exchange run on one dedicated stream (stream order = halo order)
     stream = torch.cuda.Stream(dev)
@@ -202,7 +206,7 @@ def main():
                 Xb = tx.cpu().numpy()
             eng.set_X(Xb)  # PGOAgent::setX: Nesterov restarts from the burnt-in iterate
         X_start = None
-        if rank == 0 and world == 1 and args.cpu_baseline:
+        if rank == 0 and world == 1 and args.cpu_baseline and args.precon == "block_jacobi" and args.robust == "L2":
             X_start = np.zeros(X0.size)
             eng.get_X_into(X_start)
         f_start, gn_start = central()
@@ -308,7 +312,7 @@ def main():
         "config": {"workload": f"grid3d k={args.k} ({args.k ** 3} poses), r={args.r}, "
                                f"{num_agents} agents ({A}^3 sub-cubes), Nesterov={bool(args.accel)}, "
                                f"{args.robust} cost, colour schedule ({eng.num_colors} colours), "
-                               f"RTR 1x10 tCG, block-Jacobi precond, agent status on, {args.init} init, "
+                               f"RTR 1x10 tCG, {args.precon} precond, agent status on, {args.init} init, "
                                f"burn-in {args.burnin} steps",
                    "poses": g.n, "edges": g.m, "agents": num_agents, "parallelism": par},
         "rounds_per_s": args.steps / elapsed,
