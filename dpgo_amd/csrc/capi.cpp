@@ -757,6 +757,7 @@ int dpgo_hip_problem_create_batch(int num_agents, const int* poses_per_agent, in
       h->agent_tile_off.ensure(num_agents + 1) || h->agent_np.ensure(num_agents) ||
       h->enabled.ensure(num_agents) || h->use_a.ensure(num_agents) || h->pa.ensure(static_cast<size_t>(T) * dpgo::kPartialStride) ||
       h->pb.ensure(static_cast<size_t>(T) * dpgo::kPartialStride) || h->pc.ensure(static_cast<size_t>(T) * dpgo::kPartialStride) ||
+      h->peh.ensure(static_cast<size_t>(T) * dpgo::kPartialStride) ||
       h->sums.ensure(static_cast<size_t>(num_agents) * 4) ||
       h->state.ensure(num_agents) || h->coef_a.ensure(num_agents) || h->coef_b.ensure(num_agents) ||
       h->arrive.ensure(num_agents))
@@ -1150,7 +1151,9 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
   // and is recomputed, by the same MODE_EVAL_TCG pass (bitwise the same g), if it is needed.  This
   // only chooses between storing and recomputing identical values: no result depends on it, so an
   // agent's arithmetic does not depend on which other agents share its handle.
-  bool g_valid = !(fused_tcg && single && h->predict_boundary && P.tr_max_inner > 0);
+  // (a first step forced to the full pass reads grad(x1) in that pass already: the merged HESS_QF_M's r_0)
+  bool g_valid = !(fused_tcg && single && h->predict_boundary && P.tr_max_inner > 0 &&
+                   dpgo::g_tuning[dpgo::TUNE_FIRST_STEP] != 2);
   if (fused_tcg) {
     const dpgo::FinalizeArgs fin = make_fin(h, dpgo::OP_EVAL_TCG_INIT, h->pa.p, 3, nullptr, 0, &o, en_dev);
     DPGO_TRY(eval_at(h, x1, g_valid ? h->g.p : nullptr, h->S.p, h->pa.p, dpgo::FLAG_NONE, dpgo::MODE_EVAL_TCG,
@@ -1282,13 +1285,40 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     // learns whether any agent continues (those are retracted, evaluated and tested after their tCG:
     // the *_EXPL launches below).
     const bool spec = qf0 && single && !full0;
+    // Merged tCG iteration (the default with block-Jacobi / no preconditioner): HESS_M, one finalize for
+    // the step test and the stopping test (OP_TCG_STEP_CHECK), then k_tcg_updir -- three launches per
+    // iteration instead of five, no z vector.  The exact preconditioner and TUNE_FUSE_TCG keep the
+    // classic sequence (TUNE_CLASSIC_TCG forces it).
+    const bool merged = qf0 && !fuse_tcg && dpgo::g_tuning[dpgo::TUNE_CLASSIC_TCG] == 0;
+    auto launch_merged = [&](int j, int mode, int flag, int op) -> int {
+      auto ch = make_ctx(h, flag, h->pa.p);
+      const int tag = next_tag(h);
+      tags.push_back(tag);
+      dpgo::SpmmArgs sa{h->delta.p, nullptr, nullptr, x1, h->S.p, h->Hdelta.p, nullptr, h->minv.p, nullptr, pmode};
+      sa.rvec = j == 0 ? h->g.p : h->rv.p;
+      dpgo::OptScalars os = o;
+      os.first_full = mode == dpgo::MODE_HESS_QF_M ? 1 : 0;
+      dpgo::FinalizeArgs fin = make_fin(h, op, h->pa.p, 7, nullptr, 0, &os, nullptr, 1, tag);
+      fin.pc = h->peh.p;
+      fin.nq_c = 1;
+      DPGO_TRY(spmm_then_finalize(h, mode, ch, sa, fin));
+      auto cu = make_ctx(h, dpgo::FLAG_TCG_MODE, h->peh.p);
+      HIP_TRY(dpgo::launch_tcg_updir(r, b, cu, x1, h->minv.p, pmode, h->delta.p, h->Hdelta.p, h->eta.p,
+                                     j == 0 ? h->g.p : h->rv.p, h->rv.p, j == 0 ? 1 : 0,
+                                     j + 1 == P.tr_max_inner ? 1 : 0));
+      return DPGO_HIP_OK;
+    };
     auto launch_candidate = [&](int run_flag, int filter) -> int {
       auto cr = make_ctx(h, run_flag, h->pa.p);
       HIP_TRY(dpgo::launch_retract(r, b, cr, x1, h->eta.p, 1.0, x2, h->g.p, nullptr, h->delta.p));
       // single Run: only f(x2) and |grad(x2)| are consumed (fOpt / gradNormOpt), |grad(x2)| only as a
       // statistic
       const int rtag = next_tag(h);
-      const dpgo::FinalizeArgs fin = make_fin(h, dpgo::OP_RHO, h->pa.p, 2, h->pb.p, 2, &o, nullptr, 2, rtag, filter);
+      dpgo::FinalizeArgs fin = make_fin(h, dpgo::OP_RHO, h->pa.p, 2, h->pb.p, 2, &o, nullptr, 2, rtag, filter);
+      if (merged) {  // the last k_tcg_updir's <eta_old, Hdelta>, folded before the rho test
+        fin.pc = h->peh.p;
+        fin.nq_c = 1;
+      }
       if (single)
         DPGO_TRY(eval_at(h, x2, nullptr, nullptr, h->pb.p, run_flag, stats ? dpgo::MODE_EVAL : dpgo::MODE_F,
                          nullptr, dpgo::PRECON_NONE, &fin));
@@ -1299,7 +1329,43 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     };
     int launched = 0, rtag = 0;
     bool cg_agents = !qf0;  // some agent may still be in tCG after the first step test
-    if (P.tr_max_inner > 0) {
+    if (merged) {
+      // first step: MODE_QF (boundary predicted; CG-step agents then get a HESS_M pass and the stopping
+      // test alone) or the full HESS_QF_M pass; one published status per iteration, one iteration queued
+      // ahead of the status the host waits for
+      if (full0) {
+        DPGO_TRY(launch_merged(0, dpgo::MODE_HESS_QF_M, dpgo::FLAG_TCG, dpgo::OP_TCG_STEP_CHECK));
+      } else {
+        DPGO_TRY(launch_step(dpgo::MODE_QF));
+        if (spec) {
+          rtag = launch_candidate(dpgo::FLAG_RUN_IMPL, 1);
+          if (rtag < 0) return rtag;
+        }
+      }
+      launched = 1;
+      for (int j = 0; j < P.tr_max_inner; ++j) {
+        bool act = false;
+        if (j == 0 && !full0) {
+          DPGO_TRY(wait_published(h, step_tags[0], &act));  // after the QF step test
+          h->predict_boundary = !act;
+          cg_agents = act;
+          if (!act) break;
+          if (!g_valid)  // the CG-step agents' gradient (EVAL_TCG skipped storing it; same pass again)
+            DPGO_TRY(eval_at(h, x1, h->g.p, h->S.p, h->pa.p, dpgo::FLAG_TCG_CG, dpgo::MODE_EVAL_TCG, h->delta.p, pmode));
+          DPGO_TRY(launch_merged(0, dpgo::MODE_HESS_M, dpgo::FLAG_TCG_CG, dpgo::OP_TCG_CHECK_M));
+        }
+        if (launched < P.tr_max_inner) {  // lookahead: iteration j+1 queued while j runs
+          DPGO_TRY(launch_merged(launched, dpgo::MODE_HESS_M, dpgo::FLAG_TCG, dpgo::OP_TCG_STEP_CHECK));
+          ++launched;
+        }
+        DPGO_TRY(wait_published(h, tags[j], &act));  // after iteration j's step and stopping tests
+        if (j == 0 && full0) {
+          h->predict_boundary = !act;
+          cg_agents = act;
+        }
+        if (!act) break;
+      }
+    } else if (P.tr_max_inner > 0) {
       DPGO_TRY(launch_step(full0 ? dpgo::MODE_HESS_QF : qf0 ? dpgo::MODE_QF : dpgo::MODE_HESS));
       if (spec) {
         rtag = launch_candidate(dpgo::FLAG_RUN_IMPL, 1);
@@ -1308,7 +1374,7 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
       if (!qf0) DPGO_TRY(launch_rest(0, false));
       launched = 1;
     }
-    for (int j = 0; j < P.tr_max_inner; ++j) {
+    for (int j = 0; !merged && j < P.tr_max_inner; ++j) {
       bool act = false;
       DPGO_TRY(wait_published(h, step_tags[j], &act));  // after the step test of iteration j
       if (j == 0) {

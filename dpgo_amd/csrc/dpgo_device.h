@@ -40,6 +40,8 @@ struct AgentState {
   int eta_implicit;  // tCG stopped at its first step on the boundary: eta = step delta is not
                      // materialised (k_retract reads delta; g_eta / eta_Heta set by OP_TCG_STEP)
   int ready;         // PGOAgentStatus::readyToTerminate of the last update (OP_STATUS)
+  int eh_pending;    // merged tCG: a k_tcg_updir left <eta_old, Hdelta> partials (FinalizeArgs::pc) that the
+                     // next OP_TCG_STEP_CHECK / OP_RHO folds into eta_Heta with step and d_Hd
   double status_rel_change;  // PGOAgentStatus::relativeChange = |X - XPrev| / sqrt(n) (OP_STATUS)
   // cumulative statistics since the handle was created (never reset; read by dpgo_hip_stats)
   int st_calls;      // optimize calls in which the agent was enabled

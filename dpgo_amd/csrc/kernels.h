@@ -6,15 +6,23 @@
 
 namespace dpgo {
 
-constexpr int kPartialStride = 4;  // doubles of partial sums per tile
+constexpr int kPartialStride = 8;  // doubles of partial sums per tile
+constexpr int kMaxTot = 12;        // quantities one finalize reduces (pa + pb + pc)
 
 // X.Q SpMM epilogues: XQ (V Q), XQ_G (X Q + G), EVAL (g = P_X(XQ+G), S, f / |g|^2 partials),
 // HESS (Riemannian Hessian), F (f partial only), EVAL_TCG (EVAL + tCG start: delta = -P_X(g Minv),
 // partial <z, g>)
 // CERT: V (Q - Lambda(X)) = VQ - [V_Y S | 0] (the certificate matrix, no projection)
+// HESS_M / HESS_QF_M (the merged tCG iteration): HESS / HESS_QF plus the partials the stopping test and
+// beta need as polynomials in alpha (|r|^2, <r,Hd>, |Hd|^2, <z,r>, 2<z,Hd>, <Minv Hd,Hd>, see k_spmm)
 enum SpmmMode { MODE_XQ = 0, MODE_XQ_G = 1, MODE_EVAL = 2, MODE_HESS = 3, MODE_F = 4, MODE_EVAL_TCG = 5, MODE_CERT = 6,
-                MODE_QF = 7, MODE_HESS_QF = 8 };
-constexpr int kSpmmModes = 9;
+                MODE_QF = 7, MODE_HESS_QF = 8, MODE_HESS_M = 9, MODE_HESS_QF_M = 10 };
+constexpr int kSpmmModes = 11;
+__host__ __device__ constexpr bool mode_merged(int m) { return m == MODE_HESS_M || m == MODE_HESS_QF_M; }
+__host__ __device__ constexpr bool mode_hess(int m) {
+  return m == MODE_HESS || m == MODE_HESS_QF || m == MODE_HESS_M || m == MODE_HESS_QF_M;
+}
+__host__ __device__ constexpr bool mode_snap(int m) { return m == MODE_HESS_QF || m == MODE_HESS_QF_M; }
 // Per-agent tile gating: RUN skips agents out of the RTR Run, TCG those whose tCG stopped, TCG_MODE
 // those with no tCG step pending, MOVED those whose single-Run candidate was accepted.
 enum FlagKind { FLAG_NONE = 0, FLAG_RUN = 1, FLAG_TCG = 2, FLAG_TCG_MODE = 3, FLAG_MOVED = 4, FLAG_TCG_CG = 5,
@@ -32,7 +40,9 @@ enum FinalizeOp {
   OP_REL_CHANGE = 6,
   OP_SUM = 7,
   OP_EVAL_TCG_INIT = 8,  // OP_EVAL_INIT then OP_TCG_INIT from one fused pass (f, |g|^2, <z,g>)
-  OP_STATUS = 9          // PGOAgent status: relativeChange = sqrt(|X - XPrev|^2 / n), readyToTerminate
+  OP_STATUS = 9,         // PGOAgent status: relativeChange = sqrt(|X - XPrev|^2 / n), readyToTerminate
+  OP_TCG_STEP_CHECK = 10,  // merged tCG iteration: OP_TCG_STEP then OP_TCG_CHECK from one HESS_M pass
+  OP_TCG_CHECK_M = 11      // OP_TCG_CHECK from a HESS_M pass whose step an earlier (MODE_QF) test decided
 };
 
 // Per-iteration trace (ROPTLIB ITERRESULT, src/QuadraticOptimizer.cpp:82-86): one record of
@@ -103,6 +113,8 @@ struct FinalizeArgs {
   const int* agent_enabled;     // optional [num_agents]
   const double* pa;
   const double* pb;
+  const double* pc;             // third operand (nq_c quantities; the merged tCG's <eta, Hdelta> partials)
+  int nq_c;
   AgentState* state;
   double* out_sums;             // OP_SUM: [num_agents * 4]
   OptScalars opt;
@@ -120,7 +132,7 @@ struct FinalizeArgs {
 // SpMM modes that can run a fused finalize (SpmmArgs::fin_arrive); the others ignore it.
 __host__ __device__ constexpr bool spmm_fusable(int mode) {
   return mode == MODE_EVAL || mode == MODE_EVAL_TCG || mode == MODE_F || mode == MODE_QF || mode == MODE_HESS ||
-         mode == MODE_HESS_QF;
+         mode == MODE_HESS_QF || mode == MODE_HESS_M || mode == MODE_HESS_QF_M;
 }
 
 // Operands of one SpMM launch (unused ones may be null).
@@ -134,7 +146,8 @@ struct SpmmArgs {
   double* S_out;        // S (EVAL)
   const double* Minv;   // block-Jacobi inverses (EVAL_TCG)
   double* delta;        // tCG direction (EVAL_TCG)
-  int pmode;            // PreconMode (EVAL_TCG)
+  int pmode;            // PreconMode (EVAL_TCG, HESS_M)
+  const double* rvec;   // HESS_M: the tCG residual r_j (grad on the first iteration)
   // Fused finalize (null = none): the last block of each agent to arrive runs k_finalize's work for
   // that agent (fin), so no separate k_finalize launch follows the SpMM.  fin_arrive[agent] counts
   // arrivals and is reset to 0 by that last block.
@@ -191,6 +204,8 @@ struct RobustParams {
 // Runtime-selectable kernel variants (A/B tuning in one process; see tools/spmm_ab.py).
 enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH = 2, TUNE_FUSE_TCG = 3,
                TUNE_FIRST_STEP = 4,  // 0: predicted from the previous call, 1: always MODE_QF, 2: always MODE_HESS_QF
+               TUNE_CLASSIC_TCG = 5,  // 1: five launches per tCG iteration (HESS, step test, update, check, dir)
+                                      //    instead of the merged three (HESS_M, step + check, k_tcg_updir)
                TUNE_COUNT = 8 };
 // variant of the edge-stream SpMM used unless TUNE_EDGE_VARIANT overrides it (bit 0: XCD-aware
 // tile remap; v >> 1: minimum waves per SIMD the register allocation must allow, none/4/5/6)
@@ -218,6 +233,12 @@ hipError_t launch_tcg_update(int r, int b, const LaunchCtx& c, const double* X, 
 // update) instead of a separate k_finalize launch; null = read the decision from the state.
 hipError_t launch_tcg_dir(int r, int b, const LaunchCtx& c, const double* z, double* delta,
                           const FinalizeArgs* fin = nullptr, int* arrive = nullptr);
+// Merged tCG iteration (after OP_TCG_STEP_CHECK): eta += step delta with the partial <eta_old, Hdelta>
+// into c.partials slot 0; for agents that continue also r += alpha Hdelta and delta = -Prec(r) + beta delta
+// (z never stored).  first: eta = 0 and r_in = grad; last: no r / delta update (tCG ends at MAXITER).
+hipError_t launch_tcg_updir(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
+                            double* delta, const double* Hdelta, double* eta, const double* r_in, double* rv,
+                            int first, int last);
 hipError_t launch_retract(int r, int b, const LaunchCtx& c, const double* X, const double* V, double scale,
                           double* out, const double* g, const double* HV, const double* delta_impl = nullptr);
 hipError_t launch_tangent(int r, int b, const LaunchCtx& c, const double* X, const double* V, double* out);

@@ -451,7 +451,436 @@ constexpr int evar_waves(int v) { return ((v >> 1) & 3) == 0 ? 1 : 3 + ((v >> 1)
 constexpr bool evar_pre(int v) { return (v & 8) != 0; }
 
 
-__device__ void finalize_agent(const FinalizeArgs& f, int agent);
+// column k of the packed block-Jacobi inverse (row-major b x b)
+template <int B>
+__device__ __forceinline__ void minv_col(const double* __restrict__ Minv, long j, int k, bool ok, double (&mk)[B]) {
+#pragma unroll
+  for (int u = 0; u < B; ++u) mk[u] = ok ? Minv[j * diag_width(B - 1) + minv_index<B>(u, k < B ? k : 0)] : 0.0;
+}
+
+// Column k of z = Prec(v) = P_X(v Minv) from column k of v (the quad holds the pose), Yx = the pose's
+// Y block on every lane (quad_gather_y of X): the EVAL_TCG epilogue's formula.
+template <int R, int B>
+__device__ __forceinline__ void precond_col(const double (&Yx)[R][B - 1], const double* __restrict__ Minv, long j,
+                                            int k, bool ok, int pmode, const double (&vc)[R], double (&zc)[R]) {
+  constexpr int D = B - 1;
+  if (pmode == PRECON_NONE) {
+#pragma unroll
+    for (int a = 0; a < R; ++a) zc[a] = vc[a];
+    return;
+  }
+  double Vf[R][B];
+  quad_gather<R, B>(vc, Vf);
+  double mk[B];
+  minv_col<B>(Minv, j, k, ok, mk);
+  double zq[R];
+#pragma unroll
+  for (int a = 0; a < R; ++a) {
+    double sacc = 0.0;
+#pragma unroll
+    for (int u = 0; u < B; ++u) sacc = fma(Vf[a][u], mk[u], sacc);
+    zq[a] = sacc;
+  }
+  double S3[D][D];
+  sym_ytm_cols<R, D>(Yx, zq, S3);
+  sub_y_times_col<R, D>(Yx, S3, k, zq, zc);
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-agent finalize: reduce tile partials in a fixed order, run the scalar logic of the
+// RTR / tCG state machine (A.4) on device.
+// ------------------------------------------------------------------------------------------
+// Next per-iteration trace record of the agent (zeroed, status -1), or nullptr when tracing is off or
+// the agent's buffer is full (trace_n still counts, so the host sees the overflow).
+__device__ __forceinline__ double* trace_record(const FinalizeArgs& f, int agent, AgentState& s, int op) {
+  if (f.trace == nullptr) return nullptr;
+  const int i = s.trace_n++;
+  if (i >= f.trace_cap) return nullptr;
+  double* t = f.trace + (static_cast<long>(agent) * f.trace_cap + i) * kTraceWidth;
+#pragma unroll
+  for (int q = 0; q < kTraceWidth; ++q) t[q] = 0.0;
+  t[TR_OP] = op;
+  t[TR_STATUS] = -1.0;
+  return t;
+}
+
+// Cumulative statistics at the start of an optimize call (OP_EVAL_INIT / OP_EVAL_TCG_INIT).
+__device__ __forceinline__ void count_call(const FinalizeArgs& f, int agent, AgentState& s) {
+  const bool en = f.agent_enabled ? f.agent_enabled[agent] != 0 : true;
+  if (!en) return;
+  s.st_calls += 1;
+  if (!s.run_active) s.st_early += 1;
+}
+
+// Reduced totals: pa's quantities first, then pb's, and pc's at the fixed slots kPcSlot.. (static register
+// indices in the scalar logic, whatever nq_a / nq_b are).
+constexpr int kPcSlot = kMaxTot - 2;
+__device__ __forceinline__ const double* part_src(const FinalizeArgs& f, int q, int& qq) {
+  if (q < f.nq_a) {
+    qq = q;
+    return f.pa;
+  }
+  if (q < f.nq_a + f.nq_b && q < kPcSlot) {
+    qq = q - f.nq_a;
+    return f.pb;
+  }
+  if (q >= kPcSlot && q - kPcSlot < f.nq_c) {
+    qq = q - kPcSlot;
+    return f.pc;
+  }
+  return nullptr;
+}
+
+// Merged tCG: fold the previous k_tcg_updir's <eta_old, Hdelta> (pc) into <eta, Heta> with that
+// iteration's step and d_Hd -- OP_TCG_CHECK's recurrence, one launch later.
+__device__ __forceinline__ void fold_eta_heta(const FinalizeArgs& f, const double (&tot)[kMaxTot], AgentState& s) {
+  if (!s.eh_pending || f.nq_c < 1) return;
+  s.eh_pending = 0;
+  s.eta_Heta += s.step * (2.0 * tot[kPcSlot] + s.step * s.d_Hd);
+}
+
+// tCG step test (A.4 steps 1-3) on d_Hd = <delta, Hess[delta]>: alpha, the trust-region / negative
+// curvature test, tau.  Shared by OP_TCG_STEP and the merged OP_TCG_STEP_CHECK.
+__device__ __forceinline__ void tcg_step_test(const FinalizeArgs& f, int agent, double d_Hd, AgentState& s) {
+  const OptScalars& o = f.opt;
+  s.d_Hd = d_Hd;
+  const double alpha = s.z_r / d_Hd;
+  const double e_Pe_new = s.e_Pe + 2.0 * alpha * s.e_Pd + alpha * alpha * s.d_Pd;
+  const double D2 = s.Delta * s.Delta;
+  s.alpha = alpha;
+  s.tcg_iters += 1;
+  if (s.tcg_iters == 1 && o.first_full) s.st_first_full += 1;
+  double* tr = trace_record(f, agent, s, OP_TCG_STEP);
+  if (tr) {
+    tr[TR_J] = s.tcg_iters - 1;
+    tr[TR_DHD] = d_Hd;
+    tr[TR_ALPHA] = alpha;
+    tr[TR_DELTA] = s.Delta;
+    tr[TR_RUN] = s.runs;
+    tr[TR_ZR] = s.z_r;           // <z, r> the step uses
+    tr[TR_NORM_R] = s.norm_r0;   // |r_0| of this tCG
+  }
+  if (d_Hd <= 0.0 || e_Pe_new >= D2) {
+    const double tau = (-s.e_Pd + sqrt(s.e_Pd * s.e_Pd + s.d_Pd * (D2 - s.e_Pe))) / s.d_Pd;
+    s.tau = tau;
+    s.step = tau;
+    s.tcg_mode = 1;
+    s.tcg_status = d_Hd <= 0.0 ? TCG_NEGCURVTURE : TCG_EXCREGION;
+    s.tcg_active = 0;
+    if (tr) {
+      tr[TR_TAU] = tau;
+      tr[TR_STATUS] = s.tcg_status;
+    }
+    if (s.tcg_iters == 1) {
+      // first step on the boundary (the common RBCD case): eta = tau delta and Heta = tau Hdelta
+      // stay implicit.  delta = -z, so <g, eta> = -tau <z, g> and <eta, Heta> = tau^2 <delta, Hdelta>
+      // (the same products as the explicit dots up to rounding)
+      s.eta_implicit = 1;
+      s.g_eta = -tau * s.z_r;
+      s.eta_Heta = tau * tau * d_Hd;
+      s.st_implicit += 1;
+    }
+  } else {
+    s.e_Pe = e_Pe_new;
+    s.step = alpha;
+    s.tcg_mode = 0;
+    s.st_cg_steps += 1;
+  }
+}
+
+// tCG stopping test after a CG step (A.4 step 5) on |r_new|^2 and <z_new, r_new>: LCON / SCON exit, or
+// beta and the e_Pd / d_Pd recurrences.  Shared by OP_TCG_CHECK and the merged ops.
+__device__ __forceinline__ void tcg_stop_test(const FinalizeArgs& f, int agent, double norm_r2, double z_r_new,
+                                              AgentState& s) {
+  const OptScalars& o = f.opt;
+  const double norm_r = sqrt(norm_r2);
+  const int j = s.tcg_iters - 1;
+  const double r0t = pow(s.norm_r0, o.theta);
+  double* tr = trace_record(f, agent, s, OP_TCG_CHECK);
+  if (tr) {
+    tr[TR_J] = j;
+    tr[TR_NORM_R] = norm_r;
+    tr[TR_RUN] = s.runs;
+  }
+  if (j >= o.min_inner && norm_r <= s.norm_r0 * fmin(r0t, o.kappa)) {
+    s.tcg_status = o.kappa < r0t ? TCG_LCON : TCG_SCON;
+    s.tcg_active = 0;
+    if (tr) tr[TR_STATUS] = s.tcg_status;
+    return;
+  }
+  const double beta = z_r_new / s.z_r;
+  if (tr) {
+    tr[TR_ZR] = z_r_new;
+    tr[TR_BETA] = beta;
+  }
+  s.beta = beta;
+  s.e_Pd = beta * (s.e_Pd + s.alpha * s.d_Pd);
+  s.d_Pd = z_r_new + beta * beta * s.d_Pd;
+  s.z_r = z_r_new;
+}
+
+// Merged stopping test: |r_{j+1}|^2 and <z_{j+1}, r_{j+1}> as one-step polynomials in alpha over the
+// HESS_M partials of r_j and Hdelta_j (r_{j+1} = r_j + alpha Hd, z_{j+1} = z_j + alpha Prec(Hd)):
+//   tot[1] |r|^2, tot[2] <r,Hd>, tot[3] |Hd|^2, tot[4] <z,r>, tot[5] 2<z,Hd>, tot[6] <Minv Hd, Hd>.
+// The base terms are recomputed from the stored r_j every iteration, so rounding does not accumulate.
+__device__ __forceinline__ void merged_stop_test(const FinalizeArgs& f, int agent, const double (&tot)[kMaxTot],
+                                                 AgentState& s) {
+  s.eh_pending = 1;  // the k_tcg_updir that applies this step leaves <eta_old, Hdelta> in pc
+  if (s.tcg_mode != 0) return;
+  const double a = s.step;
+  const double nr2 = fmax(tot[1] + a * (2.0 * tot[2] + a * tot[3]), 0.0);
+  const double zr_new = tot[4] + a * (tot[5] + a * tot[6]);
+  tcg_stop_test(f, agent, nr2, zr_new, s);
+}
+
+// The RTR / tCG scalar logic of one agent on its reduced partials tot[] (one thread).
+__device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent, const double (&tot)[kMaxTot],
+                                                AgentState& s) {
+  const int nq = f.nq_a + f.nq_b;
+  const OptScalars& o = f.opt;
+  const bool filtered = (f.agent_filter == 1 && !s.eta_implicit) || (f.agent_filter == 2 && s.eta_implicit);
+  switch (filtered ? -1 : f.op) {
+    case OP_EVAL_INIT: {  // after EVAL at the initial iterate
+      s.f1 = tot[0];
+      s.ngf = sqrt(tot[1]);
+      s.f_init = s.f1;
+      s.ngf_init = s.ngf;
+      s.f2 = s.f1;
+      s.ngf2 = s.ngf;
+      s.Delta = o.Delta0;
+      s.Delta_max = o.Delta_max;
+      s.run_active = f.agent_enabled ? (f.agent_enabled[agent] != 0 && !(s.ngf < o.tol)) : !(s.ngf < o.tol);
+      count_call(f, agent, s);
+      s.accepted = 0;
+      s.runs = 0;
+      s.outer_iters = 0;
+      s.gave_up = 0;
+      s.tcg_status = -1;
+      s.tcg_iters = 0;
+      s.tcg_active = 0;
+      s.tcg_mode = 2;
+      s.eta_implicit = 0;
+      s.eh_pending = 0;
+      break;
+    }
+    case OP_EVAL: {
+      s.f1 = tot[0];
+      s.ngf = sqrt(tot[1]);
+      break;
+    }
+    case OP_EVAL_TCG_INIT: {  // OP_EVAL_INIT, then OP_TCG_INIT with <z, g> = tot[2], |r|^2 = |g|^2
+      s.f1 = tot[0];
+      s.ngf = sqrt(tot[1]);
+      s.f_init = s.f1;
+      s.ngf_init = s.ngf;
+      s.f2 = s.f1;
+      s.ngf2 = s.ngf;
+      s.Delta = o.Delta0;
+      s.Delta_max = o.Delta_max;
+      s.run_active = f.agent_enabled ? (f.agent_enabled[agent] != 0 && !(s.ngf < o.tol)) : !(s.ngf < o.tol);
+      count_call(f, agent, s);
+      s.accepted = 0;
+      s.runs = 0;
+      s.outer_iters = 0;
+      s.gave_up = 0;
+      s.tcg_status = -1;
+      s.tcg_iters = 0;
+      s.copy_pending = 0;
+      s.tcg_mode = 2;
+      s.eta_implicit = 0;
+      s.eh_pending = 0;
+      if (!s.run_active) {
+        s.tcg_active = 0;
+        break;
+      }
+      s.z_r = tot[2];
+      s.d_Pd = s.z_r;
+      s.e_Pe = 0.0;
+      s.e_Pd = 0.0;
+      s.norm_r0 = sqrt(tot[1]);
+      s.tcg_active = 1;
+      s.tcg_status = TCG_MAXITER;
+      s.eta_Heta = 0.0;
+      break;
+    }
+    case OP_TCG_INIT: {
+      s.copy_pending = 0;
+      s.eta_implicit = 0;
+      s.eh_pending = 0;
+      if (!s.run_active) {
+        s.tcg_active = 0;
+        s.tcg_mode = 2;
+        break;
+      }
+      s.z_r = tot[0];
+      s.d_Pd = s.z_r;
+      s.e_Pe = 0.0;
+      s.e_Pd = 0.0;
+      s.norm_r0 = sqrt(tot[1]);
+      s.tcg_active = 1;
+      s.tcg_mode = 2;
+      s.tcg_status = TCG_MAXITER;
+      s.tcg_iters = 0;
+      s.eta_Heta = 0.0;
+      break;
+    }
+    case OP_TCG_STEP: {  // after k_spmm<HESS>: tot[0] = <delta, H delta>
+      if (!s.tcg_active) {
+        s.tcg_mode = 2;
+        break;
+      }
+      tcg_step_test(f, agent, tot[0], s);
+      break;
+    }
+    case OP_TCG_CHECK: {  // after k_tcg_update: tot[0] = <z,r>, tot[1] = |r|^2, tot[2] = <eta_old, Hdelta>
+      if (s.tcg_mode == 2 || s.eta_implicit) break;
+      s.eta_Heta += s.step * (2.0 * tot[2] + s.step * s.d_Hd);  // <eta, Heta> after eta += step delta
+      if (s.tcg_mode != 0) break;
+      tcg_stop_test(f, agent, tot[1], tot[0], s);
+      break;
+    }
+    case OP_TCG_STEP_CHECK: {  // merged iteration after k_spmm<HESS_M>: tot[0] = d_Hd, tot[1..6] (merged_stop_test)
+      fold_eta_heta(f, tot, s);
+      if (!s.tcg_active) {
+        s.tcg_mode = 2;
+        break;
+      }
+      s.z_r = tot[4];  // <z_j, r_j> recomputed from the stored r_j (the first: EVAL_TCG's <z, g> again)
+      tcg_step_test(f, agent, tot[0], s);
+      if (s.eta_implicit) break;
+      merged_stop_test(f, agent, tot, s);
+      break;
+    }
+    case OP_TCG_CHECK_M: {  // after k_spmm<HESS_M> over the agents a MODE_QF step test sent on a CG step
+      if (s.tcg_mode != 0 || s.eta_implicit) break;
+      merged_stop_test(f, agent, tot, s);
+      break;
+    }
+    case OP_RHO: {  // pa: <g,eta> ; pb: f(x2), |grad(x2)|^2 (<eta,Heta> carried by OP_TCG_CHECK)
+      fold_eta_heta(f, tot, s);
+      if (!s.run_active) break;
+      s.tcg_active = 0;
+      s.tcg_mode = 2;
+      if (!s.eta_implicit) s.g_eta = tot[0];
+      s.f2 = tot[2];
+      s.ngf2 = sqrt(tot[3]);
+      const double denom = -s.g_eta - 0.5 * s.eta_Heta;
+      s.rho = (s.f1 - s.f2) / denom;
+      s.accepted = s.rho > 0.1 ? 1 : 0;
+      double* tr = trace_record(f, agent, s, OP_RHO);
+      if (tr) {
+        tr[TR_J] = s.outer_iters;
+        tr[TR_F1] = s.f1;
+        tr[TR_F2] = s.f2;
+        tr[TR_RHO] = s.rho;
+        tr[TR_DELTA] = s.Delta;
+        tr[TR_ACCEPTED] = s.accepted;
+        tr[TR_NGF] = s.ngf;
+        tr[TR_STATUS] = s.tcg_status;
+        tr[TR_RUN] = s.runs;
+        tr[TR_ALPHA] = s.tcg_iters;  // inner iterations of this Run
+      }
+      s.st_runs += 1;
+      s.st_tcg_iters += s.tcg_iters;
+#pragma unroll
+      for (int q = 0; q < 5; ++q)  // static indices: the state stays in registers
+        if (s.tcg_status == q) s.st_status[q] += 1;
+      if (s.rho < 0.25) {
+        s.Delta = 0.25 * s.Delta;
+      } else if (s.rho > 0.75 && (s.tcg_status == TCG_EXCREGION || s.tcg_status == TCG_NEGCURVTURE)) {
+        s.Delta = fmin(2.0 * s.Delta, s.Delta_max);
+      }
+      s.outer_iters += 1;
+      s.copy_pending = o.single_run ? 0 : s.accepted;
+      if (o.single_run) {
+        // QuadraticOptimizer::trustRegion Max_Iteration == 1 wrapper (src/QuadraticOptimizer.cpp:92-110)
+        s.runs += 1;
+        if (s.accepted) {
+          s.run_active = 0;
+        } else if (s.runs - 1 > 10) {
+          s.gave_up = 1;
+          s.run_active = 0;
+          s.st_gave_up += 1;
+        } else {
+          const double radius = s.Delta_max / 4.0;
+          s.Delta = radius;
+          s.Delta_max = radius;
+        }
+      } else {
+        if (s.accepted) {
+          s.f1 = s.f2;
+          s.ngf = s.ngf2;
+        }
+        if (s.ngf < o.tol || s.outer_iters >= o.max_iter) s.run_active = 0;
+      }
+      break;
+    }
+    case OP_REL_CHANGE: {
+      s.rel_change = sqrt(tot[0] / static_cast<double>(f.agent_num_poses[agent]));
+      break;
+    }
+    case OP_STATUS: {  // PGOAgent::iterate status (src/PGOAgent.cpp:700-716), tot[0] = |X - XPrev|^2
+      const double rc = sqrt(tot[0] / static_cast<double>(f.agent_num_poses[agent]));
+      const double ratio = f.conv_ratio ? f.conv_ratio[agent] : 1.0;
+      s.status_rel_change = rc;
+      s.ready = (rc > o.rel_tol || ratio < o.min_ratio) ? 0 : 1;
+      break;
+    }
+    case OP_SUM: {
+      f.out_sums[agent * 4 + 0] = tot[0];
+      if (nq > 1) f.out_sums[agent * 4 + 1] = tot[1];
+      if (nq > 2) f.out_sums[agent * 4 + 2] = tot[2];
+      if (nq > 3) f.out_sums[agent * 4 + 3] = tot[3];
+      break;
+    }
+    default:
+      break;
+  }
+  if (f.pub != nullptr) {
+    const int flag = f.pub_kind == 1 ? s.tcg_active : s.run_active;
+    __hip_atomic_store(&f.pub[agent], (f.pub_tag << 1) | (flag ? 1 : 0), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+
+// Both reductions below evaluate the classic 256-wide LDS halving tree over per-thread serial sums
+// (thread t sums tiles t, t + 256, ...; then pairs t, t + w for w = 128 .. 1), so fused and separate
+// finalizes give bitwise the same sums.
+static_assert(kThreads == 256, "the finalize reductions restate a 256-thread reduction tree");
+
+// Fused path (one wave of the last-arriving SpMM block): lane l plays threads l, l + 64, l + 128,
+// l + 192 (the two cross-wave levels in registers) and the six in-wave levels are shuffles (lane t
+// adds lane t + w: the same pairs in the same order).  No LDS and no barrier; the state is read and
+// written in place (a register copy would cost the SpMM ~50 VGPRs and a wave per SIMD of occupancy).
+__device__ __forceinline__ void finalize_agent(const FinalizeArgs& f, int agent) {
+  const int l = static_cast<int>(threadIdx.x) & 63;
+  const int t0 = f.agent_tile_off[agent], t1 = f.agent_tile_off[agent + 1];
+  double tot[kMaxTot];
+#pragma unroll
+  for (int q = 0; q < kMaxTot; ++q) {
+    tot[q] = 0.0;
+    int qq = 0;
+    const double* src = part_src(f, q, qq);
+    if (src == nullptr) continue;
+    double a4[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      double sv = 0.0;
+      for (int t = t0 + l + 64 * v; t < t1; t += kThreads)
+        sv += f.coherent ? __hip_atomic_load(&src[t * kPartialStride + qq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                         : src[t * kPartialStride + qq];
+      a4[v] = sv;
+    }
+    double x = (a4[0] + a4[2]) + (a4[1] + a4[3]);
+#pragma unroll
+    for (int w = 32; w > 0; w >>= 1) x += __shfl_down(x, w, 64);
+    tot[q] = x;
+  }
+  if (l != 0) return;
+  finalize_scalar(f, agent, tot, f.state[agent]);
+}
+
 template <int NQ>
 __device__ void prologue_finalize(const FinalizeArgs& f, int agent, int* arrive, AgentState& sh);
 __device__ void finalize_arrive(const FinalizeArgs& f, int agent, int* arrive, const AgentState& sh);
@@ -502,8 +931,8 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
 
   // epilogue operands issued ahead of the edge loop (edge-stream variant bit 3)
   constexpr bool PRE = FMT == QFMT_EDGES && evar_pre(VAR);
-  constexpr bool PRE_S = PRE && (MODE == MODE_HESS || MODE == MODE_HESS_QF || MODE == MODE_QF || MODE == MODE_CERT);
-  constexpr bool PRE_X = PRE && (MODE == MODE_HESS || MODE == MODE_HESS_QF);
+  constexpr bool PRE_S = PRE && (mode_hess(MODE) || MODE == MODE_QF || MODE == MODE_CERT);
+  constexpr bool PRE_X = PRE && mode_hess(MODE);
   constexpr bool PRE_M = PRE && MODE == MODE_EVAL_TCG;
   double pre_x[R], pre_s[s_width(D)], pre_m[B];
   int pre_slot = -1;
@@ -560,8 +989,8 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     constexpr bool NODIAG = MODE == MODE_QF;
     if (p.ok) {
       const double* s_rec = reinterpret_cast<const double*>(s_rec2);
-      if constexpr (MODE == MODE_HESS || MODE == MODE_HESS_QF) {
-        constexpr bool SNAP = MODE == MODE_HESS_QF;
+      if constexpr (mode_hess(MODE)) {
+        constexpr bool SNAP = mode_snap(MODE);
         if (staged)
           spmm_accumulate_edges_hq<R, B, true, SNAP>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc,
                                                      i0, s_rec, e0, acc, xin, qch);
@@ -729,7 +1158,7 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     }
     double parts[1] = {own ? dpart : 0.0};
     block_partials<1>(parts, c.partials, p.tile, args.fin_mode == 2);
-  } else if constexpr (MODE == MODE_HESS || MODE == MODE_HESS_QF) {
+  } else if constexpr (mode_hess(MODE)) {
     double vcol[R], xcol[R];
 #pragma unroll
     for (int a = 0; a < R; ++a) vcol[a] = xin[a];
@@ -746,7 +1175,7 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
       for (int v = 0; v < D; ++v)
         S[u][v] = PRE_S ? pre_s[sym_index<D>(u, v)] : (p.ok ? S_in[p.j * s_width(D) + sym_index<D>(u, v)] : 0.0);
     double dpart = 0.0;
-    if constexpr (MODE == MODE_HESS_QF && FMT == QFMT_EDGES)  // the first step's d_Hd by the MODE_QF formula
+    if constexpr (mode_snap(MODE) && FMT == QFMT_EDGES)  // the first step's d_Hd by the MODE_QF formula
       dpart = qf_first_step_dhd<R, B>(q, p.j, p.k, p.ok, vcol, qch, S);  // (first: its temporaries die here)
     double Vf[R][D], Xf[R][D];
     quad_gather_y<R, D>(vcol, Vf);
@@ -756,7 +1185,7 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     double S2[D][D];
     sym_ytm_cols<R, D>(Xf, h1, S2);
     sub_y_times_col<R, D>(Xf, S2, p.k, h1, hc);  // tangent projection at X
-    if constexpr (MODE == MODE_HESS) {
+    if constexpr (!mode_snap(MODE)) {
 #pragma unroll
       for (int a = 0; a < R; ++a) dpart = fma(vcol[a], hc[a], dpart);
     } else if constexpr (FMT != QFMT_EDGES) {  // BSR MODE_QF's: <V, h1>, h1 = VQ - V_Y S
@@ -764,11 +1193,55 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
       for (int a = 0; a < R; ++a) dpart = fma(vcol[a], h1[a], dpart);
     }
     store_vec<R>(out, off, own, hc);
-    double parts[1] = {own ? dpart : 0.0};
-    block_partials<1>(parts, c.partials, p.tile, args.fin_mode == 2);
+    if constexpr (mode_merged(MODE)) {
+      // Merged tCG iteration: the stopping test and beta of this iteration are decided with the step
+      // test, before r is updated, from one-step polynomials in alpha (r' = r + alpha Hd, z' = z + alpha
+      // Prec(Hd)): |r|^2, <r,Hd>, |Hd|^2, <z,r>, 2<z,Hd>, <Hd Minv, Hd> (the last two use <Prec(Hd), r> =
+      // <z, Hd> and P_X self-adjoint on the tangent Hd).  z = P_X(r Minv) is formed here and in
+      // k_tcg_updir (precond_col), never stored.
+      double rcol[R], zc[R], mq[R];
+      load_col<R, B>(args.rvec, p.j, p.k, p.ok, rcol);
+      precond_col<R, B>(Xf, args.Minv, p.j, p.k, p.ok, args.pmode, rcol, zc);
+      if (args.pmode == PRECON_NONE) {
+#pragma unroll
+        for (int a = 0; a < R; ++a) mq[a] = hc[a];
+      } else {
+        double mk[B];
+        minv_col<B>(args.Minv, p.j, p.k, p.ok, mk);
+        double Hf[R][B];
+        quad_gather<R, B>(hc, Hf);
+#pragma unroll
+        for (int a = 0; a < R; ++a) {
+          double sacc = 0.0;
+#pragma unroll
+          for (int u = 0; u < B; ++u) sacc = fma(Hf[a][u], mk[u], sacc);
+          mq[a] = sacc;
+        }
+      }
+      double rr = 0.0, rh = 0.0, hh = 0.0, zr = 0.0, zh = 0.0, mh = 0.0;
+#pragma unroll
+      for (int a = 0; a < R; ++a) {
+        rr = fma(rcol[a], rcol[a], rr);
+        rh = fma(rcol[a], hc[a], rh);
+        hh = fma(hc[a], hc[a], hh);
+        zr = fma(zc[a], rcol[a], zr);
+        zh = fma(zc[a], hc[a], zh);
+        mh = fma(mq[a], hc[a], mh);
+      }
+      double parts[7] = {own ? dpart : 0.0, own ? rr : 0.0, own ? rh : 0.0, own ? hh : 0.0,
+                         own ? zr : 0.0,    own ? 2.0 * zh : 0.0, own ? mh : 0.0};
+      block_partials<7>(parts, c.partials, p.tile, args.fin_mode == 2);
+    } else {
+      double parts[1] = {own ? dpart : 0.0};
+      block_partials<1>(parts, c.partials, p.tile, args.fin_mode == 2);
+    }
   }
   if constexpr (spmm_fusable(MODE)) spmm_arrive(args, p.agent);
 }
+
+// Everything below k_spmm except its mode instantiations is compiled once (the TU without
+// DPGO_SPMM_TU); the SpMM modes are instantiated in parallel TUs (kernels.hip -DDPGO_SPMM_TU=1..5).
+#ifndef DPGO_SPMM_TU
 
 // ------------------------------------------------------------------------------------------
 // Block-Jacobi preconditioner applied to a full pose: z = P_X(v (Q_jj + 0.1 I)^-1)
@@ -956,6 +1429,59 @@ __global__ __launch_bounds__(kThreads) void k_tcg_dir(LaunchCtx c, const double*
 #pragma unroll
     for (int a = 0; a < R; ++a) delta[off + a] = fma(beta, delta[off + a], -z[off + a]);
   }
+}
+
+// Merged tCG iteration, after OP_TCG_STEP_CHECK (A.4 steps 4-6 of the classic update / direction pair):
+// eta += step delta with the partial <eta_old, Hdelta> (folded into <eta, Heta> by the next finalize);
+// for agents whose tCG continues r += alpha Hdelta, z = P_X(r Minv) (precond_col, not stored) and
+// delta = -z + beta delta.  first: eta = 0 and r_in = grad; last: tCG ends here (MAXITER), no r / delta.
+template <int R, int B>
+__global__ __launch_bounds__(kThreads) void k_tcg_updir(LaunchCtx c, const double* __restrict__ X,
+                                                        const double* __restrict__ Minv, int pmode,
+                                                        double* __restrict__ delta, const double* __restrict__ Hdelta,
+                                                        double* __restrict__ eta, const double* r_in, double* rv,
+                                                        int first, int last) {
+  const PoseLane p = pose_lane<B>(c);
+  if (tile_skipped(c, p.agent)) return;  // FLAG_TCG_MODE: no step pending
+  const AgentState& st = c.state[p.agent];
+  if (st.eta_implicit) return;  // first-step boundary exit: eta stays implicit (k_retract)
+  const bool own = p.ok && p.k < B;
+  const long off = p.j * (R * B) + p.k * R;
+  const double step = st.step;
+  const bool cont = st.tcg_mode == 0 && st.tcg_active != 0 && !last;
+  double dcol[R], hcol[R], ecol[R];
+  load_col<R, B>(delta, p.j, p.k, p.ok, dcol);
+  load_col<R, B>(Hdelta, p.j, p.k, p.ok, hcol);
+  if (first) {
+#pragma unroll
+    for (int a = 0; a < R; ++a) ecol[a] = 0.0;
+  } else {
+    load_col<R, B>(eta, p.j, p.k, p.ok, ecol);
+  }
+  double eh = 0.0;
+#pragma unroll
+  for (int a = 0; a < R; ++a) eh = fma(ecol[a], hcol[a], eh);
+#pragma unroll
+  for (int a = 0; a < R; ++a) ecol[a] = fma(step, dcol[a], ecol[a]);
+  store_vec<R>(eta, off, own, ecol);
+  if (cont) {  // uniform per agent
+    constexpr int D = B - 1;
+    const double beta = st.beta;
+    double rcol[R], xcol[R];
+    load_col<R, B>(r_in, p.j, p.k, p.ok, rcol);
+    load_col<R, B>(X, p.j, p.k, p.ok, xcol);
+#pragma unroll
+    for (int a = 0; a < R; ++a) rcol[a] = fma(step, hcol[a], rcol[a]);
+    double Yx[R][D], zc[R], dn[R];
+    quad_gather_y<R, D>(xcol, Yx);
+    precond_col<R, B>(Yx, Minv, p.j, p.k, p.ok, pmode, rcol, zc);
+#pragma unroll
+    for (int a = 0; a < R; ++a) dn[a] = fma(beta, dcol[a], -zc[a]);
+    store_vec<R>(rv, off, own, rcol);
+    store_vec<R>(delta, off, own, dn);
+  }
+  double parts[1] = {own ? eh : 0.0};
+  block_partials<1>(parts, c.partials, p.tile);
 }
 
 // x2 = R_x1(scale * eta) (QF retraction, A.2) with partials <g,eta> and, when HV is given, <eta,HV>
@@ -1351,326 +1877,6 @@ __global__ __launch_bounds__(kThreads) void k_accept(LaunchCtx c, const double* 
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// Per-agent finalize: reduce tile partials in a fixed order, run the scalar logic of the
-// RTR / tCG state machine (A.4) on device.
-// ------------------------------------------------------------------------------------------
-// Next per-iteration trace record of the agent (zeroed, status -1), or nullptr when tracing is off or
-// the agent's buffer is full (trace_n still counts, so the host sees the overflow).
-__device__ __forceinline__ double* trace_record(const FinalizeArgs& f, int agent, AgentState& s, int op) {
-  if (f.trace == nullptr) return nullptr;
-  const int i = s.trace_n++;
-  if (i >= f.trace_cap) return nullptr;
-  double* t = f.trace + (static_cast<long>(agent) * f.trace_cap + i) * kTraceWidth;
-#pragma unroll
-  for (int q = 0; q < kTraceWidth; ++q) t[q] = 0.0;
-  t[TR_OP] = op;
-  t[TR_STATUS] = -1.0;
-  return t;
-}
-
-// Cumulative statistics at the start of an optimize call (OP_EVAL_INIT / OP_EVAL_TCG_INIT).
-__device__ __forceinline__ void count_call(const FinalizeArgs& f, int agent, AgentState& s) {
-  const bool en = f.agent_enabled ? f.agent_enabled[agent] != 0 : true;
-  if (!en) return;
-  s.st_calls += 1;
-  if (!s.run_active) s.st_early += 1;
-}
-
-// The RTR / tCG scalar logic of one agent on its reduced partials tot[] (one thread).
-__device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent, const double (&tot)[4],
-                                                AgentState& s) {
-  const int nq = f.nq_a + f.nq_b;
-  const OptScalars& o = f.opt;
-  const bool filtered = (f.agent_filter == 1 && !s.eta_implicit) || (f.agent_filter == 2 && s.eta_implicit);
-  switch (filtered ? -1 : f.op) {
-    case OP_EVAL_INIT: {  // after EVAL at the initial iterate
-      s.f1 = tot[0];
-      s.ngf = sqrt(tot[1]);
-      s.f_init = s.f1;
-      s.ngf_init = s.ngf;
-      s.f2 = s.f1;
-      s.ngf2 = s.ngf;
-      s.Delta = o.Delta0;
-      s.Delta_max = o.Delta_max;
-      s.run_active = f.agent_enabled ? (f.agent_enabled[agent] != 0 && !(s.ngf < o.tol)) : !(s.ngf < o.tol);
-      count_call(f, agent, s);
-      s.accepted = 0;
-      s.runs = 0;
-      s.outer_iters = 0;
-      s.gave_up = 0;
-      s.tcg_status = -1;
-      s.tcg_iters = 0;
-      s.tcg_active = 0;
-      s.tcg_mode = 2;
-      s.eta_implicit = 0;
-      break;
-    }
-    case OP_EVAL: {
-      s.f1 = tot[0];
-      s.ngf = sqrt(tot[1]);
-      break;
-    }
-    case OP_EVAL_TCG_INIT: {  // OP_EVAL_INIT, then OP_TCG_INIT with <z, g> = tot[2], |r|^2 = |g|^2
-      s.f1 = tot[0];
-      s.ngf = sqrt(tot[1]);
-      s.f_init = s.f1;
-      s.ngf_init = s.ngf;
-      s.f2 = s.f1;
-      s.ngf2 = s.ngf;
-      s.Delta = o.Delta0;
-      s.Delta_max = o.Delta_max;
-      s.run_active = f.agent_enabled ? (f.agent_enabled[agent] != 0 && !(s.ngf < o.tol)) : !(s.ngf < o.tol);
-      count_call(f, agent, s);
-      s.accepted = 0;
-      s.runs = 0;
-      s.outer_iters = 0;
-      s.gave_up = 0;
-      s.tcg_status = -1;
-      s.tcg_iters = 0;
-      s.copy_pending = 0;
-      s.tcg_mode = 2;
-      s.eta_implicit = 0;
-      if (!s.run_active) {
-        s.tcg_active = 0;
-        break;
-      }
-      s.z_r = tot[2];
-      s.d_Pd = s.z_r;
-      s.e_Pe = 0.0;
-      s.e_Pd = 0.0;
-      s.norm_r0 = sqrt(tot[1]);
-      s.tcg_active = 1;
-      s.tcg_status = TCG_MAXITER;
-      s.eta_Heta = 0.0;
-      break;
-    }
-    case OP_TCG_INIT: {
-      s.copy_pending = 0;
-      s.eta_implicit = 0;
-      if (!s.run_active) {
-        s.tcg_active = 0;
-        s.tcg_mode = 2;
-        break;
-      }
-      s.z_r = tot[0];
-      s.d_Pd = s.z_r;
-      s.e_Pe = 0.0;
-      s.e_Pd = 0.0;
-      s.norm_r0 = sqrt(tot[1]);
-      s.tcg_active = 1;
-      s.tcg_mode = 2;
-      s.tcg_status = TCG_MAXITER;
-      s.tcg_iters = 0;
-      s.eta_Heta = 0.0;
-      break;
-    }
-    case OP_TCG_STEP: {  // after k_spmm<HESS>: tot[0] = <delta, H delta>
-      if (!s.tcg_active) {
-        s.tcg_mode = 2;
-        break;
-      }
-      const double d_Hd = tot[0];
-      s.d_Hd = d_Hd;
-      const double alpha = s.z_r / d_Hd;
-      const double e_Pe_new = s.e_Pe + 2.0 * alpha * s.e_Pd + alpha * alpha * s.d_Pd;
-      const double D2 = s.Delta * s.Delta;
-      s.alpha = alpha;
-      s.tcg_iters += 1;
-      if (s.tcg_iters == 1 && o.first_full) s.st_first_full += 1;
-      double* tr = trace_record(f, agent, s, OP_TCG_STEP);
-      if (tr) {
-        tr[TR_J] = s.tcg_iters - 1;
-        tr[TR_DHD] = d_Hd;
-        tr[TR_ALPHA] = alpha;
-        tr[TR_DELTA] = s.Delta;
-        tr[TR_RUN] = s.runs;
-        tr[TR_ZR] = s.z_r;           // <z, r> the step uses
-        tr[TR_NORM_R] = s.norm_r0;   // |r_0| of this tCG
-      }
-      if (d_Hd <= 0.0 || e_Pe_new >= D2) {
-        const double tau = (-s.e_Pd + sqrt(s.e_Pd * s.e_Pd + s.d_Pd * (D2 - s.e_Pe))) / s.d_Pd;
-        s.tau = tau;
-        s.step = tau;
-        s.tcg_mode = 1;
-        s.tcg_status = d_Hd <= 0.0 ? TCG_NEGCURVTURE : TCG_EXCREGION;
-        s.tcg_active = 0;
-        if (tr) {
-          tr[TR_TAU] = tau;
-          tr[TR_STATUS] = s.tcg_status;
-        }
-        if (s.tcg_iters == 1) {
-          // first step on the boundary (the common RBCD case): eta = tau delta and Heta = tau Hdelta
-          // stay implicit.  delta = -z, so <g, eta> = -tau <z, g> and <eta, Heta> = tau^2 <delta, Hdelta>
-          // (the same products as the explicit dots up to rounding)
-          s.eta_implicit = 1;
-          s.g_eta = -tau * s.z_r;
-          s.eta_Heta = tau * tau * d_Hd;
-          s.st_implicit += 1;
-        }
-      } else {
-        s.e_Pe = e_Pe_new;
-        s.step = alpha;
-        s.tcg_mode = 0;
-        s.st_cg_steps += 1;
-      }
-      break;
-    }
-    case OP_TCG_CHECK: {  // after k_tcg_update: tot[0] = <z,r>, tot[1] = |r|^2, tot[2] = <eta_old, Hdelta>
-      if (s.tcg_mode == 2 || s.eta_implicit) break;
-      s.eta_Heta += s.step * (2.0 * tot[2] + s.step * s.d_Hd);  // <eta, Heta> after eta += step delta
-      if (s.tcg_mode != 0) break;
-      const double norm_r = sqrt(tot[1]);
-      const int j = s.tcg_iters - 1;
-      const double r0t = pow(s.norm_r0, o.theta);
-      double* tr = trace_record(f, agent, s, OP_TCG_CHECK);
-      if (tr) {
-        tr[TR_J] = j;
-        tr[TR_NORM_R] = norm_r;
-        tr[TR_RUN] = s.runs;
-      }
-      if (j >= o.min_inner && norm_r <= s.norm_r0 * fmin(r0t, o.kappa)) {
-        s.tcg_status = o.kappa < r0t ? TCG_LCON : TCG_SCON;
-        s.tcg_active = 0;
-        if (tr) tr[TR_STATUS] = s.tcg_status;
-        break;
-      }
-      const double z_r_new = tot[0];
-      const double beta = z_r_new / s.z_r;
-      if (tr) {
-        tr[TR_ZR] = z_r_new;
-        tr[TR_BETA] = beta;
-      }
-      s.beta = beta;
-      s.e_Pd = beta * (s.e_Pd + s.alpha * s.d_Pd);
-      s.d_Pd = z_r_new + beta * beta * s.d_Pd;
-      s.z_r = z_r_new;
-      break;
-    }
-    case OP_RHO: {  // pa: <g,eta> ; pb: f(x2), |grad(x2)|^2 (<eta,Heta> carried by OP_TCG_CHECK)
-      if (!s.run_active) break;
-      s.tcg_active = 0;
-      s.tcg_mode = 2;
-      if (!s.eta_implicit) s.g_eta = tot[0];
-      s.f2 = tot[2];
-      s.ngf2 = sqrt(tot[3]);
-      const double denom = -s.g_eta - 0.5 * s.eta_Heta;
-      s.rho = (s.f1 - s.f2) / denom;
-      s.accepted = s.rho > 0.1 ? 1 : 0;
-      double* tr = trace_record(f, agent, s, OP_RHO);
-      if (tr) {
-        tr[TR_J] = s.outer_iters;
-        tr[TR_F1] = s.f1;
-        tr[TR_F2] = s.f2;
-        tr[TR_RHO] = s.rho;
-        tr[TR_DELTA] = s.Delta;
-        tr[TR_ACCEPTED] = s.accepted;
-        tr[TR_NGF] = s.ngf;
-        tr[TR_STATUS] = s.tcg_status;
-        tr[TR_RUN] = s.runs;
-        tr[TR_ALPHA] = s.tcg_iters;  // inner iterations of this Run
-      }
-      s.st_runs += 1;
-      s.st_tcg_iters += s.tcg_iters;
-#pragma unroll
-      for (int q = 0; q < 5; ++q)  // static indices: the state stays in registers
-        if (s.tcg_status == q) s.st_status[q] += 1;
-      if (s.rho < 0.25) {
-        s.Delta = 0.25 * s.Delta;
-      } else if (s.rho > 0.75 && (s.tcg_status == TCG_EXCREGION || s.tcg_status == TCG_NEGCURVTURE)) {
-        s.Delta = fmin(2.0 * s.Delta, s.Delta_max);
-      }
-      s.outer_iters += 1;
-      s.copy_pending = o.single_run ? 0 : s.accepted;
-      if (o.single_run) {
-        // QuadraticOptimizer::trustRegion Max_Iteration == 1 wrapper (src/QuadraticOptimizer.cpp:92-110)
-        s.runs += 1;
-        if (s.accepted) {
-          s.run_active = 0;
-        } else if (s.runs - 1 > 10) {
-          s.gave_up = 1;
-          s.run_active = 0;
-          s.st_gave_up += 1;
-        } else {
-          const double radius = s.Delta_max / 4.0;
-          s.Delta = radius;
-          s.Delta_max = radius;
-        }
-      } else {
-        if (s.accepted) {
-          s.f1 = s.f2;
-          s.ngf = s.ngf2;
-        }
-        if (s.ngf < o.tol || s.outer_iters >= o.max_iter) s.run_active = 0;
-      }
-      break;
-    }
-    case OP_REL_CHANGE: {
-      s.rel_change = sqrt(tot[0] / static_cast<double>(f.agent_num_poses[agent]));
-      break;
-    }
-    case OP_STATUS: {  // PGOAgent::iterate status (src/PGOAgent.cpp:700-716), tot[0] = |X - XPrev|^2
-      const double rc = sqrt(tot[0] / static_cast<double>(f.agent_num_poses[agent]));
-      const double ratio = f.conv_ratio ? f.conv_ratio[agent] : 1.0;
-      s.status_rel_change = rc;
-      s.ready = (rc > o.rel_tol || ratio < o.min_ratio) ? 0 : 1;
-      break;
-    }
-    case OP_SUM: {
-      f.out_sums[agent * 4 + 0] = tot[0];
-      if (nq > 1) f.out_sums[agent * 4 + 1] = tot[1];
-      if (nq > 2) f.out_sums[agent * 4 + 2] = tot[2];
-      if (nq > 3) f.out_sums[agent * 4 + 3] = tot[3];
-      break;
-    }
-    default:
-      break;
-  }
-  if (f.pub != nullptr) {
-    const int flag = f.pub_kind == 1 ? s.tcg_active : s.run_active;
-    __hip_atomic_store(&f.pub[agent], (f.pub_tag << 1) | (flag ? 1 : 0), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
-
-
-// Both reductions below evaluate the classic 256-wide LDS halving tree over per-thread serial sums
-// (thread t sums tiles t, t + 256, ...; then pairs t, t + w for w = 128 .. 1), so fused and separate
-// finalizes give bitwise the same sums.
-static_assert(kThreads == 256, "the finalize reductions restate a 256-thread reduction tree");
-
-// Fused path (one wave of the last-arriving SpMM block): lane l plays threads l, l + 64, l + 128,
-// l + 192 (the two cross-wave levels in registers) and the six in-wave levels are shuffles (lane t
-// adds lane t + w: the same pairs in the same order).  No LDS and no barrier; the state is read and
-// written in place (a register copy would cost the SpMM ~50 VGPRs and a wave per SIMD of occupancy).
-__device__ __forceinline__ void finalize_agent(const FinalizeArgs& f, int agent) {
-  const int l = static_cast<int>(threadIdx.x) & 63;
-  const int t0 = f.agent_tile_off[agent], t1 = f.agent_tile_off[agent + 1];
-  const int nq = f.nq_a + f.nq_b;
-  double tot[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    if (q >= nq) break;
-    const double* src = q < f.nq_a ? f.pa : f.pb;
-    const int qq = q < f.nq_a ? q : q - f.nq_a;
-    double a4[4];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      double sv = 0.0;
-      for (int t = t0 + l + 64 * v; t < t1; t += kThreads)
-        sv += f.coherent ? __hip_atomic_load(&src[t * kPartialStride + qq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                         : src[t * kPartialStride + qq];
-      a4[v] = sv;
-    }
-    double x = (a4[0] + a4[2]) + (a4[1] + a4[3]);
-#pragma unroll
-    for (int w = 32; w > 0; w >>= 1) x += __shfl_down(x, w, 64);
-    tot[q] = x;
-  }
-  if (l != 0) return;
-  finalize_scalar(f, agent, tot, f.state[agent]);
-}
-
 // Separate launch (grid = #agents, block = 256): every thread loads its tiles' partials, the two
 // cross-wave levels go through LDS once for all quantities and the in-wave levels are shuffles; the
 // agent's state is staged in LDS while the partials load and written back after the scalar logic.
@@ -1679,30 +1885,34 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
   const int agent = blockIdx.x;
   const int t0 = f.agent_tile_off[agent], t1 = f.agent_tile_off[agent + 1];
   constexpr int kStateWords = static_cast<int>(sizeof(AgentState) / sizeof(double));
-  __shared__ double red[4][kThreads];
+  __shared__ double red[kMaxTot][kThreads];
   __shared__ AgentState sh_state;
   if (threadIdx.x < kStateWords)
     reinterpret_cast<double*>(&sh_state)[threadIdx.x] = reinterpret_cast<const double*>(&f.state[agent])[threadIdx.x];
-  const int nq = f.nq_a + f.nq_b;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  double acc[kMaxTot];
+  const double* srcs[kMaxTot];
+  int qqs[kMaxTot];
+#pragma unroll
+  for (int q = 0; q < kMaxTot; ++q) {
+    acc[q] = 0.0;
+    srcs[q] = part_src(f, q, qqs[q]);
+  }
   for (int t = t0 + threadIdx.x; t < t1; t += kThreads) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (q >= nq) break;
-      const double* src = q < f.nq_a ? f.pa : f.pb;
-      const int qq = q < f.nq_a ? q : q - f.nq_a;
-      acc[q] += src[t * kPartialStride + qq];
-    }
+    for (int q = 0; q < kMaxTot; ++q)
+      if (srcs[q] != nullptr) acc[q] += srcs[q][t * kPartialStride + qqs[q]];
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) red[q][threadIdx.x] = acc[q];
+  for (int q = 0; q < kMaxTot; ++q)
+    if (srcs[q] != nullptr) red[q][threadIdx.x] = acc[q];
   __syncthreads();
   if (threadIdx.x >= 64) return;
   const int l = threadIdx.x;
-  double tot[4] = {0.0, 0.0, 0.0, 0.0};
+  double tot[kMaxTot];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    if (q >= nq) break;
+  for (int q = 0; q < kMaxTot; ++q) {
+    tot[q] = 0.0;
+    if (srcs[q] == nullptr) continue;
     double v = (red[q][l] + red[q][l + 128]) + (red[q][l + 64] + red[q][l + 192]);
 #pragma unroll
     for (int w = 32; w > 0; w >>= 1) v += __shfl_down(v, w, 64);
@@ -1741,9 +1951,9 @@ __device__ void prologue_finalize(const FinalizeArgs& f, int agent, int* arrive,
   for (int t = t0 + threadIdx.x; t < t1; t += kThreads) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-      const double* src = q < f.nq_a ? f.pa : f.pb;
-      const int qq = q < f.nq_a ? q : q - f.nq_a;
-      acc[q] += src[t * kPartialStride + qq];
+      int qq = 0;
+      const double* src = part_src(f, q, qq);
+      if (src != nullptr) acc[q] += src[t * kPartialStride + qq];
     }
   }
 #pragma unroll
@@ -1751,7 +1961,9 @@ __device__ void prologue_finalize(const FinalizeArgs& f, int agent, int* arrive,
   __syncthreads();
   if (threadIdx.x < 64) {
     const int l = threadIdx.x;
-    double tot[4] = {0.0, 0.0, 0.0, 0.0};
+    double tot[kMaxTot];
+#pragma unroll
+    for (int q = 0; q < kMaxTot; ++q) tot[q] = 0.0;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       double v = (red[q][l] + red[q][l + 128]) + (red[q][l + 64] + red[q][l + 192]);
@@ -2224,6 +2436,8 @@ __global__ __launch_bounds__(kThreads) void k_assemble_G(GEdges e, int nslots, c
   for (int c = 0; c < B; ++c) gblk[static_cast<long>(s) * (R * B) + c * R + a] = L[c];
 }
 
+#endif  // !DPGO_SPMM_TU
+
 // ------------------------------------------------------------------------------------------
 // Host-side launchers with (r, b) dispatch
 // ------------------------------------------------------------------------------------------
@@ -2245,6 +2459,11 @@ __global__ __launch_bounds__(kThreads) void k_assemble_G(GEdges e, int nslots, c
     default: return hipErrorInvalidValue;                  \
   }
 
+// one SpMM mode over every (r, b) and Q format (instantiated in the DPGO_SPMM_TU translation units)
+template <int MODE>
+hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const SpmmArgs& a);
+
+#ifndef DPGO_SPMM_TU
 int g_tuning[TUNE_COUNT] = {0, -1, 1, 0, 0, 0, 0, 0};
 
 bool supported_rb(int r, int b) {
@@ -2252,7 +2471,7 @@ bool supported_rb(int r, int b) {
   if (b == 4) return r >= 3 && r <= 8;
   return false;
 }
-
+#else
 namespace {
 
 template <int MODE, int VAR, int FMT>
@@ -2274,26 +2493,55 @@ hipError_t spmm_variant54(int var, dim3 grid, const LaunchCtx& c, const QView& q
   return hipSuccess;
 }
 
+}  // namespace
+
 template <int MODE>
 hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const SpmmArgs& a) {
   if (q.fmt == QFMT_EDGES) {
-    constexpr bool kPreMode = MODE == MODE_HESS || MODE == MODE_HESS_QF || MODE == MODE_QF || MODE == MODE_EVAL_TCG;
-    if (kPreMode && r == 5 && b == 4 && g_tuning[TUNE_EPI_PREFETCH] > 0 && g_tuning[TUNE_EDGE_VARIANT] < 0)
-    {
-      k_spmm<5, 4, MODE, kEdgeDefaultVariant | 8, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
-      return hipSuccess;
+    constexpr bool kPreMode = mode_hess(MODE) || MODE == MODE_QF || MODE == MODE_EVAL_TCG;
+    if constexpr (kPreMode) {
+      if (r == 5 && b == 4 && g_tuning[TUNE_EPI_PREFETCH] > 0 && g_tuning[TUNE_EDGE_VARIANT] < 0) {
+        k_spmm<5, 4, MODE, kEdgeDefaultVariant | 8, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+        return hipSuccess;
+      }
     }
     const int var = g_tuning[TUNE_EDGE_VARIANT] < 0 ? kEdgeDefaultVariant : g_tuning[TUNE_EDGE_VARIANT];
-    if (MODE == MODE_XQ && r == 5 && b == 4 && var != kEdgeDefaultVariant)
-      return spmm_variant54<QFMT_EDGES>(var, grid, c, q, a);
+    if constexpr (MODE == MODE_XQ) {
+      if (r == 5 && b == 4 && var != kEdgeDefaultVariant) return spmm_variant54<QFMT_EDGES>(var, grid, c, q, a);
+    }
     return spmm_rb<MODE, kEdgeDefaultVariant, QFMT_EDGES>(r, b, grid, c, q, a);
   }
   const int var = g_tuning[TUNE_SPMM_VARIANT];
-  if (MODE == MODE_XQ && r == 5 && b == 4 && var != 0) return spmm_variant54<QFMT_BSR>(var, grid, c, q, a);
+  if constexpr (MODE == MODE_XQ) {
+    if (r == 5 && b == 4 && var != 0) return spmm_variant54<QFMT_BSR>(var, grid, c, q, a);
+  }
   return spmm_rb<MODE, 0, QFMT_BSR>(r, b, grid, c, q, a);
 }
 
-}  // namespace
+#define DPGO_SPMM_INST(M) template hipError_t spmm_mode<M>(int, int, dim3, const LaunchCtx&, const QView&, const SpmmArgs&);
+#if DPGO_SPMM_TU == 1
+DPGO_SPMM_INST(MODE_XQ)
+DPGO_SPMM_INST(MODE_XQ_G)
+#elif DPGO_SPMM_TU == 2
+DPGO_SPMM_INST(MODE_EVAL)
+DPGO_SPMM_INST(MODE_F)
+DPGO_SPMM_INST(MODE_CERT)
+#elif DPGO_SPMM_TU == 3
+DPGO_SPMM_INST(MODE_HESS)
+DPGO_SPMM_INST(MODE_QF)
+#elif DPGO_SPMM_TU == 4
+DPGO_SPMM_INST(MODE_HESS_QF)
+DPGO_SPMM_INST(MODE_EVAL_TCG)
+#elif DPGO_SPMM_TU == 5
+DPGO_SPMM_INST(MODE_HESS_M)
+DPGO_SPMM_INST(MODE_HESS_QF_M)
+#else
+#error "DPGO_SPMM_TU must be 1..5"
+#endif
+#undef DPGO_SPMM_INST
+#endif  // DPGO_SPMM_TU
+
+#ifndef DPGO_SPMM_TU
 
 hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const QView& q, const SpmmArgs& a) {
   if (c.num_tiles == 0) return hipSuccess;
@@ -2309,6 +2557,8 @@ hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const QView& 
     case MODE_CERT: e = spmm_mode<MODE_CERT>(r, b, grid, c, q, a); break;
     case MODE_QF: e = spmm_mode<MODE_QF>(r, b, grid, c, q, a); break;
     case MODE_HESS_QF: e = spmm_mode<MODE_HESS_QF>(r, b, grid, c, q, a); break;
+    case MODE_HESS_M: e = spmm_mode<MODE_HESS_M>(r, b, grid, c, q, a); break;
+    case MODE_HESS_QF_M: e = spmm_mode<MODE_HESS_QF_M>(r, b, grid, c, q, a); break;
     default: break;
   }
   if (e != hipSuccess) return e;
@@ -2343,6 +2593,15 @@ hipError_t launch_tcg_dir(int r, int b, const LaunchCtx& c, const double* z, dou
   } else {
     DPGO_DISPATCH(r, b, (k_tcg_dir<R, B, false><<<c.num_tiles, kThreads, 0, c.stream>>>(c, z, delta, FinalizeArgs{}, nullptr)));
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_tcg_updir(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
+                            double* delta, const double* Hdelta, double* eta, const double* r_in, double* rv,
+                            int first, int last) {
+  if (c.num_tiles == 0) return hipSuccess;
+  DPGO_DISPATCH(r, b, (k_tcg_updir<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, Minv, pmode, delta, Hdelta, eta,
+                                                                                  r_in, rv, first, last)));
   return hipGetLastError();
 }
 
@@ -2701,5 +2960,7 @@ hipError_t launch_bj_inverse(int b, int n, const QView& q, double shift, double*
     return hipErrorInvalidValue;
   return hipGetLastError();
 }
+
+#endif  // !DPGO_SPMM_TU
 
 }  // namespace dpgo

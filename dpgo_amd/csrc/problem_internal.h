@@ -119,6 +119,7 @@ struct dpgo_hip_problem_s {
   // |X_out - X_in|^2 partials of the single-Run output select: each tile written once, in the Run
   // its agent's outcome was decided (an in-place X_in is overwritten by then)
   dpgo::DevBuf<double> pc;
+  dpgo::DevBuf<double> peh;  // merged tCG: k_tcg_updir's <eta_old, Hdelta> partials (FinalizeArgs::pc)
   dpgo::DevBuf<dpgo::AgentState> state;
   std::vector<dpgo::AgentState> h_state;
   // per-agent arrival counts of a k_spmm with a fused finalize (0 between launches)

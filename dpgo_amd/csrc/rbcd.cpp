@@ -871,6 +871,11 @@ int dpgo_rbcd_bytes(dpgo_rbcd e, double* bytes, double* evaltcg_bytes_per_color)
   const double P = pose_bytes(e), b = e->b, d = e->d;
   const double blk = b * b * 8.0 + 4.0, DW = 8.0 * b * (b + 1) / 2, SW = 8.0 * d * (d + 1) / 2;
   double total = e->host_bytes;
+  // the merged tCG iteration (capi.cpp optimize_dev_status): HESS_M also reads r and Minv; k_tcg_updir
+  // replaces the update / direction pair and no z vector is written or read
+  const bool merged = e->P.precon != DPGO_PRECON_EXACT && g_tuning[TUNE_CLASSIC_TCG] == 0 &&
+                      g_tuning[TUNE_FUSE_TCG] <= 0;
+  const double mx = merged ? P + DW : 0.0;  // HESS_M's extra operands per pose
   for (int c = 0; c < e->ncolors; ++c) {
     dpgo_hip_problem h = e->prob[c];
     if (evaltcg_bytes_per_color) evaltcg_bytes_per_color[c] = 0.0;
@@ -893,12 +898,19 @@ int dpgo_rbcd_bytes(dpgo_rbcd e, double* bytes, double* evaltcg_bytes_per_color)
       total += calls * evaltcg;
       // first step test: the each-edge-once pass (QF), or the full pass storing Hess[delta] (HESS_QF,
       // counted as taken by agents that continue with CG steps)
-      total += (runs - full) * (half_in + z.n * SW) + full * (full_in + z.n * (P + SW + P));
-      total += (iters - runs + std::max(0.0, runs - impl - full)) * (full_in + z.n * (P + SW + P));  // HESS
-      // tCG updates: a CG step reads delta, Hdelta, eta, r, X, Minv and writes eta, r, z; a boundary step
-      // reads delta, Hdelta, eta and writes eta (the first step of a tCG reads no eta)
-      total += cg * z.n * (8.0 * P + DW) - runs * z.n * P + (bnd - impl) * z.n * 4.0 * P;
-      total += std::max(0.0, cg - lcon - maxit) * z.n * 3.0 * P;                 // tCG directions
+      total += (runs - full) * (half_in + z.n * SW) + full * (full_in + z.n * (P + SW + P + mx));
+      total += (iters - runs + std::max(0.0, runs - impl - full)) * (full_in + z.n * (P + SW + P + mx));  // HESS
+      if (merged) {
+        // k_tcg_updir: every explicit step reads delta, Hdelta, eta and writes eta (the first reads no eta);
+        // a CG step that continues also reads r, X, Minv and writes r, delta
+        total += (cg + bnd - impl) * z.n * 4.0 * P - runs * z.n * P;
+        total += std::max(0.0, cg - lcon - maxit) * z.n * (4.0 * P + DW);
+      } else {
+        // tCG updates: a CG step reads delta, Hdelta, eta, r, X, Minv and writes eta, r, z; a boundary step
+        // reads delta, Hdelta, eta and writes eta (the first step of a tCG reads no eta)
+        total += cg * z.n * (8.0 * P + DW) - runs * z.n * P + (bnd - impl) * z.n * 4.0 * P;
+        total += std::max(0.0, cg - lcon - maxit) * z.n * 3.0 * P;                 // tCG directions
+      }
       total += runs * z.n * 3.0 * P + (runs - impl) * z.n * 1.0 * P;            // retraction (+ g)
       total += runs * (half_in + gread);                                          // f(x2)
       if (e->P.status) total += calls * z.n * 2.0 * P;                            // status |X - XPrev|
@@ -927,6 +939,8 @@ int dpgo_rbcd_mode_bytes(dpgo_rbcd e, int color, double* out) {
     out[MODE_EVAL_TCG] += full_in + z.n * (SW + DW + P) + gread;
     out[MODE_HESS] += full_in + z.n * (P + SW + P);
     out[MODE_HESS_QF] += full_in + z.n * (P + SW + P);
+    out[MODE_HESS_M] += full_in + z.n * (P + SW + P + P + DW);  // + r, Minv
+    out[MODE_HESS_QF_M] += full_in + z.n * (P + SW + P + P + DW);
     out[MODE_QF] += half_in + z.n * SW;
     out[MODE_F] += half_in + gread;
   }

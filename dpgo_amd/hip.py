@@ -102,7 +102,7 @@ STATS_FIELDS = ["calls", "early", "runs", "tcg_iters", "NEGCURVTURE", "EXCREGION
 TRACE_WIDTH = 16
 TRACE_FIELDS = ["op", "j", "f1", "f2", "rho", "Delta", "alpha", "beta", "tau", "d_Hd", "norm_r", "z_r", "status",
                 "accepted", "ngf", "run"]
-SPMM_MODES = ["XQ", "XQ_G", "EVAL", "HESS", "F", "EVAL_TCG", "CERT", "QF", "HESS_QF"]
+SPMM_MODES = ["XQ", "XQ_G", "EVAL", "HESS", "F", "EVAL_TCG", "CERT", "QF", "HESS_QF", "HESS_M", "HESS_QF_M"]
 
 EXPORTED_SYMBOLS = [s[0] for s in _SIGS]
 

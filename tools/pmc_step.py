@@ -18,7 +18,7 @@ import sqlite3
 import subprocess
 import sys
 
-MODES = ["XQ", "XQ_G", "EVAL", "HESS", "F", "EVAL_TCG", "CERT", "QF", "HESS_QF"]
+MODES = ["XQ", "XQ_G", "EVAL", "HESS", "F", "EVAL_TCG", "CERT", "QF", "HESS_QF", "HESS_M", "HESS_QF_M"]
 CALIB_MB = 512
 
 
