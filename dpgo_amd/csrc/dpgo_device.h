@@ -27,6 +27,7 @@ struct AgentState {
   double norm_r0, alpha, tau, beta, step;
   double g_eta, eta_Heta, rho, rel_change;  // eta_Heta: carried through tCG as a scalar (OP_TCG_CHECK)
   double d_Hd;                              // <delta, Hdelta> of the last step test
+  double r_stop;  // tCG stopping threshold |r_0| min(|r_0|^theta, kappa), set with |r_0|
   int tcg_active;   // tCG still iterating
   int tcg_mode;     // update kernel: 0 CG step (alpha), 1 boundary step (tau) + stop, 2 idle
   int tcg_status;   // 0 NEGCURVTURE 1 EXCREGION 2 LCON 3 SCON 4 MAXITER, -1 none
@@ -40,6 +41,7 @@ struct AgentState {
   int eta_implicit;  // tCG stopped at its first step on the boundary: eta = step delta is not
                      // materialised (k_retract reads delta; g_eta / eta_Heta set by OP_TCG_STEP)
   int ready;         // PGOAgentStatus::readyToTerminate of the last update (OP_STATUS)
+  int r_stop_lcon;   // the threshold's kind: kappa < |r_0|^theta (LCON) or not (SCON)
   int eh_pending;    // merged tCG: a k_tcg_updir left <eta_old, Hdelta> partials (FinalizeArgs::pc) that the
                      // next OP_TCG_STEP_CHECK / OP_RHO folds into eta_Heta with step and d_Hd
   double status_rel_change;  // PGOAgentStatus::relativeChange = |X - XPrev| / sqrt(n) (OP_STATUS)

@@ -7,7 +7,7 @@
 namespace dpgo {
 
 constexpr int kPartialStride = 8;  // doubles of partial sums per tile
-constexpr int kMaxTot = 12;        // quantities one finalize reduces (pa + pb + pc)
+constexpr int kMaxTot = 8;         // quantities one finalize reduces (pa + pb, and pc at the last slot)
 
 // X.Q SpMM epilogues: XQ (V Q), XQ_G (X Q + G), EVAL (g = P_X(XQ+G), S, f / |g|^2 partials),
 // HESS (Riemannian Hessian), F (f partial only), EVAL_TCG (EVAL + tCG start: delta = -P_X(g Minv),

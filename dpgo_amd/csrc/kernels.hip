@@ -514,7 +514,7 @@ __device__ __forceinline__ void count_call(const FinalizeArgs& f, int agent, Age
 
 // Reduced totals: pa's quantities first, then pb's, and pc's at the fixed slots kPcSlot.. (static register
 // indices in the scalar logic, whatever nq_a / nq_b are).
-constexpr int kPcSlot = kMaxTot - 2;
+constexpr int kPcSlot = kMaxTot - 1;
 __device__ __forceinline__ const double* part_src(const FinalizeArgs& f, int q, int& qq) {
   if (q < f.nq_a) {
     qq = q;
@@ -588,6 +588,13 @@ __device__ __forceinline__ void tcg_step_test(const FinalizeArgs& f, int agent, 
   }
 }
 
+// |r_0| min(|r_0|^theta, kappa), the stopping test's threshold, once per tCG (A.4)
+__device__ __forceinline__ void set_r_stop(const OptScalars& o, AgentState& s) {
+  const double r0t = pow(s.norm_r0, o.theta);
+  s.r_stop = s.norm_r0 * fmin(r0t, o.kappa);
+  s.r_stop_lcon = o.kappa < r0t ? 1 : 0;
+}
+
 // tCG stopping test after a CG step (A.4 step 5) on |r_new|^2 and <z_new, r_new>: LCON / SCON exit, or
 // beta and the e_Pd / d_Pd recurrences.  Shared by OP_TCG_CHECK and the merged ops.
 __device__ __forceinline__ void tcg_stop_test(const FinalizeArgs& f, int agent, double norm_r2, double z_r_new,
@@ -595,15 +602,14 @@ __device__ __forceinline__ void tcg_stop_test(const FinalizeArgs& f, int agent, 
   const OptScalars& o = f.opt;
   const double norm_r = sqrt(norm_r2);
   const int j = s.tcg_iters - 1;
-  const double r0t = pow(s.norm_r0, o.theta);
   double* tr = trace_record(f, agent, s, OP_TCG_CHECK);
   if (tr) {
     tr[TR_J] = j;
     tr[TR_NORM_R] = norm_r;
     tr[TR_RUN] = s.runs;
   }
-  if (j >= o.min_inner && norm_r <= s.norm_r0 * fmin(r0t, o.kappa)) {
-    s.tcg_status = o.kappa < r0t ? TCG_LCON : TCG_SCON;
+  if (j >= o.min_inner && norm_r <= s.r_stop) {
+    s.tcg_status = s.r_stop_lcon ? TCG_LCON : TCG_SCON;
     s.tcg_active = 0;
     if (tr) tr[TR_STATUS] = s.tcg_status;
     return;
@@ -698,6 +704,7 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       s.e_Pe = 0.0;
       s.e_Pd = 0.0;
       s.norm_r0 = sqrt(tot[1]);
+      set_r_stop(o, s);
       s.tcg_active = 1;
       s.tcg_status = TCG_MAXITER;
       s.eta_Heta = 0.0;
@@ -717,6 +724,7 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       s.e_Pe = 0.0;
       s.e_Pd = 0.0;
       s.norm_r0 = sqrt(tot[1]);
+      set_r_stop(o, s);
       s.tcg_active = 1;
       s.tcg_mode = 2;
       s.tcg_status = TCG_MAXITER;
@@ -1881,29 +1889,31 @@ __global__ __launch_bounds__(kThreads) void k_accept(LaunchCtx c, const double* 
 // cross-wave levels go through LDS once for all quantities and the in-wave levels are shuffles; the
 // agent's state is staged in LDS while the partials load and written back after the scalar logic.
 static_assert(sizeof(AgentState) % sizeof(double) == 0, "AgentState is staged as doubles");
+template <int NQ>
 __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
+  static_assert(NQ <= kMaxTot, "finalize slots");
   const int agent = blockIdx.x;
   const int t0 = f.agent_tile_off[agent], t1 = f.agent_tile_off[agent + 1];
   constexpr int kStateWords = static_cast<int>(sizeof(AgentState) / sizeof(double));
-  __shared__ double red[kMaxTot][kThreads];
+  __shared__ double red[NQ][kThreads];
   __shared__ AgentState sh_state;
   if (threadIdx.x < kStateWords)
     reinterpret_cast<double*>(&sh_state)[threadIdx.x] = reinterpret_cast<const double*>(&f.state[agent])[threadIdx.x];
-  double acc[kMaxTot];
-  const double* srcs[kMaxTot];
-  int qqs[kMaxTot];
+  double acc[NQ];
+  const double* srcs[NQ];
+  int qqs[NQ];
 #pragma unroll
-  for (int q = 0; q < kMaxTot; ++q) {
+  for (int q = 0; q < NQ; ++q) {
     acc[q] = 0.0;
     srcs[q] = part_src(f, q, qqs[q]);
   }
   for (int t = t0 + threadIdx.x; t < t1; t += kThreads) {
 #pragma unroll
-    for (int q = 0; q < kMaxTot; ++q)
+    for (int q = 0; q < NQ; ++q)
       if (srcs[q] != nullptr) acc[q] += srcs[q][t * kPartialStride + qqs[q]];
   }
 #pragma unroll
-  for (int q = 0; q < kMaxTot; ++q)
+  for (int q = 0; q < NQ; ++q)
     if (srcs[q] != nullptr) red[q][threadIdx.x] = acc[q];
   __syncthreads();
   if (threadIdx.x >= 64) return;
@@ -1912,7 +1922,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
 #pragma unroll
   for (int q = 0; q < kMaxTot; ++q) {
     tot[q] = 0.0;
-    if (srcs[q] == nullptr) continue;
+    if (q >= NQ || srcs[q] == nullptr) continue;
     double v = (red[q][l] + red[q][l + 128]) + (red[q][l + 64] + red[q][l + 192]);
 #pragma unroll
     for (int w = 32; w > 0; w >>= 1) v += __shfl_down(v, w, 64);
@@ -2697,7 +2707,11 @@ hipError_t launch_precond_finish(int r, int b, const LaunchCtx& c, const double*
 
 hipError_t launch_finalize(const FinalizeArgs& f, int num_agents, hipStream_t stream) {
   if (num_agents == 0) return hipSuccess;
-  k_finalize<<<num_agents, kThreads, 0, stream>>>(f);
+  // four slots cover every op but the merged tCG's (seven HESS_M partials) and those carrying pc
+  if (f.nq_c > 0 || f.nq_a + f.nq_b > 4)
+    k_finalize<kMaxTot><<<num_agents, kThreads, 0, stream>>>(f);
+  else
+    k_finalize<4><<<num_agents, kThreads, 0, stream>>>(f);
   return hipGetLastError();
 }
 
