@@ -449,6 +449,8 @@ constexpr bool var_xcd(int v) { return v == 4 || v == 5 || v == 6; }
 constexpr bool evar_xcd(int v) { return (v & 1) != 0; }
 constexpr int evar_waves(int v) { return ((v >> 1) & 3) == 0 ? 1 : 3 + ((v >> 1) & 3); }
 constexpr bool evar_pre(int v) { return (v & 8) != 0; }
+// bit 4: the merged tCG epilogue's operands (r_j, the Minv column) also loaded before the edge loop
+constexpr bool evar_pre_r(int v) { return (v & 16) != 0; }
 
 
 // column k of the packed block-Jacobi inverse (row-major b x b)
@@ -461,8 +463,8 @@ __device__ __forceinline__ void minv_col(const double* __restrict__ Minv, long j
 // Column k of z = Prec(v) = P_X(v Minv) from column k of v (the quad holds the pose), Yx = the pose's
 // Y block on every lane (quad_gather_y of X): the EVAL_TCG epilogue's formula.
 template <int R, int B>
-__device__ __forceinline__ void precond_col(const double (&Yx)[R][B - 1], const double* __restrict__ Minv, long j,
-                                            int k, bool ok, int pmode, const double (&vc)[R], double (&zc)[R]) {
+__device__ __forceinline__ void precond_col_mk(const double (&Yx)[R][B - 1], const double (&mk)[B], int k, int pmode,
+                                               const double (&vc)[R], double (&zc)[R]) {
   constexpr int D = B - 1;
   if (pmode == PRECON_NONE) {
 #pragma unroll
@@ -471,8 +473,6 @@ __device__ __forceinline__ void precond_col(const double (&Yx)[R][B - 1], const 
   }
   double Vf[R][B];
   quad_gather<R, B>(vc, Vf);
-  double mk[B];
-  minv_col<B>(Minv, j, k, ok, mk);
   double zq[R];
 #pragma unroll
   for (int a = 0; a < R; ++a) {
@@ -484,6 +484,14 @@ __device__ __forceinline__ void precond_col(const double (&Yx)[R][B - 1], const 
   double S3[D][D];
   sym_ytm_cols<R, D>(Yx, zq, S3);
   sub_y_times_col<R, D>(Yx, S3, k, zq, zc);
+}
+
+template <int R, int B>
+__device__ __forceinline__ void precond_col(const double (&Yx)[R][B - 1], const double* __restrict__ Minv, long j,
+                                            int k, bool ok, int pmode, const double (&vc)[R], double (&zc)[R]) {
+  double mk[B];
+  if (pmode != PRECON_NONE) minv_col<B>(Minv, j, k, ok, mk);
+  precond_col_mk<R, B>(Yx, mk, k, pmode, vc, zc);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -942,8 +950,13 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
   constexpr bool PRE_S = PRE && (mode_hess(MODE) || MODE == MODE_QF || MODE == MODE_CERT);
   constexpr bool PRE_X = PRE && mode_hess(MODE);
   constexpr bool PRE_M = PRE && MODE == MODE_EVAL_TCG;
-  double pre_x[R], pre_s[s_width(D)], pre_m[B];
+  constexpr bool PRE_R = PRE && mode_merged(MODE) && evar_pre_r(VAR);
+  double pre_x[R], pre_s[s_width(D)], pre_m[B], pre_r[R], pre_mk[B];
   int pre_slot = -1;
+  if constexpr (PRE_R) {
+    load_col<R, B>(args.rvec, p.j, p.k, p.ok, pre_r);
+    if (args.pmode != PRECON_NONE) minv_col<B>(args.Minv, p.j, p.k, p.ok, pre_mk);
+  }
   if constexpr (PRE_X) load_col<R, B>(X, p.j, p.k, p.ok, pre_x);
   if constexpr (PRE_S) {
 #pragma unroll
@@ -1183,8 +1196,10 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
       for (int v = 0; v < D; ++v)
         S[u][v] = PRE_S ? pre_s[sym_index<D>(u, v)] : (p.ok ? S_in[p.j * s_width(D) + sym_index<D>(u, v)] : 0.0);
     double dpart = 0.0;
-    if constexpr (mode_snap(MODE) && FMT == QFMT_EDGES)  // the first step's d_Hd by the MODE_QF formula
+    if constexpr (mode_snap(MODE) && FMT == QFMT_EDGES) {  // the first step's d_Hd by the MODE_QF formula
       dpart = qf_first_step_dhd<R, B>(q, p.j, p.k, p.ok, vcol, qch, S);  // (first: its temporaries die here)
+      __builtin_amdgcn_sched_barrier(0);
+    }
     double Vf[R][D], Xf[R][D];
     quad_gather_y<R, D>(vcol, Vf);
     quad_gather_y<R, D>(xcol, Xf);
@@ -1202,29 +1217,33 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     }
     store_vec<R>(out, off, own, hc);
     if constexpr (mode_merged(MODE)) {
+      // phase fence: the merged operands are loaded only after the Hessian column is out, so the HESS
+      // epilogue's temporaries are dead (otherwise the scheduler hoists these loads above it and HESS_QF_M
+      // needs 210 VGPRs, 2 waves / SIMD)
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
       // Merged tCG iteration: the stopping test and beta of this iteration are decided with the step
       // test, before r is updated, from one-step polynomials in alpha (r' = r + alpha Hd, z' = z + alpha
       // Prec(Hd)): |r|^2, <r,Hd>, |Hd|^2, <z,r>, 2<z,Hd>, <Hd Minv, Hd> (the last two use <Prec(Hd), r> =
       // <z, Hd> and P_X self-adjoint on the tangent Hd).  z = P_X(r Minv) is formed here and in
       // k_tcg_updir (precond_col), never stored.
-      double rcol[R], zc[R], mq[R];
-      load_col<R, B>(args.rvec, p.j, p.k, p.ok, rcol);
-      precond_col<R, B>(Xf, args.Minv, p.j, p.k, p.ok, args.pmode, rcol, zc);
-      if (args.pmode == PRECON_NONE) {
+      double rcol[R], zc[R], mk[B];
+      if constexpr (PRE_R) {
 #pragma unroll
-        for (int a = 0; a < R; ++a) mq[a] = hc[a];
+        for (int a = 0; a < R; ++a) rcol[a] = pre_r[a];
+#pragma unroll
+        for (int u = 0; u < B; ++u) mk[u] = pre_mk[u];
       } else {
-        double mk[B];
-        minv_col<B>(args.Minv, p.j, p.k, p.ok, mk);
-        double Hf[R][B];
-        quad_gather<R, B>(hc, Hf);
+        load_col<R, B>(args.rvec, p.j, p.k, p.ok, rcol);
+        if (args.pmode != PRECON_NONE) minv_col<B>(args.Minv, p.j, p.k, p.ok, mk);
+      }
+      if constexpr (mode_snap(MODE)) {
+        // the first tCG step only (HESS_QF_M): z_0 = -delta_0 exactly (EVAL_TCG formed delta_0 = -Prec(g)
+        // with this formula), so <z_0, r_0> is bitwise EVAL_TCG's <z, g> and no Prec(r) is formed
 #pragma unroll
-        for (int a = 0; a < R; ++a) {
-          double sacc = 0.0;
-#pragma unroll
-          for (int u = 0; u < B; ++u) sacc = fma(Hf[a][u], mk[u], sacc);
-          mq[a] = sacc;
-        }
+        for (int a = 0; a < R; ++a) zc[a] = -vcol[a];
+      } else {
+        precond_col_mk<R, B>(Xf, mk, p.k, args.pmode, rcol, zc);
       }
       double rr = 0.0, rh = 0.0, hh = 0.0, zr = 0.0, zh = 0.0, mh = 0.0;
 #pragma unroll
@@ -1234,7 +1253,40 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
         hh = fma(hc[a], hc[a], hh);
         zr = fma(zc[a], rcol[a], zr);
         zh = fma(zc[a], hc[a], zh);
-        mh = fma(mq[a], hc[a], mh);
+      }
+      if (args.pmode == PRECON_NONE) {
+        mh = hh;
+      } else {
+        // <Hd Minv, Hd> of the pose, column-locally: lane k adds Minv_kk |h_k|^2 and Minv_{k,k^x} <h_k, h_{k^x}>
+        // for x = 1, 2, 3 (each off-diagonal pair once from either lane): one partner column at a time (no
+        // full-pose gather: HESS_QF_M's registers)
+        const int kc = p.k < B ? p.k : 0;
+        const bool act = p.k < B;
+        auto pair = [&](int x, const double (&hp)[R]) {
+          const int pk = p.k ^ x;
+          double m = 0.0;
+#pragma unroll
+          for (int u = 0; u < B; ++u) m = pk == u ? mk[u] : m;  // Minv_{pk, k} = column k's entry pk
+          if (pk >= B || !act) m = 0.0;
+          double t = 0.0;
+#pragma unroll
+          for (int a = 0; a < R; ++a) t = fma(hc[a], hp[a], t);
+          mh = fma(m, t, mh);
+        };
+        double mkk = 0.0;
+#pragma unroll
+        for (int u = 0; u < B; ++u) mkk = kc == u ? mk[u] : mkk;
+        mh = act ? mkk * hh : 0.0;
+        double hp[R];
+#pragma unroll
+        for (int a = 0; a < R; ++a) hp[a] = dpp_f64<0xB1>(hc[a]);  // quad_perm [1,0,3,2]: partner k^1
+        pair(1, hp);
+#pragma unroll
+        for (int a = 0; a < R; ++a) hp[a] = dpp_f64<0x4E>(hc[a]);  // [2,3,0,1]: k^2
+        pair(2, hp);
+#pragma unroll
+        for (int a = 0; a < R; ++a) hp[a] = dpp_f64<0x1B>(hc[a]);  // [3,2,1,0]: k^3
+        pair(3, hp);
       }
       double parts[7] = {own ? dpart : 0.0, own ? rr : 0.0, own ? rh : 0.0, own ? hh : 0.0,
                          own ? zr : 0.0,    own ? 2.0 * zh : 0.0, own ? mh : 0.0};
@@ -2509,6 +2561,16 @@ template <int MODE>
 hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const SpmmArgs& a) {
   if (q.fmt == QFMT_EDGES) {
     constexpr bool kPreMode = mode_hess(MODE) || MODE == MODE_QF || MODE == MODE_EVAL_TCG;
+    if constexpr (mode_merged(MODE)) {
+      const int mp = g_tuning[TUNE_MERGED_PREFETCH];
+      if (r == 5 && b == 4 && g_tuning[TUNE_EPI_PREFETCH] > 0 && g_tuning[TUNE_EDGE_VARIANT] < 0 && mp > 0) {
+        if (mp == 1)
+          k_spmm<5, 4, MODE, kEdgeDefaultVariant | 8 | 16, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+        else
+          k_spmm<5, 4, MODE, kEdgeDefaultVariant | 2 | 8 | 16, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+        return hipSuccess;
+      }
+    }
     if constexpr (kPreMode) {
       if (r == 5 && b == 4 && g_tuning[TUNE_EPI_PREFETCH] > 0 && g_tuning[TUNE_EDGE_VARIANT] < 0) {
         k_spmm<5, 4, MODE, kEdgeDefaultVariant | 8, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
