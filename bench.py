@@ -259,7 +259,8 @@ def main():
     # the SURVEY 8d model over every agent of the colour (both colours' launches averaged)
     mb = [eng.mode_bytes(c) for c in range(eng.num_colors)]
     step_ms = 1e3 * elapsed / args.steps
-    traffic = measured_traffic()
+    # the committed PMC figures are per launch of the 1M-pose, 64-agent, one-GPU workload only
+    traffic = measured_traffic() if (args.k == 100 and A == 4 and world == 1) else None
     per_mode = {}
     for m, v in ktimes.items():
         avg = v[0] / max(v[1], 1)

@@ -206,7 +206,7 @@ enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH =
                TUNE_FIRST_STEP = 4,  // 0: predicted from the previous call, 1: always MODE_QF, 2: always MODE_HESS_QF
                TUNE_CLASSIC_TCG = 5,  // 1: five launches per tCG iteration (HESS, step test, update, check, dir)
                                       //    instead of the merged three (HESS_M, step + check, k_tcg_updir)
-               TUNE_MERGED_PREFETCH = 6,  // HESS_M's r / Minv loaded before the edge loop: 1, with >= 4 waves: 2
+               TUNE_MERGED_PREFETCH = 6,  // HESS_M variants: r / Minv loaded before the edge loop (1; with >= 4 waves: 2); 5-wave register budget (3)
                TUNE_COUNT = 8 };
 // variant of the edge-stream SpMM used unless TUNE_EDGE_VARIANT overrides it (bit 0: XCD-aware
 // tile remap; v >> 1: minimum waves per SIMD the register allocation must allow, none/4/5/6)

@@ -2566,8 +2566,10 @@ hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q
       if (r == 5 && b == 4 && g_tuning[TUNE_EPI_PREFETCH] > 0 && g_tuning[TUNE_EDGE_VARIANT] < 0 && mp > 0) {
         if (mp == 1)
           k_spmm<5, 4, MODE, kEdgeDefaultVariant | 8 | 16, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
-        else
+        else if (mp == 2)
           k_spmm<5, 4, MODE, kEdgeDefaultVariant | 2 | 8 | 16, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+        else  // no prefetch, register budget for 5 waves / SIMD
+          k_spmm<5, 4, MODE, kEdgeDefaultVariant | 4 | 8, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
         return hipSuccess;
       }
     }
