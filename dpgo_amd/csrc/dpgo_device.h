@@ -85,9 +85,34 @@ __device__ __forceinline__ double qsum(double v) {
 }
 
 // deterministic full-wave sum (butterfly); every lane gets the total
+// value of lane l + 32 (lanes 0-31; gfx950 v_permlane32_swap on both halves of the double)
+__device__ __forceinline__ double lane_plus32(double v) {
+  const long long l = __double_as_longlong(v);
+  const int lo = static_cast<int>(l), hi = static_cast<int>(l >> 32);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  return __longlong_as_double((static_cast<long long>(b[1]) << 32) | static_cast<unsigned int>(a[1]));
+}
+// value of lane l + 16 (lanes of rows 0 and 2; v_permlane16_swap)
+__device__ __forceinline__ double lane_plus16(double v) {
+  const long long l = __double_as_longlong(v);
+  const int lo = static_cast<int>(l), hi = static_cast<int>(l >> 32);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __longlong_as_double((static_cast<long long>(b[1]) << 32) | static_cast<unsigned int>(a[1]));
+}
+
+// Sum over the 64 lanes, valid in LANE 0 ONLY: the halving tree lane 0 sees with __shfl_down or
+// __shfl_xor (v_l + v_{l+32}, then + 16, 8, 4, 2, 1) -- the same additions in the same order, so bitwise
+// the same -- from two permlane swaps and four DPP row shifts (row_shl:n, lane l reads l + n) instead of
+// twelve ds_bpermute round trips.
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  v += lane_plus32(v);
+  v += lane_plus16(v);
+  v += dpp_f64<0x108>(v);
+  v += dpp_f64<0x104>(v);
+  v += dpp_f64<0x102>(v);
+  v += dpp_f64<0x101>(v);
   return v;
 }
 

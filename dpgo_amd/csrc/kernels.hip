@@ -889,9 +889,7 @@ __device__ __forceinline__ void finalize_agent(const FinalizeArgs& f, int agent)
       a4[v] = sv;
     }
     double x = (a4[0] + a4[2]) + (a4[1] + a4[3]);
-#pragma unroll
-    for (int w = 32; w > 0; w >>= 1) x += __shfl_down(x, w, 64);
-    tot[q] = x;
+    tot[q] = wave_sum(x);  // lane 0's halving tree
   }
   if (l != 0) return;
   finalize_scalar(f, agent, tot, f.state[agent]);
@@ -1200,11 +1198,15 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
       dpart = qf_first_step_dhd<R, B>(q, p.j, p.k, p.ok, vcol, qch, S);  // (first: its temporaries die here)
       __builtin_amdgcn_sched_barrier(0);
     }
-    double Vf[R][D], Xf[R][D];
-    quad_gather_y<R, D>(vcol, Vf);
-    quad_gather_y<R, D>(xcol, Xf);
     double h1[R], hc[R];
-    sub_y_times_col<R, D>(Vf, S, p.k, qc, h1);  // VQ - V_Y S
+    {
+      double Vf[R][D];
+      quad_gather_y<R, D>(vcol, Vf);
+      sub_y_times_col<R, D>(Vf, S, p.k, qc, h1);  // VQ - V_Y S
+    }
+    __builtin_amdgcn_sched_barrier(0);  // V's gathered rows die before X's are gathered (register peak)
+    double Xf[R][D];
+    quad_gather_y<R, D>(xcol, Xf);
     double S2[D][D];
     sym_ytm_cols<R, D>(Xf, h1, S2);
     sub_y_times_col<R, D>(Xf, S2, p.k, h1, hc);  // tangent projection at X
@@ -1976,9 +1978,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
     tot[q] = 0.0;
     if (q >= NQ || srcs[q] == nullptr) continue;
     double v = (red[q][l] + red[q][l + 128]) + (red[q][l + 64] + red[q][l + 192]);
-#pragma unroll
-    for (int w = 32; w > 0; w >>= 1) v += __shfl_down(v, w, 64);
-    tot[q] = v;
+    tot[q] = wave_sum(v);  // lane 0's halving tree
   }
   if (l != 0) return;
   // the scalar logic runs on a register copy: a chain of dependent LDS accesses costs microseconds
@@ -2029,9 +2029,7 @@ __device__ void prologue_finalize(const FinalizeArgs& f, int agent, int* arrive,
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       double v = (red[q][l] + red[q][l + 128]) + (red[q][l + 64] + red[q][l + 192]);
-#pragma unroll
-      for (int w = 32; w > 0; w >>= 1) v += __shfl_down(v, w, 64);
-      tot[q] = v;
+      tot[q] = wave_sum(v);  // lane 0's halving tree
     }
     if (l == 0) {
       FinalizeArgs g = f;
@@ -2568,8 +2566,10 @@ hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q
           k_spmm<5, 4, MODE, kEdgeDefaultVariant | 8 | 16, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
         else if (mp == 2)
           k_spmm<5, 4, MODE, kEdgeDefaultVariant | 2 | 8 | 16, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
-        else  // no prefetch, register budget for 5 waves / SIMD
+        else if (mp == 3)  // epilogue prefetch, register budget for 5 waves / SIMD
           k_spmm<5, 4, MODE, kEdgeDefaultVariant | 4 | 8, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+        else  // no epilogue prefetch, register budget for 5 waves / SIMD
+          k_spmm<5, 4, MODE, kEdgeDefaultVariant | 4, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
         return hipSuccess;
       }
     }

@@ -1,2 +1,4 @@
 cd $GRAFT_REPO_ROOT && \
-DPGO_BENCH_ONE_DEVICE=1 timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --k 48 --burnin 20 --cpu-baseline 0 > gpurun_out/r02n_bench_2rank_rehearsal.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r02o_gputest.log 2>&1 && \
+timeout -k 10 300 python3 -u tools/step_ab.py --key 5 --values 0 1 --rounds 2 > gpurun_out/r02o_ab.log 2>&1 && \
+timeout -k 10 300 python3 -u tools/step_ab.py --key 5 --values 0 1 --rounds 2 --k 50 --agents-per-axis 2 > gpurun_out/r02o_ab_share.log 2>&1
