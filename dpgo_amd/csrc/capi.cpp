@@ -601,20 +601,22 @@ int download_sums(dpgo_hip_problem h) {
 // launch lookahead the next iteration's status may overwrite this one before the host looks; a
 // later status is at least as recent, so it answers the question too).  Returns whether any
 // agent's flag is set.  Falls back to a stream synchronisation after 20 s (never expected).
-int wait_published(dpgo_hip_problem h, int tag, bool* any) {
+int wait_published(dpgo_hip_problem h, int tag, bool* any, bool* any_cg = nullptr) {
   const auto t0 = std::chrono::steady_clock::now();
   for (long spin = 0;; ++spin) {
-    bool all = true, a = false;
+    bool all = true, a = false, c = false;
     for (int k = 0; k < h->K; ++k) {
       const int v = __atomic_load_n(&h->pub_host[k], __ATOMIC_ACQUIRE);
-      if ((v >> 1) < tag) {
+      if ((v >> 2) < tag) {
         all = false;
         break;
       }
       a |= (v & 1) != 0;
+      c |= (v & 2) != 0;
     }
     if (all) {
       *any = a;
+      if (any_cg) *any_cg = c;
       return DPGO_HIP_OK;
     }
     if ((spin & 1023) == 1023 &&
@@ -626,7 +628,7 @@ int wait_published(dpgo_hip_problem h, int tag, bool* any) {
 }
 
 int next_tag(dpgo_hip_problem h) {
-  if (h->pub_tag >= 0x3FFFFFF0) {  // keep tags monotonic: reset the words once, after draining
+  if (h->pub_tag >= 0x1FFFFFF0) {  // keep tags monotonic: reset the words once, after draining
     (void)hipStreamSynchronize(h->stream);
     std::memset(h->pub_host, 0, sizeof(int) * h->K);
     h->pub_tag = 0;
@@ -1292,15 +1294,15 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     // iteration instead of five, no z vector.  The exact preconditioner and TUNE_FUSE_TCG keep the
     // classic sequence (TUNE_CLASSIC_TCG forces it).
     const bool merged = qf0 && !fuse_tcg && dpgo::g_tuning[dpgo::TUNE_CLASSIC_TCG] == 0;
-    auto launch_merged = [&](int j, int mode, int flag, int op) -> int {
+    auto launch_merged = [&](int j, int mode, int flag, int op, bool publish = true) -> int {
       auto ch = make_ctx(h, flag, h->pa.p);
-      const int tag = next_tag(h);
+      const int tag = publish ? next_tag(h) : 0;
       tags.push_back(tag);
       dpgo::SpmmArgs sa{h->delta.p, nullptr, nullptr, x1, h->S.p, h->Hdelta.p, nullptr, h->minv.p, nullptr, pmode};
       sa.rvec = j == 0 ? h->g.p : h->rv.p;
       dpgo::OptScalars os = o;
       os.first_full = mode == dpgo::MODE_HESS_QF_M ? 1 : 0;
-      dpgo::FinalizeArgs fin = make_fin(h, op, h->pa.p, 7, nullptr, 0, &os, nullptr, 1, tag);
+      dpgo::FinalizeArgs fin = make_fin(h, op, h->pa.p, 7, nullptr, 0, &os, nullptr, publish ? 1 : 0, tag);
       fin.pc = h->peh.p;
       fin.nq_c = 1;
       DPGO_TRY(spmm_then_finalize(h, mode, ch, sa, fin));
@@ -1331,7 +1333,17 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     };
     int launched = 0, rtag = 0;
     bool cg_agents = !qf0;  // some agent may still be in tCG after the first step test
-    if (merged) {
+    // Every iteration queued at once, no status published inside tCG (the CG regime, where tCG runs
+    // to MAXITER or close: agents that stop skip their tiles, an all-stopped iteration costs three
+    // near-empty launches).  Adaptive (default): when the previous call's tCG took CG steps.
+    const int la = dpgo::g_tuning[dpgo::TUNE_TCG_LOOKAHEAD];
+    const bool all_ahead = merged && single && full0 && la != 1 && (la == 2 || !h->predict_boundary);
+    if (all_ahead) {
+      for (int j = 0; j < P.tr_max_inner; ++j)
+        DPGO_TRY(launch_merged(j, j == 0 ? dpgo::MODE_HESS_QF_M : dpgo::MODE_HESS_M, dpgo::FLAG_TCG,
+                               dpgo::OP_TCG_STEP_CHECK, false));
+      cg_agents = true;
+    } else if (merged) {
       // first step: MODE_QF (boundary predicted; CG-step agents then get a HESS_M pass and the stopping
       // test alone) or the full HESS_QF_M pass; one published status per iteration, one iteration queued
       // ahead of the status the host waits for
@@ -1428,8 +1440,9 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
       HIP_TRY(dpgo::launch_select(r, b, cm, X_in, X_in, nullptr, X_in, X_out));
     }
     if (round + 1 < max_rounds) {  // radius-shrink retry / next outer iteration needed?
-      bool any = false;
-      DPGO_TRY(wait_published(h, rtag, &any));
+      bool any = false, any_cg = false;
+      DPGO_TRY(wait_published(h, rtag, &any, &any_cg));
+      if (all_ahead) h->predict_boundary = !any_cg;  // (published by the rho test: no status inside tCG)
       if (!any) break;
     }
   }

@@ -121,7 +121,7 @@ struct FinalizeArgs {
   // zero-copy status publication to host-mapped memory: pub[agent] = (tag << 1) | flag
   int* pub;                     // nullptr = none
   int pub_tag;
-  int pub_kind;                 // 1: tcg_active, 2: run_active
+  int pub_kind;                 // 1: tcg_active, 2: run_active (+ bit 1: the Run's tCG took a CG step)
   int agent_filter;             // 0: every agent; 1 / 2: only agents whose eta is / is not implicit
   int coherent;                 // read the partials with agent-scope loads (fused, SpmmArgs::fin_mode 2)
   const double* conv_ratio;     // OP_STATUS: per-agent converged loop-closure ratio (nullptr = 1)
@@ -206,6 +206,8 @@ enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH =
                TUNE_FIRST_STEP = 4,  // 0: predicted from the previous call, 1: always MODE_QF, 2: always MODE_HESS_QF
                TUNE_CLASSIC_TCG = 5,  // 1: five launches per tCG iteration (HESS, step test, update, check, dir)
                                       //    instead of the merged three (HESS_M, step + check, k_tcg_updir)
+               TUNE_TCG_LOOKAHEAD = 7,  // merged single-Run tCG with the full first pass: 0 adaptive, 1 one
+                                        // iteration queued ahead of a published status, 2 every iteration queued
                TUNE_MERGED_PREFETCH = 6,  // HESS_M variants: r / Minv loaded before the edge loop (1; with >= 4 waves: 2); 5-wave register budget (3)
                TUNE_COUNT = 8 };
 // variant of the edge-stream SpMM used unless TUNE_EDGE_VARIANT overrides it (bit 0: XCD-aware

@@ -853,8 +853,10 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       break;
   }
   if (f.pub != nullptr) {
+    // word = tag << 2 | cg << 1 | flag; cg (rho test only): this Run's tCG took more than one step
     const int flag = f.pub_kind == 1 ? s.tcg_active : s.run_active;
-    __hip_atomic_store(&f.pub[agent], (f.pub_tag << 1) | (flag ? 1 : 0), __ATOMIC_RELAXED,
+    const int cg = f.pub_kind == 2 && s.tcg_iters > 1 ? 2 : 0;
+    __hip_atomic_store(&f.pub[agent], (f.pub_tag << 2) | cg | (flag ? 1 : 0), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
@@ -2062,7 +2064,8 @@ __device__ void finalize_arrive(const FinalizeArgs& f, int agent, int* arrive, c
     reinterpret_cast<double*>(&f.state[agent])[threadIdx.x] = reinterpret_cast<const double*>(&sh)[threadIdx.x];
   if (threadIdx.x == 0 && f.pub != nullptr) {
     const int flag = f.pub_kind == 1 ? sh.tcg_active : sh.run_active;
-    __hip_atomic_store(&f.pub[agent], (f.pub_tag << 1) | (flag ? 1 : 0), __ATOMIC_RELAXED,
+    const int cg = f.pub_kind == 2 && sh.tcg_iters > 1 ? 2 : 0;
+    __hip_atomic_store(&f.pub[agent], (f.pub_tag << 2) | cg | (flag ? 1 : 0), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }

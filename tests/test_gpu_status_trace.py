@@ -369,3 +369,31 @@ def test_merged_tcg_matches_classic(hip):
     assert np.linalg.norm(out[0][0] - out[1][0]) <= 1e-10 * np.linalg.norm(out[0][0])
     assert np.array_equal(out[0][1][:, :12], out[1][1][:, :12])
     assert out[0][1][:, 10].sum() > 0  # CG steps were taken
+
+
+def test_tcg_lookahead_bitwise(hip):
+    """How the host queues the merged tCG (tuning key TUNE_TCG_LOOKAHEAD: 1 = one iteration ahead of a
+    status published by every finalize, 2 = every iteration queued at once with no status inside tCG, 0
+    = adaptive) changes no arithmetic: bitwise the same iterates and counters over 40 engine iterations
+    that mix first-step boundary exits and CG steps."""
+    g = hip.Graph.grid3d(12, seed=5)
+    aop = g.grid_partition(2)
+    X0, _, _ = g.distributed_init(aop, 5, hip.lifting_matrix(3, 5), gpu=True, rtol=1e-12, dev_layout=True)
+    out = []
+    for la in (1, 2, 0):
+        hip.set_tuning(7, la)
+        try:
+            e = hip.Rbcd(g, aop, np.zeros(8, np.int32), 0, 1, hip.rbcd_params(r=5, acceleration=1))
+            e.set_X(X0)
+            for it in range(40):
+                e.pre_exchange(it % e.num_colors)
+                e.update(it % e.num_colors, None)
+            X = np.zeros(X0.size)
+            e.get_X_into(X)
+            out.append((X, e.stats().copy()))
+        finally:
+            hip.set_tuning(7, 0)
+    for other in out[1:]:
+        assert np.array_equal(out[0][0], other[0])
+        assert np.array_equal(out[0][1][:, :12], other[1][:, :12])
+    assert out[0][1][:, 10].sum() > 0  # CG steps were taken
