@@ -71,7 +71,8 @@ dpgo::LaunchCtx make_ctx(dpgo_hip_problem h, int flag_kind, double* partials) {
 namespace {
 
 dpgo::QView qview(dpgo_hip_problem h) {
-  return dpgo::QView{h->rowptr.p, h->col.p, h->blocks.p, h->inc_ptr.p, h->inc.p, h->rec.p, h->diag.p, h->rec_first.p, h->fmt};
+  return dpgo::QView{h->rowptr.p, h->col.p, h->blocks.p, h->inc_ptr.p, h->inc.p, h->rec.p, h->diag.p, h->rec_first.p,
+                     h->sv_ptr.p, h->sv_ids.p, h->inc_sv.p, h->fmt};
 }
 
 int check_handle(dpgo_hip_problem h) {
@@ -234,6 +235,39 @@ int sync_q_edges(dpgo_hip_problem h) {
     int o = 0;
     for (int u = 0; u < b; ++u)
       for (int v = u; v < b; ++v) diag[p * DW + o++] = full[static_cast<size_t>(p) * b * b + v * b + u];
+  }
+  // second-visit staging tables per tile (see QView)
+  {
+    const int T = h->num_tiles;
+    std::vector<int> sv_ptr(T + 1, 0), sv_ids;
+    std::vector<int2> inc_sv(inc.size());
+    std::vector<int> ids;
+    for (int t = 0; t < T; ++t) {
+      const int j0 = h->h_tile_start[t], j1 = j0 + h->h_tile_count[t];
+      const int e0 = lowcnt[j0];
+      ids.clear();
+      for (int z = deg[j0]; z < deg[j1]; ++z)
+        if ((inc[z].x >> 1) < e0) ids.push_back(inc[z].x >> 1);
+      std::sort(ids.begin(), ids.end());
+      ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+      const int ns = static_cast<int>(ids.size());
+      for (int z = deg[j0]; z < deg[j1]; ++z) {
+        const int id = inc[z].x >> 1;
+        const int slot = id < e0 ? static_cast<int>(std::lower_bound(ids.begin(), ids.end(), id) - ids.begin())
+                                 : ns + id - e0;
+        inc_sv[z] = make_int2(2 * slot + (inc[z].x & 1), inc[z].y);
+      }
+      sv_ids.insert(sv_ids.end(), ids.begin(), ids.end());
+      sv_ptr[t + 1] = static_cast<int>(sv_ids.size());
+    }
+    if (sv_ids.empty()) sv_ids.push_back(0);
+    HIP_TRY(h->sv_ptr.ensure(T + 1));
+    HIP_TRY(h->sv_ids.ensure(sv_ids.size()));
+    HIP_TRY(h->inc_sv.ensure(inc_sv.size()));
+    HIP_TRY(hipMemcpyAsync(h->sv_ptr.p, sv_ptr.data(), sizeof(int) * (T + 1), hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipMemcpyAsync(h->sv_ids.p, sv_ids.data(), sizeof(int) * sv_ids.size(), hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipMemcpyAsync(h->inc_sv.p, inc_sv.data(), sizeof(int2) * inc_sv.size(), hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));  // the host vectors above die here
   }
   h->nnz_inc = deg[h->N];
   h->num_edges = m;

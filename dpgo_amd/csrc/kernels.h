@@ -95,6 +95,12 @@ struct QView {
   const double* rec;      // EDGES [m * edge_rec_width(d)]
   const double* diag;     // EDGES [n * diag_width(d)]
   const int* rec_first;   // EDGES [n + 1] first edge id first-visited by pose j (ids in visit order)
+  // EDGES, second-visit staging (tile-indexed): sv_ids[sv_ptr[t] ..] = the ascending ids of the edges tile
+  // t visits second; inc_sv = inc with tile-local record slots (second visits 0 .. ns-1 in that order,
+  // first visit id -> ns + id - rec_first[tile's first pose]), the same ascending order per pose
+  const int* sv_ptr;
+  const int* sv_ids;
+  const int2* inc_sv;
   int fmt;                // QFormat
 };
 
@@ -209,7 +215,8 @@ enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH =
                TUNE_TCG_LOOKAHEAD = 7,  // merged single-Run tCG with the full first pass: 0 adaptive, 1 one
                                         // iteration queued ahead of a published status, 2 every iteration queued
                TUNE_MERGED_PREFETCH = 6,  // HESS_M variants: r / Minv loaded before the edge loop (1; with >= 4 waves: 2); 5-wave register budget (3)
-               TUNE_COUNT = 8 };
+               TUNE_SV_STAGE = 8,  // 1: HESS passes stage the tile's second-visit records in LDS too
+               TUNE_COUNT = 12 };
 // variant of the edge-stream SpMM used unless TUNE_EDGE_VARIANT overrides it (bit 0: XCD-aware
 // tile remap; v >> 1: minimum waves per SIMD the register allocation must allow, none/4/5/6)
 constexpr int kEdgeDefaultVariant = 1;

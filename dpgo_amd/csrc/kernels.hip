@@ -370,23 +370,27 @@ __device__ __forceinline__ void snapshot_half(const double (&acc)[R][B], int k, 
 // forms -- then the other incidences, then the diagonal.  SNAP (MODE_HESS_QF): that first-visit sum
 // is reduce-scattered into qch on the way (bitwise the QF pass's), so one pass gives Hess[V] and the
 // first step's d_Hd; MODE_HESS runs the same order, so both passes give bitwise the same Hess[V].
-template <int R, int B, bool STAGED, bool SNAP>
+// SV (second-visit staging): s_inc holds QView::inc_sv, whose record fields are tile-local LDS slots
+// (second visits 0 .. sv_ns - 1, first visit id -> sv_ns + id - e0), so every incidence reads its record
+// from LDS; the phase boundaries move to slot space and the order of additions is unchanged.
+template <int R, int B, bool STAGED, bool SNAP, bool SV = false>
 __device__ __forceinline__ void spmm_accumulate_edges_hq(const QView& q, const double* __restrict__ in, long j,
                                                          int k, int beg, int end, const int2* s_inc, int i0,
                                                          const double* s_rec, int e0, double (&acc)[R][B],
-                                                         double (&xown)[R], double (&qch)[R]) {
+                                                         double (&xown)[R], double (&qch)[R], int sv_ns = 0) {
   const int kc = k < B ? k : 0;
   const bool act = k < B;
-  const int rf = q.rec_first[j];
+  const int rf = SV ? sv_ns + q.rec_first[j] - e0 : q.rec_first[j];
   int midh = end;
   if constexpr (STAGED) {
+    const int bnd = SV ? sv_ns : e0, rbase = SV ? 0 : e0;
     int mid = beg;  // second visits (ids below the tile's range) | first visits of earlier poses of the tile
-    while (mid < end && (s_inc[mid - i0].x >> 1) < e0) ++mid;
+    while (mid < end && (s_inc[mid - i0].x >> 1) < bnd) ++mid;
     while (midh > mid && (s_inc[midh - 1 - i0].x >> 1) >= rf) --midh;
-    edge_loop<R, B, true, true>(q, in, kc, midh, end, s_inc, i0, s_rec, e0, acc);
+    edge_loop<R, B, true, true>(q, in, kc, midh, end, s_inc, i0, s_rec, rbase, acc);
     if constexpr (SNAP) snapshot_half<R, B>(acc, k, act, qch);
-    edge_loop<R, B, true, false>(q, in, kc, beg, mid, s_inc, i0, s_rec, e0, acc);
-    edge_loop<R, B, true, true>(q, in, kc, mid, midh, s_inc, i0, s_rec, e0, acc);
+    edge_loop<R, B, true, SV>(q, in, kc, beg, mid, s_inc, i0, s_rec, rbase, acc);
+    edge_loop<R, B, true, true>(q, in, kc, mid, midh, s_inc, i0, s_rec, rbase, acc);
   } else {
     while (midh > beg && (q.inc[midh - 1].x >> 1) >= rf) --midh;
     edge_loop<R, B, false, false>(q, in, kc, midh, end, s_inc, i0, s_rec, e0, acc);
@@ -451,6 +455,9 @@ constexpr int evar_waves(int v) { return ((v >> 1) & 3) == 0 ? 1 : 3 + ((v >> 1)
 constexpr bool evar_pre(int v) { return (v & 8) != 0; }
 // bit 4: the merged tCG epilogue's operands (r_j, the Minv column) also loaded before the edge loop
 constexpr bool evar_pre_r(int v) { return (v & 16) != 0; }
+// bit 5: second-visit records staged in LDS with the first visits (QView::sv_*, the HESS passes)
+constexpr bool evar_sv(int v) { return (v & 32) != 0; }
+constexpr int kSvStage = 376;  // records staged per tile with second visits: 3 blocks of ~53 KB LDS per CU
 
 
 // column k of the packed block-Jacobi inverse (row-major b x b)
@@ -989,22 +996,37 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     // as whole 128-byte lines per pose quad: they skip the LDS stage (less LDS, more resident waves).
     constexpr bool HALF = MODE == MODE_F || MODE == MODE_QF;
     constexpr bool STAGE = !HALF || kHalfStaged;
-    constexpr int RW = edge_rec_width(B - 1), NREC = STAGE ? rec_stage<B - 1>() : 2;
+    constexpr bool SVS = STAGE && mode_hess(MODE) && evar_sv(VAR);
+    constexpr int RW = edge_rec_width(B - 1), NREC = SVS ? kSvStage : STAGE ? rec_stage<B - 1>() : 2;
     constexpr int NINC = STAGE ? kIncStage : 2;
     __shared__ int2 s_inc[NINC];
     __shared__ int s_ptr[kTilePoses + 1];
-    __shared__ int s_e[2];
+    __shared__ int s_e[4];
     __shared__ f64x2 s_rec2[NREC * RW / 2];
     const int t0 = c.tile_start[p.tile], cnt = c.tile_count[p.tile];
     if (static_cast<int>(threadIdx.x) <= cnt) s_ptr[threadIdx.x] = q.inc_ptr[t0 + threadIdx.x];
     if (threadIdx.x < 2) s_e[threadIdx.x] = q.rec_first[t0 + (threadIdx.x ? cnt : 0)];
+    if (SVS && threadIdx.x >= 2 && threadIdx.x < 4) s_e[threadIdx.x] = q.sv_ptr[p.tile + threadIdx.x - 2];
     __syncthreads();
     const int i0 = s_ptr[0], ni = s_ptr[cnt] - i0, e0 = s_e[0], ne = s_e[1] - e0;
-    const bool staged = STAGE && ni <= NINC && ne <= NREC;
+    const int sv0 = SVS ? s_e[2] : 0, ns = SVS ? s_e[3] - s_e[2] : 0;
+    const bool staged = STAGE && ni <= NINC && ns + ne <= NREC;
     if (staged) {
-      for (int x = threadIdx.x; x < ni; x += kThreads) s_inc[x] = q.inc[i0 + x];
-      const f64x2* src = reinterpret_cast<const f64x2*>(q.rec) + static_cast<long>(e0) * (RW / 2);
-      for (int x = threadIdx.x; x < ne * (RW / 2); x += kThreads) s_rec2[x] = src[x];
+      if constexpr (SVS) {
+        for (int x = threadIdx.x; x < ni; x += kThreads) s_inc[x] = q.inc_sv[i0 + x];
+        // second-visit records gathered whole (RW / 2 lanes per record, 16-byte loads), first visits after
+        const f64x2* all = reinterpret_cast<const f64x2*>(q.rec);
+        for (int x = threadIdx.x; x < ns * (RW / 2); x += kThreads) {
+          const int rr = x / (RW / 2), w = x - rr * (RW / 2);
+          s_rec2[x] = all[static_cast<long>(q.sv_ids[sv0 + rr]) * (RW / 2) + w];
+        }
+        const f64x2* src = all + static_cast<long>(e0) * (RW / 2);
+        for (int x = threadIdx.x; x < ne * (RW / 2); x += kThreads) s_rec2[ns * (RW / 2) + x] = src[x];
+      } else {
+        for (int x = threadIdx.x; x < ni; x += kThreads) s_inc[x] = q.inc[i0 + x];
+        const f64x2* src = reinterpret_cast<const f64x2*>(q.rec) + static_cast<long>(e0) * (RW / 2);
+        for (int x = threadIdx.x; x < ne * (RW / 2); x += kThreads) s_rec2[x] = src[x];
+      }
     }
     if constexpr (STAGE) __syncthreads();
     constexpr bool NODIAG = MODE == MODE_QF;
@@ -1013,8 +1035,8 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
       if constexpr (mode_hess(MODE)) {
         constexpr bool SNAP = mode_snap(MODE);
         if (staged)
-          spmm_accumulate_edges_hq<R, B, true, SNAP>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc,
-                                                     i0, s_rec, e0, acc, xin, qch);
+          spmm_accumulate_edges_hq<R, B, true, SNAP, SVS>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1],
+                                                          s_inc, i0, s_rec, e0, acc, xin, qch, ns);
         else
           spmm_accumulate_edges_hq<R, B, false, SNAP>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc,
                                                       i0, s_rec, e0, acc, xin, qch);
@@ -2527,7 +2549,7 @@ template <int MODE>
 hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const SpmmArgs& a);
 
 #ifndef DPGO_SPMM_TU
-int g_tuning[TUNE_COUNT] = {0, -1, 1, 0, 0, 0, 0, 0};
+int g_tuning[TUNE_COUNT] = {0, -1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 
 bool supported_rb(int r, int b) {
   if (b == 3) return r >= 2 && r <= 8;
@@ -2562,6 +2584,12 @@ template <int MODE>
 hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const SpmmArgs& a) {
   if (q.fmt == QFMT_EDGES) {
     constexpr bool kPreMode = mode_hess(MODE) || MODE == MODE_QF || MODE == MODE_EVAL_TCG;
+    if constexpr (mode_hess(MODE)) {
+      if (r == 5 && b == 4 && g_tuning[TUNE_SV_STAGE] > 0 && g_tuning[TUNE_EDGE_VARIANT] < 0) {
+        k_spmm<5, 4, MODE, kEdgeDefaultVariant | 8 | 32, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+        return hipSuccess;
+      }
+    }
     if constexpr (mode_merged(MODE)) {
       const int mp = g_tuning[TUNE_MERGED_PREFETCH];
       if (r == 5 && b == 4 && g_tuning[TUNE_EPI_PREFETCH] > 0 && g_tuning[TUNE_EDGE_VARIANT] < 0 && mp > 0) {

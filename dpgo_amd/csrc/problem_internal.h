@@ -87,6 +87,10 @@ struct dpgo_hip_problem_s {
   long nnzb = 0;
   dpgo::DevBuf<int> inc_ptr, rec_first;
   dpgo::DevBuf<int2> inc;
+  // second-visit staging: per tile the sorted ids of its second-visit edges (sv_ptr / sv_ids) and the
+  // incidences with tile-local record slots (inc_sv: second visits 0.., first visits after them)
+  dpgo::DevBuf<int> sv_ptr, sv_ids;
+  dpgo::DevBuf<int2> inc_sv;
   dpgo::DevBuf<double> rec, diag;
   long nnz_inc = 0, num_edges = 0;
   // on-device reweighting (dpgo_hip_set_edge_weights_dev): unweighted measurement per record slot
