@@ -635,22 +635,24 @@ int download_sums(dpgo_hip_problem h) {
 // launch lookahead the next iteration's status may overwrite this one before the host looks; a
 // later status is at least as recent, so it answers the question too).  Returns whether any
 // agent's flag is set.  Falls back to a stream synchronisation after 20 s (never expected).
-int wait_published(dpgo_hip_problem h, int tag, bool* any, bool* any_cg = nullptr) {
+int wait_published(dpgo_hip_problem h, int tag, bool* any, bool* any_cg = nullptr, bool* any_never = nullptr) {
   const auto t0 = std::chrono::steady_clock::now();
   for (long spin = 0;; ++spin) {
-    bool all = true, a = false, c = false;
+    bool all = true, a = false, c = false, nv = false;
     for (int k = 0; k < h->K; ++k) {
       const int v = __atomic_load_n(&h->pub_host[k], __ATOMIC_ACQUIRE);
-      if ((v >> 2) < tag) {
+      if ((v >> 3) < tag) {
         all = false;
         break;
       }
       a |= (v & 1) != 0;
       c |= (v & 2) != 0;
+      nv |= (v & 4) != 0;
     }
     if (all) {
       *any = a;
       if (any_cg) *any_cg = c;
+      if (any_never) *any_never = nv;
       return DPGO_HIP_OK;
     }
     if ((spin & 1023) == 1023 &&
@@ -662,7 +664,7 @@ int wait_published(dpgo_hip_problem h, int tag, bool* any, bool* any_cg = nullpt
 }
 
 int next_tag(dpgo_hip_problem h) {
-  if (h->pub_tag >= 0x1FFFFFF0) {  // keep tags monotonic: reset the words once, after draining
+  if (h->pub_tag >= 0x0FFFFFF0) {  // keep tags monotonic: reset the words once, after draining
     (void)hipStreamSynchronize(h->stream);
     std::memset(h->pub_host, 0, sizeof(int) * h->K);
     h->pub_tag = 0;
@@ -1251,6 +1253,7 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
   const bool stats = results != nullptr || P.verbose;
   const bool direct = single && !stats && X_out != X_in;
   double* x2 = direct ? X_out : h->x2.p;
+  bool status_done = false;  // the status was folded into the last rho test for every agent
   for (int round = 0; round < max_rounds; ++round) {
     // ---- truncated CG (A.4)
     if (round > 0 || !fused_tcg) {
@@ -1323,6 +1326,9 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     // learns whether any agent continues (those are retracted, evaluated and tested after their tCG:
     // the *_EXPL launches below).
     const bool spec = qf0 && single && !full0;
+    // PGOAgent status folded into the retraction + rho test of a single Run (no k_sqdiff / OP_STATUS pass);
+    // agents that never ran this call (|grad| < tol) are the separate pass's, run only when some did
+    const bool status_fold = st != nullptr && single && dpgo::g_tuning[dpgo::TUNE_STATUS_PASS] == 0;
     // Merged tCG iteration (the default with block-Jacobi / no preconditioner): HESS_M, one finalize for
     // the step test and the stopping test (OP_TCG_STEP_CHECK), then k_tcg_updir -- three launches per
     // iteration instead of five, no z vector.  The exact preconditioner and TUNE_FUSE_TCG keep the
@@ -1348,11 +1354,20 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     };
     auto launch_candidate = [&](int run_flag, int filter) -> int {
       auto cr = make_ctx(h, run_flag, h->pa.p);
-      HIP_TRY(dpgo::launch_retract(r, b, cr, x1, h->eta.p, 1.0, x2, h->g.p, nullptr, h->delta.p));
+      HIP_TRY(dpgo::launch_retract(r, b, cr, x1, h->eta.p, 1.0, x2, h->g.p, nullptr, h->delta.p,
+                                   status_fold ? st->ref : nullptr));
       // single Run: only f(x2) and |grad(x2)| are consumed (fOpt / gradNormOpt), |grad(x2)| only as a
       // statistic
       const int rtag = next_tag(h);
-      dpgo::FinalizeArgs fin = make_fin(h, dpgo::OP_RHO, h->pa.p, 2, h->pb.p, 2, &o, nullptr, 2, rtag, filter);
+      dpgo::OptScalars orho = o;
+      if (status_fold) {
+        orho.status_fold = 1;
+        orho.rel_tol = st->rel_tol;
+        orho.min_ratio = st->min_ratio;
+      }
+      dpgo::FinalizeArgs fin = make_fin(h, dpgo::OP_RHO, h->pa.p, status_fold ? 4 : 2, h->pb.p, 2, &orho, nullptr, 2,
+                                        rtag, filter);
+      if (status_fold) fin.conv_ratio = st->conv_ratio;
       if (merged) {  // the last k_tcg_updir's <eta_old, Hdelta>, folded before the rho test
         fin.pc = h->peh.p;
         fin.nq_c = 1;
@@ -1474,8 +1489,9 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
       HIP_TRY(dpgo::launch_select(r, b, cm, X_in, X_in, nullptr, X_in, X_out));
     }
     if (round + 1 < max_rounds) {  // radius-shrink retry / next outer iteration needed?
-      bool any = false, any_cg = false;
-      DPGO_TRY(wait_published(h, rtag, &any, &any_cg));
+      bool any = false, any_cg = false, any_never = false;
+      DPGO_TRY(wait_published(h, rtag, &any, &any_cg, &any_never));
+      status_done = status_fold && !any_never && !any;
       if (all_ahead) h->predict_boundary = !any_cg;  // (published by the rho test: no status inside tCG)
       if (!any) break;
     }
@@ -1489,7 +1505,7 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
   const bool want = results != nullptr || P.verbose;
   // QuadraticOptimizer relativeChange against the input (the output select's partials, ref X_in)
   if (want) DPGO_TRY(finalize(h, dpgo::OP_REL_CHANGE, h->pc.p, 1, nullptr, 0));
-  if (st) {
+  if (st && !status_done) {
     // the output select left |X_out - X_in|^2 in pc: reuse it when the status reference is X_in
     // itself (an in-place update without acceleration)
     const bool reuse = st->ref == X_in && !direct;

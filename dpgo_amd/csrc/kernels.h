@@ -109,6 +109,8 @@ struct OptScalars {
   double rel_tol, min_ratio;  // OP_STATUS: PGOAgentParameters relChangeTol, robustOptMinConvergenceRatio
   int min_inner, max_iter, single_run;
   int first_full;  // OP_TCG_STEP of a first step measured by MODE_HESS_QF (statistics only)
+  int status_fold;  // OP_RHO of a single Run also sets the PGOAgent status of the agents it decides from
+                    // k_retract's |x2 - ref|^2 / |x1 - ref|^2 partials (pa slots 2, 3)
 };
 
 struct FinalizeArgs {
@@ -127,7 +129,8 @@ struct FinalizeArgs {
   // zero-copy status publication to host-mapped memory: pub[agent] = (tag << 1) | flag
   int* pub;                     // nullptr = none
   int pub_tag;
-  int pub_kind;                 // 1: tcg_active, 2: run_active (+ bit 1: the Run's tCG took a CG step)
+  int pub_kind;                 // 1: tcg_active, 2: run_active (+ bit 1: the Run's tCG took a CG step, bit 2:
+                                // the agent never ran in this call)
   int agent_filter;             // 0: every agent; 1 / 2: only agents whose eta is / is not implicit
   int coherent;                 // read the partials with agent-scope loads (fused, SpmmArgs::fin_mode 2)
   const double* conv_ratio;     // OP_STATUS: per-agent converged loop-closure ratio (nullptr = 1)
@@ -216,6 +219,7 @@ enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH =
                                         // iteration queued ahead of a published status, 2 every iteration queued
                TUNE_MERGED_PREFETCH = 6,  // HESS_M variants: r / Minv loaded before the edge loop (1; with >= 4 waves: 2); 5-wave register budget (3)
                TUNE_SV_STAGE = 8,  // 1: HESS passes stage the tile's second-visit records in LDS too
+               TUNE_STATUS_PASS = 9,  // 1: the agent status by its own pass (k_sqdiff + OP_STATUS), not folded
                TUNE_COUNT = 12 };
 // variant of the edge-stream SpMM used unless TUNE_EDGE_VARIANT overrides it (bit 0: XCD-aware
 // tile remap; v >> 1: minimum waves per SIMD the register allocation must allow, none/4/5/6)
@@ -249,8 +253,11 @@ hipError_t launch_tcg_dir(int r, int b, const LaunchCtx& c, const double* z, dou
 hipError_t launch_tcg_updir(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
                             double* delta, const double* Hdelta, double* eta, const double* r_in, double* rv,
                             int first, int last);
+// status_ref (optional, with g): also the partials |out - ref|^2 and |X - ref|^2 (slots 2, 3) for the status
+// folded into the rho test (OptScalars::status_fold)
 hipError_t launch_retract(int r, int b, const LaunchCtx& c, const double* X, const double* V, double scale,
-                          double* out, const double* g, const double* HV, const double* delta_impl = nullptr);
+                          double* out, const double* g, const double* HV, const double* delta_impl = nullptr,
+                          const double* status_ref = nullptr);
 hipError_t launch_tangent(int r, int b, const LaunchCtx& c, const double* X, const double* V, double* out);
 hipError_t launch_precond(int r, int b, const LaunchCtx& c, const double* X, const double* Minv, int pmode,
                           const double* V, double* out);

@@ -654,6 +654,16 @@ __device__ __forceinline__ void merged_stop_test(const FinalizeArgs& f, int agen
   tcg_stop_test(f, agent, nr2, zr_new, s);
 }
 
+// PGOAgentStatus after an update (src/PGOAgent.cpp:700-716): relativeChange = sqrt(|X - XPrev|^2 / n),
+// readyToTerminate with GNC's converged-loop-closure ratio
+__device__ __forceinline__ void set_status(const FinalizeArgs& f, int agent, double d2, AgentState& s) {
+  const OptScalars& o = f.opt;
+  const double rc = sqrt(d2 / static_cast<double>(f.agent_num_poses[agent]));
+  const double ratio = f.conv_ratio ? f.conv_ratio[agent] : 1.0;
+  s.status_rel_change = rc;
+  s.ready = (rc > o.rel_tol || ratio < o.min_ratio) ? 0 : 1;
+}
+
 // The RTR / tCG scalar logic of one agent on its reduced partials tot[] (one thread).
 __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent, const double (&tot)[kMaxTot],
                                                 AgentState& s) {
@@ -779,14 +789,15 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       merged_stop_test(f, agent, tot, s);
       break;
     }
-    case OP_RHO: {  // pa: <g,eta> ; pb: f(x2), |grad(x2)|^2 (<eta,Heta> carried by OP_TCG_CHECK)
+    case OP_RHO: {  // pa: <g,eta> [, <eta,HV>, |x2 - ref|^2, |x1 - ref|^2]; pb: f(x2), |grad(x2)|^2
       fold_eta_heta(f, tot, s);
       if (!s.run_active) break;
+      const bool sfold = o.status_fold && f.nq_a == 4;  // pa carries the status partials (slots 2, 3)
       s.tcg_active = 0;
       s.tcg_mode = 2;
       if (!s.eta_implicit) s.g_eta = tot[0];
-      s.f2 = tot[2];
-      s.ngf2 = sqrt(tot[3]);
+      s.f2 = sfold ? tot[4] : tot[2];
+      s.ngf2 = sqrt(sfold ? tot[5] : tot[3]);
       const double denom = -s.g_eta - 0.5 * s.eta_Heta;
       s.rho = (s.f1 - s.f2) / denom;
       s.accepted = s.rho > 0.1 ? 1 : 0;
@@ -829,6 +840,9 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
           s.Delta = radius;
           s.Delta_max = radius;
         }
+        // the output is decided (accepted -> x2, gave up -> the input): its status from the retraction's
+        // partials (a retry Run decides later)
+        if (sfold && !s.run_active) set_status(f, agent, s.accepted && !s.gave_up ? tot[2] : tot[3], s);
       } else {
         if (s.accepted) {
           s.f1 = s.f2;
@@ -843,10 +857,7 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       break;
     }
     case OP_STATUS: {  // PGOAgent::iterate status (src/PGOAgent.cpp:700-716), tot[0] = |X - XPrev|^2
-      const double rc = sqrt(tot[0] / static_cast<double>(f.agent_num_poses[agent]));
-      const double ratio = f.conv_ratio ? f.conv_ratio[agent] : 1.0;
-      s.status_rel_change = rc;
-      s.ready = (rc > o.rel_tol || ratio < o.min_ratio) ? 0 : 1;
+      set_status(f, agent, tot[0], s);
       break;
     }
     case OP_SUM: {
@@ -860,10 +871,12 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       break;
   }
   if (f.pub != nullptr) {
-    // word = tag << 2 | cg << 1 | flag; cg (rho test only): this Run's tCG took more than one step
+    // word = tag << 3 | never << 2 | cg << 1 | flag (rho test only: cg = this Run's tCG took more than one
+    // step, never = the agent did not run in this call)
     const int flag = f.pub_kind == 1 ? s.tcg_active : s.run_active;
     const int cg = f.pub_kind == 2 && s.tcg_iters > 1 ? 2 : 0;
-    __hip_atomic_store(&f.pub[agent], (f.pub_tag << 2) | cg | (flag ? 1 : 0), __ATOMIC_RELAXED,
+    const int never = f.pub_kind == 2 && s.runs == 0 && !s.run_active ? 4 : 0;
+    __hip_atomic_store(&f.pub[agent], (f.pub_tag << 3) | never | cg | (flag ? 1 : 0), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
@@ -1580,7 +1593,8 @@ __global__ __launch_bounds__(kThreads) void k_retract(LaunchCtx c, const double*
                                                       double* __restrict__ out,
                                                       const double* __restrict__ g,
                                                       const double* __restrict__ HV,
-                                                      const double* __restrict__ delta_impl) {
+                                                      const double* __restrict__ delta_impl,
+                                                      const double* __restrict__ status_ref) {
   constexpr int D = B - 1;
   const PoseLane p = pose_lane<B>(c);
   if (tile_skipped(c, p.agent)) return;
@@ -1620,8 +1634,23 @@ __global__ __launch_bounds__(kThreads) void k_retract(LaunchCtx c, const double*
         for (int a = 0; a < R; ++a) eh = fma(vcol[a], hcol[a], eh);
       }
     }
-    double parts[2] = {own ? ge : 0.0, own ? eh : 0.0};
-    block_partials<2>(parts, c.partials, p.tile);
+    if (status_ref != nullptr) {  // |out - ref|^2, |X - ref|^2: the status of either outcome (k_sqdiff's sums)
+      double d2 = 0.0, d1 = 0.0;
+      if (own) {
+#pragma unroll
+        for (int a = 0; a < R; ++a) {
+          const double rf = status_ref[off + a];
+          const double e2 = oc[a] - rf, e1 = xcol[a] - rf;
+          d2 = fma(e2, e2, d2);
+          d1 = fma(e1, e1, d1);
+        }
+      }
+      double parts[4] = {own ? ge : 0.0, own ? eh : 0.0, d2, d1};
+      block_partials<4>(parts, c.partials, p.tile);
+    } else {
+      double parts[2] = {own ? ge : 0.0, own ? eh : 0.0};
+      block_partials<2>(parts, c.partials, p.tile);
+    }
   }
 }
 
@@ -2087,7 +2116,8 @@ __device__ void finalize_arrive(const FinalizeArgs& f, int agent, int* arrive, c
   if (threadIdx.x == 0 && f.pub != nullptr) {
     const int flag = f.pub_kind == 1 ? sh.tcg_active : sh.run_active;
     const int cg = f.pub_kind == 2 && sh.tcg_iters > 1 ? 2 : 0;
-    __hip_atomic_store(&f.pub[agent], (f.pub_tag << 2) | cg | (flag ? 1 : 0), __ATOMIC_RELAXED,
+    const int never = f.pub_kind == 2 && sh.runs == 0 && !sh.run_active ? 4 : 0;
+    __hip_atomic_store(&f.pub[agent], (f.pub_tag << 3) | never | cg | (flag ? 1 : 0), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
@@ -2711,10 +2741,11 @@ hipError_t launch_tcg_updir(int r, int b, const LaunchCtx& c, const double* X, c
 }
 
 hipError_t launch_retract(int r, int b, const LaunchCtx& c, const double* X, const double* V, double scale,
-                          double* out, const double* g, const double* HV, const double* delta_impl) {
+                          double* out, const double* g, const double* HV, const double* delta_impl,
+                          const double* status_ref) {
   if (c.num_tiles == 0) return hipSuccess;
-  DPGO_DISPATCH(r, b,
-                (k_retract<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, V, scale, out, g, HV, delta_impl)));
+  DPGO_DISPATCH(r, b, (k_retract<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, V, scale, out, g, HV, delta_impl,
+                                                                               status_ref)));
   return hipGetLastError();
 }
 

@@ -397,3 +397,36 @@ def test_tcg_lookahead_bitwise(hip):
         assert np.array_equal(out[0][0], other[0])
         assert np.array_equal(out[0][1][:, :12], other[1][:, :12])
     assert out[0][1][:, 10].sum() > 0  # CG steps were taken
+
+
+@pytest.mark.parametrize("accel", [False, True])
+def test_status_fold_bitwise(hip, accel):
+    """The PGOAgent status folded into the retraction and the rho test (the default) against its own
+    k_sqdiff + OP_STATUS pass (tuning key TUNE_STATUS_PASS): bitwise the same relativeChange, the same
+    readyToTerminate, the same iterates, in the boundary regime and the CG regime."""
+    g = hip.Graph.grid3d(12, seed=5)
+    aop = g.grid_partition(2)
+    X0, _, _ = g.distributed_init(aop, 5, hip.lifting_matrix(3, 5), gpu=True, rtol=1e-12, dev_layout=True)
+    Xc = g.chain_init_dev_layout(5, hip.lifting_matrix(3, 5))
+    out = []
+    for sep in (1, 0):
+        hip.set_tuning(9, sep)
+        try:
+            e = hip.Rbcd(g, aop, np.zeros(8, np.int32), 0, 1, hip.rbcd_params(r=5, acceleration=int(accel)))
+            res = []
+            for start in (Xc, X0):
+                e.set_X(start)
+                for it in range(12):
+                    e.pre_exchange(it % e.num_colors)
+                    e.update(it % e.num_colors, None)
+                    rc, rd = e.status()
+                    res.append((rc.copy(), rd.copy()))
+            X = np.zeros(X0.size)
+            e.get_X_into(X)
+            out.append((X, res))
+        finally:
+            hip.set_tuning(9, 0)
+    assert np.array_equal(out[0][0], out[1][0])
+    for (rc0, rd0), (rc1, rd1) in zip(out[0][1], out[1][1]):
+        assert np.array_equal(rc0, rc1)
+        assert np.array_equal(rd0, rd1)
