@@ -217,6 +217,20 @@ __device__ __forceinline__ void load_col(const double* __restrict__ P, long j, i
   }
 }
 
+// Column k of pose j's Y block only (lanes k < b - 1; the translation lane gets zeros): for operands that
+// only enter through quad_gather_y (tangent projections, preconditioner projections)
+template <int R, int B>
+__device__ __forceinline__ void load_col_y(const double* __restrict__ P, long j, int k, bool ok, double (&col)[R]) {
+  if (ok && k < B - 1) {
+    const double* p = P + j * (R * B) + k * R;
+#pragma unroll
+    for (int a = 0; a < R; ++a) col[a] = p[a];
+  } else {
+#pragma unroll
+    for (int a = 0; a < R; ++a) col[a] = 0.0;
+  }
+}
+
 template <int R, int B>
 __device__ __forceinline__ void store_col(double* __restrict__ P, long j, int k, bool ok,
                                           const double (&full)[R][B]) {

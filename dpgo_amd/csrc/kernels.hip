@@ -977,7 +977,7 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     load_col<R, B>(args.rvec, p.j, p.k, p.ok, pre_r);
     if (args.pmode != PRECON_NONE) minv_col<B>(args.Minv, p.j, p.k, p.ok, pre_mk);
   }
-  if constexpr (PRE_X) load_col<R, B>(X, p.j, p.k, p.ok, pre_x);
+  if constexpr (PRE_X) load_col_y<R, B>(X, p.j, p.k, p.ok, pre_x);  // X enters HESS only through its Y block
   if constexpr (PRE_S) {
 #pragma unroll
     for (int q = 0; q < s_width(D); ++q) pre_s[q] = p.ok ? S_in[p.j * s_width(D) + q] : 0.0;
@@ -1222,7 +1222,7 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
 #pragma unroll
       for (int a = 0; a < R; ++a) xcol[a] = pre_x[a];
     } else {
-      load_col<R, B>(X, p.j, p.k, p.ok, xcol);
+      load_col_y<R, B>(X, p.j, p.k, p.ok, xcol);
     }
     double S[D][D];
 #pragma unroll
@@ -1568,7 +1568,7 @@ __global__ __launch_bounds__(kThreads) void k_tcg_updir(LaunchCtx c, const doubl
     const double beta = st.beta;
     double rcol[R], xcol[R];
     load_col<R, B>(r_in, p.j, p.k, p.ok, rcol);
-    load_col<R, B>(X, p.j, p.k, p.ok, xcol);
+    load_col_y<R, B>(X, p.j, p.k, p.ok, xcol);  // only X's Y block enters Prec
 #pragma unroll
     for (int a = 0; a < R; ++a) rcol[a] = fma(step, hcol[a], rcol[a]);
     double Yx[R][D], zc[R], dn[R];

@@ -13,7 +13,8 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdpgo_hip.so")
+# DPGO_HIP_LIB: another build of the library (tools/ A/B runs against a previous build only)
+LIB_PATH = os.environ.get("DPGO_HIP_LIB") or os.path.join(_HERE, "libdpgo_hip.so")
 
 PRECON_EXACT, PRECON_BLOCK_JACOBI, PRECON_NONE = 0, 1, 2
 QFMT_BSR, QFMT_EDGES = 0, 1
