@@ -236,8 +236,11 @@ int sync_q_edges(dpgo_hip_problem h) {
     for (int u = 0; u < b; ++u)
       for (int v = u; v < b; ++v) diag[p * DW + o++] = full[static_cast<size_t>(p) * b * b + v * b + u];
   }
-  // second-visit staging tables per tile (see QView)
-  {
+  // second-visit staging tables per tile (see QView), only for the TUNE_SV_STAGE experiment
+  h->sv_ptr.release();
+  h->sv_ids.release();
+  h->inc_sv.release();
+  if (dpgo::g_tuning[dpgo::TUNE_SV_STAGE] > 0) {
     const int T = h->num_tiles;
     std::vector<int> sv_ptr(T + 1, 0), sv_ids;
     std::vector<int2> inc_sv(inc.size());

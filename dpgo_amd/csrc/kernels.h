@@ -217,8 +217,9 @@ enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH =
                                       //    instead of the merged three (HESS_M, step + check, k_tcg_updir)
                TUNE_TCG_LOOKAHEAD = 7,  // merged single-Run tCG with the full first pass: 0 adaptive, 1 one
                                         // iteration queued ahead of a published status, 2 every iteration queued
-               TUNE_MERGED_PREFETCH = 6,  // HESS_M variants: r / Minv loaded before the edge loop (1; with >= 4 waves: 2); 5-wave register budget (3)
-               TUNE_SV_STAGE = 8,  // 1: HESS passes stage the tile's second-visit records in LDS too
+               TUNE_MERGED_PREFETCH = 6,  // 1: HESS_M's r / Minv loaded before the edge loop (measured slower)
+               TUNE_SV_STAGE = 8,  // 1: HESS passes stage the tile's second-visit records in LDS too (the
+                                   //    tables are built when Q is set with this on; measured slower)
                TUNE_STATUS_PASS = 9,  // 1: the agent status by its own pass (k_sqdiff + OP_STATUS), not folded
                TUNE_COUNT = 12 };
 // variant of the edge-stream SpMM used unless TUNE_EDGE_VARIANT overrides it (bit 0: XCD-aware

@@ -2615,7 +2615,7 @@ hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q
   if (q.fmt == QFMT_EDGES) {
     constexpr bool kPreMode = mode_hess(MODE) || MODE == MODE_QF || MODE == MODE_EVAL_TCG;
     if constexpr (mode_hess(MODE)) {
-      if (r == 5 && b == 4 && g_tuning[TUNE_SV_STAGE] > 0 && g_tuning[TUNE_EDGE_VARIANT] < 0) {
+      if (r == 5 && b == 4 && g_tuning[TUNE_SV_STAGE] > 0 && g_tuning[TUNE_EDGE_VARIANT] < 0 && q.sv_ptr != nullptr) {
         k_spmm<5, 4, MODE, kEdgeDefaultVariant | 8 | 32, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
         return hipSuccess;
       }
@@ -2623,14 +2623,8 @@ hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q
     if constexpr (mode_merged(MODE)) {
       const int mp = g_tuning[TUNE_MERGED_PREFETCH];
       if (r == 5 && b == 4 && g_tuning[TUNE_EPI_PREFETCH] > 0 && g_tuning[TUNE_EDGE_VARIANT] < 0 && mp > 0) {
-        if (mp == 1)
-          k_spmm<5, 4, MODE, kEdgeDefaultVariant | 8 | 16, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
-        else if (mp == 2)
-          k_spmm<5, 4, MODE, kEdgeDefaultVariant | 2 | 8 | 16, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
-        else if (mp == 3)  // epilogue prefetch, register budget for 5 waves / SIMD
-          k_spmm<5, 4, MODE, kEdgeDefaultVariant | 4 | 8, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
-        else  // no epilogue prefetch, register budget for 5 waves / SIMD
-          k_spmm<5, 4, MODE, kEdgeDefaultVariant | 4, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+        // (measured slower: occupancy 4 -> 3; the 5-wave register budgets measured spill)
+        k_spmm<5, 4, MODE, kEdgeDefaultVariant | 8 | 16, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
         return hipSuccess;
       }
     }
