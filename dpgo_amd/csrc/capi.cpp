@@ -475,6 +475,19 @@ int sync_chol(dpgo_hip_problem h) {
   std::vector<int> frows, brows;
   schedule(flev, frows, h->fw_lvl);
   schedule(blev, brows, h->bw_lvl);
+  // levels whose longest row is long (the dense separator rows near the top of the elimination tree) run
+  // one wave per row instead of one quad per row
+  auto wide = [&](const std::vector<int>& lptr, const std::vector<int>& rows, const std::vector<int>& ptr,
+                  std::vector<int>& out) {
+    out.assign(lptr.empty() ? 0 : lptr.size() - 1, 0);
+    for (size_t l = 0; l + 1 < lptr.size(); ++l) {
+      int mx = 0;
+      for (int x = lptr[l]; x < lptr[l + 1]; ++x) mx = std::max(mx, ptr[rows[x] + 1] - ptr[rows[x]]);
+      out[l] = mx > dpgo::kTrsvWideRow ? 1 : 0;
+    }
+  };
+  wide(h->fw_lvl, frows, fptr, h->fw_wide);
+  wide(h->bw_lvl, brows, bptr, h->bw_wide);
   auto up_i = [&](DevBuf<int>& d, const std::vector<int>& v) -> int {
     HIP_TRY(d.ensure(std::max<size_t>(v.size(), 1)));
     if (!v.empty()) HIP_TRY(hipMemcpyAsync(d.p, v.data(), sizeof(int) * v.size(), hipMemcpyHostToDevice, h->stream));
@@ -513,10 +526,10 @@ int exact_precond(dpgo_hip_problem h, const double* in, double* z_out, double* d
     const dpgo::TrsvView bw{h->bw_ptr.p, h->bw_col.p, h->bw_blk.p, h->linv.p, 0};
     for (size_t l = 0; l + 1 < h->fw_lvl.size(); ++l)
       HIP_TRY(dpgo::launch_trsv_level(h->r, h->b, fw, h->fw_rows.p + h->fw_lvl[l], h->fw_lvl[l + 1] - h->fw_lvl[l], in,
-                                      h->tA.p, h->stream));
+                                      h->tA.p, h->stream, h->fw_wide[l]));
     for (size_t l = 0; l + 1 < h->bw_lvl.size(); ++l)
       HIP_TRY(dpgo::launch_trsv_level(h->r, h->b, bw, h->bw_rows.p + h->bw_lvl[l], h->bw_lvl[l + 1] - h->bw_lvl[l],
-                                      h->tA.p, h->tB.p, h->stream));
+                                      h->tA.p, h->tB.p, h->stream, h->bw_wide[l]));
     zraw = h->tB.p;
   }
   auto c = make_ctx(h, flag, partials);

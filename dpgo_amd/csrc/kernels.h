@@ -280,8 +280,10 @@ hipError_t launch_accept(int r, int b, const LaunchCtx& c, const double* x2, con
                          double* x1, double* g, double* S);
 hipError_t launch_finalize(const FinalizeArgs& f, int num_agents, hipStream_t stream);
 // sol[j] = (rhs[j] - sum_k sol[k] blk_jk) dinv_j for the `count` poses rows[] of one level
+// wide: one wave per row (its 16 quads split the row's entries), for levels with long rows
+constexpr int kTrsvWideRow = 16;
 hipError_t launch_trsv_level(int r, int b, const TrsvView& t, const int* rows, int count, const double* rhs,
-                             double* sol, hipStream_t stream);
+                             double* sol, hipStream_t stream, int wide = 0);
 // z = P_X(zraw) (or z = zraw when project == 0); optional z_out / delta_out = -z; partials
 // <z, rref>, |rref|^2 per tile
 hipError_t launch_precond_finish(int r, int b, const LaunchCtx& c, const double* X, const double* zraw,

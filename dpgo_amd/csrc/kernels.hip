@@ -2389,12 +2389,17 @@ __global__ __launch_bounds__(kThreads) void k_weights_to_slots(int m, const int*
 // L_jj^-T, backward Z_j = (Y_j - sum_i Z_i L_ij) L_jj^-1.  One quad per pose row, outer-product
 // accumulation + quad reduce-scatter as in the SpMM; every row of a level is independent.
 // ------------------------------------------------------------------------------------------
-template <int R, int B>
+// WIDE: one wave per row, quad g of the wave takes entries g, g + 16, ... and the 16 partial sums are
+// added over the wave (lane bits 2..5) before the diagonal solve; otherwise one quad per row.
+template <int R, int B, bool WIDE>
 __global__ __launch_bounds__(kThreads) void k_trsv_level(TrsvView t, const int* __restrict__ rows, int count,
                                                          const double* __restrict__ rhs, double* __restrict__ sol) {
   const int k = threadIdx.x & 3;
-  const int q = blockIdx.x * (kThreads / 4) + (threadIdx.x >> 2);
-  if (q >= count) return;  // whole quad leaves together
+  constexpr int kRowsPerBlock = WIDE ? kThreads / 64 : kThreads / 4;
+  constexpr int kStride = WIDE ? 16 : 1;
+  const int q = blockIdx.x * kRowsPerBlock + static_cast<int>(threadIdx.x) / (WIDE ? 64 : 4);
+  const int g = WIDE ? (static_cast<int>(threadIdx.x) & 63) >> 2 : 0;
+  if (q >= count) return;  // whole quad / wave leaves together
   const int kc = k < B ? k : 0;
   const long j = rows[q];
   double acc[R][B];
@@ -2402,7 +2407,7 @@ __global__ __launch_bounds__(kThreads) void k_trsv_level(TrsvView t, const int* 
   for (int a = 0; a < R; ++a)
 #pragma unroll
     for (int c = 0; c < B; ++c) acc[a][c] = 0.0;
-  for (int z = t.ptr[j]; z < t.ptr[j + 1]; ++z) {
+  for (int z = t.ptr[j] + g; z < t.ptr[j + 1]; z += kStride) {
     const long i = t.col[z];
     const double* br = t.blk + static_cast<long>(z) * (B * B) + kc * B;
     const double* xi = sol + i * (R * B) + kc * R;
@@ -2415,6 +2420,14 @@ __global__ __launch_bounds__(kThreads) void k_trsv_level(TrsvView t, const int* 
     for (int a = 0; a < R; ++a)
 #pragma unroll
       for (int c = 0; c < B; ++c) acc[a][c] = fma(x[a], bk[c], acc[a][c]);
+  }
+  if constexpr (WIDE) {
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int c = 0; c < B; ++c)
+#pragma unroll
+        for (int off = 4; off < 64; off <<= 1) acc[a][c] += __shfl_xor(acc[a][c], off, 64);
   }
   const bool act = k < B;
 #pragma unroll
@@ -2437,7 +2450,7 @@ __global__ __launch_bounds__(kThreads) void k_trsv_level(TrsvView t, const int* 
     for (int c = 0; c < B; ++c) acc[a][c] = act ? w[a] * dv[c] : 0.0;
   double y[R];
   quad_reduce_scatter<R, B>(acc, k, y);
-  if (act) {
+  if (act && g == 0) {
     double* sj = sol + j * (R * B) + k * R;
 #pragma unroll
     for (int a = 0; a < R; ++a) sj[a] = y[a];
@@ -2810,10 +2823,15 @@ hipError_t launch_assemble_G(int r, int b, const GEdges& e, int nslots, const do
 }
 
 hipError_t launch_trsv_level(int r, int b, const TrsvView& t, const int* rows, int count, const double* rhs,
-                             double* sol, hipStream_t stream) {
+                             double* sol, hipStream_t stream, int wide) {
   if (count == 0) return hipSuccess;
-  const int grid = (count + kThreads / 4 - 1) / (kThreads / 4);
-  DPGO_DISPATCH(r, b, (k_trsv_level<R, B><<<grid, kThreads, 0, stream>>>(t, rows, count, rhs, sol)));
+  if (wide) {
+    const int grid = (count + kThreads / 64 - 1) / (kThreads / 64);
+    DPGO_DISPATCH(r, b, (k_trsv_level<R, B, true><<<grid, kThreads, 0, stream>>>(t, rows, count, rhs, sol)));
+  } else {
+    const int grid = (count + kThreads / 4 - 1) / (kThreads / 4);
+    DPGO_DISPATCH(r, b, (k_trsv_level<R, B, false><<<grid, kThreads, 0, stream>>>(t, rows, count, rhs, sol)));
+  }
   return hipGetLastError();
 }
 

@@ -115,6 +115,7 @@ struct dpgo_hip_problem_s {
   dpgo::DevBuf<int> fw_ptr, fw_col, bw_ptr, bw_col, fw_rows, bw_rows;
   dpgo::DevBuf<double> fw_blk, bw_blk, linv;
   std::vector<int> fw_lvl, bw_lvl;  // level pointers into fw_rows / bw_rows
+  std::vector<int> fw_wide, bw_wide;  // per level: its longest row has more entries than a quad should walk
   long chol_blocks = 0;
 
   // work
