@@ -54,16 +54,16 @@ def _close(a, b, tol):
     ("sphere2500", 3, 10, 1e-1, 10.0, 50),
     ("smallGrid3D", 5, 1, 1e-2, 100.0, 10),   # updateX settings (:1131-1137)
 ])
-@pytest.mark.parametrize("precon", ["bj", "bj-classic", "exact"])
+@pytest.mark.parametrize("precon", ["bj", "bj-classic", "none", "none-classic", "exact"])
 def test_rtr_trace_matches_oracle(hip, name, r, iters, tol, radius, inner, precon):
     """Every tCG step (d_Hd, alpha, tau, status), stopping test (|r|, <z, r>, beta, status) and rho test
     (f1, f2, rho, Delta, accepted, |grad|, status, inner iterations) of the device RTR equals the
     oracle's at 1e-10 relative (rho: cancellation-aware), in the same order.  "bj": the merged tCG
     iteration (stopping test from one-step polynomials in alpha), "bj-classic": the five-launch sequence
     (tuning key TUNE_CLASSIC_TCG); the exact factor always runs the classic one."""
-    hip.set_tuning(5, 1 if precon == "bj-classic" else 0)
+    hip.set_tuning(5, 1 if precon.endswith("-classic") else 0)
     try:
-        _rtr_trace_case(hip, name, r, iters, tol, radius, inner, precon.split("-")[0], merged=precon == "bj")
+        _rtr_trace_case(hip, name, r, iters, tol, radius, inner, precon.split("-")[0], merged=precon in ("bj", "none"))
     finally:
         hip.set_tuning(5, 0)
 
@@ -74,7 +74,7 @@ def _rtr_trace_case(hip, name, r, iters, tol, radius, inner, precon, merged):
     Q = O.connection_laplacian(meas, n)
     P = O.QuadraticProblem(n, d, r)
     P.set_Q(Q)
-    P.precon_mode = O.PRECON_BLOCK_JACOBI if precon == "bj" else O.PRECON_EXACT
+    P.precon_mode = {"bj": O.PRECON_BLOCK_JACOBI, "none": O.PRECON_NONE, "exact": O.PRECON_EXACT}[precon]
     X0 = O.lifting_matrix(d, r) @ O.chordal_initialization(d, n, meas)
     trace = []
     Xo, res = O.optimize(P, X0, O.OptParams(tr_iterations=iters, tr_tolerance=tol, tr_initial_radius=radius,
@@ -83,7 +83,8 @@ def _rtr_trace_case(hip, name, r, iters, tol, radius, inner, precon, merged):
     H.set_Q_scipy(0, Q)
     H.set_trace(4096)
     p = hip.default_params(tr_iterations=iters, tr_tolerance=tol, tr_initial_radius=radius, tr_max_inner=inner,
-                           precon=hip.PRECON_BLOCK_JACOBI if precon == "bj" else hip.PRECON_EXACT)
+                           precon={"bj": hip.PRECON_BLOCK_JACOBI, "none": hip.PRECON_NONE,
+                                   "exact": hip.PRECON_EXACT}[precon])
     Xh, rh = H.optimize(X0, p)
     got = H.get_trace(0)
     exp = _expected_records(trace)
@@ -94,14 +95,19 @@ def _rtr_trace_case(hip, name, r, iters, tol, radius, inner, precon, merged):
     # Quantities that shrink inside one tCG (d_Hd, alpha, |r|, <z, r>, beta, tau) are measured against
     # their largest magnitude in that tCG: their terms cancel, so their rounding floor is set by it.
     # rho = (f1 - f2) / model decrease: f1 - f2 loses the digits |f1| / |f1 - f2|.
-    tol = 1e-10 if precon == "bj" else 1e-7
+    tol = 1e-7 if precon == "exact" else 1e-10
+    if precon == "none":
+        # unpreconditioned tCG: 50 inner iterations on smallGrid3D amplify the summation-order rounding
+        # (the classic sequence, the oracle's own operations, differs by 1.6e-9 of |r| at iteration 8 and
+        # the merged one by 8e-8 at 11): the bars of this case are 1e-6
+        tol = 1e-6
     # The merged tCG iteration forms |r_{j+1}|^2 and <z_{j+1}, r_{j+1}> (hence beta) from one-step
     # polynomials in alpha over r_j and Hd_j: exact in exact arithmetic, but the sum cancels by the factor
     # <z_j, r_j> / <z_{j+1}, r_{j+1}>, so on a fast-converging tCG the directions after a large drop carry
     # eps times that factor (measured: 2e-10 of the largest d_Hd on tinyGrid3D).  The tCG-internal
     # quantities get 1e-8 of their scale there; costs, rho, gradient norms, statuses, iteration counts and
     # X keep the classic bars (the classic sequence itself is held to 1e-10 by "bj-classic").
-    tcg_tol = 1e-8 if merged else tol
+    tcg_tol = max(1e-8, tol) if merged else tol
     scale, run_id = {}, None
     for g, e in zip(got, exp):
         if e["op"] == 5 or run_id != g["run"]:
@@ -144,7 +150,7 @@ def _rtr_trace_case(hip, name, r, iters, tol, radius, inner, precon, merged):
     for s, name_ in ((O.TCG_NEGCURVTURE, "NEGCURVTURE"), (O.TCG_EXCREGION, "EXCREGION"), (O.TCG_LCON, "LCON"),
                      (O.TCG_SCON, "SCON"), (O.TCG_MAXITER, "MAXITER")):
         assert st[name_] == sum(1 for t in runs if t["status"] == s)
-    assert rel(Xh, Xo) <= 1e-8
+    assert rel(Xh, Xo) <= max(1e-8, tol)
 
 
 @pytest.mark.parametrize("batched", [False, True])
