@@ -488,6 +488,49 @@ int sync_chol(dpgo_hip_problem h) {
   };
   wide(h->fw_lvl, frows, fptr, h->fw_wide);
   wide(h->bw_lvl, brows, bptr, h->bw_wide);
+  std::vector<int> agent_of(h->N, 0);
+  for (int a = 0; a < h->K; ++a)
+    for (long p = h->pose_off[a]; p < h->pose_off[a] + h->n_agent[a]; ++p) agent_of[p] = a;
+  auto chains = [&](const std::vector<int>& lptr, const std::vector<int>& rows, std::vector<dpgo_hip_problem_s::TrsvChain>& out,
+                    std::vector<int>& captr, std::vector<int>& crows) {
+    out.clear();
+    captr.assign(1, 0);
+    crows.clear();
+    const int nl = lptr.empty() ? 0 : static_cast<int>(lptr.size()) - 1;
+    std::vector<int> seen(h->K, -1);
+    auto chainable = [&](int l) {
+      for (int x = lptr[l]; x < lptr[l + 1]; ++x) {
+        const int a = agent_of[rows[x]];
+        if (seen[a] == l) return false;
+        seen[a] = l;
+      }
+      return true;
+    };
+    int l = 0;
+    while (l < nl) {
+      int e = l;
+      while (e < nl && chainable(e)) ++e;
+      if (e - l >= 2) {  // levels [l, e): per agent its rows in level order
+        std::vector<std::vector<int>> per(h->K);
+        for (int m = l; m < e; ++m)
+          for (int x = lptr[m]; x < lptr[m + 1]; ++x) per[agent_of[rows[x]]].push_back(rows[x]);
+        dpgo_hip_problem_s::TrsvChain c{l, e, static_cast<int>(captr.size()) - 1, 0};
+        for (int a = 0; a < h->K; ++a)
+          if (!per[a].empty()) {
+            crows.insert(crows.end(), per[a].begin(), per[a].end());
+            captr.push_back(static_cast<int>(crows.size()));
+            ++c.nblk;
+          }
+        out.push_back(c);
+        l = e;
+      } else {
+        l = std::max(e, l + 1);
+      }
+    }
+  };
+  std::vector<int> fcaptr, fcrows, bcaptr, bcrows;
+  chains(h->fw_lvl, frows, h->fw_chain, fcaptr, fcrows);
+  chains(h->bw_lvl, brows, h->bw_chain, bcaptr, bcrows);
   auto up_i = [&](DevBuf<int>& d, const std::vector<int>& v) -> int {
     HIP_TRY(d.ensure(std::max<size_t>(v.size(), 1)));
     if (!v.empty()) HIP_TRY(hipMemcpyAsync(d.p, v.data(), sizeof(int) * v.size(), hipMemcpyHostToDevice, h->stream));
@@ -508,6 +551,10 @@ int sync_chol(dpgo_hip_problem h) {
   DPGO_TRY(up_d(h->linv, linv));
   DPGO_TRY(up_i(h->fw_rows, frows));
   DPGO_TRY(up_i(h->bw_rows, brows));
+  DPGO_TRY(up_i(h->fw_captr, fcaptr));
+  DPGO_TRY(up_i(h->fw_crows, fcrows));
+  DPGO_TRY(up_i(h->bw_captr, bcaptr));
+  DPGO_TRY(up_i(h->bw_crows, bcrows));
   HIP_TRY(hipStreamSynchronize(h->stream));
   h->chol_blocks = blocks;
   h->chol_state = 1;
@@ -524,12 +571,27 @@ int exact_precond(dpgo_hip_problem h, const double* in, double* z_out, double* d
   if (h->chol_state == 1) {
     const dpgo::TrsvView fw{h->fw_ptr.p, h->fw_col.p, h->fw_blk.p, h->linv.p, 1};
     const dpgo::TrsvView bw{h->bw_ptr.p, h->bw_col.p, h->bw_blk.p, h->linv.p, 0};
-    for (size_t l = 0; l + 1 < h->fw_lvl.size(); ++l)
-      HIP_TRY(dpgo::launch_trsv_level(h->r, h->b, fw, h->fw_rows.p + h->fw_lvl[l], h->fw_lvl[l + 1] - h->fw_lvl[l], in,
-                                      h->tA.p, h->stream, h->fw_wide[l]));
-    for (size_t l = 0; l + 1 < h->bw_lvl.size(); ++l)
-      HIP_TRY(dpgo::launch_trsv_level(h->r, h->b, bw, h->bw_rows.p + h->bw_lvl[l], h->bw_lvl[l + 1] - h->bw_lvl[l],
-                                      h->tA.p, h->tB.p, h->stream, h->bw_wide[l]));
+    // level by level, except chains of levels with one row per agent: one launch per chain
+    auto sweep = [&](const dpgo::TrsvView& t, const std::vector<int>& lvl, const std::vector<int>& wide_l,
+                     const DevBuf<int>& rows, const std::vector<dpgo_hip_problem_s::TrsvChain>& ch,
+                     const DevBuf<int>& captr, const DevBuf<int>& crows, const double* rhs, double* sol) -> int {
+      const bool use_chains = dpgo::g_tuning[dpgo::TUNE_TRSV_CHAINS] == 0;
+      size_t c = 0;
+      for (size_t l = 0; l + 1 < lvl.size();) {
+        while (c < ch.size() && static_cast<size_t>(ch[c].l0) < l) ++c;
+        if (use_chains && c < ch.size() && static_cast<size_t>(ch[c].l0) == l) {
+          HIP_TRY(dpgo::launch_trsv_chain(h->r, h->b, t, captr.p + ch[c].a0, ch[c].nblk, crows.p, rhs, sol, h->stream));
+          l = static_cast<size_t>(ch[c].l1);
+          continue;
+        }
+        HIP_TRY(dpgo::launch_trsv_level(h->r, h->b, t, rows.p + lvl[l], lvl[l + 1] - lvl[l], rhs, sol, h->stream,
+                                        wide_l[l]));
+        ++l;
+      }
+      return DPGO_HIP_OK;
+    };
+    DPGO_TRY(sweep(fw, h->fw_lvl, h->fw_wide, h->fw_rows, h->fw_chain, h->fw_captr, h->fw_crows, in, h->tA.p));
+    DPGO_TRY(sweep(bw, h->bw_lvl, h->bw_wide, h->bw_rows, h->bw_chain, h->bw_captr, h->bw_crows, h->tA.p, h->tB.p));
     zraw = h->tB.p;
   }
   auto c = make_ctx(h, flag, partials);

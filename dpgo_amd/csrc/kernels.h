@@ -221,6 +221,7 @@ enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH =
                TUNE_SV_STAGE = 8,  // 1: HESS passes stage the tile's second-visit records in LDS too (the
                                    //    tables are built when Q is set with this on; measured slower)
                TUNE_STATUS_PASS = 9,  // 1: the agent status by its own pass (k_sqdiff + OP_STATUS), not folded
+               TUNE_TRSV_CHAINS = 10,  // 1: the exact preconditioner's chains of levels solved level by level
                TUNE_COUNT = 12 };
 // variant of the edge-stream SpMM used unless TUNE_EDGE_VARIANT overrides it (bit 0: XCD-aware
 // tile remap; v >> 1: minimum waves per SIMD the register allocation must allow, none/4/5/6)
@@ -280,6 +281,10 @@ hipError_t launch_accept(int r, int b, const LaunchCtx& c, const double* x2, con
                          double* x1, double* g, double* S);
 hipError_t launch_finalize(const FinalizeArgs& f, int num_agents, hipStream_t stream);
 // sol[j] = (rhs[j] - sum_k sol[k] blk_jk) dinv_j for the `count` poses rows[] of one level
+// A chain of levels: workgroup b walks rows[aptr[b] .. aptr[b + 1]) in order (one agent's rows, at most one
+// per level), the row's entries split over the workgroup's 64 quads
+hipError_t launch_trsv_chain(int r, int b, const TrsvView& t, const int* aptr, int nblk, const int* rows,
+                             const double* rhs, double* sol, hipStream_t stream);
 // wide: one wave per row (its 16 quads split the row's entries), for levels with long rows
 constexpr int kTrsvWideRow = 16;
 hipError_t launch_trsv_level(int r, int b, const TrsvView& t, const int* rows, int count, const double* rhs,

@@ -2457,6 +2457,87 @@ __global__ __launch_bounds__(kThreads) void k_trsv_level(TrsvView t, const int* 
   }
 }
 
+// A chain of levels in one launch: workgroup b walks one agent's rows (at most one per level, so each row's
+// dependencies inside the chain are earlier rows of the same workgroup) in level order.  Per row the 64
+// quads split the entries; the partial sums meet over the wave (lanes 4.. apart) and then over the four
+// waves through LDS; wave 0 solves the diagonal block and stores; the barrier after it publishes the row
+// to the next one (workgroup-scope release / acquire: same CU).
+template <int R, int B>
+__global__ __launch_bounds__(kThreads) void k_trsv_chain(TrsvView t, const int* __restrict__ aptr,
+                                                         const int* __restrict__ rows, const double* __restrict__ rhs,
+                                                         double* sol) {
+  __shared__ double red[kThreads / 64][4][R * B];
+  const int k = threadIdx.x & 3, quad = threadIdx.x >> 2, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kc = k < B ? k : 0;
+  const bool act = k < B;
+  const int x0 = aptr[blockIdx.x], x1 = aptr[blockIdx.x + 1];
+  for (int x = x0; x < x1; ++x) {
+    const long j = rows[x];
+    double acc[R][B];
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int c = 0; c < B; ++c) acc[a][c] = 0.0;
+    for (int z = t.ptr[j] + quad; z < t.ptr[j + 1]; z += kThreads / 4) {
+      const long i = t.col[z];
+      const double* br = t.blk + static_cast<long>(z) * (B * B) + kc * B;
+      const double* xi = sol + i * (R * B) + kc * R;
+      double xv[R], bk[B];
+#pragma unroll
+      for (int a = 0; a < R; ++a) xv[a] = xi[a];
+#pragma unroll
+      for (int c = 0; c < B; ++c) bk[c] = br[c];
+#pragma unroll
+      for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int c = 0; c < B; ++c) acc[a][c] = fma(xv[a], bk[c], acc[a][c]);
+    }
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int c = 0; c < B; ++c)
+#pragma unroll
+        for (int off = 4; off < 64; off <<= 1) acc[a][c] += __shfl_xor(acc[a][c], off, 64);
+    if (lane < 4) {
+#pragma unroll
+      for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int c = 0; c < B; ++c) red[wave][lane][a * B + c] = acc[a][c];
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int c = 0; c < B; ++c) {
+          const double v = ((red[0][k][a * B + c] + red[1][k][a * B + c]) + red[2][k][a * B + c]) + red[3][k][a * B + c];
+          acc[a][c] = act ? v : 0.0;
+        }
+      double w[R];
+      quad_reduce_scatter<R, B>(acc, k, w);
+      const double* rj = rhs + j * (R * B) + kc * R;
+#pragma unroll
+      for (int a = 0; a < R; ++a) w[a] = rj[a] - w[a];
+      double dv[B];
+      const double* dj = t.dinv + j * (B * B);
+#pragma unroll
+      for (int c = 0; c < B; ++c) dv[c] = t.forward ? dj[c * B + kc] : dj[kc * B + c];
+#pragma unroll
+      for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int c = 0; c < B; ++c) acc[a][c] = act ? w[a] * dv[c] : 0.0;
+      double y[R];
+      quad_reduce_scatter<R, B>(acc, k, y);
+      if (act && quad == 0) {
+        double* sj = sol + j * (R * B) + k * R;
+#pragma unroll
+        for (int a = 0; a < R; ++a) sj[a] = y[a];
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <int R, int B>
 __global__ __launch_bounds__(kThreads) void k_precond_finish(LaunchCtx c, const double* __restrict__ X,
                                                              const double* __restrict__ zraw,
@@ -2832,6 +2913,13 @@ hipError_t launch_trsv_level(int r, int b, const TrsvView& t, const int* rows, i
     const int grid = (count + kThreads / 4 - 1) / (kThreads / 4);
     DPGO_DISPATCH(r, b, (k_trsv_level<R, B, false><<<grid, kThreads, 0, stream>>>(t, rows, count, rhs, sol)));
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_trsv_chain(int r, int b, const TrsvView& t, const int* aptr, int nblk, const int* rows,
+                             const double* rhs, double* sol, hipStream_t stream) {
+  if (nblk == 0) return hipSuccess;
+  DPGO_DISPATCH(r, b, (k_trsv_chain<R, B><<<nblk, kThreads, 0, stream>>>(t, aptr, rows, rhs, sol)));
   return hipGetLastError();
 }
 

@@ -116,6 +116,14 @@ struct dpgo_hip_problem_s {
   dpgo::DevBuf<double> fw_blk, bw_blk, linv;
   std::vector<int> fw_lvl, bw_lvl;  // level pointers into fw_rows / bw_rows
   std::vector<int> fw_wide, bw_wide;  // per level: its longest row has more entries than a quad should walk
+  // chains: runs of consecutive levels with at most one row per agent (the dense separators near the top of
+  // each agent's elimination tree), solved by one launch with one workgroup per agent walking its rows
+  struct TrsvChain {
+    int l0, l1;      // levels [l0, l1)
+    int a0, nblk;    // its agents' row lists: (fw|bw)_captr[a0 .. a0 + nblk]
+  };
+  std::vector<TrsvChain> fw_chain, bw_chain;
+  dpgo::DevBuf<int> fw_captr, fw_crows, bw_captr, bw_crows;
   long chol_blocks = 0;
 
   // work
