@@ -222,11 +222,18 @@ int dpgo_hip_certify(dpgo_hip_problem h, const double* X, int max_iters, double 
                      double* residual, int* iters, double* eigvec);
 
 /* ---- measurement helpers ----------------------------------------------------------------*/
-/* Select a compiled kernel variant for A/B timing (r = 5, d = 3 only).  key 0: BSR X.Q SpMM
+/* Select a compiled kernel variant / host sequence for A/B timing (process-wide; every setting gives
+ * results within the documented bars, most bitwise the default's).  key 0: BSR X.Q SpMM
  * neighbour-loop variant 0 = 1 neighbour/step (default), 1 = same with non-temporal block loads,
  * 2 = 2 neighbours/step, 3 = 4 neighbours/step, 4 = 4 + XCD-aware tile remap, 5 = 2 + XCD remap,
  * 6 = 1 + XCD remap.  key 1: edge-stream variant for every SpMM mode (same numbering over
- * incidences; -1 = the compiled default). */
+ * incidences; -1 = the compiled default).  key 2: epilogue operands ahead of the edge loop (1, default).
+ * key 3: consumer-side tCG finalize (classic sequence).  key 4: first tCG step kind (0 predicted,
+ * 1 each-edge-once pass, 2 full pass).  key 5: 1 = the classic five-launch tCG iteration instead of the
+ * merged one.  key 6: 1 = HESS_M operands prefetched.  key 7: tCG queueing (0 adaptive, 1 one iteration
+ * ahead, 2 all at once).  key 8: 1 = second-visit record staging (set before Q).  key 9: 1 = the agent
+ * status by its own pass instead of folded into the rho test.  key 10: 1 = the exact preconditioner
+ * level by level (no chained levels).  DESIGN.md records each key's measurement. */
 int dpgo_hip_set_tuning(int key, int value);
 /* Algorithmic HBM bytes of one X.Q SpMM over this handle: BSR blocks + indices + X + Y, or, for
  * an edge-stream Q, every edge record once + 8 B per incidence + pointers + X + Y. */
