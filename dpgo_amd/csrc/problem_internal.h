@@ -161,6 +161,9 @@ struct dpgo_hip_problem_s {
   };
   std::vector<TimedLaunch> timed;
   std::vector<hipEvent_t> ev_pool;
+  // completed timed launches drained out of `timed` (bounded event count on long timed runs)
+  double timed_ms[dpgo::kSpmmModes] = {};
+  long long timed_n[dpgo::kSpmmModes] = {};
   ~dpgo_hip_problem_s() {
     for (auto& t : timed) {
       (void)hipEventDestroy(t.a);
@@ -197,6 +200,8 @@ int eval_sums_dev(dpgo_hip_problem h, const double* X);
 int download_sums_public(dpgo_hip_problem h, std::vector<double>& out);
 // X.Q launch with the handle's optional event timing
 int spmm_launch(dpgo_hip_problem h, int mode, const LaunchCtx& c, const SpmmArgs& a);
-// synchronise and add the elapsed ms / launch counts of the timed launches per SpmmMode (8 modes)
+// synchronise and add the elapsed ms / launch counts of the timed launches per SpmmMode (kSpmmModes)
 int take_spmm_times(dpgo_hip_problem h, double* ms_per_mode, long long* launches_per_mode);
+// fold completed (wait: all) timed launches into the handle's per-mode running totals
+int drain_timed(dpgo_hip_problem h, bool wait);
 }  // namespace dpgo

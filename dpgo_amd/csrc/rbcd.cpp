@@ -927,6 +927,8 @@ int dpgo_rbcd_bytes(dpgo_rbcd e, double* bytes, double* evaltcg_bytes_per_color)
 
 // Algorithmic bytes of ONE X.Q launch per SpMM mode over every agent of a colour (the same per-agent
 // terms as dpgo_rbcd_bytes): the per-launch figure the in-step roofline divides by the launch time.
+static_assert(kSpmmModes == DPGO_SPMM_MODES, "include/dpgo_rbcd.h DPGO_SPMM_MODES != kSpmmModes");
+
 int dpgo_rbcd_mode_bytes(dpgo_rbcd e, int color, double* out) {
   if (!e || !out || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
   const double P = pose_bytes(e), b = e->b, d = e->d;
@@ -1028,6 +1030,8 @@ int dpgo_rbcd_counters(dpgo_rbcd e, long long* agent_updates, long long* iterati
 // RCCL is resolved at run time: the copy already in the process when there is one (the loader matches
 // its soname, so a caller that created the communicator and this library use the same instance),
 // otherwise the system librccl.  Nothing here links RCCL, so the library loads without it.
+static_assert(sizeof(ncclUniqueId) == DPGO_RCCL_ID_BYTES, "DPGO_RCCL_ID_BYTES != sizeof(ncclUniqueId)");
+
 namespace {
 struct RcclApi {
   void* lib = nullptr;

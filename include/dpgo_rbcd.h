@@ -11,8 +11,9 @@
  * one colour class of the agent-adjacency graph is "selected" (doOptimization = true,
  * src/PGOAgent.cpp:642-718); all other agents run iterate(false).  Selected agents on a GPU are
  * solved as ONE batched dpgo_hip_problem (their Q blocks are independent).  Neighbour public poses
- * cross ranks through caller-owned device buffers (the caller moves them with RCCL
- * all_to_all); same-rank neighbours are read directly from device memory.
+ * cross ranks either through the library's own RCCL exchange (dpgo_rbcd_comm_init / dpgo_rbcd_exchange)
+ * or through caller-owned device buffers the caller moves itself (dpgo_rbcd_pack, then e.g. an RCCL
+ * all_to_all, then dpgo_rbcd_update); same-rank neighbours are read directly from device memory.
  * Robust cost: L2 (default, the throughput setting) or any of the reference's RobustCostType with
  * on-device loop-closure reweighting every robust_opt_inner_iters iterations (PGOAgent::iterate +
  * updateLoopClosuresWeights, src/PGOAgent.cpp:642-718, 1174-1244; RobustCost, src/DPGO_robust.cpp).
@@ -196,8 +197,9 @@ int dpgo_rccl_unique_id(void* id_out);
 int dpgo_rbcd_comm_init(dpgo_rbcd e, const void* id);
 int dpgo_rbcd_comm_attach(dpgo_rbcd e, void* comm);
 int dpgo_rbcd_exchange(dpgo_rbcd e, const double** recv_dev);
-/* SpMM modes of the per-mode arrays: XQ, XQ_G, EVAL, HESS, F, EVAL_TCG, CERT, QF, HESS_QF */
-#define DPGO_SPMM_MODES 9
+/* SpMM modes of the per-mode arrays, in this order: XQ, XQ_G, EVAL, HESS, F, EVAL_TCG, CERT, QF, HESS_QF,
+ * HESS_M, HESS_QF_M (the last two: the merged tCG iteration's Hessian passes) */
+#define DPGO_SPMM_MODES 11
 /* Algorithmic bytes of one X.Q launch over every agent of `color`, per SpMM mode (out[DPGO_SPMM_MODES], indexed as
  * dpgo_rbcd_kernel_times; 0 for modes the engine does not launch in a step). */
 int dpgo_rbcd_mode_bytes(dpgo_rbcd e, int color, double* out);

@@ -8,8 +8,30 @@ import platform
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(_HERE, "_build", "libdpgo_cpu.so")
+LIB_V3 = os.path.join(_HERE, "_build", "libdpgo_cpu.so")
+LIB_V4 = os.path.join(_HERE, "_build", "libdpgo_cpu_v4.so")
 _lib = None
+
+
+def _host_flags():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("flags"):
+                return set(line.split(":", 1)[1].split())
+    except OSError:
+        pass
+    return set()
+
+
+def _pick_lib():
+    """The AVX-512 (x86-64-v4) build when the host has it (the GPU box's Zen 5 EPYC), else x86-64-v3."""
+    f = _host_flags()
+    if {"avx512f", "avx512bw", "avx512dq", "avx512vl", "avx512cd"} <= f and os.path.exists(LIB_V4):
+        return LIB_V4, "x86-64-v4 (AVX-512)"
+    return LIB_V3, "x86-64-v3 (AVX2/FMA)"
+
+
+LIB, ISA = _pick_lib()
 
 
 def lib():
@@ -145,6 +167,18 @@ def max_threads():
     return int(lib().dpgo_cpu_max_threads())
 
 
+def host_cores():
+    """(threads the baseline runs, CPUs this process may run on, OpenMP's default team): the baseline uses
+    OpenMP's team (OMP_NUM_THREADS: on the GPU box the pool's per-GPU host share, 16) capped by the affinity
+    mask, never more than a colour's agents can use."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    omp = max_threads()
+    return max(1, min(omp, avail, 32)), avail, omp
+
+
 def engine_baseline(graph, agent_of_pose, X_start, r, accel, num_agents, warmup=3, rounds=20):
     """The like-for-like host baseline: oracle/cpu runs the engine's colour schedule from the GPU's
     timed-region start X (fresh Nesterov, as after set_X), with the reference's preconditioner
@@ -156,7 +190,7 @@ def engine_baseline(graph, agent_of_pose, X_start, r, accel, num_agents, warmup=
     arrays = graph.arrays()
     E = CpuRbcd(graph.d, r, arrays, graph.n, agent_of_pose, num_agents, accel)
     E.set_X(X_start)
-    T = max_threads()
+    T, avail, omp = host_cores()
     per_colour = min(sum(1 for c in E.colors if c == 0), sum(1 for c in E.colors if c == 1) or 10 ** 9)
     ns = min(warmup + rounds, per_colour)
     _, sec = E.iterate(threads=T, timed_serial=ns)  # iteration 0: ns updates serially, the rest in parallel
@@ -171,9 +205,11 @@ def engine_baseline(graph, agent_of_pose, X_start, r, accel, num_agents, warmup=
     upd = float(np.median(sel_counts[warmup:]))
     res = {"value": upd / med, "unit": "RBCD agent-updates/s", "cores": T, "kind": "port",
            "sample": (f"oracle/cpu colour-schedule RBCD (L2, Nesterov={bool(accel)}, block-Jacobi on both sides: "
-                      f"CHOLMOD absent) from the GPU timed region's start X; all cores: median of {rounds} colour "
-                      f"iterations ({upd:.0f} agent updates each, OpenMP over them) after {warmup} warm-up; "
-                      f"one core: median of {max(len(serial) - warmup, 0)} single agent updates after {warmup}"),
+                      f"CHOLMOD absent) from the GPU timed region's start X; {T} OpenMP threads (of {avail} CPUs in "
+                      f"the affinity mask; OMP team {omp}): median of {rounds} colour iterations ({upd:.0f} agent "
+                      f"updates each, OpenMP over them) after {warmup} warm-up; one thread: median of "
+                      f"{max(len(serial) - warmup, 0)} single agent updates after {warmup}"),
+           "threads": T, "affinity_cpus": avail, "omp_max_threads": omp, "isa": ISA,
            "seconds_per_iteration_all_cores": med,
            "single_thread": {"value": 1.0 / one if one > 0 else None, "seconds_per_agent_update": one,
                              "cores": 1},

@@ -203,13 +203,17 @@ def _grid_outliers(hip, k, seed, frac, rng_seed):
     return g, g0, meas
 
 
-@pytest.mark.parametrize("accel,robust,alg", [(False, "L2", "RTR"), (True, "L2", "RTR"), (True, "GNC_TLS", "RTR"),
-                                              (False, "GNC_TLS", "RTR"), (False, "L2", "RGD"), (True, "L2", "RGD")])
-def test_engine_status_and_counters_match_oracle(hip, accel, robust, alg):
+@pytest.mark.parametrize("accel,robust,alg,want", [(False, "L2", "RTR", False), (True, "L2", "RTR", False),
+                                                   (True, "GNC_TLS", "RTR", False), (False, "GNC_TLS", "RTR", False),
+                                                   (False, "L2", "RGD", False), (True, "L2", "RGD", False),
+                                                   (False, "L2", "RGD", True), (True, "L2", "RTR", True)])
+def test_engine_status_and_counters_match_oracle(hip, accel, robust, alg, want):
     """Per selected agent: PGOAgentStatus relativeChange = |X - XPrev| / sqrt(n) and readyToTerminate
     (relChangeTol 5e-3; GNC_TLS: converged loop-closure ratio >= 0.8) after every iteration, and the
     cumulative solver counters (Runs, tCG iterations and exits) over the run, against the oracle's
-    PGOAgent colour schedule (RGD: src/PGOAgent.cpp:1133, QuadraticOptimizer::gradientDescent)."""
+    PGOAgent colour schedule (RGD: src/PGOAgent.cpp:1133, QuadraticOptimizer::gradientDescent).  want: the
+    updates also return per-agent ROPTResults (the in-place update's status must not be recomputed from the
+    overwritten XPrev)."""
     k, A, r = 6, 2, 5
     if robust == "L2":
         g, meas = _grid_meas(hip, k, 3)
@@ -231,7 +235,9 @@ def test_engine_status_and_counters_match_oracle(hip, accel, robust, alg):
     for it in range(iters):
         c = it % e.num_colors
         e.pre_exchange(c)
-        e.update(c, None)
+        res = e.update(c, None, want_results=want)
+        if want:
+            assert len(res) == int(e.agents_per_color[c])
     out = np.zeros(X0.size)
     e.get_X_into(out)
     assert rel(hip.from_dev_layout(out, r), Xo) <= 1e-9

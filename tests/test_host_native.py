@@ -216,3 +216,24 @@ def test_cpu_engine_matches_oracle_colour_schedule(accel):
         else:
             pending.append(t)
     assert list(st[:, 2]) == list(runs)
+
+
+def build_abi_check(tmp_path):
+    """tests/c/abi_check.c compiled against include/*.h and linked to the in-tree libdpgo_hip.so."""
+    exe = str(tmp_path / "abi_check")
+    libdir = os.path.join(ROOT, "dpgo_amd")
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    "-I", "/opt/rocm/include", os.path.join(ROOT, "tests", "c", "abi_check.c"), "-o", exe,
+                    "-L", libdir, "-ldpgo_hip", "-Wl,-rpath," + libdir], check=True)
+    return exe
+
+
+def test_c_header_constants_match_library(H, tmp_path):
+    """A C caller sizes its per-mode / per-agent arrays from the header: the header's constants must be the
+    library's (the Python binding's mode list is the library's kSpmmModes order)."""
+    exe = build_abi_check(tmp_path)
+    out = subprocess.run([exe, "consts"], capture_output=True, text=True, check=True).stdout
+    vals = dict((k, int(v)) for k, v in (ln.split() for ln in out.strip().splitlines()))
+    assert vals["DPGO_SPMM_MODES"] == len(H.SPMM_MODES) == 11
+    assert vals["DPGO_STATS_INTS"] == H.STATS_INTS
+    assert vals["DPGO_RCCL_ID_BYTES"] == 128
