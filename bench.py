@@ -86,6 +86,9 @@ def main():
     ap.add_argument("--exchange", default="torch", choices=["torch", "native"],
                     help="N > 1 halo exchange: torch.distributed all_to_all_single (RCCL), or the library's own "
                          "RCCL group send/recv (dpgo_rbcd_comm_init / dpgo_rbcd_exchange)")
+    ap.add_argument("--halo", default="color", choices=["color", "full"],
+                    help="N > 1: color = per-colour halo (only the poses the selected colour's agents read, "
+                         "dpgo_rbcd_pack_color / update_color); full = every public pose every iteration")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--boundary-leg", type=int, default=1,
                     help="also time the same steps from the odometry chain initialisation (round 1's regime: every "
@@ -176,10 +179,32 @@ def main():
             dist.all_to_all_single(recv, send, out_splits, in_splits)
         return recv.data_ptr()
 
+    # per-colour halos: splits and views per colour (the buffers are sized by the full plan)
+    c_in = [[int(x) for x in v] for v in eng.send_counts_color]
+    c_out = [[int(x) for x in v] for v in eng.recv_counts_color]
+
+    def exchange_color(c):
+        if world == 1:
+            return None
+        if native:
+            return eng.exchange_color(c)
+        eng.pack_color(c, send.data_ptr())
+        ns, nr = sum(c_in[c]), sum(c_out[c])
+        if one_device:
+            recv_h = torch.empty(nr, dtype=recv.dtype)
+            dist.all_to_all_single(recv_h, send[:ns].cpu(), c_out[c], c_in[c])
+            recv[:nr].copy_(recv_h)
+        else:
+            dist.all_to_all_single(recv[:nr], send[:ns], c_out[c], c_in[c])
+        return recv.data_ptr()
+
     def step():
         for c in range(eng.num_colors):
             eng.pre_exchange(c)
-            eng.update(c, exchange())
+            if args.halo == "color":
+                eng.update_color(c, exchange_color(c))
+            else:
+                eng.update(c, exchange())
 
     def central():
         """Central cost and |RieGrad| of the whole graph (examples/MultiRobotExample.cpp:229-235)."""
@@ -297,9 +322,10 @@ def main():
     elif one_device:
         par = f"{world} ranks on ONE device (rehearsal), halo all_to_all over gloo through host copies"
     elif native:
-        par = f"agents over {world} GPUs (2x2x2 super-cubes), halo by the library's RCCL group send/recv over xGMI"
+        par = (f"agents over {world} GPUs (2x2x2 super-cubes), {args.halo} halo by the library's RCCL group "
+               f"send/recv over xGMI")
     else:
-        par = f"agents over {world} GPUs (2x2x2 super-cubes), halo all_to_all_single over RCCL/xGMI"
+        par = f"agents over {world} GPUs (2x2x2 super-cubes), {args.halo} halo all_to_all_single over RCCL/xGMI"
     out = {
         "metric": METRIC,
         "value": value,
@@ -362,6 +388,10 @@ def main():
         "setup_s": setup_s,
         "init": init_info,
     }
+    out["halo"] = {"kind": args.halo if world > 1 else "none (one rank)",
+                   "bytes_sent_per_step_this_rank": 8.0 * (sum(sum(v) for v in c_in) if args.halo == "color"
+                                                           else eng.num_colors * int(eng.send_counts.sum())),
+                   "full_plan_bytes_per_exchange": 8.0 * int(eng.send_counts.sum())}
     if X_start is not None:
         try:
             from oracle import cpu_port

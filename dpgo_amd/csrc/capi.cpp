@@ -7,13 +7,17 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
+#include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "chol_internal.h"
@@ -366,10 +370,10 @@ int sync_q(dpgo_hip_problem h) {
 // ---------------------------------------------------------------------------------------------
 // Exact preconditioner: the reference factorises P = Q + 0.1 I with CHOLMOD in
 // setQ (src/QuadraticProblem.cpp:37-41).  Here the factor is built on the host the first time the
-// EXACT mode is used after a setQ, per agent (agents are independent blocks), and uploaded as
-// forward / backward block rows plus a level schedule shared by the batch (level l of every agent
-// runs in one launch).
-constexpr size_t kMaxCholBlocks = 40u * 1000u * 1000u;
+// EXACT mode is used after a setQ, per agent (agents are independent blocks, factorised in parallel
+// host threads), as nested-dissection supernodes (chol.cpp), and uploaded as dense panels plus one
+// work list per tree level shared by the batch (level l of every agent runs in one launch per sweep).
+constexpr long kMaxCholDoubles = 3L << 30;  // 24 GiB of panels per handle
 
 void agent_bsr(dpgo_hip_problem h, int a, HostBSR& out) {
   if (h->q_fmt[a] == dpgo::QFMT_BSR) {
@@ -398,6 +402,19 @@ void agent_bsr(dpgo_hip_problem h, int a, HostBSR& out) {
   out = std::move(B.out);
 }
 
+// host threads for the per-agent factorisations: DPGO_CHOL_THREADS, else OMP_NUM_THREADS (the GPU box
+// sets it to the per-GPU host share), else the hardware count, at most 16
+int chol_threads(int K) {
+  int t = 0;
+  for (const char* var : {"DPGO_CHOL_THREADS", "OMP_NUM_THREADS"})
+    if (const char* s = std::getenv(var)) {
+      t = std::atoi(s);
+      if (t > 0) break;
+    }
+  if (t <= 0) t = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  return std::max(1, std::min(t, K));
+}
+
 int sync_chol(dpgo_hip_problem h) {
   if (h->chol_state != 0) return DPGO_HIP_OK;
   if (h->host_weights_stale) {  // weights changed on the device: bring the host measurement copy up to date
@@ -414,209 +431,185 @@ int sync_chol(dpgo_hip_problem h) {
     }
     h->host_weights_stale = false;
   }
-  const int b = h->b, bb = b * b;
-  std::vector<int> fptr(h->N + 1, 0), bptr(h->N + 1, 0), fcol, bcol, flev(h->N, 0), blev(h->N, 0);
-  std::vector<double> fblk, bblk, linv(static_cast<size_t>(h->N) * bb, 0.0);
-  // per pose (global) forward / backward entries, collected then laid out in CSR
-  std::vector<std::vector<std::pair<int, long>>> frow(h->N), brow(h->N);
-  std::vector<dpgo::BlockCholesky> Ls(h->K);
-  long blocks = 0;
-  for (int a = 0; a < h->K; ++a) {
-    HostBSR Q;
-    agent_bsr(h, a, Q);
-    std::string err;
-    if (dpgo::block_cholesky(h->n_agent[a], b, Q.rowptr, Q.col, Q.blocks, 0.1, kMaxCholBlocks - blocks, Ls[a], err) !=
-        0) {
-      if (err.find("positive definite") != std::string::npos) {
+  const int b = h->b, r = h->r, K = h->K;
+  // ---- per-agent factorisations, in parallel host threads
+  std::vector<dpgo::SupernodalFactor> Fs(K);
+  std::vector<std::string> errs(K);
+  std::vector<int> rcs(K, 0);
+  {
+    std::atomic<int> next{0}, done{0};
+    const auto t0 = std::chrono::steady_clock::now();
+    std::mutex log_mu;
+    auto work = [&]() {
+      for (int a = next++; a < K; a = next++) {
+        HostBSR Q;
+        agent_bsr(h, a, Q);
+        rcs[a] = dpgo::supernodal_cholesky(h->n_agent[a], b, Q.rowptr, Q.col, Q.blocks, 0.1, kMaxCholDoubles, Fs[a],
+                                           errs[a]);
+        // a long factorisation reports progress (a silent process looks hung to a supervisor)
+        const int k = ++done;
+        const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (sec > 5.0) {
+          std::lock_guard<std::mutex> lk(log_mu);
+          std::fprintf(stderr, "[dpgo_hip] exact preconditioner: %d / %d agents factorised (%.1f s)\n", k, K, sec);
+        }
+      }
+    };
+    const int nt = chol_threads(K);
+    std::vector<std::thread> pool;
+    for (int i = 1; i < nt; ++i) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+  }
+  long total = 0;
+  for (int a = 0; a < K; ++a) {
+    if (rcs[a] != 0) {
+      if (errs[a].find("positive definite") != std::string::npos) {
         // src/QuadraticProblem.cpp:81-86: the solve fails -> "Preconditioner failed", out = in
-        std::printf("[dpgo_hip] Preconditioner failed (agent %d: %s); using the identity.\n", a, err.c_str());
+        std::printf("[dpgo_hip] Preconditioner failed (agent %d: %s); using the identity.\n", a, errs[a].c_str());
         h->chol_state = 2;
         return DPGO_HIP_OK;
       }
-      return fail(DPGO_HIP_EINVAL, err);
+      return fail(DPGO_HIP_EINVAL, errs[a]);
     }
-    blocks += static_cast<long>(Ls[a].rowidx.size());
+    total += Fs[a].panel_doubles;
   }
-  for (int a = 0; a < h->K; ++a) {
-    const dpgo::BlockCholesky& L = Ls[a];
+  if (total > kMaxCholDoubles)
+    return fail(DPGO_HIP_EINVAL, "exact preconditioner: the supernodal panels of the batch would exceed 24 GiB "
+                                 "(use DPGO_PRECON_BLOCK_JACOBI for this size)");
+  // ---- the batch's node list (agents in order, each in postorder), work lists per tree level
+  std::vector<int> base(K + 1, 0);
+  for (int a = 0; a < K; ++a) base[a + 1] = base[a] + static_cast<int>(Fs[a].nodes.size());
+  const int nn = base[K];
+  std::vector<long> panel_off(nn), f_off(nn), u_off(nn);
+  std::vector<int> s_(nn), t_(nn), poses_off(nn), poses, cpos_off(nn), cpos;
+  std::vector<int2> contrib;
+  int maxd = 0;
+  long fo = 0, uo = 0, po = 0;
+  for (int a = 0; a < K; ++a) {
+    const auto& nodes = Fs[a].nodes;
     const long off = h->pose_off[a];
-    auto G = [&](int newi) { return static_cast<int>(off + L.perm[newi]); };
-    std::vector<int> lf(L.n, 0), lb(L.n, 0);
-    for (int k = 0; k < L.n; ++k) {
-      for (int p = L.colptr[k] + 1; p < L.colptr[k + 1]; ++p) {
-        const int i = L.rowidx[p];
-        lf[i] = std::max(lf[i], lf[k] + 1);
-        frow[G(i)].push_back({G(k), static_cast<long>(a) << 40 | p});  // F_ik = L_ik^T
-        brow[G(k)].push_back({G(i), static_cast<long>(a) << 40 | p});  // L_ik
+    for (size_t x = 0; x < nodes.size(); ++x) {
+      const int g = base[a] + static_cast<int>(x);
+      const dpgo::SnNode& nd = nodes[x];
+      const int s = static_cast<int>(nd.S.size()), t = static_cast<int>(nd.R.size());
+      s_[g] = s;
+      t_[g] = t;
+      panel_off[g] = po;
+      po += static_cast<long>(nd.panel.size());
+      f_off[g] = fo;
+      fo += static_cast<long>(dpgo::sn_pad(s * b) + dpgo::sn_pad(t * b)) * r;
+      u_off[g] = uo;
+      uo += static_cast<long>(t) * b * r;
+      poses_off[g] = static_cast<int>(poses.size());
+      for (int v : nd.S) poses.push_back(static_cast<int>(off + v));
+      for (int v : nd.R) poses.push_back(static_cast<int>(off + v));
+      // per frontal position, its children's contributions in child order
+      std::vector<std::vector<int2>> at(s + t);
+      for (int c : nd.children) {
+        const dpgo::SnNode& ch = nodes[c];
+        for (size_t i = 0; i < ch.R.size(); ++i) at[ch.to_parent[i]].push_back(make_int2(base[a] + c, static_cast<int>(i)));
       }
-      // diagonal inverse (lower triangular) -> linv row-major
-      const double* D = &L.blocks[static_cast<size_t>(L.colptr[k]) * bb];
-      double* Iv = &linv[static_cast<size_t>(G(k)) * bb];
-      for (int c = 0; c < b; ++c) {  // column c of D^-1 by forward substitution on e_c
-        for (int u = 0; u < b; ++u) {
-          double s = (u == c) ? 1.0 : 0.0;
-          for (int w = 0; w < u; ++w) s -= D[u * b + w] * Iv[w * b + c];
-          Iv[u * b + c] = s / D[u * b + u];
+      cpos_off[g] = static_cast<int>(cpos.size());
+      cpos.push_back(static_cast<int>(contrib.size()));
+      for (int p = 0; p < s + t; ++p) {
+        contrib.insert(contrib.end(), at[p].begin(), at[p].end());
+        cpos.push_back(static_cast<int>(contrib.size()));
+      }
+      maxd = std::max(maxd, nd.depth);
+    }
+  }
+  std::vector<int2> items;
+  h->sn_levels.assign(maxd + 1, {});
+  for (int dep = 0; dep <= maxd; ++dep) {
+    auto& L = h->sn_levels[dep];
+    L.asm0 = static_cast<int>(items.size());
+    for (int a = 0; a < K; ++a)
+      for (size_t x = 0; x < Fs[a].nodes.size(); ++x)
+        if (Fs[a].nodes[x].depth == dep) {
+          const int g = base[a] + static_cast<int>(x);
+          const int rows = dpgo::sn_pad(s_[g] * b) + dpgo::sn_pad(t_[g] * b);
+          for (int blk = 0; blk * dpgo::kThreads < rows; ++blk) items.push_back(make_int2(g, blk));
         }
-      }
-    }
-    for (int j = L.n - 1; j >= 0; --j)
-      for (int p = L.colptr[j] + 1; p < L.colptr[j + 1]; ++p) lb[j] = std::max(lb[j], lb[L.rowidx[p]] + 1);
-    for (int j = 0; j < L.n; ++j) {
-      flev[G(j)] = lf[j];
-      blev[G(j)] = lb[j];
-    }
+    L.asm_n = static_cast<int>(items.size()) - L.asm0;
+    L.fwd0 = static_cast<int>(items.size());
+    for (int a = 0; a < K; ++a)
+      for (size_t x = 0; x < Fs[a].nodes.size(); ++x)
+        if (Fs[a].nodes[x].depth == dep) {
+          const int g = base[a] + static_cast<int>(x);
+          const int nI = (dpgo::sn_pad(s_[g] * b) + dpgo::sn_pad(t_[g] * b)) / dpgo::kSnTile;
+          for (int I = 0; I < nI; ++I) items.push_back(make_int2(g, I));
+        }
+    L.fwd_n = static_cast<int>(items.size()) - L.fwd0;
+    L.bwd0 = static_cast<int>(items.size());
+    for (int a = 0; a < K; ++a)
+      for (size_t x = 0; x < Fs[a].nodes.size(); ++x)
+        if (Fs[a].nodes[x].depth == dep) {
+          const int g = base[a] + static_cast<int>(x);
+          const int nJ = dpgo::sn_pad(s_[g] * b) / dpgo::kSnTile;
+          for (int J = 0; J < nJ; ++J) items.push_back(make_int2(g, J));
+        }
+    L.bwd_n = static_cast<int>(items.size()) - L.bwd0;
   }
-  auto block_of = [&](long code) -> const double* {
-    const int a = static_cast<int>(code >> 40);
-    const long p = code & ((1L << 40) - 1);
-    return &Ls[a].blocks[static_cast<size_t>(p) * bb];
-  };
-  for (long j = 0; j < h->N; ++j) {
-    for (auto& [k, code] : frow[j]) {
-      fcol.push_back(k);
-      const double* Lb = block_of(code);
-      for (int u = 0; u < b; ++u)
-        for (int v = 0; v < b; ++v) fblk.push_back(Lb[v * b + u]);  // transpose
-    }
-    fptr[j + 1] = static_cast<int>(fcol.size());
-    for (auto& [i, code] : brow[j]) {
-      bcol.push_back(i);
-      const double* Lb = block_of(code);
-      bblk.insert(bblk.end(), Lb, Lb + bb);
-    }
-    bptr[j + 1] = static_cast<int>(bcol.size());
-  }
-  auto schedule = [&](const std::vector<int>& lev, std::vector<int>& rows, std::vector<int>& lptr) {
-    int nl = 0;
-    for (int x : lev) nl = std::max(nl, x + 1);
-    lptr.assign(nl + 1, 0);
-    for (int x : lev) ++lptr[x + 1];
-    for (int l = 0; l < nl; ++l) lptr[l + 1] += lptr[l];
-    rows.assign(lev.size(), 0);
-    std::vector<int> fill(lptr.begin(), lptr.end() - 1);
-    for (long j = 0; j < static_cast<long>(lev.size()); ++j) rows[fill[lev[j]]++] = static_cast<int>(j);
-  };
-  std::vector<int> frows, brows;
-  schedule(flev, frows, h->fw_lvl);
-  schedule(blev, brows, h->bw_lvl);
-  // levels whose longest row is long (the dense separator rows near the top of the elimination tree) run
-  // one wave per row instead of one quad per row
-  auto wide = [&](const std::vector<int>& lptr, const std::vector<int>& rows, const std::vector<int>& ptr,
-                  std::vector<int>& out) {
-    out.assign(lptr.empty() ? 0 : lptr.size() - 1, 0);
-    for (size_t l = 0; l + 1 < lptr.size(); ++l) {
-      int mx = 0;
-      for (int x = lptr[l]; x < lptr[l + 1]; ++x) mx = std::max(mx, ptr[rows[x] + 1] - ptr[rows[x]]);
-      out[l] = mx > dpgo::kTrsvWideRow ? 1 : 0;
-    }
-  };
-  wide(h->fw_lvl, frows, fptr, h->fw_wide);
-  wide(h->bw_lvl, brows, bptr, h->bw_wide);
-  std::vector<int> agent_of(h->N, 0);
-  for (int a = 0; a < h->K; ++a)
-    for (long p = h->pose_off[a]; p < h->pose_off[a] + h->n_agent[a]; ++p) agent_of[p] = a;
-  auto chains = [&](const std::vector<int>& lptr, const std::vector<int>& rows, std::vector<dpgo_hip_problem_s::TrsvChain>& out,
-                    std::vector<int>& captr, std::vector<int>& crows) {
-    out.clear();
-    captr.assign(1, 0);
-    crows.clear();
-    const int nl = lptr.empty() ? 0 : static_cast<int>(lptr.size()) - 1;
-    std::vector<int> seen(h->K, -1);
-    auto chainable = [&](int l) {
-      for (int x = lptr[l]; x < lptr[l + 1]; ++x) {
-        const int a = agent_of[rows[x]];
-        if (seen[a] == l) return false;
-        seen[a] = l;
-      }
-      return true;
-    };
-    int l = 0;
-    while (l < nl) {
-      int e = l;
-      while (e < nl && chainable(e)) ++e;
-      if (e - l >= 2) {  // levels [l, e): per agent its rows in level order
-        std::vector<std::vector<int>> per(h->K);
-        for (int m = l; m < e; ++m)
-          for (int x = lptr[m]; x < lptr[m + 1]; ++x) per[agent_of[rows[x]]].push_back(rows[x]);
-        dpgo_hip_problem_s::TrsvChain c{l, e, static_cast<int>(captr.size()) - 1, 0};
-        for (int a = 0; a < h->K; ++a)
-          if (!per[a].empty()) {
-            crows.insert(crows.end(), per[a].begin(), per[a].end());
-            captr.push_back(static_cast<int>(crows.size()));
-            ++c.nblk;
-          }
-        out.push_back(c);
-        l = e;
-      } else {
-        l = std::max(e, l + 1);
-      }
-    }
-  };
-  std::vector<int> fcaptr, fcrows, bcaptr, bcrows;
-  chains(h->fw_lvl, frows, h->fw_chain, fcaptr, fcrows);
-  chains(h->bw_lvl, brows, h->bw_chain, bcaptr, bcrows);
-  auto up_i = [&](DevBuf<int>& d, const std::vector<int>& v) -> int {
+  // ---- upload
+  auto up = [&](auto& d, const auto& v) -> int {
+    using T = typename std::decay_t<decltype(v)>::value_type;
     HIP_TRY(d.ensure(std::max<size_t>(v.size(), 1)));
-    if (!v.empty()) HIP_TRY(hipMemcpyAsync(d.p, v.data(), sizeof(int) * v.size(), hipMemcpyHostToDevice, h->stream));
+    if (!v.empty()) HIP_TRY(hipMemcpy(d.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
     return DPGO_HIP_OK;
   };
-  auto up_d = [&](DevBuf<double>& d, const std::vector<double>& v) -> int {
-    HIP_TRY(d.ensure(std::max<size_t>(v.size(), 1)));
-    if (!v.empty())
-      HIP_TRY(hipMemcpyAsync(d.p, v.data(), sizeof(double) * v.size(), hipMemcpyHostToDevice, h->stream));
-    return DPGO_HIP_OK;
-  };
-  DPGO_TRY(up_i(h->fw_ptr, fptr));
-  DPGO_TRY(up_i(h->fw_col, fcol));
-  DPGO_TRY(up_d(h->fw_blk, fblk));
-  DPGO_TRY(up_i(h->bw_ptr, bptr));
-  DPGO_TRY(up_i(h->bw_col, bcol));
-  DPGO_TRY(up_d(h->bw_blk, bblk));
-  DPGO_TRY(up_d(h->linv, linv));
-  DPGO_TRY(up_i(h->fw_rows, frows));
-  DPGO_TRY(up_i(h->bw_rows, brows));
-  DPGO_TRY(up_i(h->fw_captr, fcaptr));
-  DPGO_TRY(up_i(h->fw_crows, fcrows));
-  DPGO_TRY(up_i(h->bw_captr, bcaptr));
-  DPGO_TRY(up_i(h->bw_crows, bcrows));
   HIP_TRY(hipStreamSynchronize(h->stream));
-  h->chol_blocks = blocks;
+  HIP_TRY(h->sn_panel.ensure(std::max<long>(po, 1)));
+  for (int a = 0; a < K; ++a) {
+    for (size_t x = 0; x < Fs[a].nodes.size(); ++x) {
+      const auto& P = Fs[a].nodes[x].panel;
+      if (!P.empty())
+        HIP_TRY(hipMemcpy(h->sn_panel.p + panel_off[base[a] + x], P.data(), sizeof(double) * P.size(),
+                          hipMemcpyHostToDevice));
+    }
+    dpgo::SupernodalFactor().nodes.swap(Fs[a].nodes);  // release the host panels
+  }
+  DPGO_TRY(up(h->sn_panel_off, panel_off));
+  DPGO_TRY(up(h->sn_f_off, f_off));
+  DPGO_TRY(up(h->sn_u_off, u_off));
+  DPGO_TRY(up(h->sn_s, s_));
+  DPGO_TRY(up(h->sn_t, t_));
+  DPGO_TRY(up(h->sn_poses_off, poses_off));
+  DPGO_TRY(up(h->sn_poses, poses));
+  DPGO_TRY(up(h->sn_cpos_off, cpos_off));
+  DPGO_TRY(up(h->sn_cpos, cpos));
+  DPGO_TRY(up(h->sn_contrib, contrib));
+  DPGO_TRY(up(h->sn_items, items));
+  HIP_TRY(h->sn_F.ensure(std::max<long>(fo, 1)));
+  HIP_TRY(h->sn_U.ensure(std::max<long>(uo, 1)));
+  h->chol_doubles = po;
   h->chol_state = 1;
   return DPGO_HIP_OK;
 }
 
-// z = P_X(in (Q + 0.1 I)^-1) for every agent (QuadraticProblem::PreConditioner, :75-87): forward
-// and backward level sweeps into the tA / tB work vectors, then projection + partials <z, rref>,
-// |rref|^2 (pass rref = in).  With a failed factorisation z = in, unprojected, as the reference.
+// z = P_X(in (Q + 0.1 I)^-1) for every agent (QuadraticProblem::PreConditioner, :75-87): the forward sweep
+// up the supernodal trees into tA, the backward sweep down into tB (one launch per level and kernel), then
+// projection + partials <z, rref>, |rref|^2 (pass rref = in).  With a failed factorisation z = in,
+// unprojected, as the reference.
 int exact_precond(dpgo_hip_problem h, const double* in, double* z_out, double* delta_out, const double* X,
                   const double* rref, double* partials, int flag) {
   DPGO_TRY(sync_chol(h));
   const double* zraw = in;
   if (h->chol_state == 1) {
-    const dpgo::TrsvView fw{h->fw_ptr.p, h->fw_col.p, h->fw_blk.p, h->linv.p, 1};
-    const dpgo::TrsvView bw{h->bw_ptr.p, h->bw_col.p, h->bw_blk.p, h->linv.p, 0};
-    // level by level, except chains of levels with one row per agent: one launch per chain
-    auto sweep = [&](const dpgo::TrsvView& t, const std::vector<int>& lvl, const std::vector<int>& wide_l,
-                     const DevBuf<int>& rows, const std::vector<dpgo_hip_problem_s::TrsvChain>& ch,
-                     const DevBuf<int>& captr, const DevBuf<int>& crows, const double* rhs, double* sol) -> int {
-      const bool use_chains = dpgo::g_tuning[dpgo::TUNE_TRSV_CHAINS] == 0;
-      size_t c = 0;
-      for (size_t l = 0; l + 1 < lvl.size();) {
-        while (c < ch.size() && static_cast<size_t>(ch[c].l0) < l) ++c;
-        if (use_chains && c < ch.size() && static_cast<size_t>(ch[c].l0) == l) {
-          HIP_TRY(dpgo::launch_trsv_chain(h->r, h->b, t, captr.p + ch[c].a0, ch[c].nblk, crows.p, rhs, sol, h->stream));
-          l = static_cast<size_t>(ch[c].l1);
-          continue;
-        }
-        HIP_TRY(dpgo::launch_trsv_level(h->r, h->b, t, rows.p + lvl[l], lvl[l + 1] - lvl[l], rhs, sol, h->stream,
-                                        wide_l[l]));
-        ++l;
-      }
-      return DPGO_HIP_OK;
-    };
-    DPGO_TRY(sweep(fw, h->fw_lvl, h->fw_wide, h->fw_rows, h->fw_chain, h->fw_captr, h->fw_crows, in, h->tA.p));
-    DPGO_TRY(sweep(bw, h->bw_lvl, h->bw_wide, h->bw_rows, h->bw_chain, h->bw_captr, h->bw_crows, h->tA.p, h->tB.p));
+    const dpgo::SnView v{h->sn_panel.p, h->sn_panel_off.p, h->sn_s.p,    h->sn_t.p,    h->sn_poses_off.p,
+                         h->sn_poses.p, h->sn_f_off.p,     h->sn_u_off.p, h->sn_cpos_off.p, h->sn_cpos.p,
+                         h->sn_contrib.p, h->sn_F.p,       h->sn_U.p};
+    const int2* it = h->sn_items.p;
+    const int nl = static_cast<int>(h->sn_levels.size());
+    for (int l = nl - 1; l >= 0; --l) {
+      const auto& L = h->sn_levels[l];
+      HIP_TRY(dpgo::launch_sn_assemble(h->r, h->b, v, it + L.asm0, L.asm_n, in, h->stream));
+      HIP_TRY(dpgo::launch_sn_fwd(h->r, h->b, v, it + L.fwd0, L.fwd_n, h->tA.p, h->stream));
+    }
+    for (int l = 0; l < nl; ++l) {
+      const auto& L = h->sn_levels[l];
+      HIP_TRY(dpgo::launch_sn_bwd(h->r, h->b, v, it + L.bwd0, L.bwd_n, h->tA.p, h->tB.p, h->stream));
+    }
     zraw = h->tB.p;
   }
   auto c = make_ctx(h, flag, partials);
@@ -1447,6 +1440,7 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
       dpgo::FinalizeArgs fin = make_fin(h, op, h->pa.p, 7, nullptr, 0, &os, nullptr, publish ? 1 : 0, tag);
       fin.pc = h->peh.p;
       fin.nq_c = 1;
+      fin.dd_mask = 0x7E;  // |r|^2 .. <Minv Hd, Hd> are double-double partials (k_spmm MODE_HESS_M)
       DPGO_TRY(spmm_then_finalize(h, mode, ch, sa, fin));
       auto cu = make_ctx(h, dpgo::FLAG_TCG_MODE, h->peh.p);
       HIP_TRY(dpgo::launch_tcg_updir(r, b, cu, x1, h->minv.p, pmode, h->delta.p, h->Hdelta.p, h->eta.p,

@@ -116,6 +116,48 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+
+// ---- double-double (hi + lo, |lo| <= ulp(hi) / 2): exact products and compensated sums for the merged
+// tCG iteration's one-step polynomials, whose terms cancel by the tCG's residual drop (kernels.hip,
+// merged_stop_test).  Error-free transformations: two_sum (Knuth), two_prod (FMA).  Nothing here may be
+// reassociated; hipcc does not (no fast-math) and contraction cannot touch the add-only sequences.
+struct dd {
+  double hi, lo;
+};
+__device__ __forceinline__ dd dd_fast2(double a, double b) {  // |a| >= |b|
+  const double s = a + b;
+  return {s, b - (s - a)};
+}
+__device__ __forceinline__ dd dd_two_sum(double a, double b) {
+  const double s = a + b, bb = s - a;
+  return {s, (a - (s - bb)) + (b - bb)};
+}
+__device__ __forceinline__ dd dd_add(dd x, dd y) {
+  const dd s = dd_two_sum(x.hi, y.hi);
+  return dd_fast2(s.hi, s.lo + (x.lo + y.lo));
+}
+// x + a b with the product exact
+__device__ __forceinline__ dd dd_fma(dd x, double a, double b) {
+  const double p = a * b;
+  return dd_add(x, {p, __builtin_fma(a, b, -p)});
+}
+__device__ __forceinline__ dd dd_mul_d(dd x, double a) {
+  const double p = x.hi * a;
+  return dd_fast2(p, __builtin_fma(x.hi, a, -p) + x.lo * a);
+}
+__device__ __forceinline__ double dd_val(dd x) { return x.hi + x.lo; }
+
+// wave_sum in double-double (same pairs, same order; valid in lane 0 only)
+__device__ __forceinline__ dd wave_sum_dd(dd v) {
+  v = dd_add(v, {lane_plus32(v.hi), lane_plus32(v.lo)});
+  v = dd_add(v, {lane_plus16(v.hi), lane_plus16(v.lo)});
+  v = dd_add(v, {dpp_f64<0x108>(v.hi), dpp_f64<0x108>(v.lo)});
+  v = dd_add(v, {dpp_f64<0x104>(v.hi), dpp_f64<0x104>(v.lo)});
+  v = dd_add(v, {dpp_f64<0x102>(v.hi), dpp_f64<0x102>(v.lo)});
+  v = dd_add(v, {dpp_f64<0x101>(v.hi), dpp_f64<0x101>(v.lo)});
+  return v;
+}
+
 // Reduce-scatter over the quad: lane k ends with col = sum over the 4 lanes of acc[:, k].  Round 1
 // (lanes k, k^1) sums the two columns of k's parity, round 2 (lanes k, k^2) column k: the same
 // additions in the same order as qsum, so the result equals qsum's bitwise.

@@ -110,48 +110,8 @@ struct SysBuilder {
   }
 };
 
-// Direct solve with the host block Cholesky (blocks handed over column-major); rhs [row][bs][nr]
+// Direct solve with the host supernodal Cholesky (blocks handed over column-major); rhs [row][bs][nr]
 int solve_direct(const BlockSys& S, int nr, std::vector<double>& rhs_x, std::string& err);
-
-// Solve (L L^T) x = rhs in place; rhs indexed by the ORIGINAL pose order, b values per pose.
-void chol_solve(const BlockCholesky& L, std::vector<double>& rhs) {
-  const int n = L.n, b = L.b, bb = b * b;
-  std::vector<double> y(static_cast<size_t>(n) * b);
-  for (int j = 0; j < n; ++j)
-    for (int u = 0; u < b; ++u) y[static_cast<size_t>(j) * b + u] = rhs[static_cast<size_t>(L.perm[j]) * b + u];
-  for (int j = 0; j < n; ++j) {  // forward: L y = rhs, by columns
-    const double* D = &L.blocks[static_cast<size_t>(L.colptr[j]) * bb];
-    double* yj = &y[static_cast<size_t>(j) * b];
-    for (int u = 0; u < b; ++u) {
-      double s = yj[u];
-      for (int w = 0; w < u; ++w) s -= D[u * b + w] * yj[w];
-      yj[u] = s / D[u * b + u];
-    }
-    for (int p = L.colptr[j] + 1; p < L.colptr[j + 1]; ++p) {
-      const double* Lij = &L.blocks[static_cast<size_t>(p) * bb];
-      double* yi = &y[static_cast<size_t>(L.rowidx[p]) * b];
-      for (int u = 0; u < b; ++u)
-        for (int w = 0; w < b; ++w) yi[u] -= Lij[u * b + w] * yj[w];
-    }
-  }
-  for (int j = n - 1; j >= 0; --j) {  // backward: L^T x = y
-    double* yj = &y[static_cast<size_t>(j) * b];
-    for (int p = L.colptr[j] + 1; p < L.colptr[j + 1]; ++p) {
-      const double* Lij = &L.blocks[static_cast<size_t>(p) * bb];
-      const double* xi = &y[static_cast<size_t>(L.rowidx[p]) * b];
-      for (int w = 0; w < b; ++w)
-        for (int u = 0; u < b; ++u) yj[w] -= Lij[u * b + w] * xi[u];
-    }
-    const double* D = &L.blocks[static_cast<size_t>(L.colptr[j]) * bb];
-    for (int u = b - 1; u >= 0; --u) {
-      double s = yj[u];
-      for (int w = u + 1; w < b; ++w) s -= D[w * b + u] * yj[w];
-      yj[u] = s / D[u * b + u];
-    }
-  }
-  for (int j = 0; j < n; ++j)
-    for (int u = 0; u < b; ++u) rhs[static_cast<size_t>(L.perm[j]) * b + u] = y[static_cast<size_t>(j) * b + u];
-}
 
 // projectToRotationGroup (src/DPGO_utils.cpp:478-492) of a d x d row-major matrix: U V^T from a
 // one-sided Jacobi SVD; if det(U) det(V) < 0 the column of U with the smallest singular value
@@ -219,13 +179,13 @@ int solve_direct(const BlockSys& S, int nr, std::vector<double>& rhs_x, std::str
   for (size_t k = 0; k < S.col.size(); ++k)
     for (int u = 0; u < bs; ++u)
       for (int v = 0; v < bs; ++v) cm[k * b2 + v * bs + u] = S.blk[k * b2 + u * bs + v];
-  BlockCholesky L;
-  if (block_cholesky(n, bs, S.rowptr, S.col, cm, 0.0, 200u * 1000u * 1000u, L, err) != 0) return -1;
+  SupernodalFactor L;
+  if (supernodal_cholesky(n, bs, S.rowptr, S.col, cm, 0.0, 1L << 31, L, err) != 0) return -1;
   for (int a = 0; a < nr; ++a) {
     std::vector<double> x(static_cast<size_t>(n) * bs);
     for (int p = 0; p < n; ++p)
       for (int v = 0; v < bs; ++v) x[static_cast<size_t>(p) * bs + v] = rhs_x[(static_cast<size_t>(p) * bs + v) * nr + a];
-    chol_solve(L, x);
+    supernodal_solve(L, x);
     for (int p = 0; p < n; ++p)
       for (int v = 0; v < bs; ++v) rhs_x[(static_cast<size_t>(p) * bs + v) * nr + a] = x[static_cast<size_t>(p) * bs + v];
   }

@@ -6,7 +6,8 @@
 
 namespace dpgo {
 
-constexpr int kPartialStride = 8;  // doubles of partial sums per tile
+constexpr int kPartialStride = 16;  // doubles of partial sums per tile
+constexpr int kDdLo = 8;  // a double-double partial keeps its low part this many slots after its high part
 constexpr int kMaxTot = 8;         // quantities one finalize reduces (pa + pb, and pc at the last slot)
 
 // X.Q SpMM epilogues: XQ (V Q), XQ_G (X Q + G), EVAL (g = P_X(XQ+G), S, f / |g|^2 partials),
@@ -134,6 +135,7 @@ struct FinalizeArgs {
   int agent_filter;             // 0: every agent; 1 / 2: only agents whose eta is / is not implicit
   int coherent;                 // read the partials with agent-scope loads (fused, SpmmArgs::fin_mode 2)
   const double* conv_ratio;     // OP_STATUS: per-agent converged loop-closure ratio (nullptr = 1)
+  int dd_mask;                  // bit q: pa quantity q is double-double (low part at slot + kDdLo), reduced as such
   double* trace;                // per-iteration records [agent][trace_cap][kTraceWidth] (nullptr = off)
   int trace_cap;
 };
@@ -178,16 +180,24 @@ struct GEdges {
   const double* w;
 };
 
-// One triangle of the exact preconditioner's block factor P = L L^T, as block rows over batch-global
-// pose indices (chol.cpp): forward rows hold F_jk = L_jk^T (k earlier in the elimination order),
-// backward rows hold L_ij (i later); blocks row-major so lane k reads row k.  dinv = L_jj^-1
-// row-major; the forward pass applies L_jj^-T (reads it transposed).
-struct TrsvView {
-  const int* ptr;
-  const int* col;
-  const double* blk;
-  const double* dinv;
-  int forward;
+// The exact preconditioner's supernodal factor on the device (chol_internal.h: per supernode the panel
+// [L_SS^-1 ; L_RS L_SS^-1] in kSnTileDev-square tiles), batch-global pose ids.  Frontal vectors F
+// ((S_pad + R_pad) scalar rows x r) and update vectors U (t b rows x r) are work space.
+constexpr int kSnTileDev = 64;
+struct SnView {
+  const double* panel;
+  const long* panel_off;  // [nodes] first double of the node's panel
+  const int* s;           // [nodes] poses in S
+  const int* t;           // [nodes] poses in R
+  const int* poses_off;   // [nodes] into poses: S then R
+  const int* poses;
+  const long* f_off;      // [nodes] into F
+  const long* u_off;      // [nodes] into U
+  const int* cpos_off;    // [nodes] into cpos: s + t + 1 pointers into contrib per node
+  const int* cpos;
+  const int2* contrib;    // per frontal position: (child node, index in the child's R), children in order
+  double* F;
+  double* U;
 };
 
 // Loop closures one engine colour class reweights (PGOAgent::updateLoopClosuresWeights,
@@ -221,7 +231,6 @@ enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH =
                TUNE_SV_STAGE = 8,  // 1: HESS passes stage the tile's second-visit records in LDS too (the
                                    //    tables are built when Q is set with this on; measured slower)
                TUNE_STATUS_PASS = 9,  // 1: the agent status by its own pass (k_sqdiff + OP_STATUS), not folded
-               TUNE_TRSV_CHAINS = 10,  // 1: the exact preconditioner's chains of levels solved level by level
                TUNE_COUNT = 12 };
 // variant of the edge-stream SpMM used unless TUNE_EDGE_VARIANT overrides it (bit 0: XCD-aware
 // tile remap; v >> 1: minimum waves per SIMD the register allocation must allow, none/4/5/6)
@@ -231,6 +240,8 @@ extern int g_tuning[TUNE_COUNT];
 bool supported_rb(int r, int b);
 hipError_t launch_gather_poses(int count, int rb, const int* idx, const double* A, const double* Bsrc, double* dst,
                                hipStream_t stream);
+// dst pose idx[s] = src pose s, s < count
+hipError_t launch_scatter_poses(int count, int rb, const int* idx, const double* src, double* dst, hipStream_t stream);
 hipError_t launch_assemble_G(int r, int b, const GEdges& e, int nslots, const double* Xa, const double* Xb,
                              double* gblk, hipStream_t stream);
 hipError_t launch_spmm(int r, int b, int mode, const LaunchCtx& c, const QView& q, const SpmmArgs& a);
@@ -280,15 +291,13 @@ hipError_t launch_select(int r, int b, const LaunchCtx& c, const double* A, cons
 hipError_t launch_accept(int r, int b, const LaunchCtx& c, const double* x2, const double* g2, const double* S2,
                          double* x1, double* g, double* S);
 hipError_t launch_finalize(const FinalizeArgs& f, int num_agents, hipStream_t stream);
-// sol[j] = (rhs[j] - sum_k sol[k] blk_jk) dinv_j for the `count` poses rows[] of one level
-// A chain of levels: workgroup b walks rows[aptr[b] .. aptr[b + 1]) in order (one agent's rows, at most one
-// per level), the row's entries split over the workgroup's 64 quads
-hipError_t launch_trsv_chain(int r, int b, const TrsvView& t, const int* aptr, int nblk, const int* rows,
-                             const double* rhs, double* sol, hipStream_t stream);
-// wide: one wave per row (its 16 quads split the row's entries), for levels with long rows
-constexpr int kTrsvWideRow = 16;
-hipError_t launch_trsv_level(int r, int b, const TrsvView& t, const int* rows, int count, const double* rhs,
-                             double* sol, hipStream_t stream, int wide = 0);
+// exact preconditioner, one tree level of one sweep: items = (node, row block of kThreads rows) /
+// (node, row tile) / (node, column tile); rhs, y, x in the engine's pose layout
+hipError_t launch_sn_assemble(int r, int b, const SnView& v, const int2* items, int count, const double* rhs,
+                              hipStream_t stream);
+hipError_t launch_sn_fwd(int r, int b, const SnView& v, const int2* items, int count, double* y, hipStream_t stream);
+hipError_t launch_sn_bwd(int r, int b, const SnView& v, const int2* items, int count, const double* y, double* x,
+                         hipStream_t stream);
 // z = P_X(zraw) (or z = zraw when project == 0); optional z_out / delta_out = -z; partials
 // <z, rref>, |rref|^2 per tile
 hipError_t launch_precond_finish(int r, int b, const LaunchCtx& c, const double* X, const double* zraw,

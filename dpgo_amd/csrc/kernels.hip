@@ -79,6 +79,44 @@ __device__ __forceinline__ void block_partials(double (&v)[NQ], double* __restri
   }
 }
 
+// One plain partial (slot 0) and ND double-double partials (high parts at slots 1.., low parts kDdLo
+// slots later), reduced in double-double over the wave and the block in block_partials' order.
+template <int ND>
+__device__ __forceinline__ void block_partials_dd(double v0, dd (&v)[ND], double* __restrict__ partials, int tile,
+                                                  bool coherent = false) {
+  __shared__ double red[4][1 + 2 * ND];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v0 = wave_sum(v0);
+#pragma unroll
+  for (int q = 0; q < ND; ++q) v[q] = wave_sum_dd(v[q]);
+  if (lane == 0) {
+    red[wave][0] = v0;
+#pragma unroll
+    for (int q = 0; q < ND; ++q) {
+      red[wave][1 + 2 * q] = v[q].hi;
+      red[wave][2 + 2 * q] = v[q].lo;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    auto put = [&](int slot, double t) {
+      if (coherent)
+        __hip_atomic_store(&partials[tile * kPartialStride + slot], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        partials[tile * kPartialStride + slot] = t;
+    };
+    put(0, ((red[0][0] + red[1][0]) + red[2][0]) + red[3][0]);
+#pragma unroll
+    for (int q = 0; q < ND; ++q) {
+      dd t{red[0][1 + 2 * q], red[0][2 + 2 * q]};
+#pragma unroll
+      for (int w = 1; w < 4; ++w) t = dd_add(t, {red[w][1 + 2 * q], red[w][2 + 2 * q]});
+      put(1 + q, t.hi);
+      put(1 + q + kDdLo, t.lo);
+    }
+  }
+}
+
 struct PoseLane {
   int lane, wave, k, tile, agent, pslot;
   long j;
@@ -644,14 +682,19 @@ __device__ __forceinline__ void tcg_stop_test(const FinalizeArgs& f, int agent, 
 // HESS_M partials of r_j and Hdelta_j (r_{j+1} = r_j + alpha Hd, z_{j+1} = z_j + alpha Prec(Hd)):
 //   tot[1] |r|^2, tot[2] <r,Hd>, tot[3] |Hd|^2, tot[4] <z,r>, tot[5] 2<z,Hd>, tot[6] <Minv Hd, Hd>.
 // The base terms are recomputed from the stored r_j every iteration, so rounding does not accumulate.
+// The partials arrive as double-double (tot = high, lo = low parts) and the polynomials are evaluated in
+// double-double: their terms cancel by the tCG's residual drop, and exact terms leave only the final
+// rounding (the classic sequence's direct inner products of r', z' agree to a few ulps).
 __device__ __forceinline__ void merged_stop_test(const FinalizeArgs& f, int agent, const double (&tot)[kMaxTot],
-                                                 AgentState& s) {
+                                                 const double (&lo)[kMaxTot], AgentState& s) {
   s.eh_pending = 1;  // the k_tcg_updir that applies this step leaves <eta_old, Hdelta> in pc
   if (s.tcg_mode != 0) return;
   const double a = s.step;
-  const double nr2 = fmax(tot[1] + a * (2.0 * tot[2] + a * tot[3]), 0.0);
-  const double zr_new = tot[4] + a * (tot[5] + a * tot[6]);
-  tcg_stop_test(f, agent, nr2, zr_new, s);
+  const dd t1{tot[1], lo[1]}, t2{tot[2], lo[2]}, t3{tot[3], lo[3]}, t4{tot[4], lo[4]}, t5{tot[5], lo[5]},
+      t6{tot[6], lo[6]};
+  const dd n = dd_add(t1, dd_mul_d(dd_add(dd_mul_d(t2, 2.0), dd_mul_d(t3, a)), a));
+  const dd z = dd_add(t4, dd_mul_d(dd_add(t5, dd_mul_d(t6, a)), a));
+  tcg_stop_test(f, agent, fmax(dd_val(n), 0.0), dd_val(z), s);
 }
 
 // PGOAgentStatus after an update (src/PGOAgent.cpp:700-716): relativeChange = sqrt(|X - XPrev|^2 / n),
@@ -666,7 +709,7 @@ __device__ __forceinline__ void set_status(const FinalizeArgs& f, int agent, dou
 
 // The RTR / tCG scalar logic of one agent on its reduced partials tot[] (one thread).
 __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent, const double (&tot)[kMaxTot],
-                                                AgentState& s) {
+                                                const double (&lo)[kMaxTot], AgentState& s) {
   const int nq = f.nq_a + f.nq_b;
   const OptScalars& o = f.opt;
   const bool filtered = (f.agent_filter == 1 && !s.eta_implicit) || (f.agent_filter == 2 && s.eta_implicit);
@@ -778,15 +821,17 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
         s.tcg_mode = 2;
         break;
       }
-      s.z_r = tot[4];  // <z_j, r_j> recomputed from the stored r_j (the first: EVAL_TCG's <z, g> again)
+      // <z_j, r_j> recomputed from the stored r_j; the first step keeps EVAL_TCG's <z, g> (the same inner
+      // product as a plain sum: a first step decided by MODE_QF uses that one, bitwise the same step)
+      if (s.tcg_iters > 0) s.z_r = tot[4] + lo[4];
       tcg_step_test(f, agent, tot[0], s);
       if (s.eta_implicit) break;
-      merged_stop_test(f, agent, tot, s);
+      merged_stop_test(f, agent, tot, lo, s);
       break;
     }
     case OP_TCG_CHECK_M: {  // after k_spmm<HESS_M> over the agents a MODE_QF step test sent on a CG step
       if (s.tcg_mode != 0 || s.eta_implicit) break;
-      merged_stop_test(f, agent, tot, s);
+      merged_stop_test(f, agent, tot, lo, s);
       break;
     }
     case OP_RHO: {  // pa: <g,eta> [, <eta,HV>, |x2 - ref|^2, |x1 - ref|^2]; pb: f(x2), |grad(x2)|^2
@@ -894,27 +939,43 @@ static_assert(kThreads == 256, "the finalize reductions restate a 256-thread red
 __device__ __forceinline__ void finalize_agent(const FinalizeArgs& f, int agent) {
   const int l = static_cast<int>(threadIdx.x) & 63;
   const int t0 = f.agent_tile_off[agent], t1 = f.agent_tile_off[agent + 1];
-  double tot[kMaxTot];
+  double tot[kMaxTot], lo[kMaxTot];
+  auto ld = [&](const double* src, int t, int slot) {
+    return f.coherent ? __hip_atomic_load(&src[t * kPartialStride + slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : src[t * kPartialStride + slot];
+  };
 #pragma unroll
   for (int q = 0; q < kMaxTot; ++q) {
     tot[q] = 0.0;
+    lo[q] = 0.0;
     int qq = 0;
     const double* src = part_src(f, q, qq);
     if (src == nullptr) continue;
+    if ((f.dd_mask >> q) & 1) {  // double-double quantity: the same tree in double-double
+      dd a4[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        dd sv{0.0, 0.0};
+        for (int t = t0 + l + 64 * v; t < t1; t += kThreads) sv = dd_add(sv, {ld(src, t, qq), ld(src, t, qq + kDdLo)});
+        a4[v] = sv;
+      }
+      const dd x = wave_sum_dd(dd_add(dd_add(a4[0], a4[2]), dd_add(a4[1], a4[3])));
+      tot[q] = x.hi;
+      lo[q] = x.lo;
+      continue;
+    }
     double a4[4];
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       double sv = 0.0;
-      for (int t = t0 + l + 64 * v; t < t1; t += kThreads)
-        sv += f.coherent ? __hip_atomic_load(&src[t * kPartialStride + qq], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                         : src[t * kPartialStride + qq];
+      for (int t = t0 + l + 64 * v; t < t1; t += kThreads) sv += ld(src, t, qq);
       a4[v] = sv;
     }
     double x = (a4[0] + a4[2]) + (a4[1] + a4[3]);
     tot[q] = wave_sum(x);  // lane 0's halving tree
   }
   if (l != 0) return;
-  finalize_scalar(f, agent, tot, f.state[agent]);
+  finalize_scalar(f, agent, tot, lo, f.state[agent]);
 }
 
 template <int NQ>
@@ -1284,14 +1345,16 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
       } else {
         precond_col_mk<R, B>(Xf, mk, p.k, args.pmode, rcol, zc);
       }
-      double rr = 0.0, rh = 0.0, hh = 0.0, zr = 0.0, zh = 0.0, mh = 0.0;
+      // double-double partials (exact products, compensated sums): the stopping test combines them as
+      // polynomials in alpha whose terms cancel by the residual drop (merged_stop_test)
+      dd rr{0.0, 0.0}, rh{0.0, 0.0}, hh{0.0, 0.0}, zr{0.0, 0.0}, zh{0.0, 0.0}, mh{0.0, 0.0};
 #pragma unroll
       for (int a = 0; a < R; ++a) {
-        rr = fma(rcol[a], rcol[a], rr);
-        rh = fma(rcol[a], hc[a], rh);
-        hh = fma(hc[a], hc[a], hh);
-        zr = fma(zc[a], rcol[a], zr);
-        zh = fma(zc[a], hc[a], zh);
+        rr = dd_fma(rr, rcol[a], rcol[a]);
+        rh = dd_fma(rh, rcol[a], hc[a]);
+        hh = dd_fma(hh, hc[a], hc[a]);
+        zr = dd_fma(zr, zc[a], rcol[a]);
+        zh = dd_fma(zh, zc[a], hc[a]);
       }
       if (args.pmode == PRECON_NONE) {
         mh = hh;
@@ -1307,15 +1370,15 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
 #pragma unroll
           for (int u = 0; u < B; ++u) m = pk == u ? mk[u] : m;  // Minv_{pk, k} = column k's entry pk
           if (pk >= B || !act) m = 0.0;
-          double t = 0.0;
+          dd t{0.0, 0.0};
 #pragma unroll
-          for (int a = 0; a < R; ++a) t = fma(hc[a], hp[a], t);
-          mh = fma(m, t, mh);
+          for (int a = 0; a < R; ++a) t = dd_fma(t, hc[a], hp[a]);
+          mh = dd_add(mh, dd_mul_d(t, m));
         };
         double mkk = 0.0;
 #pragma unroll
         for (int u = 0; u < B; ++u) mkk = kc == u ? mk[u] : mkk;
-        mh = act ? mkk * hh : 0.0;
+        mh = act ? dd_mul_d(hh, mkk) : dd{0.0, 0.0};
         double hp[R];
 #pragma unroll
         for (int a = 0; a < R; ++a) hp[a] = dpp_f64<0xB1>(hc[a]);  // quad_perm [1,0,3,2]: partner k^1
@@ -1327,9 +1390,10 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
         for (int a = 0; a < R; ++a) hp[a] = dpp_f64<0x1B>(hc[a]);  // [3,2,1,0]: k^3
         pair(3, hp);
       }
-      double parts[7] = {own ? dpart : 0.0, own ? rr : 0.0, own ? rh : 0.0, own ? hh : 0.0,
-                         own ? zr : 0.0,    own ? 2.0 * zh : 0.0, own ? mh : 0.0};
-      block_partials<7>(parts, c.partials, p.tile, args.fin_mode == 2);
+      const dd zero{0.0, 0.0};
+      dd parts[6] = {own ? rr : zero, own ? rh : zero, own ? hh : zero, own ? zr : zero,
+                     own ? dd{2.0 * zh.hi, 2.0 * zh.lo} : zero, own ? mh : zero};
+      block_partials_dd<6>(own ? dpart : 0.0, parts, c.partials, p.tile, args.fin_mode == 2);
     } else {
       double parts[1] = {own ? dpart : 0.0};
       block_partials<1>(parts, c.partials, p.tile, args.fin_mode == 2);
@@ -2003,40 +2067,62 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
   const int t0 = f.agent_tile_off[agent], t1 = f.agent_tile_off[agent + 1];
   constexpr int kStateWords = static_cast<int>(sizeof(AgentState) / sizeof(double));
   __shared__ double red[NQ][kThreads];
+  __shared__ double red_lo[NQ][kThreads];  // low parts of double-double quantities (f.dd_mask)
   __shared__ AgentState sh_state;
   if (threadIdx.x < kStateWords)
     reinterpret_cast<double*>(&sh_state)[threadIdx.x] = reinterpret_cast<const double*>(&f.state[agent])[threadIdx.x];
-  double acc[NQ];
+  double acc[NQ], accl[NQ];
   const double* srcs[NQ];
   int qqs[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     acc[q] = 0.0;
+    accl[q] = 0.0;
     srcs[q] = part_src(f, q, qqs[q]);
   }
   for (int t = t0 + threadIdx.x; t < t1; t += kThreads) {
 #pragma unroll
-    for (int q = 0; q < NQ; ++q)
-      if (srcs[q] != nullptr) acc[q] += srcs[q][t * kPartialStride + qqs[q]];
+    for (int q = 0; q < NQ; ++q) {
+      if (srcs[q] == nullptr) continue;
+      const double v = srcs[q][t * kPartialStride + qqs[q]];
+      if ((f.dd_mask >> q) & 1) {
+        const dd a = dd_add({acc[q], accl[q]}, {v, srcs[q][t * kPartialStride + qqs[q] + kDdLo]});
+        acc[q] = a.hi;
+        accl[q] = a.lo;
+      } else {
+        acc[q] += v;
+      }
+    }
   }
 #pragma unroll
   for (int q = 0; q < NQ; ++q)
-    if (srcs[q] != nullptr) red[q][threadIdx.x] = acc[q];
+    if (srcs[q] != nullptr) {
+      red[q][threadIdx.x] = acc[q];
+      red_lo[q][threadIdx.x] = accl[q];
+    }
   __syncthreads();
   if (threadIdx.x >= 64) return;
   const int l = threadIdx.x;
-  double tot[kMaxTot];
+  double tot[kMaxTot], lo[kMaxTot];
 #pragma unroll
   for (int q = 0; q < kMaxTot; ++q) {
     tot[q] = 0.0;
+    lo[q] = 0.0;
     if (q >= NQ || srcs[q] == nullptr) continue;
+    if ((f.dd_mask >> q) & 1) {
+      auto at = [&](int i) { return dd{red[q][i], red_lo[q][i]}; };
+      const dd x = wave_sum_dd(dd_add(dd_add(at(l), at(l + 128)), dd_add(at(l + 64), at(l + 192))));
+      tot[q] = x.hi;
+      lo[q] = x.lo;
+      continue;
+    }
     double v = (red[q][l] + red[q][l + 128]) + (red[q][l + 64] + red[q][l + 192]);
     tot[q] = wave_sum(v);  // lane 0's halving tree
   }
   if (l != 0) return;
   // the scalar logic runs on a register copy: a chain of dependent LDS accesses costs microseconds
   AgentState st = sh_state;
-  finalize_scalar(f, agent, tot, st);
+  finalize_scalar(f, agent, tot, lo, st);
   double* dst = reinterpret_cast<double*>(&f.state[agent]);
   const double* srcw = reinterpret_cast<const double*>(&st);
 #pragma unroll
@@ -2088,7 +2174,8 @@ __device__ void prologue_finalize(const FinalizeArgs& f, int agent, int* arrive,
       FinalizeArgs g = f;
       g.pub = nullptr;  // published once, by the last block (finalize_arrive)
       AgentState st = sh;  // register copy (see k_finalize)
-      finalize_scalar(g, agent, tot, st);
+      const double nolo[kMaxTot] = {};  // the classic ops' quantities are plain sums
+      finalize_scalar(g, agent, tot, nolo, st);
       sh = st;
     }
   }
@@ -2384,157 +2471,223 @@ __global__ __launch_bounds__(kThreads) void k_weights_to_slots(int m, const int*
 
 // ------------------------------------------------------------------------------------------
 // Exact preconditioner (QuadraticProblem::PreConditioner with the Cholesky factor of Q + 0.1 I,
-// src/QuadraticProblem.cpp:37-41, 75-87): level-scheduled block triangular solves.  In row form
-// the r right-hand sides are the pose blocks themselves: forward Y_j = (V_j - sum_k Y_k L_jk^T)
-// L_jj^-T, backward Z_j = (Y_j - sum_i Z_i L_ij) L_jj^-1.  One quad per pose row, outer-product
-// accumulation + quad reduce-scatter as in the SpMM; every row of a level is independent.
+// src/QuadraticProblem.cpp:37-41, 75-87): supernodal triangular solves as dense panel products
+// (chol_internal.h: Panel = [L_SS^-1 ; L_RS L_SS^-1] per supernode).  In row form the r right-hand
+// sides of scalar row c = pose j column k are the r doubles of column k of pose block j (the engine's
+// layout), so every "vector" element is r doubles.  One launch per tree level and sweep:
+//   k_sn_assemble  frontal vector f of every supernode of the level: [rhs_S ; 0_R] + its children's
+//                  update vectors (extend-add as a gather, children in order: deterministic)
+//   k_sn_fwd       per (supernode, row tile): y_S = L_SS^-1 f_S into y; u = f_R - (L_RS L_SS^-1) f_S
+//   k_sn_bwd       per (supernode, column tile): x_S = L_SS^-T y_S - (L_RS L_SS^-1)^T x_R into x
+// A workgroup streams its panel tiles (row-major 64 x 64 scalars) once; thread (rq, cq) = (t >> 4,
+// t & 15) owns rows 4 rq .. 4 rq + 3 and columns 4 cq .. 4 cq + 3 of every tile, with the tile's 64
+// vector elements staged in LDS; the next tile's 16 panel values are loaded before the current ones
+// are consumed.  Memory-bound: 8 bytes of panel per 2 r flops.
 // ------------------------------------------------------------------------------------------
-// WIDE: one wave per row, quad g of the wave takes entries g, g + 16, ... and the 16 partial sums are
-// added over the wave (lane bits 2..5) before the diagonal solve; otherwise one quad per row.
-template <int R, int B, bool WIDE>
-__global__ __launch_bounds__(kThreads) void k_trsv_level(TrsvView t, const int* __restrict__ rows, int count,
-                                                         const double* __restrict__ rhs, double* __restrict__ sol) {
-  const int k = threadIdx.x & 3;
-  constexpr int kRowsPerBlock = WIDE ? kThreads / 64 : kThreads / 4;
-  constexpr int kStride = WIDE ? 16 : 1;
-  const int q = blockIdx.x * kRowsPerBlock + static_cast<int>(threadIdx.x) / (WIDE ? 64 : 4);
-  const int g = WIDE ? (static_cast<int>(threadIdx.x) & 63) >> 2 : 0;
-  if (q >= count) return;  // whole quad / wave leaves together
-  const int kc = k < B ? k : 0;
-  const long j = rows[q];
-  double acc[R][B];
+__device__ __forceinline__ int sn_pad_dev(int scalars) { return (scalars + kSnTileDev - 1) / kSnTileDev * kSnTileDev; }
+__device__ __forceinline__ long sn_tile_dev(int ns, int I, int J) {
+  return I < ns ? static_cast<long>(I) * (I + 1) / 2 + J
+                : static_cast<long>(ns) * (ns + 1) / 2 + static_cast<long>(I - ns) * ns + J;
+}
+
+// rows 4 rq .. 4 rq + 3, columns 4 cq .. 4 cq + 3 of a tile
+__device__ __forceinline__ void sn_load_tile(const double* __restrict__ tile, int rq, int cq, double (&p)[4][4]) {
 #pragma unroll
-  for (int a = 0; a < R; ++a)
-#pragma unroll
-    for (int c = 0; c < B; ++c) acc[a][c] = 0.0;
-  for (int z = t.ptr[j] + g; z < t.ptr[j + 1]; z += kStride) {
-    const long i = t.col[z];
-    const double* br = t.blk + static_cast<long>(z) * (B * B) + kc * B;
-    const double* xi = sol + i * (R * B) + kc * R;
-    double x[R], bk[B];
-#pragma unroll
-    for (int a = 0; a < R; ++a) x[a] = xi[a];
-#pragma unroll
-    for (int c = 0; c < B; ++c) bk[c] = br[c];
-#pragma unroll
-    for (int a = 0; a < R; ++a)
-#pragma unroll
-      for (int c = 0; c < B; ++c) acc[a][c] = fma(x[a], bk[c], acc[a][c]);
-  }
-  if constexpr (WIDE) {
-#pragma unroll
-    for (int a = 0; a < R; ++a)
-#pragma unroll
-      for (int c = 0; c < B; ++c)
-#pragma unroll
-        for (int off = 4; off < 64; off <<= 1) acc[a][c] += __shfl_xor(acc[a][c], off, 64);
-  }
-  const bool act = k < B;
-#pragma unroll
-  for (int a = 0; a < R; ++a)
-#pragma unroll
-    for (int c = 0; c < B; ++c) acc[a][c] = act ? acc[a][c] : 0.0;
-  double w[R];
-  quad_reduce_scatter<R, B>(acc, k, w);  // lane c: column c of sum_k sol_k blk_jk
-  const double* rj = rhs + j * (R * B) + kc * R;
-#pragma unroll
-  for (int a = 0; a < R; ++a) w[a] = rj[a] - w[a];
-  // times the diagonal inverse: lane u contributes w[:, u] (x) Dinv[u, :]
-  double dv[B];
-  const double* dj = t.dinv + j * (B * B);
-#pragma unroll
-  for (int c = 0; c < B; ++c) dv[c] = t.forward ? dj[c * B + kc] : dj[kc * B + c];
-#pragma unroll
-  for (int a = 0; a < R; ++a)
-#pragma unroll
-    for (int c = 0; c < B; ++c) acc[a][c] = act ? w[a] * dv[c] : 0.0;
-  double y[R];
-  quad_reduce_scatter<R, B>(acc, k, y);
-  if (act && g == 0) {
-    double* sj = sol + j * (R * B) + k * R;
-#pragma unroll
-    for (int a = 0; a < R; ++a) sj[a] = y[a];
+  for (int i = 0; i < 4; ++i) {
+    const f64x2* src = reinterpret_cast<const f64x2*>(tile + (rq * 4 + i) * kSnTileDev + cq * 4);
+    const f64x2 a = src[0], c = src[1];
+    p[i][0] = a.x;
+    p[i][1] = a.y;
+    p[i][2] = c.x;
+    p[i][3] = c.y;
   }
 }
 
-// A chain of levels in one launch: workgroup b walks one agent's rows (at most one per level, so each row's
-// dependencies inside the chain are earlier rows of the same workgroup) in level order.  Per row the 64
-// quads split the entries; the partial sums meet over the wave (lanes 4.. apart) and then over the four
-// waves through LDS; wave 0 solves the diagonal block and stores; the barrier after it publishes the row
-// to the next one (workgroup-scope release / acquire: same CU).
-template <int R, int B>
-__global__ __launch_bounds__(kThreads) void k_trsv_chain(TrsvView t, const int* __restrict__ aptr,
-                                                         const int* __restrict__ rows, const double* __restrict__ rhs,
-                                                         double* sol) {
-  __shared__ double red[kThreads / 64][4][R * B];
-  const int k = threadIdx.x & 3, quad = threadIdx.x >> 2, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int kc = k < B ? k : 0;
-  const bool act = k < B;
-  const int x0 = aptr[blockIdx.x], x1 = aptr[blockIdx.x + 1];
-  for (int x = x0; x < x1; ++x) {
-    const long j = rows[x];
-    double acc[R][B];
+template <int R>
+__global__ __launch_bounds__(kThreads) void k_sn_assemble(SnView v, const int2* __restrict__ items, int b,
+                                                          const double* __restrict__ rhs) {
+  const int2 it = items[blockIdx.x];
+  const int node = it.x, row = it.y * kThreads + static_cast<int>(threadIdx.x);
+  const int s = v.s[node], t = v.t[node], sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), Rp = sn_pad_dev(tb);
+  if (row >= Sp + Rp) return;
+  double val[R];
 #pragma unroll
-    for (int a = 0; a < R; ++a)
+  for (int a = 0; a < R; ++a) val[a] = 0.0;
+  int pos = -1, k = 0;
+  if (row < Sp) {
+    if (row < sb) {
+      pos = row / b;
+      k = row - pos * b;
+      const double* src = rhs + (static_cast<long>(v.poses[v.poses_off[node] + pos]) * b + k) * R;
 #pragma unroll
-      for (int c = 0; c < B; ++c) acc[a][c] = 0.0;
-    for (int z = t.ptr[j] + quad; z < t.ptr[j + 1]; z += kThreads / 4) {
-      const long i = t.col[z];
-      const double* br = t.blk + static_cast<long>(z) * (B * B) + kc * B;
-      const double* xi = sol + i * (R * B) + kc * R;
-      double xv[R], bk[B];
-#pragma unroll
-      for (int a = 0; a < R; ++a) xv[a] = xi[a];
-#pragma unroll
-      for (int c = 0; c < B; ++c) bk[c] = br[c];
-#pragma unroll
-      for (int a = 0; a < R; ++a)
-#pragma unroll
-        for (int c = 0; c < B; ++c) acc[a][c] = fma(xv[a], bk[c], acc[a][c]);
+      for (int a = 0; a < R; ++a) val[a] = src[a];
     }
+  } else if (row - Sp < tb) {
+    const int rr = row - Sp;
+    pos = s + rr / b;
+    k = rr - (rr / b) * b;
+  }
+  if (pos >= 0) {
+    const int* cp = v.cpos + v.cpos_off[node] + pos;
+    for (int e = cp[0]; e < cp[1]; ++e) {
+      const int2 ce = v.contrib[e];
+      const double* src = v.U + v.u_off[ce.x] + (static_cast<long>(ce.y) * b + k) * R;
 #pragma unroll
-    for (int a = 0; a < R; ++a)
-#pragma unroll
-      for (int c = 0; c < B; ++c)
-#pragma unroll
-        for (int off = 4; off < 64; off <<= 1) acc[a][c] += __shfl_xor(acc[a][c], off, 64);
-    if (lane < 4) {
-#pragma unroll
-      for (int a = 0; a < R; ++a)
-#pragma unroll
-        for (int c = 0; c < B; ++c) red[wave][lane][a * B + c] = acc[a][c];
+      for (int a = 0; a < R; ++a) val[a] += src[a];
     }
+  }
+  double* dst = v.F + v.f_off[node] + static_cast<long>(row) * R;
+#pragma unroll
+  for (int a = 0; a < R; ++a) dst[a] = val[a];
+}
+
+template <int R>
+__global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __restrict__ items, int b,
+                                                     double* __restrict__ y) {
+  __shared__ double sf[kSnTileDev * R];
+  const int2 it = items[blockIdx.x];
+  const int node = it.x, I = it.y;
+  const int s = v.s[node], t = v.t[node], sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), ns = Sp / kSnTileDev;
+  const double* __restrict__ f = v.F + v.f_off[node];
+  const double* __restrict__ panel = v.panel + v.panel_off[node];
+  const int tid = static_cast<int>(threadIdx.x), rq = tid >> 4, cq = tid & 15;
+  double acc[4][R];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int a = 0; a < R; ++a) acc[i][a] = 0.0;
+  const int nJ = I < ns ? I + 1 : ns;
+  constexpr int kTileD = kSnTileDev * kSnTileDev;
+  double p[4][4], pn[4][4];
+  if (nJ > 0) sn_load_tile(panel + sn_tile_dev(ns, I, 0) * kTileD, rq, cq, p);
+  for (int J = 0; J < nJ; ++J) {
+    if (J + 1 < nJ) sn_load_tile(panel + sn_tile_dev(ns, I, J + 1) * kTileD, rq, cq, pn);
+    __syncthreads();  // the previous tile's reads of sf are done
+    for (int x = tid; x < kSnTileDev * R; x += kThreads) sf[x] = f[static_cast<long>(J) * kSnTileDev * R + x];
     __syncthreads();
-    if (wave == 0) {
 #pragma unroll
-      for (int a = 0; a < R; ++a)
+    for (int c = 0; c < 4; ++c) {
+      double fc[R];
 #pragma unroll
-        for (int c = 0; c < B; ++c) {
-          const double v = ((red[0][k][a * B + c] + red[1][k][a * B + c]) + red[2][k][a * B + c]) + red[3][k][a * B + c];
-          acc[a][c] = act ? v : 0.0;
-        }
-      double w[R];
-      quad_reduce_scatter<R, B>(acc, k, w);
-      const double* rj = rhs + j * (R * B) + kc * R;
+      for (int a = 0; a < R; ++a) fc[a] = sf[(cq * 4 + c) * R + a];
 #pragma unroll
-      for (int a = 0; a < R; ++a) w[a] = rj[a] - w[a];
-      double dv[B];
-      const double* dj = t.dinv + j * (B * B);
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int c = 0; c < B; ++c) dv[c] = t.forward ? dj[c * B + kc] : dj[kc * B + c];
+        for (int a = 0; a < R; ++a) acc[i][a] = fma(p[i][c], fc[a], acc[i][a]);
+    }
 #pragma unroll
-      for (int a = 0; a < R; ++a)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int c = 0; c < B; ++c) acc[a][c] = act ? w[a] * dv[c] : 0.0;
-      double y[R];
-      quad_reduce_scatter<R, B>(acc, k, y);
-      if (act && quad == 0) {
-        double* sj = sol + j * (R * B) + k * R;
+      for (int c = 0; c < 4; ++c) p[i][c] = pn[i][c];
+  }
+  // sum over the 16 column groups (lanes cq = 0..15 of a 16-lane group, fixed order)
 #pragma unroll
-        for (int a = 0; a < R; ++a) sj[a] = y[a];
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int a = 0; a < R; ++a) {
+      double x = acc[i][a];
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) x += __shfl_xor(x, off, 64);
+      acc[i][a] = x;
+    }
+  if (cq != 0) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = I * kSnTileDev + rq * 4 + i;
+    if (row < sb) {  // y_S
+      const int pos = row / b, k = row - pos * b;
+      double* dst = y + (static_cast<long>(v.poses[v.poses_off[node] + pos]) * b + k) * R;
+#pragma unroll
+      for (int a = 0; a < R; ++a) dst[a] = acc[i][a];
+    } else if (row >= Sp && row - Sp < tb) {  // update u = f_R - M f_S
+      const double* fr = f + static_cast<long>(row) * R;
+      double* dst = v.U + v.u_off[node] + static_cast<long>(row - Sp) * R;
+#pragma unroll
+      for (int a = 0; a < R; ++a) dst[a] = fr[a] - acc[i][a];
+    }
+  }
+}
+
+template <int R>
+__global__ __launch_bounds__(kThreads) void k_sn_bwd(SnView v, const int2* __restrict__ items, int b,
+                                                     const double* __restrict__ y, double* __restrict__ x) {
+  __shared__ double sg[kSnTileDev * R];
+  __shared__ double red[kThreads / 64][16][4 * R];
+  const int2 it = items[blockIdx.x];
+  const int node = it.x, J = it.y;
+  const int s = v.s[node], t = v.t[node], sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), Rp = sn_pad_dev(tb);
+  const int ns = Sp / kSnTileDev, nI = (Sp + Rp) / kSnTileDev;
+  const double* __restrict__ panel = v.panel + v.panel_off[node];
+  const int* __restrict__ poses = v.poses + v.poses_off[node];
+  const int tid = static_cast<int>(threadIdx.x), rq = tid >> 4, cq = tid & 15;
+  double acc[4][R];  // columns 4 cq + c
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int a = 0; a < R; ++a) acc[c][a] = 0.0;
+  constexpr int kTileD = kSnTileDev * kSnTileDev;
+  double p[4][4], pn[4][4];
+  if (J < nI) sn_load_tile(panel + sn_tile_dev(ns, J, J) * kTileD, rq, cq, p);
+  for (int I = J; I < nI; ++I) {
+    if (I + 1 < nI) sn_load_tile(panel + sn_tile_dev(ns, I + 1, J) * kTileD, rq, cq, pn);
+    __syncthreads();
+    // g rows of tile I: y_S on the S part, -x_R on the R part, 0 on padding
+    for (int e = tid; e < kSnTileDev * R; e += kThreads) {
+      const int rl = e / R, a = e - rl * R, row = I * kSnTileDev + rl;
+      double g = 0.0;
+      if (row < sb) {
+        const int pos = row / b, k = row - pos * b;
+        g = y[(static_cast<long>(poses[pos]) * b + k) * R + a];
+      } else if (row >= Sp && row - Sp < tb) {
+        const int rr = row - Sp, q = rr / b, k = rr - q * b;
+        g = -x[(static_cast<long>(poses[s + q]) * b + k) * R + a];
       }
+      sg[e] = g;
     }
     __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      double gi[R];
+#pragma unroll
+      for (int a = 0; a < R; ++a) gi[a] = sg[(rq * 4 + i) * R + a];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int a = 0; a < R; ++a) acc[c][a] = fma(p[i][c], gi[a], acc[c][a]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) p[i][c] = pn[i][c];
+  }
+  // sum over the 16 row groups: the 4 of a wave (lane bits 4, 5), then the 4 waves in order
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int a = 0; a < R; ++a) {
+      double z = acc[c][a];
+      z += __shfl_xor(z, 16, 64);
+      z += __shfl_xor(z, 32, 64);
+      acc[c][a] = z;
+    }
+  if (lane < 16) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int a = 0; a < R; ++a) red[wave][lane][c * R + a] = acc[c][a];
+  }
+  __syncthreads();
+  if (tid >= 16) return;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int col = J * kSnTileDev + tid * 4 + c;
+    if (col >= sb) continue;
+    const int pos = col / b, k = col - pos * b;
+    double* dst = x + (static_cast<long>(poses[pos]) * b + k) * R;
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+      dst[a] = ((red[0][tid][c * R + a] + red[1][tid][c * R + a]) + red[2][tid][c * R + a]) + red[3][tid][c * R + a];
   }
 }
 
@@ -2590,6 +2743,15 @@ __global__ __launch_bounds__(kThreads) void k_gather_poses(int count, int rb, co
   const int s = static_cast<int>(t / rb), e = static_cast<int>(t % rb);
   const int i = idx[s];
   dst[t] = i >= 0 ? A[static_cast<long>(i) * rb + e] : Bsrc[static_cast<long>(-1 - i) * rb + e];
+}
+
+// dst[idx[s]] = src[s] for count pose blocks of rb doubles (a per-colour halo into its receive slots)
+__global__ __launch_bounds__(kThreads) void k_scatter_poses(int count, int rb, const int* __restrict__ idx,
+                                                            const double* __restrict__ src, double* __restrict__ dst) {
+  const long t = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= static_cast<long>(count) * rb) return;
+  const int s = static_cast<int>(t / rb), e = static_cast<int>(t % rb);
+  dst[static_cast<long>(idx[s]) * rb + e] = src[t];
 }
 
 // G assembly (PGOAgent::constructGMatrix, src/PGOAgent.cpp:783-859).  For G slot s (a public
@@ -2894,6 +3056,13 @@ hipError_t launch_gather_poses(int count, int rb, const int* idx, const double* 
   return hipGetLastError();
 }
 
+hipError_t launch_scatter_poses(int count, int rb, const int* idx, const double* src, double* dst, hipStream_t stream) {
+  if (count == 0) return hipSuccess;
+  const long total = static_cast<long>(count) * rb;
+  k_scatter_poses<<<static_cast<int>((total + kThreads - 1) / kThreads), kThreads, 0, stream>>>(count, rb, idx, src, dst);
+  return hipGetLastError();
+}
+
 hipError_t launch_assemble_G(int r, int b, const GEdges& e, int nslots, const double* Xa, const double* Xb,
                              double* gblk, hipStream_t stream) {
   if (nslots == 0) return hipSuccess;
@@ -2903,23 +3072,35 @@ hipError_t launch_assemble_G(int r, int b, const GEdges& e, int nslots, const do
   return hipGetLastError();
 }
 
-hipError_t launch_trsv_level(int r, int b, const TrsvView& t, const int* rows, int count, const double* rhs,
-                             double* sol, hipStream_t stream, int wide) {
-  if (count == 0) return hipSuccess;
-  if (wide) {
-    const int grid = (count + kThreads / 64 - 1) / (kThreads / 64);
-    DPGO_DISPATCH(r, b, (k_trsv_level<R, B, true><<<grid, kThreads, 0, stream>>>(t, rows, count, rhs, sol)));
-  } else {
-    const int grid = (count + kThreads / 4 - 1) / (kThreads / 4);
-    DPGO_DISPATCH(r, b, (k_trsv_level<R, B, false><<<grid, kThreads, 0, stream>>>(t, rows, count, rhs, sol)));
+#define DPGO_DISPATCH_R(R_, CALL)                          \
+  switch (R_) {                                            \
+    case 2: { constexpr int R = 2; CALL; break; }          \
+    case 3: { constexpr int R = 3; CALL; break; }          \
+    case 4: { constexpr int R = 4; CALL; break; }          \
+    case 5: { constexpr int R = 5; CALL; break; }          \
+    case 6: { constexpr int R = 6; CALL; break; }          \
+    case 7: { constexpr int R = 7; CALL; break; }          \
+    case 8: { constexpr int R = 8; CALL; break; }          \
+    default: return hipErrorInvalidValue;                  \
   }
+
+hipError_t launch_sn_assemble(int r, int b, const SnView& v, const int2* items, int count, const double* rhs,
+                              hipStream_t stream) {
+  if (count == 0) return hipSuccess;
+  DPGO_DISPATCH_R(r, (k_sn_assemble<R><<<count, kThreads, 0, stream>>>(v, items, b, rhs)));
   return hipGetLastError();
 }
 
-hipError_t launch_trsv_chain(int r, int b, const TrsvView& t, const int* aptr, int nblk, const int* rows,
-                             const double* rhs, double* sol, hipStream_t stream) {
-  if (nblk == 0) return hipSuccess;
-  DPGO_DISPATCH(r, b, (k_trsv_chain<R, B><<<nblk, kThreads, 0, stream>>>(t, aptr, rows, rhs, sol)));
+hipError_t launch_sn_fwd(int r, int b, const SnView& v, const int2* items, int count, double* y, hipStream_t stream) {
+  if (count == 0) return hipSuccess;
+  DPGO_DISPATCH_R(r, (k_sn_fwd<R><<<count, kThreads, 0, stream>>>(v, items, b, y)));
+  return hipGetLastError();
+}
+
+hipError_t launch_sn_bwd(int r, int b, const SnView& v, const int2* items, int count, const double* y, double* x,
+                         hipStream_t stream) {
+  if (count == 0) return hipSuccess;
+  DPGO_DISPATCH_R(r, (k_sn_bwd<R><<<count, kThreads, 0, stream>>>(v, items, b, y, x)));
   return hipGetLastError();
 }
 

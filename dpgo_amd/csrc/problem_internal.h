@@ -110,21 +110,17 @@ struct dpgo_hip_problem_s {
 
   int precon = DPGO_PRECON_BLOCK_JACOBI;
 
-  // exact preconditioner: block Cholesky of Q + 0.1 I (chol.cpp), level-scheduled solves
+  // exact preconditioner: supernodal Cholesky of Q + 0.1 I (chol.cpp), one launch per tree level and sweep
   int chol_state = 0;  // 0 stale, 1 ready, 2 Q + 0.1 I not positive definite (identity, as the reference)
-  dpgo::DevBuf<int> fw_ptr, fw_col, bw_ptr, bw_col, fw_rows, bw_rows;
-  dpgo::DevBuf<double> fw_blk, bw_blk, linv;
-  std::vector<int> fw_lvl, bw_lvl;  // level pointers into fw_rows / bw_rows
-  std::vector<int> fw_wide, bw_wide;  // per level: its longest row has more entries than a quad should walk
-  // chains: runs of consecutive levels with at most one row per agent (the dense separators near the top of
-  // each agent's elimination tree), solved by one launch with one workgroup per agent walking its rows
-  struct TrsvChain {
-    int l0, l1;      // levels [l0, l1)
-    int a0, nblk;    // its agents' row lists: (fw|bw)_captr[a0 .. a0 + nblk]
+  dpgo::DevBuf<double> sn_panel, sn_F, sn_U;
+  dpgo::DevBuf<long> sn_panel_off, sn_f_off, sn_u_off;
+  dpgo::DevBuf<int> sn_s, sn_t, sn_poses_off, sn_poses, sn_cpos_off, sn_cpos;
+  dpgo::DevBuf<int2> sn_contrib, sn_items;
+  struct SnLevel {  // item ranges into sn_items of one tree depth
+    int asm0 = 0, asm_n = 0, fwd0 = 0, fwd_n = 0, bwd0 = 0, bwd_n = 0;
   };
-  std::vector<TrsvChain> fw_chain, bw_chain;
-  dpgo::DevBuf<int> fw_captr, fw_crows, bw_captr, bw_crows;
-  long chol_blocks = 0;
+  std::vector<SnLevel> sn_levels;  // index = depth (0 = the roots)
+  long chol_doubles = 0;
 
   // work
   dpgo::DevBuf<double> x1, x2, g, g2, S, S2, eta, rv, z, delta, Hdelta, tA, tB;

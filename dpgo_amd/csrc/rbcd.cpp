@@ -42,6 +42,14 @@ struct dpgo_rbcd_s {
   std::vector<long long> send_counts, recv_counts, send_off, recv_off;  // doubles
   long n_send_items = 0, n_recv_poses = 0;
   DevBuf<int> pack_idx, unpack_x;
+  // per-colour halo (examples/MultiRobotExample.cpp:188-213 moves only what the selected robot reads): the
+  // poses the selected colour's agents read, peer-major, ascending; received poses scatter to their RX slots
+  struct Halo {
+    std::vector<long long> send_counts, recv_counts, send_off, recv_off;  // doubles
+    long n_send = 0, n_recv = 0;
+    DevBuf<int> pack_idx, unpack_slot;
+  };
+  std::vector<Halo*> halo;
   DevBuf<double> RX;   // received neighbour poses used by updates and reweighting
   DevBuf<double> RXc;  // received neighbour poses of a central evaluation (kept apart from RX)
   // status (PGOAgent::iterate, src/PGOAgent.cpp:700-716): per colour, each agent's loop closures (problem
@@ -100,6 +108,7 @@ struct dpgo_rbcd_s {
     for (auto* g : gt) delete g;
     for (auto* g : gnc) delete g;
     for (auto* l : lc) delete l;
+    for (auto* x : halo) delete x;
   }
   size_t rb() const { return static_cast<size_t>(r) * b; }
 };
@@ -235,9 +244,80 @@ void exchange_plan(dpgo_graph g, const int* agent_of_pose, const int* agent_rank
   }
 }
 
+// The public poses the agents of colour c read this iteration: pose i (owned here) goes to peer q when an
+// edge joins it to a pose of q whose agent has colour c; pose j of peer q comes here when it joins an owned
+// pose whose agent has colour c.
+void exchange_plan_color(dpgo_graph g, const int* agent_of_pose, const int* agent_rank, const std::vector<int>& color,
+                         int c, int rank, int world, std::vector<std::set<int>>& send_set,
+                         std::vector<std::set<int>>& recv_set) {
+  send_set.assign(world, {});
+  recv_set.assign(world, {});
+  for (size_t k = 0; k < g->p1.size(); ++k) {
+    const int i = g->p1[k], j = g->p2[k];
+    const int ai = agent_of_pose[i], aj = agent_of_pose[j];
+    const int ri = agent_rank[ai], rj = agent_rank[aj];
+    if (ai == aj || ri == rj) continue;
+    if (ri == rank) {
+      if (color[aj] == c) send_set[rj].insert(i);
+      if (color[ai] == c) recv_set[rj].insert(j);
+    } else if (rj == rank) {
+      if (color[ai] == c) send_set[ri].insert(j);
+      if (color[aj] == c) recv_set[ri].insert(i);
+    }
+  }
+}
+
+// greedy colouring of the agent-adjacency graph in agent-id order (every rank computes the same)
+int agent_colors(dpgo_graph g, int num_agents, const int* agent_of_pose, std::vector<int>& color) {
+  std::vector<std::set<int>> adj(num_agents);
+  for (size_t k = 0; k < g->p1.size(); ++k) {
+    const int a1 = agent_of_pose[g->p1[k]], a2 = agent_of_pose[g->p2[k]];
+    if (a1 != a2) {
+      adj[a1].insert(a2);
+      adj[a2].insert(a1);
+    }
+  }
+  color.assign(num_agents, -1);
+  int ncolors = 0;
+  for (int a = 0; a < num_agents; ++a) {
+    std::set<int> used;
+    for (int nb : adj[a])
+      if (color[nb] >= 0) used.insert(color[nb]);
+    int c = 0;
+    while (used.count(c)) ++c;
+    color[a] = c;
+    ncolors = std::max(ncolors, c + 1);
+  }
+  return ncolors;
+}
+
 }  // namespace
 
 extern "C" {
+
+int dpgo_rbcd_plan_color(dpgo_graph g, int num_agents, const int* agent_of_pose, const int* agent_rank, int color,
+                         int rank, int world, long long* send_counts, long long* recv_counts, int* send_poses,
+                         int* recv_poses) {
+  if (!g || !agent_of_pose || !agent_rank || world <= 0 || rank < 0 || rank >= world || num_agents <= 0)
+    return fail(DPGO_HIP_EINVAL, "bad plan arguments");
+  for (int i = 0; i < g->n; ++i)
+    if (agent_of_pose[i] < 0 || agent_of_pose[i] >= num_agents) return fail(DPGO_HIP_EINVAL, "agent_of_pose out of range");
+  std::vector<int> col;
+  const int nc = agent_colors(g, num_agents, agent_of_pose, col);
+  if (color < 0 || color >= nc) return fail(DPGO_HIP_EINVAL, "bad colour");
+  std::vector<std::set<int>> ss, rs;
+  exchange_plan_color(g, agent_of_pose, agent_rank, col, color, rank, world, ss, rs);
+  long long so = 0, ro = 0;
+  for (int p = 0; p < world; ++p) {
+    if (send_counts) send_counts[p] = static_cast<long long>(ss[p].size());
+    if (recv_counts) recv_counts[p] = static_cast<long long>(rs[p].size());
+    if (send_poses)
+      for (int x : ss[p]) send_poses[so++] = x;
+    if (recv_poses)
+      for (int x : rs[p]) recv_poses[ro++] = x;
+  }
+  return DPGO_HIP_OK;
+}
 
 int dpgo_rbcd_plan(dpgo_graph g, int num_agents, const int* agent_of_pose, const int* agent_rank, int rank, int world,
                    long long* send_counts, long long* recv_counts, int* send_poses, int* recv_poses) {
@@ -320,25 +400,8 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
   }
   for (int a = 0; a < num_agents; ++a)
     if (agent_n[a] == 0) return bail(fail(DPGO_HIP_EINVAL, "every agent needs >= 1 pose"));
-  // agent adjacency + greedy colouring in agent-id order
-  std::vector<std::set<int>> adj(num_agents);
-  for (size_t k = 0; k < m; ++k) {
-    const int a1 = agent_of_pose[g->p1[k]], a2 = agent_of_pose[g->p2[k]];
-    if (a1 != a2) {
-      adj[a1].insert(a2);
-      adj[a2].insert(a1);
-    }
-  }
-  e->color.assign(num_agents, -1);
-  for (int a = 0; a < num_agents; ++a) {
-    std::set<int> used;
-    for (int nb : adj[a])
-      if (e->color[nb] >= 0) used.insert(e->color[nb]);
-    int c = 0;
-    while (used.count(c)) ++c;
-    e->color[a] = c;
-    e->ncolors = std::max(e->ncolors, c + 1);
-  }
+  // greedy colouring of the agent adjacency in agent-id order
+  e->ncolors = agent_colors(g, num_agents, agent_of_pose, e->color);
   // owned agents, colour-major
   e->color_off.assign(e->ncolors + 1, 0);
   for (int c = 0; c < e->ncolors; ++c) {
@@ -390,11 +453,37 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
   }
   e->n_send_items = static_cast<long>(pack_idx.size());
   e->n_recv_poses = rs;
+  // per-colour plans over the same RX slots
+  e->halo.assign(e->ncolors, nullptr);
+  std::vector<std::vector<int>> halo_pack(e->ncolors), halo_unpack(e->ncolors);
+  for (int c = 0; c < e->ncolors; ++c) {
+    auto* H = e->halo[c] = new dpgo_rbcd_s::Halo();
+    std::vector<std::set<int>> ss, rr;
+    exchange_plan_color(g, agent_of_pose, agent_rank, e->color, c, rank, world, ss, rr);
+    H->send_counts.assign(world, 0);
+    H->recv_counts.assign(world, 0);
+    H->send_off.assign(world + 1, 0);
+    H->recv_off.assign(world + 1, 0);
+    for (int p = 0; p < world; ++p) {
+      H->send_counts[p] = static_cast<long long>(ss[p].size()) * rbd;
+      H->recv_counts[p] = static_cast<long long>(rr[p].size()) * rbd;
+      H->send_off[p + 1] = H->send_off[p] + H->send_counts[p];
+      H->recv_off[p + 1] = H->recv_off[p] + H->recv_counts[p];
+      for (int pose : ss[p]) halo_pack[c].push_back(static_cast<int>(owned_index(pose)));
+      for (int pose : rr[p]) halo_unpack[c].push_back(static_cast<int>(recv_slot.at(pose)));
+    }
+    H->n_send = static_cast<long>(halo_pack[c].size());
+    H->n_recv = static_cast<long>(halo_unpack[c].size());
+  }
   if (hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(DPGO_HIP_EDEVICE, "stream create failed"));
   e->stream = e->own_stream;
   int rc = upload_vec(e->pack_idx, pack_idx, e->stream);
   if (rc == DPGO_HIP_OK) rc = upload_vec(e->unpack_x, unpack_x, e->stream);
+  for (int c = 0; c < e->ncolors && rc == DPGO_HIP_OK; ++c) {
+    rc = upload_vec(e->halo[c]->pack_idx, halo_pack[c], e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(e->halo[c]->unpack_slot, halo_unpack[c], e->stream);
+  }
   if (rc != DPGO_HIP_OK) return bail(rc);
   if (e->RX.ensure(std::max<long>(rs, 1) * e->rb()) != hipSuccess || e->RXc.ensure(std::max<long>(rs, 1) * e->rb()) != hipSuccess ||
       e->X.ensure(std::max<long>(e->Nown, 1) * e->rb()) != hipSuccess ||
@@ -749,6 +838,34 @@ int dpgo_rbcd_pack(dpgo_rbcd e, double* send_dev) {
   return DPGO_HIP_OK;
 }
 
+// A per-colour halo refreshes only the RX slots the selected colour reads.  With two colours that is also
+// every slot a non-selected colour's reweighting reads at the next iteration (its neighbours are exactly the
+// poses its own last exchange brought); with more colours and a robust cost the engine keeps the full halo.
+static bool halo_color_ok(dpgo_rbcd e) { return e->ncolors <= 2 || e->P.robust_cost == DPGO_ROBUST_L2; }
+
+int dpgo_rbcd_pack_color(dpgo_rbcd e, int color, double* send_dev) {
+  if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
+  if (!halo_color_ok(e)) return dpgo_rbcd_pack(e, send_dev);
+  const auto* H = e->halo[color];
+  if (H->n_send == 0) return DPGO_HIP_OK;
+  HIP_TRY(launch_gather_poses(static_cast<int>(H->n_send), static_cast<int>(e->rb()), H->pack_idx.p, e->X.p, e->X.p,
+                              send_dev, e->stream));
+  e->host_bytes += 2.0 * pose_bytes(e) * static_cast<double>(H->n_send);
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_exchange_counts_color(dpgo_rbcd e, int color, long long* send_counts, long long* recv_counts) {
+  if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
+  if (!halo_color_ok(e)) return dpgo_rbcd_exchange_counts(e, send_counts, recv_counts);
+  for (int p = 0; p < e->world; ++p) {
+    if (send_counts) send_counts[p] = e->halo[color]->send_counts[p];
+    if (recv_counts) recv_counts[p] = e->halo[color]->recv_counts[p];
+  }
+  return DPGO_HIP_OK;
+}
+
+static int update_body(dpgo_rbcd e, int color, dpgo_opt_result* results);
+
 int dpgo_rbcd_update(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_result* results) {
   if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
   const int rbs = static_cast<int>(e->rb());
@@ -758,6 +875,23 @@ int dpgo_rbcd_update(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_re
                                 e->stream));
     e->host_bytes += 2.0 * pose_bytes(e) * static_cast<double>(e->n_recv_poses);
   }
+  return update_body(e, color, results);
+}
+
+int dpgo_rbcd_update_color(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_result* results) {
+  if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
+  if (!halo_color_ok(e)) return dpgo_rbcd_update(e, color, recv_dev, results);
+  const auto* H = e->halo[color];
+  if (H->n_recv > 0) {
+    if (!recv_dev) return fail(DPGO_HIP_EINVAL, "receive buffer required");
+    HIP_TRY(launch_scatter_poses(static_cast<int>(H->n_recv), static_cast<int>(e->rb()), H->unpack_slot.p, recv_dev,
+                                 e->RX.p, e->stream));
+    e->host_bytes += 2.0 * pose_bytes(e) * static_cast<double>(H->n_recv);
+  }
+  return update_body(e, color, results);
+}
+
+static int update_body(dpgo_rbcd e, int color, dpgo_opt_result* results) {
   const bool restart = restart_now(e);
   if (e->gnc_due) {
     DPGO_TRY(reweight_color(e, color));
@@ -1132,28 +1266,46 @@ int dpgo_rbcd_comm_attach(dpgo_rbcd e, void* comm) {
   return DPGO_HIP_OK;
 }
 
+namespace {
+// one RCCL group: every peer's send and receive of a plan, on the engine stream (stream order = halo order)
+int rccl_halo(dpgo_rbcd e, const std::vector<long long>& sc, const std::vector<long long>& so,
+              const std::vector<long long>& rcn, const std::vector<long long>& ro) {
+  DPGO_TRY(rccl_check(rccl().GroupStart(), "ncclGroupStart"));
+  int rc = DPGO_HIP_OK;
+  for (int p = 0; p < e->world && rc == DPGO_HIP_OK; ++p) {
+    if (sc[p] > 0)
+      rc = rccl_check(rccl().Send(e->xsend.p + so[p], static_cast<size_t>(sc[p]), ncclFloat64, p, e->comm, e->stream),
+                      "ncclSend");
+    if (rc == DPGO_HIP_OK && rcn[p] > 0)
+      rc = rccl_check(rccl().Recv(e->xrecv.p + ro[p], static_cast<size_t>(rcn[p]), ncclFloat64, p, e->comm, e->stream),
+                      "ncclRecv");
+  }
+  const int rc_end = rccl_check(rccl().GroupEnd(), "ncclGroupEnd");
+  DPGO_TRY(rc);
+  return rc_end;
+}
+}  // namespace
+
 int dpgo_rbcd_exchange(dpgo_rbcd e, const double** recv_dev) {
   if (!e || !recv_dev) return fail(DPGO_HIP_EINVAL, "null argument");
   if (e->world > 1 && !e->comm) return fail(DPGO_HIP_ESTATE, "no communicator (dpgo_rbcd_comm_init / _attach)");
   HIP_TRY(e->xsend.ensure(std::max<long long>(e->send_off[e->world], 1)));
   HIP_TRY(e->xrecv.ensure(std::max<long long>(e->recv_off[e->world], 1)));
   DPGO_TRY(dpgo_rbcd_pack(e, e->xsend.p));
-  if (e->world > 1) {
-    // one group: every peer's send and receive, on the engine stream (stream order = halo order)
-    DPGO_TRY(rccl_check(rccl().GroupStart(), "ncclGroupStart"));
-    int rc = DPGO_HIP_OK;
-    for (int p = 0; p < e->world && rc == DPGO_HIP_OK; ++p) {
-      if (e->send_counts[p] > 0)
-        rc = rccl_check(rccl().Send(e->xsend.p + e->send_off[p], static_cast<size_t>(e->send_counts[p]), ncclFloat64, p,
-                                    e->comm, e->stream), "ncclSend");
-      if (rc == DPGO_HIP_OK && e->recv_counts[p] > 0)
-        rc = rccl_check(rccl().Recv(e->xrecv.p + e->recv_off[p], static_cast<size_t>(e->recv_counts[p]), ncclFloat64,
-                                    p, e->comm, e->stream), "ncclRecv");
-    }
-    const int rc_end = rccl_check(rccl().GroupEnd(), "ncclGroupEnd");
-    DPGO_TRY(rc);
-    DPGO_TRY(rc_end);
-  }
+  if (e->world > 1) DPGO_TRY(rccl_halo(e, e->send_counts, e->send_off, e->recv_counts, e->recv_off));
+  *recv_dev = e->xrecv.p;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_exchange_color(dpgo_rbcd e, int color, const double** recv_dev) {
+  if (!e || !recv_dev || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad argument");
+  if (!halo_color_ok(e)) return dpgo_rbcd_exchange(e, recv_dev);
+  if (e->world > 1 && !e->comm) return fail(DPGO_HIP_ESTATE, "no communicator (dpgo_rbcd_comm_init / _attach)");
+  const auto* H = e->halo[color];
+  HIP_TRY(e->xsend.ensure(std::max<long long>(e->send_off[e->world], 1)));  // the full plan bounds every colour's
+  HIP_TRY(e->xrecv.ensure(std::max<long long>(e->recv_off[e->world], 1)));
+  DPGO_TRY(dpgo_rbcd_pack_color(e, color, e->xsend.p));
+  if (e->world > 1) DPGO_TRY(rccl_halo(e, H->send_counts, H->send_off, H->recv_counts, H->recv_off));
   *recv_dev = e->xrecv.p;
   return DPGO_HIP_OK;
 }

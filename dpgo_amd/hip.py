@@ -488,6 +488,11 @@ _SIGS2 = [
     ("dpgo_rbcd_set_trace", [C.c_void_p, C.c_int], C.c_int),
     ("dpgo_rbcd_get_trace", [C.c_void_p, C.c_int, _dp, C.c_int, _ip], C.c_int),
     ("dpgo_rbcd_kernel_times", [C.c_void_p, _dp, _lp], C.c_int),
+    ("dpgo_rbcd_plan_color", [C.c_void_p, C.c_int, _ip, _ip, C.c_int, C.c_int, C.c_int, _lp, _lp, _ip, _ip], C.c_int),
+    ("dpgo_rbcd_exchange_counts_color", [C.c_void_p, C.c_int, _lp, _lp], C.c_int),
+    ("dpgo_rbcd_pack_color", [C.c_void_p, C.c_int, C.c_void_p], C.c_int),
+    ("dpgo_rbcd_update_color", [C.c_void_p, C.c_int, C.c_void_p, C.POINTER(OptResult)], C.c_int),
+    ("dpgo_rbcd_exchange_color", [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)], C.c_int),
 ]
 _SIGS.extend(_SIGS2)
 EXPORTED_SYMBOLS.extend(s[0] for s in _SIGS2)
@@ -669,6 +674,21 @@ def exchange_plan(graph: "Graph", agent_of_pose, agent_rank, rank, world):
     return ([sp_[so[p]:so[p + 1]] for p in range(world)], [rp_[ro[p]:ro[p + 1]] for p in range(world)])
 
 
+def exchange_plan_color(graph: "Graph", agent_of_pose, agent_rank, color, rank, world):
+    """Host-only per-colour halo plan (the poses colour `color`'s agents read): ([send ids per peer],
+    [recv ids per peer])."""
+    aop, ap = _i32(agent_of_pose)
+    ar, arp = _i32(agent_rank)
+    sc = np.empty(world, np.int64); rc = np.empty(world, np.int64)
+    _check(lib().dpgo_rbcd_plan_color(graph.h, len(ar), ap, arp, int(color), rank, world, sc.ctypes.data_as(_lp),
+                                      rc.ctypes.data_as(_lp), None, None))
+    sp_ = np.empty(max(int(sc.sum()), 1), np.int32); rp_ = np.empty(max(int(rc.sum()), 1), np.int32)
+    _check(lib().dpgo_rbcd_plan_color(graph.h, len(ar), ap, arp, int(color), rank, world, None, None,
+                                      sp_.ctypes.data_as(_ip), rp_.ctypes.data_as(_ip)))
+    so = np.concatenate([[0], np.cumsum(sc)]); ro = np.concatenate([[0], np.cumsum(rc)])
+    return ([sp_[so[p]:so[p + 1]] for p in range(world)], [rp_[ro[p]:ro[p + 1]] for p in range(world)])
+
+
 def lifting_matrix(d, r, seed=2):
     """Repo-defined lifting matrix YLift in St(d, r) (replaces ROPTLIB's RNG)."""
     M = np.random.default_rng(seed).standard_normal((r, d))
@@ -712,6 +732,13 @@ class Rbcd:
         sc = np.empty(world, np.int64); rc = np.empty(world, np.int64)
         _check(lib().dpgo_rbcd_exchange_counts(self.h, sc.ctypes.data_as(_lp), rc.ctypes.data_as(_lp)))
         self.send_counts, self.recv_counts = sc, rc
+        # per-colour halos (doubles per peer)
+        self.send_counts_color, self.recv_counts_color = [], []
+        for c in range(self.num_colors):
+            sc = np.empty(world, np.int64); rc = np.empty(world, np.int64)
+            _check(lib().dpgo_rbcd_exchange_counts_color(self.h, c, sc.ctypes.data_as(_lp), rc.ctypes.data_as(_lp)))
+            self.send_counts_color.append(sc)
+            self.recv_counts_color.append(rc)
 
     def close(self):
         if getattr(self, "h", None):
@@ -782,6 +809,25 @@ class Rbcd:
         rccl_unique_id() on one rank, shared by the caller."""
         buf = C.create_string_buffer(bytes(uid), 128)
         _check(lib().dpgo_rbcd_comm_init(self.h, buf))
+
+    def exchange_color(self, color):
+        """Per-colour halo by the engine's RCCL group (after pre_exchange(color)); pass the result to
+        update_color()."""
+        p = C.c_void_p()
+        _check(lib().dpgo_rbcd_exchange_color(self.h, int(color), C.byref(p)))
+        return p.value
+
+    def pack_color(self, color, send_ptr):
+        _check(lib().dpgo_rbcd_pack_color(self.h, int(color), C.c_void_p(send_ptr or 0)))
+
+    def update_color(self, color, recv_ptr, want_results=False):
+        if want_results:
+            n = int(self.agents_per_color[color])
+            res = (OptResult * max(n, 1))()
+            _check(lib().dpgo_rbcd_update_color(self.h, int(color), C.c_void_p(recv_ptr or 0), res))
+            return [res[i].as_dict() for i in range(n)]
+        _check(lib().dpgo_rbcd_update_color(self.h, int(color), C.c_void_p(recv_ptr or 0), None))
+        return None
 
     def exchange(self):
         """Pack + RCCL send/recv of the public poses (after pre_exchange); returns the device pointer of

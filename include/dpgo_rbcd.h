@@ -154,6 +154,19 @@ int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color);
 int dpgo_rbcd_pack(dpgo_rbcd e, double* send_dev);
 /* Phase 2: selected agents of colour c update from the received neighbour poses. */
 int dpgo_rbcd_update(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_result* results);
+/* Per-colour halo (examples/MultiRobotExample.cpp:188-213: only the selected robot pulls its neighbours'
+ * poses): the poses the agents of colour c read this iteration -- about half the full plan with two
+ * colours.  Same call order as the full halo: dpgo_rbcd_pre_exchange(c), dpgo_rbcd_pack_color(c) into a
+ * buffer laid out by dpgo_rbcd_exchange_counts_color(c) (peer-major, ascending global pose id), the
+ * exchange, dpgo_rbcd_update_color(c).  Results are bitwise those of the full halo.  With more than two
+ * colours and a robust cost (whose reweighting of the other colours reads their neighbours too) these
+ * fall back to the full plan and layout.  dpgo_rbcd_central_eval always takes the full plan. */
+int dpgo_rbcd_plan_color(dpgo_graph g, int num_agents, const int* agent_of_pose, const int* agent_rank, int color,
+                         int rank, int world, long long* send_counts, long long* recv_counts, int* send_poses,
+                         int* recv_poses);
+int dpgo_rbcd_exchange_counts_color(dpgo_rbcd e, int color, long long* send_counts, long long* recv_counts);
+int dpgo_rbcd_pack_color(dpgo_rbcd e, int color, double* send_dev);
+int dpgo_rbcd_update_color(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_result* results);
 /* Algorithmic HBM bytes of one X.Q SpMM over colour class c on this rank, and the timed average
  * of `reps` such launches (ms, HIP events on the engine stream). */
 int dpgo_rbcd_bench_spmm(dpgo_rbcd e, int color, int reps, double* bytes, double* ms);
@@ -197,6 +210,8 @@ int dpgo_rccl_unique_id(void* id_out);
 int dpgo_rbcd_comm_init(dpgo_rbcd e, const void* id);
 int dpgo_rbcd_comm_attach(dpgo_rbcd e, void* comm);
 int dpgo_rbcd_exchange(dpgo_rbcd e, const double** recv_dev);
+/* the per-colour halo of colour c by the same RCCL group (then dpgo_rbcd_update_color) */
+int dpgo_rbcd_exchange_color(dpgo_rbcd e, int color, const double** recv_dev);
 /* SpMM modes of the per-mode arrays, in this order: XQ, XQ_G, EVAL, HESS, F, EVAL_TCG, CERT, QF, HESS_QF,
  * HESS_M, HESS_QF_M (the last two: the merged tCG iteration's Hessian passes) */
 #define DPGO_SPMM_MODES 11

@@ -35,7 +35,7 @@ def _params(H, accel, robust):
     return H.rbcd_params(r=R, acceleration=int(accel), robust_cost=H.ROBUST[robust], robust_opt_inner_iters=3)
 
 
-def _worker(rank, world, port, accel, robust, q):
+def _worker(rank, world, port, accel, robust, q, halo="full"):
     import sys
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -60,6 +60,16 @@ def _worker(rank, world, port, accel, robust, q):
             for it in range(ITERS):
                 c = it % e.num_colors
                 e.pre_exchange(c)
+                if halo == "color":  # per-colour halo: only the poses colour c's agents read
+                    rs_c = [int(x) for x in e.recv_counts_color[c]]
+                    ss_c = [int(x) for x in e.send_counts_color[c]]
+                    e.pack_color(c, send.data_ptr())
+                    hs = send[:sum(ss_c)].cpu()
+                    hr = torch.empty(sum(rs_c), dtype=torch.float64)
+                    dist.all_to_all_single(hr, hs, rs_c, ss_c)
+                    recv[:sum(rs_c)].copy_(hr)
+                    e.update_color(c, recv.data_ptr())
+                    continue
                 e.pack(send.data_ptr())
                 hs = send.cpu()  # D2H on the current stream: ordered after the pack
                 hr = torch.empty_like(recv, device="cpu")
@@ -74,15 +84,16 @@ def _worker(rank, world, port, accel, robust, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("robust", ["L2", "GNC_TLS"])
+@pytest.mark.parametrize("robust,halo", [("L2", "full"), ("GNC_TLS", "full"), ("L2", "color"), ("GNC_TLS", "color")])
 @pytest.mark.parametrize("accel", [False, True])
-def test_two_ranks_bitwise_one_rank_and_oracle(accel, robust):
+def test_two_ranks_bitwise_one_rank_and_oracle(accel, robust, halo):
     """GNC_TLS: shared loop closures across the two ranks are reweighted by the lower-ID agent from
-    the received neighbour poses (robust_opt_inner_iters = 3: reweightings at iterations 2 and 5)."""
+    the received neighbour poses (robust_opt_inner_iters = 3: reweightings at iterations 2 and 5).
+    halo "color": per-colour halos (dpgo_rbcd_pack_color / update_color), bitwise the full halo's result."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, accel, robust, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, accel, robust, q, halo)) for r in range(2)]
     for p in procs:
         p.start()
     outs = sorted([q.get(timeout=240) for _ in range(2)], key=lambda o: o[0])

@@ -102,12 +102,11 @@ def _rtr_trace_case(hip, name, r, iters, tol, radius, inner, precon, merged):
         # the merged one by 8e-8 at 11): the bars of this case are 1e-6
         tol = 1e-6
     # The merged tCG iteration forms |r_{j+1}|^2 and <z_{j+1}, r_{j+1}> (hence beta) from one-step
-    # polynomials in alpha over r_j and Hd_j: exact in exact arithmetic, but the sum cancels by the factor
-    # <z_j, r_j> / <z_{j+1}, r_{j+1}>, so on a fast-converging tCG the directions after a large drop carry
-    # eps times that factor (measured: 2e-10 of the largest d_Hd on tinyGrid3D).  The tCG-internal
-    # quantities get 1e-8 of their scale there; costs, rho, gradient norms, statuses, iteration counts and
-    # X keep the classic bars (the classic sequence itself is held to 1e-10 by "bj-classic").
-    tcg_tol = max(1e-8, tol) if merged else tol
+    # polynomials in alpha over r_j and Hd_j, whose terms cancel by the factor <z_j, r_j> / <z_{j+1},
+    # r_{j+1}>.  Their partials are double-double (exact products, compensated sums, the polynomial in
+    # double-double: dpgo_device.h dd_*), so only the final rounding remains and the merged sequence is
+    # held to the classic bars.  (Plain double partials measured 2e-10 of the largest d_Hd on tinyGrid3D.)
+    tcg_tol = tol
     scale, run_id = {}, None
     for g, e in zip(got, exp):
         if e["op"] == 5 or run_id != g["run"]:
