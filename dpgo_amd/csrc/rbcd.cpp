@@ -34,6 +34,11 @@ struct dpgo_rbcd_s {
   std::vector<int> own_global;            // owned buffer pose index -> global pose id
   hipStream_t stream = nullptr;           // launch stream (the caller's after dpgo_rbcd_set_stream)
   hipStream_t own_stream = nullptr;       // created and destroyed by the engine
+  // N > 1: the selected colour's updateY runs on a side stream while the launch stream does the other
+  // colours' iterate(false) and the halo; dpgo_rbcd_update joins it (ev_sel) before its first launch
+  hipStream_t side = nullptr;
+  hipEvent_t ev_start = nullptr, ev_sel = nullptr;
+  bool sel_pending = false;
   std::vector<dpgo_hip_problem> prob;     // per colour (nullptr if none owned)
   DevBuf<double> X, Y, V, Xprev;
   // exchange: the public poses' X only.  With Nesterov a receiver uses its neighbours' aux poses
@@ -131,11 +136,12 @@ long color_num_poses(dpgo_rbcd e, int c) { return e->own_pose_off[e->color_off[c
 double pose_bytes(dpgo_rbcd e) { return 8.0 * static_cast<double>(e->rb()); }
 
 int polar(dpgo_rbcd e, int c, const double* A, const double* B, double ca, double cb, double* out,
-          const double* C = nullptr, double* out2 = nullptr, double* xcopy = nullptr) {
+          const double* C = nullptr, double* out2 = nullptr, double* xcopy = nullptr, hipStream_t on = nullptr) {
   dpgo_hip_problem h = e->prob[c];
   if (!h) return DPGO_HIP_OK;
   // uniform Nesterov coefficients travel as kernel arguments
   auto ctx = make_ctx(h, FLAG_NONE, h->pa.p);
+  if (on) ctx.stream = on;
   HIP_TRY(launch_polar_comb(e->r, e->b, ctx, A, B, nullptr, nullptr, out, C, ca, cb, out2, xcopy));
   e->host_bytes += pose_bytes(e) * static_cast<double>(color_num_poses(e, c)) *
                    (1.0 + (B ? 1.0 : 0.0) + (C ? 1.0 : 0.0) + 1.0 + (out2 ? 1.0 : 0.0) + (xcopy ? 1.0 : 0.0));
@@ -145,15 +151,16 @@ int polar(dpgo_rbcd e, int c, const double* A, const double* B, double ca, doubl
 // out = project((1 - alpha) X + alpha V) for colour c, preceded by the colour's deferred updateV
 // V = project(V + gamma (X - Y)) in the same pass when one is pending.  xcopy: XPrev = X (the selected
 // colour's status reference) written from the same loads.
-int nesterov_comb(dpgo_rbcd e, int c, double* out, double* xcopy = nullptr) {
+int nesterov_comb(dpgo_rbcd e, int c, double* out, double* xcopy = nullptr, hipStream_t on = nullptr) {
   dpgo_hip_problem h = e->prob[c];
   if (!h) return DPGO_HIP_OK;
   double* Xc = color_ptr(e, e->X, c);
   double* Yc = color_ptr(e, e->Y, c);
   double* Vc = color_ptr(e, e->V, c);
-  if (!e->v_pending[c]) return polar(e, c, Xc, Vc, 1.0 - e->alpha, e->alpha, out, nullptr, nullptr, xcopy);
+  if (!e->v_pending[c]) return polar(e, c, Xc, Vc, 1.0 - e->alpha, e->alpha, out, nullptr, nullptr, xcopy, on);
   e->v_pending[c] = 0;
   auto ctx = make_ctx(h, FLAG_NONE, h->pa.p);
+  if (on) ctx.stream = on;
   HIP_TRY(launch_polar_vnext(e->r, e->b, ctx, Xc, Vc, Yc, e->v_gamma[c], 1.0 - e->alpha, e->alpha, out, xcopy));
   e->host_bytes += pose_bytes(e) * static_cast<double>(color_num_poses(e, c)) * (5.0 + (xcopy ? 1.0 : 0.0));
   return DPGO_HIP_OK;
@@ -478,6 +485,10 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
   if (hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(DPGO_HIP_EDEVICE, "stream create failed"));
   e->stream = e->own_stream;
+  if (world > 1 && (hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess ||
+                    hipEventCreateWithFlags(&e->ev_start, hipEventDisableTiming) != hipSuccess ||
+                    hipEventCreateWithFlags(&e->ev_sel, hipEventDisableTiming) != hipSuccess))
+    return bail(fail(DPGO_HIP_EDEVICE, "side stream create failed"));
   int rc = upload_vec(e->pack_idx, pack_idx, e->stream);
   if (rc == DPGO_HIP_OK) rc = upload_vec(e->unpack_x, unpack_x, e->stream);
   for (int c = 0; c < e->ncolors && rc == DPGO_HIP_OK; ++c) {
@@ -687,6 +698,7 @@ int dpgo_rbcd_destroy(dpgo_rbcd e) {
 
 namespace {
 void use_stream(dpgo_rbcd e, hipStream_t s) {
+  if (e->side) (void)hipStreamSynchronize(e->side);
   e->stream = s;
   for (auto* h : e->prob)
     if (h) h->stream = s;  // verbatim: a NULL stream is the HIP null stream here
@@ -803,6 +815,15 @@ int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color) {
   const double N = static_cast<double>(e->K);
   e->gamma = (1.0 + std::sqrt(1.0 + 4.0 * N * N * e->gamma * e->gamma)) / (2.0 * N);  // updateGamma
   e->alpha = 1.0 / (e->gamma * N);                                                     // updateAlpha
+  // N > 1: the selected colour's updateY (which nothing of the halo reads) goes to the side stream, after
+  // everything queued so far; the other colours' combinations (whose X the halo sends) stay in order on the
+  // launch stream, so the pack and the exchange can start while the side stream works
+  hipStream_t on = nullptr;
+  if (e->side && e->prob[color]) {
+    HIP_TRY(hipEventRecord(e->ev_start, e->stream));
+    HIP_TRY(hipStreamWaitEvent(e->side, e->ev_start, 0));
+    on = e->side;
+  }
   for (int c = 0; c < e->ncolors; ++c) {
     if (!e->prob[c]) continue;
     double* Xc = color_ptr(e, e->X, c);
@@ -810,7 +831,11 @@ int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color) {
     if (c == color) {
       // updateY (selected); XPrev = X (:673) for the status, written from the same loads (a restart
       // iteration already copied every X above)
-      DPGO_TRY(nesterov_comb(e, c, Yc, e->P.status && !restart ? color_ptr(e, e->Xprev, c) : nullptr));
+      DPGO_TRY(nesterov_comb(e, c, Yc, e->P.status && !restart ? color_ptr(e, e->Xprev, c) : nullptr, on));
+      if (on) {
+        HIP_TRY(hipEventRecord(e->ev_sel, e->side));
+        e->sel_pending = true;
+      }
       continue;
     }
     // non-selected agents, iterate(false): updateY, updateX(false, true): X = Y (one fused pass,
@@ -892,6 +917,10 @@ int dpgo_rbcd_update_color(dpgo_rbcd e, int color, const double* recv_dev, dpgo_
 }
 
 static int update_body(dpgo_rbcd e, int color, dpgo_opt_result* results) {
+  if (e->sel_pending) {  // the selected colour's updateY from the side stream (dpgo_rbcd_pre_exchange)
+    HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_sel, 0));
+    e->sel_pending = false;
+  }
   const bool restart = restart_now(e);
   if (e->gnc_due) {
     DPGO_TRY(reweight_color(e, color));
@@ -1228,6 +1257,12 @@ int rccl_ready() {
 
 dpgo_rbcd_s::~dpgo_rbcd_s() {
   if (comm && own_comm && rccl().lib) (void)rccl().CommDestroy(comm);
+  if (side) {
+    (void)hipStreamSynchronize(side);
+    (void)hipStreamDestroy(side);
+  }
+  if (ev_start) (void)hipEventDestroy(ev_start);
+  if (ev_sel) (void)hipEventDestroy(ev_sel);
   release();
 }
 

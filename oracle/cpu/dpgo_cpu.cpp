@@ -484,9 +484,12 @@ struct SharedEdge {
 struct CpuAgent {
   Agent A;
   std::vector<long> poses;  // global ids, local order
+  std::vector<int> edges;   // global edge ids touching the agent (private and shared)
+  std::vector<double> w;    // this agent's weight per entry of edges (its own copy of a shared edge's)
   std::vector<SharedEdge> shared;
   OptStats st;
   double status_rel = 0.0;
+  double conv_ratio = 1.0;  // computeConvergedLoopClosureRatio (GNC_TLS)
   int ready = 0;
 };
 
@@ -499,14 +502,26 @@ struct CpuEngine {
   double gamma = 0.0, alpha = 0.0;
   long iteration = 0;
   std::vector<Work> work;  // per thread
+  // the graph (kept for the robust cost's reweighting and Q rebuilds)
+  int m = 0;
+  std::vector<int> p1, p2, agent_of, local;
+  std::vector<double> R, t, kappa, tau;
+  // robust cost (0: L2, 1: GNC_TLS; RobustCostParameters / PGOAgentParameters defaults)
+  int robust = 0, inner_iters = 30, gnc_max_iters = 100, gnc_iter = 0;
+  double mu = 1e-4, mu_step = 1.4, barc = 10.0, min_ratio = 0.8;
   size_t rb() const { return static_cast<size_t>(r) * b; }
 };
 
+// Q (private edges + shared-edge diagonal terms), block-Jacobi inverses, shared edges and G slots of agent
+// a from its edge list, with weights w (per entry of `edges`; nullptr = 1): PGOAgent::constructQMatrix
 void build_agent(int d, int r, int m, const int* p1, const int* p2, const double* R, const double* t, const double* kappa,
                  const double* tau, const int* agent_of, const std::vector<int>& local, int a,
-                 const std::vector<int>& edges, CpuAgent& out) {
+                 const std::vector<int>& edges, CpuAgent& out, const double* w = nullptr) {
   const int b = d + 1, bb = b * b, rb = r * b;
+  (void)m;
   Agent& A = out.A;
+  out.shared.clear();
+  A.gpose.clear();
   A.d = d;
   A.r = r;
   A.b = b;
@@ -521,13 +536,15 @@ void build_agent(int d, int r, int m, const int* p1, const int* p2, const double
     Trip tz{j, j, {0}};
     trips.push_back(tz);
   }
-  for (int e : edges) {
+  for (size_t q = 0; q < edges.size(); ++q) {
+    const int e = edges[q];
     const int i = p1[e], j = p2[e];
     const bool oi = agent_of[i] == a, oj = agent_of[j] == a;
+    const double we = w ? w[q] : 1.0;
     double T[4][4], Om[4];
     edge_T(d, &R[static_cast<size_t>(e) * d * d], &t[static_cast<size_t>(e) * d], T);
-    for (int u = 0; u < d; ++u) Om[u] = kappa[e];
-    Om[d] = tau[e];
+    for (int u = 0; u < d; ++u) Om[u] = we * kappa[e];
+    Om[d] = we * tau[e];
     Trip ii{local[i], local[i], {0}}, jj{local[j], local[j], {0}}, ij{local[i], local[j], {0}}, ji{local[j], local[i], {0}};
     for (int u = 0; u < b; ++u)
       for (int v = 0; v < b; ++v) {
@@ -638,10 +655,72 @@ void project_all(std::vector<double>& M, int r, int d, size_t rb) {
   for (size_t q = 0; q < M.size() / rb; ++q) polar_pose(r, d, &M[q * rb]);
 }
 
+// RobustCost::weight for GNC_TLS (src/DPGO_robust.cpp:23-67) at the engine's mu
+double gnc_tls_weight(const CpuEngine& E, double rr) {
+  const double rsq = rr * rr, bc = E.barc * E.barc, mu = E.mu;
+  if (rsq >= (mu + 1) / mu * bc) return 0.0;
+  if (rsq <= mu / (mu + 1) * bc) return 1.0;
+  return std::sqrt(bc * mu * (mu + 1) / rsq) - mu;
+}
+
+// computeMeasurementError (src/DPGO_utils.cpp:509-515) of edge e between global poses i and j of X
+double measurement_error(const CpuEngine& E, int e, long i, long j) {
+  const int d = E.d, r = E.r;
+  const double* Xi = &E.X[static_cast<size_t>(i) * E.rb()];
+  const double* Xj = &E.X[static_cast<size_t>(j) * E.rb()];
+  const double* Rm = &E.R[static_cast<size_t>(e) * d * d];
+  const double* tv = &E.t[static_cast<size_t>(e) * d];
+  double rot = 0.0, tr = 0.0;
+  for (int a = 0; a < r; ++a) {
+    for (int c = 0; c < d; ++c) {  // (Y1 R - Y2)[a][c]; Y column c = X[c * r + a]
+      double s = -Xj[c * r + a];
+      for (int u = 0; u < d; ++u) s += Xi[u * r + a] * Rm[u * d + c];
+      rot += s * s;
+    }
+    double s = Xj[d * r + a] - Xi[d * r + a];  // p2 - p1 - Y1 t
+    for (int u = 0; u < d; ++u) s -= Xi[u * r + a] * tv[u];
+    tr += s * s;
+  }
+  return E.kappa[e] * rot + E.tau[e] * tr;
+}
+
+// PGOAgent::updateLoopClosuresWeights (src/PGOAgent.cpp:1181-1244) then constructQMatrix: private loop
+// closures (not odometry: consecutive local indices) and the shared ones this agent owns the update of
+// (the other agent has the larger ID), at the current global X; plus the converged ratio.
+void reweight_agent(CpuEngine& E, int a) {
+  CpuAgent& c = E.ag[a];
+  long lc = 0, conv = 0;
+  for (size_t q = 0; q < c.edges.size(); ++q) {
+    const int e = c.edges[q], i = E.p1[e], j = E.p2[e];
+    const int ai = E.agent_of[i], aj = E.agent_of[j];
+    if (ai == aj) {
+      if (E.local[j] == E.local[i] + 1) continue;  // odometry: never reweighted, not a loop closure
+    } else if ((ai == a ? aj : ai) < a) {
+      ++lc;  // the other agent updates it; this copy keeps its weight
+      conv += (c.w[q] == 1.0 || c.w[q] == 0.0) ? 1 : 0;
+      continue;
+    }
+    c.w[q] = gnc_tls_weight(E, std::sqrt(measurement_error(E, e, i, j)));
+    ++lc;
+    conv += (c.w[q] == 1.0 || c.w[q] == 0.0) ? 1 : 0;
+  }
+  c.conv_ratio = lc ? static_cast<double>(conv) / static_cast<double>(lc) : std::nan("");
+  build_agent(E.d, E.r, E.m, E.p1.data(), E.p2.data(), E.R.data(), E.t.data(), E.kappa.data(), E.tau.data(),
+              E.agent_of.data(), E.local, a, c.edges, c, c.w.data());
+}
+
 // PGOAgent::iterate for agent a (selected or not) on the global state; gamma / alpha already updated
-void iterate_agent(CpuEngine& E, int a, bool selected, bool restart, Work& w) {
+void iterate_agent(CpuEngine& E, int a, bool selected, bool restart, Work& w, bool reweight = false) {
   CpuAgent& c = E.ag[a];
   const size_t rb = E.rb();
+  if (reweight) {  // shouldUpdateLoopClosureWeights: reweight, then initializeAcceleration (XPrev = V = Y = X)
+    reweight_agent(E, a);
+    if (E.accel)
+      for (long p : c.poses) {
+        std::memcpy(&E.V[static_cast<size_t>(p) * rb], &E.X[static_cast<size_t>(p) * rb], sizeof(double) * rb);
+        std::memcpy(&E.Y[static_cast<size_t>(p) * rb], &E.X[static_cast<size_t>(p) * rb], sizeof(double) * rb);
+      }
+  }
   if (selected && w.x1.size() != c.A.L()) w.init(c.A.L(), static_cast<size_t>(c.A.n) * E.d * E.d);
   std::vector<double> X, Y, V, XP;
   gather(c, E.X, X, rb);
@@ -678,7 +757,7 @@ void iterate_agent(CpuEngine& E, int a, bool selected, bool restart, Work& w) {
     double s = 0.0;
     for (size_t i = 0; i < X.size(); ++i) s += (X[i] - XP[i]) * (X[i] - XP[i]);
     c.status_rel = std::sqrt(s / static_cast<double>(c.poses.size()));
-    c.ready = c.status_rel <= 5e-3 ? 1 : 0;
+    c.ready = (c.status_rel > 5e-3 || (E.robust && c.conv_ratio < E.min_ratio)) ? 0 : 1;
   }
   scatter(c, X, E.X, rb);
 }
@@ -687,10 +766,22 @@ void iterate_agent(CpuEngine& E, int a, bool selected, bool restart, Work& w) {
 
 extern "C" {
 
+// robust: 0 = L2, 1 = GNC_TLS (reweighting every robust_inner_iters iterations, mu from 1e-4 by 1.4 per
+// reweighting for at most 100, barc 10, converged-ratio threshold 0.8: the PGOAgentParameters defaults)
 void* dpgo_cpu_rbcd_create(int d, int r, int m, const int* p1, const int* p2, const double* R, const double* t,
                            const double* kappa, const double* tau, long n, const int* agent_of_pose, int num_agents,
-                           int accel, int restart_interval) {
+                           int accel, int restart_interval, int robust, int robust_inner_iters) {
   auto* E = new CpuEngine();
+  E->robust = robust;
+  E->inner_iters = robust_inner_iters > 0 ? robust_inner_iters : 30;
+  E->m = m;
+  E->p1.assign(p1, p1 + m);
+  E->p2.assign(p2, p2 + m);
+  E->R.assign(R, R + static_cast<size_t>(m) * d * d);
+  E->t.assign(t, t + static_cast<size_t>(m) * d);
+  E->kappa.assign(kappa, kappa + m);
+  E->tau.assign(tau, tau + m);
+  E->agent_of.assign(agent_of_pose, agent_of_pose + n);
   E->d = d;
   E->r = r;
   E->b = d + 1;
@@ -727,9 +818,13 @@ void* dpgo_cpu_rbcd_create(int d, int r, int m, const int* p1, const int* p2, co
     E->color[a] = c;
     E->C = std::max(E->C, c + 1);
   }
+  E->local = local;
 #pragma omp parallel for schedule(dynamic)
-  for (int a = 0; a < num_agents; ++a)
+  for (int a = 0; a < num_agents; ++a) {
+    E->ag[a].edges = edges[a];
+    E->ag[a].w.assign(edges[a].size(), 1.0);
     build_agent(d, r, m, p1, p2, R, t, kappa, tau, agent_of_pose, local, a, edges[a], E->ag[a]);
+  }
   const size_t L = static_cast<size_t>(n) * E->rb();
   E->X.assign(L, 0.0);
   E->Y.assign(L, 0.0);
@@ -765,6 +860,11 @@ double dpgo_cpu_rbcd_iterate(void* h, int threads, double* upd_sec, int timed_se
   const int c = static_cast<int>(E->iteration % E->C);
   E->iteration += 1;
   const bool restart = E->accel && ((E->iteration + 1) % E->restart == 0);
+  // shouldUpdateLoopClosureWeights (:1174-1179): every agent reweights at the start of its iterate (the
+  // non-selected ones first, the selected ones after them, on the poses their neighbours then hold), all
+  // with this mu; RobustCost::update once afterwards; with acceleration each restarts Nesterov
+  const bool gnc = E->robust && (E->iteration + 1) % E->inner_iters == 0;
+  if (gnc && E->accel) E->gamma = E->alpha = 0.0;
   if (E->accel) {
     const double N = E->K;
     E->gamma = (1 + std::sqrt(1 + 4 * N * N * E->gamma * E->gamma)) / (2 * N);
@@ -774,19 +874,21 @@ double dpgo_cpu_rbcd_iterate(void* h, int threads, double* upd_sec, int timed_se
   for (int a = 0; a < E->K; ++a) (E->color[a] == c ? sel : oth).push_back(a);
   const int T = std::max(1, std::min(threads, static_cast<int>(E->work.size())));
 #pragma omp parallel for num_threads(T) schedule(dynamic)
-  for (int q = 0; q < static_cast<int>(oth.size()); ++q) iterate_agent(*E, oth[q], false, restart, E->work[omp_get_thread_num()]);
+  for (int q = 0; q < static_cast<int>(oth.size()); ++q)
+    iterate_agent(*E, oth[q], false, restart, E->work[omp_get_thread_num()], gnc);
   const int ns = std::min<int>(std::max(timed_serial, 0), static_cast<int>(sel.size()));
   for (int q = 0; q < ns; ++q) {
     const auto u0 = std::chrono::steady_clock::now();
-    iterate_agent(*E, sel[q], true, restart, E->work[0]);
+    iterate_agent(*E, sel[q], true, restart, E->work[0], gnc);
     if (upd_sec) upd_sec[sel[q]] = std::chrono::duration<double>(std::chrono::steady_clock::now() - u0).count();
   }
 #pragma omp parallel for num_threads(T) schedule(dynamic)
   for (int q = ns; q < static_cast<int>(sel.size()); ++q) {
     const auto u0 = std::chrono::steady_clock::now();
-    iterate_agent(*E, sel[q], true, restart, E->work[omp_get_thread_num()]);
+    iterate_agent(*E, sel[q], true, restart, E->work[omp_get_thread_num()], gnc);
     if (upd_sec) upd_sec[sel[q]] = std::chrono::duration<double>(std::chrono::steady_clock::now() - u0).count();
   }
+  if (gnc && ++E->gnc_iter <= E->gnc_max_iters) E->mu *= E->mu_step;  // RobustCost::update (:86-103)
   if (restart) E->gamma = E->alpha = 0.0;
   return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }

@@ -97,12 +97,13 @@ class CpuRbcd:
     """The engine's colour-class RBCD schedule restated on the host (L2, block-Jacobi, Nesterov with
     restart), OpenMP over the agents of a colour class.  TEST / BASELINE INFRASTRUCTURE."""
 
-    def __init__(self, d, r, arrays, n, agent_of_pose, num_agents, accel, restart_interval=30):
+    def __init__(self, d, r, arrays, n, agent_of_pose, num_agents, accel, restart_interval=30, robust="L2",
+                 robust_opt_inner_iters=30):
         L = lib()
         dp, ip, vp = C.POINTER(C.c_double), C.POINTER(C.c_int), C.c_void_p
         if not hasattr(L, "_rbcd_bound"):
             L.dpgo_cpu_rbcd_create.argtypes = [C.c_int, C.c_int, C.c_int, ip, ip, dp, dp, dp, dp, C.c_long, ip, C.c_int,
-                                               C.c_int, C.c_int]
+                                               C.c_int, C.c_int, C.c_int, C.c_int]
             L.dpgo_cpu_rbcd_create.restype = vp
             L.dpgo_cpu_rbcd_destroy.argtypes = [vp]
             L.dpgo_cpu_rbcd_set_X.argtypes = [vp, dp]
@@ -124,7 +125,8 @@ class CpuRbcd:
         self.h = L.dpgo_cpu_rbcd_create(d, r, len(p1), p1.ctypes.data_as(ip), p2.ctypes.data_as(ip),
                                         R.ctypes.data_as(dp), t.ctypes.data_as(dp), k.ctypes.data_as(dp),
                                         ta.ctypes.data_as(dp), int(n), aop.ctypes.data_as(ip), int(num_agents),
-                                        int(accel), int(restart_interval))
+                                        int(accel), int(restart_interval), {"L2": 0, "GNC_TLS": 1}[robust],
+                                        int(robust_opt_inner_iters))
         self.colors = [L.dpgo_cpu_rbcd_color(self.h, a) for a in range(self.K)]
 
     def close(self):
@@ -179,7 +181,7 @@ def host_cores():
     return max(1, min(omp, avail, 32)), avail, omp
 
 
-def engine_baseline(graph, agent_of_pose, X_start, r, accel, num_agents, warmup=3, rounds=20):
+def engine_baseline(graph, agent_of_pose, X_start, r, accel, num_agents, warmup=3, rounds=20, robust="L2"):
     """The like-for-like host baseline: oracle/cpu runs the engine's colour schedule from the GPU's
     timed-region start X (fresh Nesterov, as after set_X), with the reference's preconditioner
     replaced by block-Jacobi on both sides (CHOLMOD is absent).  Protocol: warm-up 3, then
@@ -188,7 +190,7 @@ def engine_baseline(graph, agent_of_pose, X_start, r, accel, num_agents, warmup=
       all cores:     a round = one colour iteration (every agent, OpenMP over the selected ones).
     Returns (result dict, the CPU's X after its iterations, its per-agent counters, iterations run)."""
     arrays = graph.arrays()
-    E = CpuRbcd(graph.d, r, arrays, graph.n, agent_of_pose, num_agents, accel)
+    E = CpuRbcd(graph.d, r, arrays, graph.n, agent_of_pose, num_agents, accel, robust=robust)
     E.set_X(X_start)
     T, avail, omp = host_cores()
     per_colour = min(sum(1 for c in E.colors if c == 0), sum(1 for c in E.colors if c == 1) or 10 ** 9)
@@ -204,7 +206,7 @@ def engine_baseline(graph, agent_of_pose, X_start, r, accel, num_agents, warmup=
     med = float(np.median(walls[warmup:]))
     upd = float(np.median(sel_counts[warmup:]))
     res = {"value": upd / med, "unit": "RBCD agent-updates/s", "cores": T, "kind": "port",
-           "sample": (f"oracle/cpu colour-schedule RBCD (L2, Nesterov={bool(accel)}, block-Jacobi on both sides: "
+           "sample": (f"oracle/cpu colour-schedule RBCD ({robust}, Nesterov={bool(accel)}, block-Jacobi on both sides: "
                       f"CHOLMOD absent) from the GPU timed region's start X; {T} OpenMP threads (of {avail} CPUs in "
                       f"the affinity mask; OMP team {omp}): median of {rounds} colour iterations ({upd:.0f} agent "
                       f"updates each, OpenMP over them) after {warmup} warm-up; one thread: median of "

@@ -218,6 +218,39 @@ def test_cpu_engine_matches_oracle_colour_schedule(accel):
     assert list(st[:, 2]) == list(runs)
 
 
+@pytest.mark.parametrize("accel", [False, True])
+def test_cpu_engine_gnc_tls_matches_oracle(accel):
+    """oracle/cpu's GNC_TLS (PGOAgent::updateLoopClosuresWeights, src/PGOAgent.cpp:1174-1289: reweighting every
+    robust_opt_inner_iters iterations, shared edges by the lower-ID agent only, mu schedule, Nesterov restart
+    on reweighting, converged-ratio readiness) vs the numpy PGOAgent restatement on a grid with outliers."""
+    from oracle import cpu_port
+    k, A, r, inner, iters = 6, 2, 5, 3, 8
+    g = O.grid3d(k, seed=3)
+    s = k // A
+    aop = np.array([(c[0] // s) + A * ((c[1] // s) + A * (c[2] // s)) for c in g.extra["coords"]], np.int32)
+    rng = np.random.default_rng(7)
+    lc = np.nonzero(np.abs(g.p2 - g.p1) != 1)[0]
+    bad = rng.choice(lc, size=max(1, len(lc) // 10), replace=False)
+    g.t = g.t.copy()
+    g.t[bad] += rng.normal(0.0, 5.0, size=(len(bad), 3))
+    X0 = O.lifting_matrix(3, r) @ O.chain_initialization(3, g.num_poses, g)
+    arrays = dict(p1=g.p1, p2=g.p2, R=g.R, t=g.t, kappa=g.kappa, tau=g.tau)
+    E = cpu_port.CpuRbcd(3, r, arrays, g.num_poses, aop, A ** 3, accel, robust="GNC_TLS",
+                         robust_opt_inner_iters=inner)
+    E.set_X(O.to_dev(X0))
+    for _ in range(iters):
+        E.iterate(threads=4)
+    agents = []
+    Xo, _ = O.colour_rbcd(g, aop, A ** 3, X0, iters, r, acceleration=accel, robust="GNC_TLS",
+                          robust_opt_inner_iters=inner, agents_out=agents)
+    assert rel(O.from_dev(E.get_X(), r), Xo) <= 1e-9
+    rc, rd = E.status()
+    for a, ag in enumerate(agents):
+        assert abs(rc[a] - ag.status_relative_change) <= 1e-8 * ag.status_relative_change
+        assert bool(rd[a]) == bool(ag.ready_to_terminate)
+    assert min(ag.converged_loop_closure_ratio() for ag in agents) < 1.0  # the reweighting decided some
+
+
 def build_abi_check(tmp_path):
     """tests/c/abi_check.c compiled against include/*.h and linked to the in-tree libdpgo_hip.so."""
     exe = str(tmp_path / "abi_check")
