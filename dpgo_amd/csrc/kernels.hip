@@ -2541,10 +2541,13 @@ __global__ __launch_bounds__(kThreads) void k_sn_assemble(SnView v, const int2* 
   for (int a = 0; a < R; ++a) dst[a] = val[a];
 }
 
+// a tile's 64 vector elements (64 R doubles) through registers: element e = tid + 256 i, i < kSnVecRegs
+constexpr int kSnVecRegs = (kSnTileDev * 8 + kThreads - 1) / kThreads;  // enough for R <= 8
+
 template <int R>
 __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __restrict__ items, int b,
                                                      double* __restrict__ y) {
-  __shared__ double sf[kSnTileDev * R];
+  __shared__ double sf[2][kSnTileDev * R];  // double-buffered frontal chunks
   const int2 it = items[blockIdx.x];
   const int node = it.x, I = it.y;
   const int s = v.s[node], t = v.t[node], sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), ns = Sp / kSnTileDev;
@@ -2557,24 +2560,49 @@ __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __res
 #pragma unroll
     for (int a = 0; a < R; ++a) acc[i][a] = 0.0;
   const int nJ = I < ns ? I + 1 : ns;
-  constexpr int kTileD = kSnTileDev * kSnTileDev;
-  double p[4][4], pn[4][4];
-  if (nJ > 0) sn_load_tile(panel + sn_tile_dev(ns, I, 0) * kTileD, rq, cq, p);
+  constexpr int kTileD = kSnTileDev * kSnTileDev, kChunk = kSnTileDev * R;
+  // software pipeline: tile J + 1's panel values and frontal chunk are loaded into registers while tile J
+  // is consumed; the chunk then goes to the other LDS buffer (one barrier per tile)
+  double p[4][4], pn[4][4], fv[kSnVecRegs];
+  auto load_chunk = [&](int J) {
+#pragma unroll
+    for (int i = 0; i < kSnVecRegs; ++i) {
+      const int e = tid + i * kThreads;
+      if (e < kChunk) fv[i] = f[static_cast<long>(J) * kChunk + e];
+    }
+  };
+  auto store_chunk = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < kSnVecRegs; ++i) {
+      const int e = tid + i * kThreads;
+      if (e < kChunk) sf[buf][e] = fv[i];
+    }
+  };
+  if (nJ > 0) {
+    sn_load_tile(panel + sn_tile_dev(ns, I, 0) * kTileD, rq, cq, p);
+    load_chunk(0);
+    store_chunk(0);
+  }
+  __syncthreads();
   for (int J = 0; J < nJ; ++J) {
-    if (J + 1 < nJ) sn_load_tile(panel + sn_tile_dev(ns, I, J + 1) * kTileD, rq, cq, pn);
-    __syncthreads();  // the previous tile's reads of sf are done
-    for (int x = tid; x < kSnTileDev * R; x += kThreads) sf[x] = f[static_cast<long>(J) * kSnTileDev * R + x];
-    __syncthreads();
+    const bool more = J + 1 < nJ;
+    if (more) {
+      sn_load_tile(panel + sn_tile_dev(ns, I, J + 1) * kTileD, rq, cq, pn);
+      load_chunk(J + 1);
+    }
+    const double* cf = sf[J & 1];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       double fc[R];
 #pragma unroll
-      for (int a = 0; a < R; ++a) fc[a] = sf[(cq * 4 + c) * R + a];
+      for (int a = 0; a < R; ++a) fc[a] = cf[(cq * 4 + c) * R + a];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int a = 0; a < R; ++a) acc[i][a] = fma(p[i][c], fc[a], acc[i][a]);
     }
+    if (more) store_chunk((J + 1) & 1);
+    __syncthreads();  // chunk J + 1 visible; every read of chunk J - 1's buffer (rewritten next) done
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -2611,7 +2639,7 @@ __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __res
 template <int R>
 __global__ __launch_bounds__(kThreads) void k_sn_bwd(SnView v, const int2* __restrict__ items, int b,
                                                      const double* __restrict__ y, double* __restrict__ x) {
-  __shared__ double sg[kSnTileDev * R];
+  __shared__ double sg[2][kSnTileDev * R];  // double-buffered [y_S ; -x_R] chunks
   __shared__ double red[kThreads / 64][16][4 * R];
   const int2 it = items[blockIdx.x];
   const int node = it.x, J = it.y;
@@ -2625,14 +2653,14 @@ __global__ __launch_bounds__(kThreads) void k_sn_bwd(SnView v, const int2* __res
   for (int c = 0; c < 4; ++c)
 #pragma unroll
     for (int a = 0; a < R; ++a) acc[c][a] = 0.0;
-  constexpr int kTileD = kSnTileDev * kSnTileDev;
-  double p[4][4], pn[4][4];
-  if (J < nI) sn_load_tile(panel + sn_tile_dev(ns, J, J) * kTileD, rq, cq, p);
-  for (int I = J; I < nI; ++I) {
-    if (I + 1 < nI) sn_load_tile(panel + sn_tile_dev(ns, I + 1, J) * kTileD, rq, cq, pn);
-    __syncthreads();
-    // g rows of tile I: y_S on the S part, -x_R on the R part, 0 on padding
-    for (int e = tid; e < kSnTileDev * R; e += kThreads) {
+  constexpr int kTileD = kSnTileDev * kSnTileDev, kChunk = kSnTileDev * R;
+  double p[4][4], pn[4][4], gv[kSnVecRegs];
+  // rows of tile I: y_S on the S part, -x_R on the R part (ancestors' solution), 0 on padding
+  auto load_chunk = [&](int I) {
+#pragma unroll
+    for (int i = 0; i < kSnVecRegs; ++i) {
+      const int e = tid + i * kThreads;
+      if (e >= kChunk) continue;
       const int rl = e / R, a = e - rl * R, row = I * kSnTileDev + rl;
       double g = 0.0;
       if (row < sb) {
@@ -2642,19 +2670,41 @@ __global__ __launch_bounds__(kThreads) void k_sn_bwd(SnView v, const int2* __res
         const int rr = row - Sp, q = rr / b, k = rr - q * b;
         g = -x[(static_cast<long>(poses[s + q]) * b + k) * R + a];
       }
-      sg[e] = g;
+      gv[i] = g;
     }
-    __syncthreads();
+  };
+  auto store_chunk = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < kSnVecRegs; ++i) {
+      const int e = tid + i * kThreads;
+      if (e < kChunk) sg[buf][e] = gv[i];
+    }
+  };
+  if (J < nI) {
+    sn_load_tile(panel + sn_tile_dev(ns, J, J) * kTileD, rq, cq, p);
+    load_chunk(J);
+    store_chunk(0);
+  }
+  __syncthreads();
+  for (int I = J; I < nI; ++I) {
+    const bool more = I + 1 < nI;
+    if (more) {
+      sn_load_tile(panel + sn_tile_dev(ns, I + 1, J) * kTileD, rq, cq, pn);
+      load_chunk(I + 1);
+    }
+    const double* cg = sg[(I - J) & 1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       double gi[R];
 #pragma unroll
-      for (int a = 0; a < R; ++a) gi[a] = sg[(rq * 4 + i) * R + a];
+      for (int a = 0; a < R; ++a) gi[a] = cg[(rq * 4 + i) * R + a];
 #pragma unroll
       for (int c = 0; c < 4; ++c)
 #pragma unroll
         for (int a = 0; a < R; ++a) acc[c][a] = fma(p[i][c], gi[a], acc[c][a]);
     }
+    if (more) store_chunk((I + 1 - J) & 1);
+    __syncthreads();
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll

@@ -69,6 +69,7 @@ def test_rtr_trace_matches_oracle(hip, name, r, iters, tol, radius, inner, preco
 
 
 def _rtr_trace_case(hip, name, r, iters, tol, radius, inner, precon, merged):
+    rtr_tol = tol
     meas = load_meas(name)
     d, n = meas.d, meas.num_poses
     Q = O.connection_laplacian(meas, n)
@@ -103,10 +104,19 @@ def _rtr_trace_case(hip, name, r, iters, tol, radius, inner, precon, merged):
         tol = 1e-6
     # The merged tCG iteration forms |r_{j+1}|^2 and <z_{j+1}, r_{j+1}> (hence beta) from one-step
     # polynomials in alpha over r_j and Hd_j, whose terms cancel by the factor <z_j, r_j> / <z_{j+1},
-    # r_{j+1}>.  Their partials are double-double (exact products, compensated sums, the polynomial in
-    # double-double: dpgo_device.h dd_*), so only the final rounding remains and the merged sequence is
-    # held to the classic bars.  (Plain double partials measured 2e-10 of the largest d_Hd on tinyGrid3D.)
+    # r_{j+1}>; the partials are double-double (exact products, compensated sums, the polynomial in
+    # double-double: dpgo_device.h dd_*), so the polynomials add no rounding of their own.  What remains is
+    # the trajectory's own conditioning: on tinyGrid3D the third outer iteration's tCG amplifies 1e-16
+    # differences in its starting point by ~1e5, and the float64 oracle itself is 1.3e-10 from an
+    # extended-precision Run there (test_rtr_trace_extended_precision).  The merged sequence, which rounds
+    # r' = r + alpha Hd once (FMA) where the oracle rounds twice, is held to the classic bar or to twice the
+    # oracle's own distance from the extended-precision Run, whichever is larger (computed per case, for the
+    # graphs whose dense extended-precision Run is cheap).
     tcg_tol = tol
+    if merged and precon == "bj" and iters > 1 and n * (d + 1) <= 2000:
+        ext = _rtr_extended(Q, X0, d, rtr_tol, radius, 5.0 * radius, iters, inner)
+        if [e["op"] for e in ext] == [e["op"] for e in exp]:
+            tcg_tol = max(tol, 2.0 * _trace_deviation(exp, ext))
     scale, run_id = {}, None
     for g, e in zip(got, exp):
         if e["op"] == 5 or run_id != g["run"]:
@@ -152,30 +162,19 @@ def _rtr_trace_case(hip, name, r, iters, tol, radius, inner, precon, merged):
     assert rel(Xh, Xo) <= max(1e-8, tol)
 
 
-def _tcg_extended(Q, X, d, Delta, max_inner):
-    """The first tCG of an RTR Run (A.4, block-Jacobi, G = 0) in extended precision (np.longdouble,
-    64-bit mantissa): the reference trajectory the float64 implementations are measured against."""
+def _rtr_extended(Q, X0, d, tol, Delta0, Delta_max, max_iter, max_inner):
+    """ROPTLIB RTR Run (A.4: tCG from eta = 0 with block-Jacobi, QF retraction, rho test, radius update;
+    G = 0) in extended precision (np.longdouble, 64-bit mantissa): the record sequence of
+    _expected_records, as the reference trajectory the float64 implementations are measured against."""
     L = np.longdouble
-    r = X.shape[0]
+    r = X0.shape[0]
     b = d + 1
-    n = X.shape[1] // b
+    n = X0.shape[1] // b
     Qd = Q.toarray().astype(L)
-    Xl = X.astype(L)
     P = lambda V: V.reshape(r, n, b).transpose(1, 0, 2)  # noqa: E731  pose blocks (n, r, b)
     U = lambda Pb: Pb.transpose(1, 0, 2).reshape(r, n * b)  # noqa: E731
-    Xp = P(Xl)
-    Y = Xp[:, :, :d]
-
-    def proj(V):
-        Vp = P(V).copy()
-        VY = Vp[:, :, :d]
-        M = np.swapaxes(Y, 1, 2) @ VY
-        Vp[:, :, :d] = VY - Y @ (0.5 * (M + np.swapaxes(M, 1, 2)))
-        return U(Vp)
-
-    EG = (Qd @ Xl.T).T
-    M = np.swapaxes(Y, 1, 2) @ P(EG)[:, :, :d]
-    S = 0.5 * (M + np.swapaxes(M, 1, 2))
+    ip = lambda A_, B_: np.sum(A_ * B_, dtype=L)  # noqa: E731
+    sym = lambda M: 0.5 * (M + np.swapaxes(M, 1, 2))  # noqa: E731
     Minv = np.zeros((n, b, b), L)  # (Q_jj + 0.1 I)^-1 by Gauss-Jordan in extended precision
     for j in range(n):
         A = np.concatenate([Qd[j * b:(j + 1) * b, j * b:(j + 1) * b] + L(0.1) * np.eye(b, dtype=L),
@@ -189,52 +188,131 @@ def _tcg_extended(Q, X, d, Delta, max_inner):
                     A[u] -= A[u, c] * A[c]
         Minv[j] = A[:, b:]
 
-    def hess(V):
-        H = P((Qd @ V.T).T).copy()
-        H[:, :, :d] -= P(V)[:, :, :d] @ S
-        return proj(U(H))
+    def proj(X, V):
+        Y = P(X)[:, :, :d]
+        Vp = P(V).copy()
+        VY = Vp[:, :, :d]
+        Vp[:, :, :d] = VY - Y @ sym(np.swapaxes(Y, 1, 2) @ VY)
+        return U(Vp)
 
-    prec = lambda V: proj(U(P(V) @ Minv))  # noqa: E731
-    ip = lambda A_, B_: np.sum(A_ * B_, dtype=L)  # noqa: E731
-    rv = proj(EG)
-    z = prec(rv)
-    z_r = ip(z, rv)
-    d_Pd, e_Pe, e_Pd = z_r, L(0), L(0)
-    delta = -z
-    norm_r0 = np.sqrt(ip(rv, rv))
-    recs = []
-    for j in range(max_inner):
-        Hd = hess(delta)
-        d_Hd = ip(delta, Hd)
-        alpha = z_r / d_Hd
-        e_Pe_new = e_Pe + 2 * alpha * e_Pd + alpha * alpha * d_Pd
-        recs.append(dict(op=3, j=j, d_Hd=d_Hd, alpha=alpha))
-        if d_Hd <= 0 or e_Pe_new >= L(Delta) * L(Delta):
-            break
-        e_Pe = e_Pe_new
-        rv = rv + alpha * Hd
-        norm_r = np.sqrt(ip(rv, rv))
-        if norm_r <= norm_r0 * min(norm_r0, L(0.1)):
-            recs.append(dict(op=4, j=j, norm_r=norm_r))
-            break
-        zn = prec(rv)
-        zr_new = ip(zn, rv)
-        beta = zr_new / z_r
-        recs.append(dict(op=4, j=j, norm_r=norm_r, z_r=zr_new, beta=beta))
-        z_r = zr_new
-        delta = -zn + beta * delta
-        e_Pd = beta * (e_Pd + alpha * d_Pd)
-        d_Pd = z_r + beta * beta * d_Pd
-    return recs
+    def retract(X, V):  # [qf(Y + V_Y) | p + V_p], qf by modified Gram-Schmidt (positive diagonal)
+        Pp = P(X + V).copy()
+        for j in range(n):
+            M = Pp[j, :, :d]
+            for c in range(d):
+                v = M[:, c].copy()
+                for k in range(c):
+                    v = v - np.sum(M[:, k] * v, dtype=L) * M[:, k]
+                M[:, c] = v / np.sqrt(np.sum(v * v, dtype=L))
+            Pp[j, :, :d] = M
+        return U(Pp)
+
+    egrad = lambda X: (Qd @ X.T).T  # noqa: E731
+    fval = lambda X: L(0.5) * ip(egrad(X), X)  # noqa: E731
+    x1 = X0.astype(L)
+    EG = egrad(x1)
+    f1 = fval(x1)
+    g = proj(x1, EG)
+    ngf = np.sqrt(ip(g, g))
+    Delta, it, recs = L(Delta0), 0, []
+    while not (ngf < tol) and it < max_iter:
+        S = sym(np.swapaxes(P(x1)[:, :, :d], 1, 2) @ P(EG)[:, :, :d])
+
+        def hess(V):
+            H_ = P(egrad(V)).copy()
+            H_[:, :, :d] -= P(V)[:, :, :d] @ S
+            return proj(x1, U(H_))
+
+        prec = lambda V: proj(x1, U(P(V) @ Minv))  # noqa: E731
+        eta = np.zeros_like(x1)
+        Heta = np.zeros_like(x1)
+        rv = g.copy()
+        z = prec(rv)
+        z_r = ip(z, rv)
+        d_Pd, e_Pe, e_Pd = z_r, L(0), L(0)
+        delta = -z
+        norm_r0 = np.sqrt(ip(rv, rv))
+        status, ninner = 4, max_inner
+        for j in range(max_inner):
+            Hd = hess(delta)
+            d_Hd = ip(delta, Hd)
+            alpha = z_r / d_Hd
+            e_Pe_new = e_Pe + 2 * alpha * e_Pd + alpha * alpha * d_Pd
+            rec = dict(op=3, j=j, d_Hd=d_Hd, alpha=alpha, Delta=Delta)
+            if d_Hd <= 0 or e_Pe_new >= Delta * Delta:
+                tau = (-e_Pd + np.sqrt(e_Pd * e_Pd + d_Pd * (Delta * Delta - e_Pe))) / d_Pd
+                eta = eta + tau * delta
+                Heta = Heta + tau * Hd
+                status = 0 if d_Hd <= 0 else 1
+                rec.update(tau=tau, status=status)
+                recs.append(rec)
+                ninner = j + 1
+                break
+            recs.append(rec)
+            e_Pe = e_Pe_new
+            eta = eta + alpha * delta
+            Heta = Heta + alpha * Hd
+            rv = rv + alpha * Hd
+            norm_r = np.sqrt(ip(rv, rv))
+            if norm_r <= norm_r0 * min(norm_r0, L(0.1)):
+                status = 2 if L(0.1) < norm_r0 else 3
+                recs.append(dict(op=4, j=j, norm_r=norm_r, status=status))
+                ninner = j + 1
+                break
+            zn = prec(rv)
+            zr_new = ip(zn, rv)
+            beta = zr_new / z_r
+            recs.append(dict(op=4, j=j, norm_r=norm_r, z_r=zr_new, beta=beta))
+            z_r = zr_new
+            delta = -zn + beta * delta
+            e_Pd = beta * (e_Pd + alpha * d_Pd)
+            d_Pd = z_r + beta * beta * d_Pd
+        x2 = retract(x1, eta)
+        f2 = fval(x2)
+        rho = (f1 - f2) / (-ip(g, eta) - L(0.5) * ip(eta, Heta))
+        accepted = rho > L(0.1)
+        recs.append(dict(op=5, f1=f1, f2=f2, rho=rho, Delta=Delta, accepted=float(accepted), ngf=ngf, status=status,
+                         alpha=ninner))
+        if rho < L(0.25):
+            Delta = L(0.25) * Delta
+        elif rho > L(0.75) and status in (0, 1):
+            Delta = min(2 * Delta, L(Delta_max))
+        if accepted:
+            x1, f1 = x2, f2
+            EG = egrad(x1)
+            g = proj(x1, EG)
+            ngf = np.sqrt(ip(g, g))
+        it += 1
+    return [{k: (float(v) if isinstance(v, np.floating) else v) for k, v in rec.items()} for rec in recs]
+
+
+def _trace_deviation(got, ref):
+    """Largest deviation of a trace from a reference one, per tCG quantity relative to its largest magnitude
+    in that tCG (the trace test's scale), and for the rho-test quantities relative to themselves."""
+    worst, scale = 0.0, {}
+    for g, e in zip(got, ref):
+        if e["op"] == 5:
+            for k in ("f1", "f2", "ngf"):
+                worst = max(worst, abs(g[k] - e[k]) / max(abs(e[k]), 1e-300))
+            scale = {}
+            continue
+        for k in ("d_Hd", "alpha", "norm_r", "z_r", "beta", "tau"):
+            if k in e:
+                scale[k] = max(scale.get(k, 0.0), abs(e[k]))
+        for k in ("d_Hd", "norm_r", "z_r", "beta", "tau"):
+            if k in e:
+                worst = max(worst, abs(g[k] - e[k]) / max(scale[k], 1e-300))
+    return worst
 
 
 @pytest.mark.parametrize("name,r", [("tinyGrid3D", 3), ("smallGrid3D", 5)])
-def test_merged_tcg_extended_precision_bound(hip, name, r):
-    """Bound test for the merged tCG iteration (k_spmm MODE_HESS_M, double-double stopping-test partials):
-    against an extended-precision (64-bit mantissa) restatement of the same tCG, the device's merged
-    sequence is at least as accurate as the float64 oracle (whose vector recurrences round r' = r + alpha
-    Hd twice per element).  Where the two float64 trajectories differ (tinyGrid3D after a 1e5 residual
-    drop), the difference is the oracle's own rounding, not the merged sequence's."""
+def test_rtr_trace_extended_precision(hip, name, r):
+    """The device RTR trace (localPoseGraphOptimization settings, block-Jacobi), merged and classic tCG
+    sequences, against an extended-precision (64-bit mantissa) restatement of the same Run: both within
+    1e-10 of it, as the float64 oracle is.  Where a float64 trajectory is ill-conditioned (tinyGrid3D's third
+    outer iteration amplifies 1e-16 differences in its starting point by ~1e5), every float64
+    implementation -- oracle, classic, merged -- sits at that distance from the extended-precision Run and
+    from each other; this test shows the merged sequence is no further from it than the oracle is."""
     meas = load_meas(name)
     d, n = meas.d, meas.num_poses
     Q = O.connection_laplacian(meas, n)
@@ -243,32 +321,29 @@ def test_merged_tcg_extended_precision_bound(hip, name, r):
     P_.precon_mode = O.PRECON_BLOCK_JACOBI
     X0 = O.lifting_matrix(d, r) @ O.chordal_initialization(d, n, meas)
     trace = []
-    O.optimize(P_, X0, O.OptParams(tr_iterations=1, tr_tolerance=1e-1, tr_initial_radius=10.0, tr_max_inner=50),
+    O.optimize(P_, X0, O.OptParams(tr_iterations=10, tr_tolerance=1e-1, tr_initial_radius=10.0, tr_max_inner=50),
                trace)
-    H = hip.Problem(n, d, r)
-    H.set_Q_scipy(0, Q)
-    H.set_trace(4096)
-    H.optimize(X0, hip.default_params(tr_iterations=1, tr_tolerance=1e-1, tr_initial_radius=10.0, tr_max_inner=50,
-                                      precon=hip.PRECON_BLOCK_JACOBI))
-    got = H.get_trace(0)
     ora = _expected_records(trace)
-    ext = _tcg_extended(Q, X0, d, 10.0, 50)
-    k = len(ext)
-    assert [int(g["op"]) for g in got[:k]] == [e["op"] for e in ext] == [e["op"] for e in ora[:k]]
-    worst_gpu, worst_ora = 0.0, 0.0
-    for key in ("d_Hd", "alpha", "norm_r", "z_r", "beta"):
-        vals = [float(e[key]) for e in ext if key in e]
-        if not vals:
-            continue
-        scale = max(abs(v) for v in vals)
-        for g, o, e in zip(got[:k], ora[:k], ext):
-            if key not in e:
-                continue
-            t = float(e[key])
-            worst_gpu = max(worst_gpu, abs(g[key] - t) / scale)
-            worst_ora = max(worst_ora, abs(o[key] - t) / scale)
-    print(f"{name}: max deviation from extended precision, merged GPU {worst_gpu:.2e}, float64 oracle {worst_ora:.2e}")
-    assert worst_gpu <= max(1.5 * worst_ora, 1e-13), (worst_gpu, worst_ora)
+    ext = _rtr_extended(Q, X0, d, 1e-1, 10.0, 50.0, 10, 50)
+    assert [e["op"] for e in ext] == [e["op"] for e in ora]
+    dev = {"oracle": _trace_deviation(ora, ext)}
+    for classic in (0, 1):
+        hip.set_tuning(5, classic)
+        try:
+            H = hip.Problem(n, d, r)
+            H.set_Q_scipy(0, Q)
+            H.set_trace(4096)
+            H.optimize(X0, hip.default_params(tr_iterations=10, tr_tolerance=1e-1, tr_initial_radius=10.0,
+                                              tr_max_inner=50, precon=hip.PRECON_BLOCK_JACOBI))
+            got = H.get_trace(0)
+        finally:
+            hip.set_tuning(5, 0)
+        assert [int(g["op"]) for g in got] == [e["op"] for e in ext]
+        dev["classic" if classic else "merged"] = _trace_deviation(got, ext)
+    print(f"{name}: max deviation from the extended-precision Run: " +
+          ", ".join(f"{k} {v:.2e}" for k, v in dev.items()))
+    assert dev["merged"] <= 1e-10 or dev["merged"] <= 1.5 * max(dev["oracle"], dev["classic"]), dev
+    assert dev["classic"] <= 1e-10 or dev["classic"] <= 1.5 * dev["oracle"], dev
 
 
 @pytest.mark.parametrize("batched", [False, True])
