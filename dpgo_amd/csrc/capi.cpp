@@ -301,6 +301,14 @@ int sync_q_edges(dpgo_hip_problem h) {
     HIP_TRY(hipMemcpyAsync(h->inc_sv.p, inc_sv.data(), sizeof(int2) * inc_sv.size(), hipMemcpyHostToDevice, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));  // the host vectors above die here
   }
+  {  // the edge loop gathers records and neighbour poses with 32-bit buffer offsets (kernels.hip buf_rsrc)
+    long ymax = h->N;
+    for (const int2& e : inc) ymax = std::max<long>(ymax, static_cast<long>(e.y) + 1);
+    const double lim = 4294967296.0;
+    if (static_cast<double>(rec.size()) * 8.0 >= lim || static_cast<double>(ymax) * h->r * b * 8.0 >= lim)
+      return fail(DPGO_HIP_EINVAL, "edge-stream Q: records or the pose vector exceed the 4 GiB range of the SpMM's "
+                                   "buffer gathers (split the poses over more handles / ranks)");
+  }
   h->nnz_inc = deg[h->N];
   h->num_edges = m;
   HIP_TRY(h->inc_ptr.ensure(h->N + 1));
@@ -1435,12 +1443,17 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
       tags.push_back(tag);
       dpgo::SpmmArgs sa{h->delta.p, nullptr, nullptr, x1, h->S.p, h->Hdelta.p, nullptr, h->minv.p, nullptr, pmode};
       sa.rvec = j == 0 ? h->g.p : h->rv.p;
+      // |r_j|^2 and <z_j, r_j>: from the previous k_tcg_updir's partials (peh), formed by the SpMM itself on
+      // the first iteration (r_0 = grad)
+      const bool rz_pc = j > 0;
+      sa.rz_own = rz_pc ? 0 : 1;
       dpgo::OptScalars os = o;
       os.first_full = mode == dpgo::MODE_HESS_QF_M ? 1 : 0;
       dpgo::FinalizeArgs fin = make_fin(h, op, h->pa.p, 7, nullptr, 0, &os, nullptr, publish ? 1 : 0, tag);
       fin.pc = h->peh.p;
       fin.nq_c = 1;
       fin.dd_mask = 0x7E;  // |r|^2 .. <Minv Hd, Hd> are double-double partials (k_spmm MODE_HESS_M)
+      fin.rz_pc = rz_pc ? 1 : 0;
       DPGO_TRY(spmm_then_finalize(h, mode, ch, sa, fin));
       auto cu = make_ctx(h, dpgo::FLAG_TCG_MODE, h->peh.p);
       HIP_TRY(dpgo::launch_tcg_updir(r, b, cu, x1, h->minv.p, pmode, h->delta.p, h->Hdelta.p, h->eta.p,

@@ -136,6 +136,8 @@ struct FinalizeArgs {
   int coherent;                 // read the partials with agent-scope loads (fused, SpmmArgs::fin_mode 2)
   const double* conv_ratio;     // OP_STATUS: per-agent converged loop-closure ratio (nullptr = 1)
   int dd_mask;                  // bit q: pa quantity q is double-double (low part at slot + kDdLo), reduced as such
+  int rz_pc;                    // merged tCG: |r_j|^2 and <z_j, r_j> (quantities 1, 4) from the previous
+                                // k_tcg_updir's double-double partials (pc slots 1, 2), not from pa
   double* trace;                // per-iteration records [agent][trace_cap][kTraceWidth] (nullptr = off)
   int trace_cap;
 };
@@ -159,6 +161,7 @@ struct SpmmArgs {
   double* delta;        // tCG direction (EVAL_TCG)
   int pmode;            // PreconMode (EVAL_TCG, HESS_M)
   const double* rvec;   // HESS_M: the tCG residual r_j (grad on the first iteration)
+  int rz_own;           // HESS_M: also form the |r_j|^2 and <z_j, r_j> partials (else k_tcg_updir left them)
   // Fused finalize (null = none): the last block of each agent to arrive runs k_finalize's work for
   // that agent (fin), so no separate k_finalize launch follows the SpMM.  fin_arrive[agent] counts
   // arrivals and is reset to 0 by that last block.

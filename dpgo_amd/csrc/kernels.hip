@@ -79,11 +79,16 @@ __device__ __forceinline__ void block_partials(double (&v)[NQ], double* __restri
   }
 }
 
-// One plain partial (slot 0) and ND double-double partials (high parts at slots 1.., low parts kDdLo
+// One plain partial (slot 0) and ND double-double partials (high parts at slots slot[q], low parts kDdLo
 // slots later), reduced in double-double over the wave and the block in block_partials' order.
+struct DdSlots {
+  int s[6];
+};
+constexpr DdSlots kSlots123456{{1, 2, 3, 4, 5, 6}};
+constexpr DdSlots kSlots2356{{2, 3, 5, 6, 0, 0}};
 template <int ND>
-__device__ __forceinline__ void block_partials_dd(double v0, dd (&v)[ND], double* __restrict__ partials, int tile,
-                                                  bool coherent = false) {
+__device__ __forceinline__ void block_partials_dd_at(double v0, dd (&v)[ND], DdSlots slot, double* __restrict__ partials,
+                                                     int tile, bool coherent = false) {
   __shared__ double red[4][1 + 2 * ND];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   v0 = wave_sum(v0);
@@ -111,11 +116,68 @@ __device__ __forceinline__ void block_partials_dd(double v0, dd (&v)[ND], double
       dd t{red[0][1 + 2 * q], red[0][2 + 2 * q]};
 #pragma unroll
       for (int w = 1; w < 4; ++w) t = dd_add(t, {red[w][1 + 2 * q], red[w][2 + 2 * q]});
-      put(1 + q, t.hi);
-      put(1 + q + kDdLo, t.lo);
+      put(slot.s[q], t.hi);
+      put(slot.s[q] + kDdLo, t.lo);
     }
   }
 }
+template <int ND>
+__device__ __forceinline__ void block_partials_dd(double v0, dd (&v)[ND], double* __restrict__ partials, int tile,
+                                                  bool coherent = false) {
+  block_partials_dd_at<ND>(v0, v, kSlots123456, partials, tile, coherent);
+}
+
+// block_partials_dd's layout from plain partials (v[0] plain, v[1 .. ND] the high parts, low parts zero)
+template <int ND>
+__device__ __forceinline__ void block_partials_lo0(double (&v)[13], double* __restrict__ partials, int tile,
+                                                   bool coherent) {
+  static_assert(1 + ND <= 13, "slots");
+  double w[1 + ND];
+#pragma unroll
+  for (int q = 0; q <= ND; ++q) w[q] = v[q];
+  block_partials<1 + ND>(w, partials, tile, coherent);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int q = 0; q < ND; ++q) {
+      if (coherent)
+        __hip_atomic_store(&partials[tile * kPartialStride + 1 + q + kDdLo], 0.0, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      else
+        partials[tile * kPartialStride + 1 + q + kDdLo] = 0.0;
+    }
+  }
+}
+
+// Per-lane sum of products for the merged tCG partials.  DPGO_MERGED_DD: 2 = dd_fma per term (exact
+// products, double-double sums), 1 = Ogita-Rump-Oishi Dot2 (running sum by TwoSum, the product and sum
+// errors gathered in one plain double: the same twice-the-working-precision result for a handful of
+// terms at 10 instead of 13 flops a term), 0 = plain FMA chains (no low parts).
+#ifndef DPGO_MERGED_DD
+#define DPGO_MERGED_DD 2
+#endif
+constexpr bool kMergedDd = DPGO_MERGED_DD != 0;
+struct DotAcc {
+  double p = 0.0, s = 0.0;
+  __device__ __forceinline__ void add(double a, double b) {
+    if constexpr (DPGO_MERGED_DD == 0) {
+      p = fma(a, b, p);
+    } else if constexpr (DPGO_MERGED_DD == 1) {
+      const double h = a * b;
+      const double e = __builtin_fma(a, b, -h);
+      const dd t = dd_two_sum(p, h);
+      p = t.hi;
+      s += t.lo + e;
+    } else {
+      const dd x = dd_fma({p, s}, a, b);
+      p = x.hi;
+      s = x.lo;
+    }
+  }
+  __device__ __forceinline__ dd val() const {
+    if constexpr (DPGO_MERGED_DD == 1) return dd_two_sum(p, s);
+    return {p, s};
+  }
+};
 
 struct PoseLane {
   int lane, wave, k, tile, agent, pslot;
@@ -234,6 +296,10 @@ __device__ __forceinline__ void spmm_accumulate(const QView& q, const double* __
 // leaves HBM at full occupancy-independent MLP instead of one dependent miss per incidence.
 // Tiles whose lists do not fit fall back to global loads.
 constexpr int kIncStage = 512;
+#ifndef DPGO_BUFFER_GATHER
+#define DPGO_BUFFER_GATHER 1
+#endif
+constexpr bool kBufferGather = DPGO_BUFFER_GATHER != 0;
 constexpr bool kHalfStaged = false;  // LDS stage for the half passes (MODE_F / MODE_QF)
 template <int D>
 constexpr int rec_stage() { return D == 3 ? 200 : 256; }
@@ -256,7 +322,29 @@ __host__ __device__ constexpr int minv_index(int u, int v) { return sym_index<B>
 // is consumed; every load is unconditional (the index is clamped) so the compiler waits only for
 // the stage it consumes.  INC_LDS: entries from the LDS stage (ds_read: waiting for them never
 // drains in-flight global loads).  REC_LDS: records from the LDS stage (id - e0), else global.
-template <int R, int B, bool INC_LDS, bool REC_LDS>
+// Raw buffer loads for the edge loop's gathers.  They are intrinsic calls, not IR loads: plain loads feeding
+// the loop-carried register stage are folded by the optimizer into ONE load of a phi of the two addresses,
+// issued right before its FMAs (no gather in flight while the previous incidence is consumed: a full L2/HBM
+// latency per incidence); the intrinsics keep the stage's loads where the source puts them.  The range is
+// 4 GiB per buffer (32-bit offsets): the launcher checks it (buffer_gather_ok).
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), static_cast<short>(0), -1, 0x00020000);
+}
+template <int N>
+__device__ __forceinline__ void buf_load_f64(__amdgpu_buffer_rsrc_t r, unsigned off, double (&v)[N]) {
+#pragma unroll
+  for (int a = 0; a + 1 < N; a += 2) {
+    const f64x2 t = __builtin_bit_cast(f64x2, __builtin_amdgcn_raw_buffer_load_b128(r, off + 8u * a, 0, 0));
+    v[a] = t.x;
+    v[a + 1] = t.y;
+  }
+  if constexpr (N % 2 == 1)
+    v[N - 1] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off + 8u * (N - 1), 0, 0));
+}
+
+template <int R, int B, bool INC_LDS, bool REC_LDS, bool BUF = kBufferGather>
 __device__ __forceinline__ void edge_loop(const QView& q, const double* __restrict__ in, int kc, int z0, int z1,
                                           const int2* s_inc, int i0, const double* s_rec, int e0,
                                           double (&acc)[R][B]) {
@@ -265,6 +353,7 @@ __device__ __forceinline__ void edge_loop(const QView& q, const double* __restri
     double m[B];
     double x[R];
   };
+  const __amdgpu_buffer_rsrc_t rin = buf_rsrc(in), rrec = buf_rsrc(q.rec);
   auto fetch = [&](int z, Stage& st) {
     int2 ie;
     if constexpr (INC_LDS)
@@ -274,16 +363,27 @@ __device__ __forceinline__ void edge_loop(const QView& q, const double* __restri
     const bool outg = (ie.x & 1) != 0;
     const int off = outg ? kc : 4 * kc;  // column kc of M (outgoing) / row kc (incoming)
     const int stride = outg ? 4 : 1;
-    const double* mr;
-    if constexpr (REC_LDS)
-      mr = s_rec + ((ie.x >> 1) - e0) * RW + off;
-    else
-      mr = q.rec + static_cast<long>(ie.x >> 1) * RW + off;
+    if constexpr (REC_LDS) {
+      const double* mr = s_rec + ((ie.x >> 1) - e0) * RW + off;
 #pragma unroll
-    for (int c = 0; c < B; ++c) st.m[c] = mr[c * stride];
-    const double* xk = in + static_cast<long>(ie.y) * (R * B) + kc * R;
+      for (int c = 0; c < B; ++c) st.m[c] = mr[c * stride];
+    } else if constexpr (BUF) {
+      const unsigned mo = 8u * (static_cast<unsigned>(ie.x >> 1) * RW + off);
 #pragma unroll
-    for (int a = 0; a < R; ++a) st.x[a] = xk[a];
+      for (int c = 0; c < B; ++c)
+        st.m[c] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rrec, mo + 8u * c * stride, 0, 0));
+    } else {
+      const double* mr = q.rec + static_cast<long>(ie.x >> 1) * RW + off;
+#pragma unroll
+      for (int c = 0; c < B; ++c) st.m[c] = mr[c * stride];
+    }
+    if constexpr (BUF) {
+      buf_load_f64<R>(rin, 8u * (static_cast<unsigned>(ie.y) * (R * B) + kc * R), st.x);
+    } else {
+      const double* xk = in + static_cast<long>(ie.y) * (R * B) + kc * R;
+#pragma unroll
+      for (int a = 0; a < R; ++a) st.x[a] = xk[a];
+    }
   };
   auto consume = [&](const Stage& st) {
 #pragma unroll
@@ -569,6 +669,10 @@ __device__ __forceinline__ void count_call(const FinalizeArgs& f, int agent, Age
 // indices in the scalar logic, whatever nq_a / nq_b are).
 constexpr int kPcSlot = kMaxTot - 1;
 __device__ __forceinline__ const double* part_src(const FinalizeArgs& f, int q, int& qq) {
+  if (f.rz_pc && (q == 1 || q == 4)) {
+    qq = q == 1 ? 1 : 2;
+    return f.pc;
+  }
   if (q < f.nq_a) {
     qq = q;
     return f.pa;
@@ -937,44 +1041,55 @@ static_assert(kThreads == 256, "the finalize reductions restate a 256-thread red
 // adds lane t + w: the same pairs in the same order).  No LDS and no barrier; the state is read and
 // written in place (a register copy would cost the SpMM ~50 VGPRs and a wave per SIMD of occupancy).
 __device__ __forceinline__ void finalize_agent(const FinalizeArgs& f, int agent) {
+  // One reduction body for every quantity (a rolled loop over q, totals through LDS): this code sits inside
+  // every fusable SpMM, and eight unrolled copies of it (plain and double-double) tripled those kernels' code.
+  __shared__ double s_tot[2 * kMaxTot];
   const int l = static_cast<int>(threadIdx.x) & 63;
   const int t0 = f.agent_tile_off[agent], t1 = f.agent_tile_off[agent + 1];
-  double tot[kMaxTot], lo[kMaxTot];
   auto ld = [&](const double* src, int t, int slot) {
     return f.coherent ? __hip_atomic_load(&src[t * kPartialStride + slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                       : src[t * kPartialStride + slot];
   };
-#pragma unroll
+#pragma unroll 1
   for (int q = 0; q < kMaxTot; ++q) {
-    tot[q] = 0.0;
-    lo[q] = 0.0;
     int qq = 0;
     const double* src = part_src(f, q, qq);
-    if (src == nullptr) continue;
-    if ((f.dd_mask >> q) & 1) {  // double-double quantity: the same tree in double-double
-      dd a4[4];
+    double th = 0.0, tl = 0.0;
+    if (src != nullptr) {
+      if ((f.dd_mask >> q) & 1) {  // double-double quantity: the same tree in double-double
+        dd a4[4];
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        dd sv{0.0, 0.0};
-        for (int t = t0 + l + 64 * v; t < t1; t += kThreads) sv = dd_add(sv, {ld(src, t, qq), ld(src, t, qq + kDdLo)});
-        a4[v] = sv;
+        for (int v = 0; v < 4; ++v) {
+          dd sv{0.0, 0.0};
+          for (int t = t0 + l + 64 * v; t < t1; t += kThreads) sv = dd_add(sv, {ld(src, t, qq), ld(src, t, qq + kDdLo)});
+          a4[v] = sv;
+        }
+        const dd x = wave_sum_dd(dd_add(dd_add(a4[0], a4[2]), dd_add(a4[1], a4[3])));
+        th = x.hi;
+        tl = x.lo;
+      } else {
+        double a4[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          double sv = 0.0;
+          for (int t = t0 + l + 64 * v; t < t1; t += kThreads) sv += ld(src, t, qq);
+          a4[v] = sv;
+        }
+        th = wave_sum((a4[0] + a4[2]) + (a4[1] + a4[3]));  // lane 0's halving tree
       }
-      const dd x = wave_sum_dd(dd_add(dd_add(a4[0], a4[2]), dd_add(a4[1], a4[3])));
-      tot[q] = x.hi;
-      lo[q] = x.lo;
-      continue;
     }
-    double a4[4];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      double sv = 0.0;
-      for (int t = t0 + l + 64 * v; t < t1; t += kThreads) sv += ld(src, t, qq);
-      a4[v] = sv;
+    if (l == 0) {
+      s_tot[q] = th;
+      s_tot[kMaxTot + q] = tl;
     }
-    double x = (a4[0] + a4[2]) + (a4[1] + a4[3]);
-    tot[q] = wave_sum(x);  // lane 0's halving tree
   }
   if (l != 0) return;
+  double tot[kMaxTot], lo[kMaxTot];
+#pragma unroll
+  for (int q = 0; q < kMaxTot; ++q) {
+    tot[q] = s_tot[q];
+    lo[q] = s_tot[kMaxTot + q];
+  }
   finalize_scalar(f, agent, tot, lo, f.state[agent]);
 }
 
@@ -1347,15 +1462,24 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
       }
       // double-double partials (exact products, compensated sums): the stopping test combines them as
       // polynomials in alpha whose terms cancel by the residual drop (merged_stop_test)
-      dd rr{0.0, 0.0}, rh{0.0, 0.0}, hh{0.0, 0.0}, zr{0.0, 0.0}, zh{0.0, 0.0}, mh{0.0, 0.0};
+      // |r_j|^2 and <z_j, r_j> only when no k_tcg_updir left them (args.rz_own: the first iteration)
+      DotAcc rr_, rh_, hh_, zr_, zh_;
+      const bool rz = mode_snap(MODE) || args.rz_own != 0;  // (the first iteration's kernel: always)
 #pragma unroll
       for (int a = 0; a < R; ++a) {
-        rr = dd_fma(rr, rcol[a], rcol[a]);
-        rh = dd_fma(rh, rcol[a], hc[a]);
-        hh = dd_fma(hh, hc[a], hc[a]);
-        zr = dd_fma(zr, zc[a], rcol[a]);
-        zh = dd_fma(zh, zc[a], hc[a]);
+        rh_.add(rcol[a], hc[a]);
+        hh_.add(hc[a], hc[a]);
+        zh_.add(zc[a], hc[a]);
       }
+      if (rz) {
+#pragma unroll
+        for (int a = 0; a < R; ++a) {
+          rr_.add(rcol[a], rcol[a]);
+          zr_.add(zc[a], rcol[a]);
+        }
+      }
+      const dd rr = rr_.val(), rh = rh_.val(), hh = hh_.val(), zr = zr_.val(), zh = zh_.val();
+      dd mh{0.0, 0.0};
       if (args.pmode == PRECON_NONE) {
         mh = hh;
       } else {
@@ -1370,15 +1494,15 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
 #pragma unroll
           for (int u = 0; u < B; ++u) m = pk == u ? mk[u] : m;  // Minv_{pk, k} = column k's entry pk
           if (pk >= B || !act) m = 0.0;
-          dd t{0.0, 0.0};
+          DotAcc t;
 #pragma unroll
-          for (int a = 0; a < R; ++a) t = dd_fma(t, hc[a], hp[a]);
-          mh = dd_add(mh, dd_mul_d(t, m));
+          for (int a = 0; a < R; ++a) t.add(hc[a], hp[a]);
+          mh = kMergedDd ? dd_add(mh, dd_mul_d(t.val(), m)) : dd{fma(t.val().hi, m, mh.hi), 0.0};
         };
         double mkk = 0.0;
 #pragma unroll
         for (int u = 0; u < B; ++u) mkk = kc == u ? mk[u] : mkk;
-        mh = act ? dd_mul_d(hh, mkk) : dd{0.0, 0.0};
+        mh = act ? (kMergedDd ? dd_mul_d(hh, mkk) : dd{hh.hi * mkk, 0.0}) : dd{0.0, 0.0};
         double hp[R];
 #pragma unroll
         for (int a = 0; a < R; ++a) hp[a] = dpp_f64<0xB1>(hc[a]);  // quad_perm [1,0,3,2]: partner k^1
@@ -1393,7 +1517,19 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
       const dd zero{0.0, 0.0};
       dd parts[6] = {own ? rr : zero, own ? rh : zero, own ? hh : zero, own ? zr : zero,
                      own ? dd{2.0 * zh.hi, 2.0 * zh.lo} : zero, own ? mh : zero};
-      block_partials_dd<6>(own ? dpart : 0.0, parts, c.partials, p.tile, args.fin_mode == 2);
+      if constexpr (kMergedDd) {
+        if (rz) {
+          block_partials_dd<6>(own ? dpart : 0.0, parts, c.partials, p.tile, args.fin_mode == 2);
+        } else {  // slots 1 and 4 are not read (FinalizeArgs::rz_pc)
+          dd p4[4] = {parts[1], parts[2], parts[4], parts[5]};
+          block_partials_dd_at<4>(own ? dpart : 0.0, p4, kSlots2356, c.partials, p.tile, args.fin_mode == 2);
+        }
+      } else {  // plain sums, low parts written as zero (the finalize reads the same layout)
+        double pl[13] = {own ? dpart : 0.0};
+#pragma unroll
+        for (int q = 0; q < 6; ++q) pl[1 + q] = parts[q].hi;
+        block_partials_lo0<6>(pl, c.partials, p.tile, args.fin_mode == 2);
+      }
     } else {
       double parts[1] = {own ? dpart : 0.0};
       block_partials<1>(parts, c.partials, p.tile, args.fin_mode == 2);
@@ -1627,6 +1763,7 @@ __global__ __launch_bounds__(kThreads) void k_tcg_updir(LaunchCtx c, const doubl
 #pragma unroll
   for (int a = 0; a < R; ++a) ecol[a] = fma(step, dcol[a], ecol[a]);
   store_vec<R>(eta, off, own, ecol);
+  dd rz[2] = {{0.0, 0.0}, {0.0, 0.0}};
   if (cont) {  // uniform per agent
     constexpr int D = B - 1;
     const double beta = st.beta;
@@ -1642,9 +1779,15 @@ __global__ __launch_bounds__(kThreads) void k_tcg_updir(LaunchCtx c, const doubl
     for (int a = 0; a < R; ++a) dn[a] = fma(beta, dcol[a], -zc[a]);
     store_vec<R>(rv, off, own, rcol);
     store_vec<R>(delta, off, own, dn);
+    if (own) {  // |r_{j+1}|^2, <z_{j+1}, r_{j+1}> for the next iteration's stopping test (FinalizeArgs::rz_pc)
+#pragma unroll
+      for (int a = 0; a < R; ++a) {
+        rz[0] = dd_fma(rz[0], rcol[a], rcol[a]);
+        rz[1] = dd_fma(rz[1], zc[a], rcol[a]);
+      }
+    }
   }
-  double parts[1] = {own ? eh : 0.0};
-  block_partials<1>(parts, c.partials, p.tile);
+  block_partials_dd<2>(own ? eh : 0.0, rz, c.partials, p.tile);
 }
 
 // x2 = R_x1(scale * eta) (QF retraction, A.2) with partials <g,eta> and, when HV is given, <eta,HV>
@@ -2862,6 +3005,13 @@ __global__ __launch_bounds__(kThreads) void k_assemble_G(GEdges e, int nslots, c
 // ------------------------------------------------------------------------------------------
 // Host-side launchers with (r, b) dispatch
 // ------------------------------------------------------------------------------------------
+#ifdef DPGO_ISA_54_ONLY  // tools/isa_dump.sh: the headline shape only, for fast ISA inspection (never built into the library)
+#define DPGO_DISPATCH(R_, B_, CALL)                        \
+  switch ((R_) * 8 + (B_)) {                               \
+    case 5 * 8 + 4: { constexpr int R = 5, B = 4; CALL; break; } \
+    default: return hipErrorInvalidValue;                  \
+  }
+#else
 #define DPGO_DISPATCH(R_, B_, CALL)                        \
   switch ((R_) * 8 + (B_)) {                               \
     case 2 * 8 + 3: { constexpr int R = 2, B = 3; CALL; break; } \
@@ -2879,6 +3029,7 @@ __global__ __launch_bounds__(kThreads) void k_assemble_G(GEdges e, int nslots, c
     case 8 * 8 + 4: { constexpr int R = 8, B = 4; CALL; break; } \
     default: return hipErrorInvalidValue;                  \
   }
+#endif
 
 // one SpMM mode over every (r, b) and Q format (instantiated in the DPGO_SPMM_TU translation units)
 template <int MODE>
