@@ -127,6 +127,48 @@ __device__ __forceinline__ void block_partials_dd(double v0, dd (&v)[ND], double
   block_partials_dd_at<ND>(v0, v, kSlots123456, partials, tile, coherent);
 }
 
+// block_partials_dd_at through LDS: every lane's double-double values go to `scratch` (2 ND kThreads
+// doubles, the SpMM's record stage, dead after the edge loop) and wave w reduces quantities w, w + 4:
+// one quantity per wave instead of every quantity on every wave.  Fixed order (lanes l, l + 128, l + 64,
+// l + 192, then the wave tree), so the totals are reproducible; v0 takes block_partials' path (bitwise).
+template <int ND>
+__device__ __forceinline__ void block_partials_dd_lds(double v0, dd (&v)[ND], DdSlots slot, double* __restrict__ partials,
+                                                      int tile, bool coherent, double* scratch) {
+  __shared__ double red0[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v0 = wave_sum(v0);
+  __syncthreads();  // every wave is past its edge loop: the record stage is free
+  if (lane == 0) red0[wave] = v0;
+#pragma unroll
+  for (int q = 0; q < ND; ++q) {
+    scratch[(2 * q) * kThreads + threadIdx.x] = v[q].hi;
+    scratch[(2 * q + 1) * kThreads + threadIdx.x] = v[q].lo;
+  }
+  __syncthreads();
+  auto put = [&](int sl, double t) {
+    if (coherent)
+      __hip_atomic_store(&partials[tile * kPartialStride + sl], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      partials[tile * kPartialStride + sl] = t;
+  };
+#pragma unroll
+  for (int q0 = 0; q0 < ND; q0 += 4) {
+    const int q = q0 + wave;  // wave-uniform
+    if (q < ND) {
+      auto at = [&](int i) { return dd{scratch[(2 * q) * kThreads + i], scratch[(2 * q + 1) * kThreads + i]}; };
+      const dd x = wave_sum_dd(dd_add(dd_add(at(lane), at(lane + 128)), dd_add(at(lane + 64), at(lane + 192))));
+      if (lane == 0) {
+        int sl = slot.s[0];
+#pragma unroll
+        for (int u = 1; u < ND; ++u) sl = q == u ? slot.s[u] : sl;
+        put(sl, x.hi);
+        put(sl + kDdLo, x.lo);
+      }
+    }
+  }
+  if (threadIdx.x == 0) put(0, ((red0[0] + red0[1]) + red0[2]) + red0[3]);
+}
+
 // block_partials_dd's layout from plain partials (v[0] plain, v[1 .. ND] the high parts, low parts zero)
 template <int ND>
 __device__ __forceinline__ void block_partials_lo0(double (&v)[13], double* __restrict__ partials, int tile,
@@ -1172,6 +1214,7 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
   for (int a = 0; a < R; ++a)
 #pragma unroll
     for (int cc = 0; cc < B; ++cc) acc[a][cc] = 0.0;
+  double* red_scratch = nullptr;  // merged tCG partials' LDS scratch (the record stage, after the edge loop)
 
   // column k of in_j: the edge stream reads it for the diagonal term and hands it to the epilogues
   double xin[R];
@@ -1192,6 +1235,10 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     __shared__ int s_ptr[kTilePoses + 1];
     __shared__ int s_e[4];
     __shared__ f64x2 s_rec2[NREC * RW / 2];
+    if constexpr (STAGE && mode_merged(MODE)) {
+      static_assert(NREC * RW >= 2 * 6 * kThreads, "the record stage doubles as the merged partials' scratch");
+      red_scratch = reinterpret_cast<double*>(s_rec2);
+    }
     const int t0 = c.tile_start[p.tile], cnt = c.tile_count[p.tile];
     if (static_cast<int>(threadIdx.x) <= cnt) s_ptr[threadIdx.x] = q.inc_ptr[t0 + threadIdx.x];
     if (threadIdx.x < 2) s_e[threadIdx.x] = q.rec_first[t0 + (threadIdx.x ? cnt : 0)];
@@ -1518,9 +1565,18 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
       dd parts[6] = {own ? rr : zero, own ? rh : zero, own ? hh : zero, own ? zr : zero,
                      own ? dd{2.0 * zh.hi, 2.0 * zh.lo} : zero, own ? mh : zero};
       if constexpr (kMergedDd) {
-        if (rz) {
+        if (red_scratch != nullptr) {
+          if (rz) {
+            block_partials_dd_lds<6>(own ? dpart : 0.0, parts, kSlots123456, c.partials, p.tile, args.fin_mode == 2,
+                                     red_scratch);
+          } else {  // slots 1 and 4 are not read (FinalizeArgs::rz_pc)
+            dd p4[4] = {parts[1], parts[2], parts[4], parts[5]};
+            block_partials_dd_lds<4>(own ? dpart : 0.0, p4, kSlots2356, c.partials, p.tile, args.fin_mode == 2,
+                                     red_scratch);
+          }
+        } else if (rz) {
           block_partials_dd<6>(own ? dpart : 0.0, parts, c.partials, p.tile, args.fin_mode == 2);
-        } else {  // slots 1 and 4 are not read (FinalizeArgs::rz_pc)
+        } else {
           dd p4[4] = {parts[1], parts[2], parts[4], parts[5]};
           block_partials_dd_at<4>(own ? dpart : 0.0, p4, kSlots2356, c.partials, p.tile, args.fin_mode == 2);
         }
