@@ -98,7 +98,9 @@ hipError_t pooled_event(dpgo_hip_problem h, hipEvent_t* e) {
 }  // namespace
 
 int dpgo::spmm_launch(dpgo_hip_problem h, int mode, const LaunchCtx& c, const SpmmArgs& a) {
-  if (!h->timing || c.num_tiles == 0) {
+  const bool sample = h->timing > 0 && c.num_tiles > 0 && mode >= 0 && mode < dpgo::kSpmmModes &&
+                      h->timing_seq[mode]++ % h->timing == 0;
+  if (!sample) {
     HIP_TRY(dpgo::launch_spmm(h->r, h->b, mode, c, qview(h), a));
     return DPGO_HIP_OK;
   }

@@ -2300,25 +2300,37 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
       red_lo[q][threadIdx.x] = accl[q];
     }
   __syncthreads();
-  if (threadIdx.x >= 64) return;
-  const int l = threadIdx.x;
+  // wave w reduces quantities w and w + 4 (lane 0's halving tree over the same lane pairs as the fused path)
+  __shared__ double s_tot[2 * kMaxTot];
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int q0 = 0; q0 < kMaxTot; q0 += 4) {
+    const int q = q0 + wv;  // wave-uniform
+    int qq = 0;
+    double th = 0.0, tl = 0.0;
+    if (q < NQ && part_src(f, q, qq) != nullptr) {
+      if ((f.dd_mask >> q) & 1) {
+        auto at = [&](int i) { return dd{red[q][i], red_lo[q][i]}; };
+        const dd x = wave_sum_dd(dd_add(dd_add(at(l), at(l + 128)), dd_add(at(l + 64), at(l + 192))));
+        th = x.hi;
+        tl = x.lo;
+      } else {
+        th = wave_sum((red[q][l] + red[q][l + 128]) + (red[q][l + 64] + red[q][l + 192]));
+      }
+    }
+    if (l == 0) {
+      s_tot[q] = th;
+      s_tot[kMaxTot + q] = tl;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
   double tot[kMaxTot], lo[kMaxTot];
 #pragma unroll
   for (int q = 0; q < kMaxTot; ++q) {
-    tot[q] = 0.0;
-    lo[q] = 0.0;
-    if (q >= NQ || srcs[q] == nullptr) continue;
-    if ((f.dd_mask >> q) & 1) {
-      auto at = [&](int i) { return dd{red[q][i], red_lo[q][i]}; };
-      const dd x = wave_sum_dd(dd_add(dd_add(at(l), at(l + 128)), dd_add(at(l + 64), at(l + 192))));
-      tot[q] = x.hi;
-      lo[q] = x.lo;
-      continue;
-    }
-    double v = (red[q][l] + red[q][l + 128]) + (red[q][l + 64] + red[q][l + 192]);
-    tot[q] = wave_sum(v);  // lane 0's halving tree
+    tot[q] = s_tot[q];
+    lo[q] = s_tot[kMaxTot + q];
   }
-  if (l != 0) return;
   // the scalar logic runs on a register copy: a chain of dependent LDS accesses costs microseconds
   AgentState st = sh_state;
   finalize_scalar(f, agent, tot, lo, st);

@@ -150,7 +150,8 @@ struct dpgo_hip_problem_s {
   int trace_cap = 0;
   // in-step SpMM timing (dpgo_rbcd_set_kernel_timing): HIP events around every X.Q launch on the
   // handle's stream, resolved per mode by take_spmm_times()
-  bool timing = false;
+  int timing = 0;  // 0 off, k > 0: every k-th launch of each mode (a sample: events cost dispatch gaps)
+  long long timing_seq[dpgo::kSpmmModes] = {};
   struct TimedLaunch {
     int mode;
     hipEvent_t a, b;

@@ -1130,7 +1130,10 @@ int dpgo_rbcd_get_trace(dpgo_rbcd e, int agent, double* out, int max_records, in
 int dpgo_rbcd_set_kernel_timing(dpgo_rbcd e, int on) {
   if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
   for (auto* h : e->prob)
-    if (h) h->timing = on != 0;
+    if (h) {
+      h->timing = on < 0 ? 0 : on;
+      for (auto& q : h->timing_seq) q = 0;
+    }
   return DPGO_HIP_OK;
 }
 

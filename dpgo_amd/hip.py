@@ -856,7 +856,7 @@ class Rbcd:
                 for i in range(min(n.value, cap))]
 
     def set_kernel_timing(self, on):
-        _check(lib().dpgo_rbcd_set_kernel_timing(self.h, int(bool(on))))
+        _check(lib().dpgo_rbcd_set_kernel_timing(self.h, int(on)))  # 0 off, k: every k-th launch per mode
 
     def kernel_times(self):
         """{mode: (ms summed, launches)} of the timed in-step X.Q launches since the last call."""

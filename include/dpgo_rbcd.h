@@ -218,10 +218,11 @@ int dpgo_rbcd_exchange_color(dpgo_rbcd e, int color, const double** recv_dev);
 /* Algorithmic bytes of one X.Q launch over every agent of `color`, per SpMM mode (out[DPGO_SPMM_MODES], indexed as
  * dpgo_rbcd_kernel_times; 0 for modes the engine does not launch in a step). */
 int dpgo_rbcd_mode_bytes(dpgo_rbcd e, int color, double* out);
-/* HIP events around every in-step X.Q launch (on the launch stream) while on; dpgo_rbcd_kernel_times
- * synchronises and returns, per SpMM mode (DPGO_SPMM_MODES entries, order above), the
- * summed milliseconds and launch counts since the last call. */
-int dpgo_rbcd_set_kernel_timing(dpgo_rbcd e, int on);
+/* HIP events around in-step X.Q launches (on the launch stream): `period` 0 = off, 1 = every launch, k = every
+ * k-th launch of each mode (a sample: an event pair adds a dispatch gap of a few microseconds around its launch);
+ * dpgo_rbcd_kernel_times synchronises and returns, per SpMM mode (DPGO_SPMM_MODES entries, order above), the
+ * summed milliseconds and launch counts of the timed launches since the last call. */
+int dpgo_rbcd_set_kernel_timing(dpgo_rbcd e, int period);
 /* Per-iteration RTR / tCG trace of every owned agent's updates (dpgo_hip_set_trace / _get_trace
  * records, per agent at its global index). */
 int dpgo_rbcd_set_trace(dpgo_rbcd e, int capacity);
