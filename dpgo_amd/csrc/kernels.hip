@@ -854,12 +854,14 @@ __device__ __forceinline__ void set_status(const FinalizeArgs& f, int agent, dou
 }
 
 // The RTR / tCG scalar logic of one agent on its reduced partials tot[] (one thread).
+// OPC >= 0: the op is known at compile time (a specialised k_finalize carries only that op's logic)
+template <int OPC = -1>
 __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent, const double (&tot)[kMaxTot],
                                                 const double (&lo)[kMaxTot], AgentState& s) {
   const int nq = f.nq_a + f.nq_b;
   const OptScalars& o = f.opt;
   const bool filtered = (f.agent_filter == 1 && !s.eta_implicit) || (f.agent_filter == 2 && s.eta_implicit);
-  switch (filtered ? -1 : f.op) {
+  switch (filtered ? -1 : (OPC >= 0 ? OPC : f.op)) {
     case OP_EVAL_INIT: {  // after EVAL at the initial iterate
       s.f1 = tot[0];
       s.ngf = sqrt(tot[1]);
@@ -2259,14 +2261,17 @@ __global__ __launch_bounds__(kThreads) void k_accept(LaunchCtx c, const double* 
 // cross-wave levels go through LDS once for all quantities and the in-wave levels are shuffles; the
 // agent's state is staged in LDS while the partials load and written back after the scalar logic.
 static_assert(sizeof(AgentState) % sizeof(double) == 0, "AgentState is staged as doubles");
-template <int NQ>
+// OPC >= 0: specialised for one op (the per-tCG-iteration ones): a few hundred instructions instead of every
+// op's logic -- a launch on a few CUs starts with a cold instruction cache, so the code it walks costs time.
+template <int NQ, int OPC = -1>
 __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
   static_assert(NQ <= kMaxTot, "finalize slots");
+  constexpr bool kDd = OPC < 0 || OPC == OP_TCG_STEP_CHECK || OPC == OP_TCG_CHECK_M;  // ops with dd partials
   const int agent = blockIdx.x;
   const int t0 = f.agent_tile_off[agent], t1 = f.agent_tile_off[agent + 1];
   constexpr int kStateWords = static_cast<int>(sizeof(AgentState) / sizeof(double));
   __shared__ double red[NQ][kThreads];
-  __shared__ double red_lo[NQ][kThreads];  // low parts of double-double quantities (f.dd_mask)
+  __shared__ double red_lo[kDd ? NQ : 1][kThreads];  // low parts of double-double quantities (f.dd_mask)
   __shared__ AgentState sh_state;
   if (threadIdx.x < kStateWords)
     reinterpret_cast<double*>(&sh_state)[threadIdx.x] = reinterpret_cast<const double*>(&f.state[agent])[threadIdx.x];
@@ -2284,7 +2289,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
     for (int q = 0; q < NQ; ++q) {
       if (srcs[q] == nullptr) continue;
       const double v = srcs[q][t * kPartialStride + qqs[q]];
-      if ((f.dd_mask >> q) & 1) {
+      if (kDd && ((f.dd_mask >> q) & 1)) {
         const dd a = dd_add({acc[q], accl[q]}, {v, srcs[q][t * kPartialStride + qqs[q] + kDdLo]});
         acc[q] = a.hi;
         accl[q] = a.lo;
@@ -2297,7 +2302,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
   for (int q = 0; q < NQ; ++q)
     if (srcs[q] != nullptr) {
       red[q][threadIdx.x] = acc[q];
-      red_lo[q][threadIdx.x] = accl[q];
+      if constexpr (kDd) red_lo[q][threadIdx.x] = accl[q];
     }
   __syncthreads();
   // wave w reduces quantities w and w + 4 (lane 0's halving tree over the same lane pairs as the fused path)
@@ -2309,8 +2314,8 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
     int qq = 0;
     double th = 0.0, tl = 0.0;
     if (q < NQ && part_src(f, q, qq) != nullptr) {
-      if ((f.dd_mask >> q) & 1) {
-        auto at = [&](int i) { return dd{red[q][i], red_lo[q][i]}; };
+      if (kDd && ((f.dd_mask >> q) & 1)) {
+        auto at = [&](int i) { return dd{red[q][i], red_lo[kDd ? q : 0][i]}; };
         const dd x = wave_sum_dd(dd_add(dd_add(at(l), at(l + 128)), dd_add(at(l + 64), at(l + 192))));
         th = x.hi;
         tl = x.lo;
@@ -2333,7 +2338,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
   }
   // the scalar logic runs on a register copy: a chain of dependent LDS accesses costs microseconds
   AgentState st = sh_state;
-  finalize_scalar(f, agent, tot, lo, st);
+  finalize_scalar<OPC>(f, agent, tot, lo, st);
   double* dst = reinterpret_cast<double*>(&f.state[agent]);
   const double* srcw = reinterpret_cast<const double*>(&st);
 #pragma unroll
@@ -3384,8 +3389,17 @@ hipError_t launch_precond_finish(int r, int b, const LaunchCtx& c, const double*
 hipError_t launch_finalize(const FinalizeArgs& f, int num_agents, hipStream_t stream) {
   if (num_agents == 0) return hipSuccess;
   // four slots cover every op but the merged tCG's (seven HESS_M partials) and those carrying pc
-  if (f.nq_c > 0 || f.nq_a + f.nq_b > 4)
+  const bool wide = f.nq_c > 0 || f.nq_a + f.nq_b > 4;
+  if (wide && f.op == OP_TCG_STEP_CHECK)  // every merged tCG iteration
+    k_finalize<kMaxTot, OP_TCG_STEP_CHECK><<<num_agents, kThreads, 0, stream>>>(f);
+  else if (wide && f.op == OP_RHO)
+    k_finalize<kMaxTot, OP_RHO><<<num_agents, kThreads, 0, stream>>>(f);
+  else if (wide)
     k_finalize<kMaxTot><<<num_agents, kThreads, 0, stream>>>(f);
+  else if (f.op == OP_EVAL_TCG_INIT)
+    k_finalize<4, OP_EVAL_TCG_INIT><<<num_agents, kThreads, 0, stream>>>(f);
+  else if (f.op == OP_RHO)
+    k_finalize<4, OP_RHO><<<num_agents, kThreads, 0, stream>>>(f);
   else
     k_finalize<4><<<num_agents, kThreads, 0, stream>>>(f);
   return hipGetLastError();
