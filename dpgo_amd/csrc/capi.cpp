@@ -487,6 +487,9 @@ int sync_chol(dpgo_hip_problem h) {
   if (total > kMaxCholDoubles)
     return fail(DPGO_HIP_EINVAL, "exact preconditioner: the supernodal panels of the batch would exceed 24 GiB "
                                  "(use DPGO_PRECON_BLOCK_JACOBI for this size)");
+  if (std::getenv("DPGO_VERBOSE_CHOL"))
+    std::fprintf(stderr, "[dpgo_hip] exact preconditioner: %d agents, %.3f GiB of supernodal panels\n", K,
+                 8.0 * static_cast<double>(total) / (1024.0 * 1024.0 * 1024.0));
   // ---- the batch's node list (agents in order, each in postorder), work lists per tree level
   std::vector<int> base(K + 1, 0);
   for (int a = 0; a < K; ++a) base[a + 1] = base[a] + static_cast<int>(Fs[a].nodes.size());
