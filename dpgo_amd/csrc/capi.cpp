@@ -941,6 +941,12 @@ int dpgo_hip_problem_destroy(dpgo_hip_problem h) {
     (void)hipStreamSynchronize(h->own_stream);
     (void)hipStreamDestroy(h->own_stream);
   }
+  if (h->split_stream) {
+    (void)hipStreamSynchronize(h->split_stream);
+    (void)hipStreamDestroy(h->split_stream);
+    (void)hipEventDestroy(h->split_fork);
+    (void)hipEventDestroy(h->split_join);
+  }
   (void)hipDeviceSynchronize();
   if (h->pub_host) (void)hipHostFree(h->pub_host);
   delete h;
@@ -1494,6 +1500,47 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
                          &fin));
       return rtag;
     };
+    // The same iteration over agents [a0, a1) only, on `on` (TUNE_SPLIT_STREAMS): tiles, partial slots and
+    // finalize rows of that agent range; every kernel of the iteration reads and writes only those agents'
+    // poses (Q and the tCG vectors are block-diagonal over agents), so the halves are independent and each
+    // agent's arithmetic is the unsplit launch's, bit for bit.
+    auto launch_merged_range = [&](int j, int mode, int flag, int op, int a0, int a1, hipStream_t on) -> int {
+      const int t0 = h->h_agent_tile_off[a0], t1 = h->h_agent_tile_off[a1];
+      if (t1 == t0) return DPGO_HIP_OK;
+      auto sub = [&](double* partials) {
+        dpgo::LaunchCtx c = make_ctx(h, flag, partials + static_cast<long>(t0) * dpgo::kPartialStride);
+        c.tile_agent += t0;
+        c.tile_start += t0;
+        c.tile_count += t0;
+        c.num_tiles = t1 - t0;
+        c.stream = on;
+        return c;
+      };
+      dpgo::SpmmArgs sa{h->delta.p, nullptr, nullptr, x1, h->S.p, h->Hdelta.p, nullptr, h->minv.p, nullptr, pmode};
+      sa.rvec = j == 0 ? h->g.p : h->rv.p;
+      const bool rz_pc = j > 0;
+      sa.rz_own = rz_pc ? 0 : 1;
+      dpgo::OptScalars os = o;
+      os.first_full = mode == dpgo::MODE_HESS_QF_M ? 1 : 0;
+      dpgo::FinalizeArgs fin = make_fin(h, op, h->pa.p, 7, nullptr, 0, &os, nullptr, 0, 0);
+      fin.pc = h->peh.p;
+      fin.nq_c = 1;
+      fin.dd_mask = 0x7E;
+      fin.rz_pc = rz_pc ? 1 : 0;
+      fin.agent_tile_off += a0;  // tile offsets stay global: the partial slots are the unsplit ones
+      fin.agent_num_poses += a0;
+      fin.state += a0;
+      fin.out_sums += 4 * a0;
+      if (fin.trace) fin.trace += static_cast<long>(a0) * fin.trace_cap * dpgo::kTraceWidth;
+      DPGO_TRY(dpgo::spmm_launch(h, mode, sub(h->pa.p), sa));
+      HIP_TRY(dpgo::launch_finalize(fin, a1 - a0, on));
+      auto cu = sub(h->peh.p);
+      cu.flag_kind = dpgo::FLAG_TCG_MODE;
+      HIP_TRY(dpgo::launch_tcg_updir(r, b, cu, x1, h->minv.p, pmode, h->delta.p, h->Hdelta.p, h->eta.p,
+                                     j == 0 ? h->g.p : h->rv.p, h->rv.p, j == 0 ? 1 : 0,
+                                     j + 1 == P.tr_max_inner ? 1 : 0));
+      return DPGO_HIP_OK;
+    };
     int launched = 0, rtag = 0;
     bool cg_agents = !qf0;  // some agent may still be in tCG after the first step test
     // Every iteration queued at once, no status published inside tCG (the CG regime, where tCG runs
@@ -1501,7 +1548,34 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     // near-empty launches).  Adaptive (default): when the previous call's tCG took CG steps.
     const int la = dpgo::g_tuning[dpgo::TUNE_TCG_LOOKAHEAD];
     const bool all_ahead = merged && single && full0 && la != 1 && (la == 2 || !h->predict_boundary);
-    if (all_ahead) {
+    const bool split = all_ahead && K >= 2 && h->fuse_finalize == 0 && dpgo::g_tuning[dpgo::TUNE_SPLIT_STREAMS] > 0;
+    if (split) {
+      if (!h->split_stream) {
+        HIP_TRY(hipStreamCreateWithFlags(&h->split_stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&h->split_fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&h->split_join, hipEventDisableTiming));
+      }
+      // value 2: the second half starts once the first half's first iteration is done, so the two halves run
+      // out of phase (one half's HESS_M beside the other's k_tcg_updir) rather than side by side
+      const bool offset = dpgo::g_tuning[dpgo::TUNE_SPLIT_STREAMS] == 2;
+      const int am = K / 2;
+      if (!offset) {
+        HIP_TRY(hipEventRecord(h->split_fork, h->stream));
+        HIP_TRY(hipStreamWaitEvent(h->split_stream, h->split_fork, 0));
+      }
+      for (int j = 0; j < P.tr_max_inner; ++j) {
+        const int mode = j == 0 ? dpgo::MODE_HESS_QF_M : dpgo::MODE_HESS_M;
+        DPGO_TRY(launch_merged_range(j, mode, dpgo::FLAG_TCG, dpgo::OP_TCG_STEP_CHECK, 0, am, h->stream));
+        if (offset && j == 0) {
+          HIP_TRY(hipEventRecord(h->split_fork, h->stream));
+          HIP_TRY(hipStreamWaitEvent(h->split_stream, h->split_fork, 0));
+        }
+        DPGO_TRY(launch_merged_range(j, mode, dpgo::FLAG_TCG, dpgo::OP_TCG_STEP_CHECK, am, K, h->split_stream));
+      }
+      HIP_TRY(hipEventRecord(h->split_join, h->split_stream));
+      HIP_TRY(hipStreamWaitEvent(h->stream, h->split_join, 0));
+      cg_agents = true;
+    } else if (all_ahead) {
       for (int j = 0; j < P.tr_max_inner; ++j)
         DPGO_TRY(launch_merged(j, j == 0 ? dpgo::MODE_HESS_QF_M : dpgo::MODE_HESS_M, dpgo::FLAG_TCG,
                                dpgo::OP_TCG_STEP_CHECK, false));

@@ -234,6 +234,10 @@ enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH =
                TUNE_SV_STAGE = 8,  // 1: HESS passes stage the tile's second-visit records in LDS too (the
                                    //    tables are built when Q is set with this on; measured slower)
                TUNE_STATUS_PASS = 9,  // 1: the agent status by its own pass (k_sqdiff + OP_STATUS), not folded
+               TUNE_SPLIT_STREAMS = 10,  // merged tCG queued at once: the batch's agents in two halves on two
+                                         // streams (one half's VALU-bound HESS_M beside the other's HBM-bound
+                                         // k_tcg_updir); 0 off, 1 on (default: 1M -0.7 %, the 125 k
+                                         // share -4.6 % ms/step), 2 the halves out of phase (no gain)
                TUNE_COUNT = 12 };
 // variant of the edge-stream SpMM used unless TUNE_EDGE_VARIANT overrides it (bit 0: XCD-aware
 // tile remap; v >> 1: minimum waves per SIMD the register allocation must allow, none/4/5/6)

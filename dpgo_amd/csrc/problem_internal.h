@@ -129,6 +129,10 @@ struct dpgo_hip_problem_s {
   // its agent's outcome was decided (an in-place X_in is overwritten by then)
   dpgo::DevBuf<double> pc;
   dpgo::DevBuf<double> peh;  // merged tCG: k_tcg_updir's <eta_old, Hdelta> partials (FinalizeArgs::pc)
+  // TUNE_SPLIT_STREAMS: the second half of the agents' merged tCG iterations run on split_stream, forked
+  // from / joined into the launch stream by events
+  hipStream_t split_stream = nullptr;
+  hipEvent_t split_fork = nullptr, split_join = nullptr;
   dpgo::DevBuf<dpgo::AgentState> state;
   std::vector<dpgo::AgentState> h_state;
   // per-agent arrival counts of a k_spmm with a fused finalize (0 between launches)

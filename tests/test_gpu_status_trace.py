@@ -635,3 +635,38 @@ def test_status_fold_bitwise(hip, accel):
     for (rc0, rd0), (rc1, rd1) in zip(out[0][1], out[1][1]):
         assert np.array_equal(rc0, rc1)
         assert np.array_equal(rd0, rd1)
+
+
+def test_split_streams_bitwise(hip):
+    """The merged tCG iterations queued at once with the batch's agents in two halves on two streams (tuning
+    key TUNE_SPLIT_STREAMS) give bitwise the one-stream iterates, traces and counters: the halves touch
+    disjoint agents' poses, tiles, partial slots and finalize rows."""
+    g = hip.Graph.grid3d(12, seed=5)
+    aop = g.grid_partition(2)
+    X0, _, _ = g.distributed_init(aop, 5, hip.lifting_matrix(3, 5), gpu=True, rtol=1e-12, dev_layout=True)
+    out = []
+    for split in (0, 1, 2):
+        hip.set_tuning(10, split)
+        hip.set_tuning(7, 2)  # every tCG iteration queued at once (the path the split applies to)
+        try:
+            e = hip.Rbcd(g, aop, np.zeros(8, np.int32), 0, 1, hip.rbcd_params(r=5, acceleration=1))
+            e.set_trace(512)
+            e.set_X(X0)
+            for it in range(40):
+                e.pre_exchange(it % e.num_colors)
+                e.update(it % e.num_colors, None)
+            X = np.zeros(X0.size)
+            e.get_X_into(X)
+            tr = [e.get_trace(a) for a in range(8)]
+            out.append((X, e.stats().copy(), tr))
+        finally:
+            hip.set_tuning(10, 1)
+            hip.set_tuning(7, 0)
+    for o in out[1:]:
+        assert np.array_equal(out[0][0], o[0])
+        assert np.array_equal(out[0][1], o[1])
+        for a in range(8):
+            assert len(out[0][2][a]) == len(o[2][a])
+            for x, y in zip(out[0][2][a], o[2][a]):
+                assert x == y
+    assert out[0][1][:, 10].sum() > 0  # CG steps were taken
