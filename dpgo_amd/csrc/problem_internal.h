@@ -196,6 +196,7 @@ struct StatusArgs {
 int optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params, const double* X_in, double* X_out,
                         const int* agent_enabled_host, dpgo_opt_result* results, const StatusArgs* st);
 // f / |grad|^2 / <G, X> per agent at X into the handle's sums (OP_SUM, nq 3): asynchronous
+bool merged_split(dpgo_hip_problem h);  // TUNE_SPLIT_STREAMS applies to this batch (capi.cpp)
 int eval_sums_dev(dpgo_hip_problem h, const double* X);
 // copy the per-agent sums (4 per agent) to the host (synchronises)
 int download_sums_public(dpgo_hip_problem h, std::vector<double>& out);

@@ -1109,6 +1109,12 @@ int dpgo_rbcd_mode_bytes(dpgo_rbcd e, int color, double* out) {
     out[MODE_QF] += half_in + z.n * SW;
     out[MODE_F] += half_in + gread;
   }
+  if (e->prob[color] && merged_split(e->prob[color])) {
+    // the merged tCG iterations run as two launches over the colour's agent halves (TUNE_SPLIT_STREAMS): the
+    // mean bytes of one such launch
+    out[MODE_HESS_M] *= 0.5;
+    out[MODE_HESS_QF_M] *= 0.5;
+  }
   return DPGO_HIP_OK;
 }
 

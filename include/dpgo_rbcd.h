@@ -216,7 +216,9 @@ int dpgo_rbcd_exchange_color(dpgo_rbcd e, int color, const double** recv_dev);
  * HESS_M, HESS_QF_M (the last two: the merged tCG iteration's Hessian passes) */
 #define DPGO_SPMM_MODES 11
 /* Algorithmic bytes of one X.Q launch over every agent of `color`, per SpMM mode (out[DPGO_SPMM_MODES], indexed as
- * dpgo_rbcd_kernel_times; 0 for modes the engine does not launch in a step). */
+ * dpgo_rbcd_kernel_times; 0 for modes the engine does not launch in a step).  Where the colour's merged tCG runs
+ * as two half-batch launches on two streams (small batches, tuning key 10) HESS_M / HESS_QF_M give the mean bytes
+ * of one such launch (half the colour's). */
 int dpgo_rbcd_mode_bytes(dpgo_rbcd e, int color, double* out);
 /* HIP events around in-step X.Q launches (on the launch stream): `period` 0 = off, 1 = every launch, k = every
  * k-th launch of each mode (a sample: an event pair adds a dispatch gap of a few microseconds around its launch);
