@@ -364,6 +364,10 @@ __host__ __device__ constexpr int minv_index(int u, int v) { return sym_index<B>
 // is consumed; every load is unconditional (the index is clamped) so the compiler waits only for
 // the stage it consumes.  INC_LDS: entries from the LDS stage (ds_read: waiting for them never
 // drains in-flight global loads).  REC_LDS: records from the LDS stage (id - e0), else global.
+// LDS stride of a staged edge record: one double of padding, so the records the 16 poses of a wave read at
+// once start on different banks (a 128-byte stride put all of them on two bank offsets: 4-way conflicts)
+__host__ __device__ constexpr int lds_rec_stride(int b) { return edge_rec_width(b - 1) + 1; }
+
 // Raw buffer loads for the edge loop's gathers.  They are intrinsic calls, not IR loads: plain loads feeding
 // the loop-carried register stage are folded by the optimizer into ONE load of a phi of the two addresses,
 // issued right before its FMAs (no gather in flight while the previous incidence is consumed: a full L2/HBM
@@ -406,7 +410,7 @@ __device__ __forceinline__ void edge_loop(const QView& q, const double* __restri
     const int off = outg ? kc : 4 * kc;  // column kc of M (outgoing) / row kc (incoming)
     const int stride = outg ? 4 : 1;
     if constexpr (REC_LDS) {
-      const double* mr = s_rec + ((ie.x >> 1) - e0) * RW + off;
+      const double* mr = s_rec + ((ie.x >> 1) - e0) * lds_rec_stride(B) + off;
 #pragma unroll
       for (int c = 0; c < B; ++c) st.m[c] = mr[c * stride];
     } else if constexpr (BUF) {
@@ -1236,10 +1240,11 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
     __shared__ int2 s_inc[NINC];
     __shared__ int s_ptr[kTilePoses + 1];
     __shared__ int s_e[4];
-    __shared__ f64x2 s_rec2[NREC * RW / 2];
+    constexpr int RS = lds_rec_stride(B);
+    __shared__ double s_recd[NREC * RS];
     if constexpr (STAGE && mode_merged(MODE)) {
-      static_assert(NREC * RW >= 2 * 6 * kThreads, "the record stage doubles as the merged partials' scratch");
-      red_scratch = reinterpret_cast<double*>(s_rec2);
+      static_assert(NREC * RS >= 2 * 6 * kThreads, "the record stage doubles as the merged partials' scratch");
+      red_scratch = s_recd;
     }
     const int t0 = c.tile_start[p.tile], cnt = c.tile_count[p.tile];
     if (static_cast<int>(threadIdx.x) <= cnt) s_ptr[threadIdx.x] = q.inc_ptr[t0 + threadIdx.x];
@@ -1256,20 +1261,32 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
         const f64x2* all = reinterpret_cast<const f64x2*>(q.rec);
         for (int x = threadIdx.x; x < ns * (RW / 2); x += kThreads) {
           const int rr = x / (RW / 2), w = x - rr * (RW / 2);
-          s_rec2[x] = all[static_cast<long>(q.sv_ids[sv0 + rr]) * (RW / 2) + w];
+          const f64x2 v = all[static_cast<long>(q.sv_ids[sv0 + rr]) * (RW / 2) + w];
+          s_recd[rr * RS + 2 * w] = v.x;
+          s_recd[rr * RS + 2 * w + 1] = v.y;
         }
         const f64x2* src = all + static_cast<long>(e0) * (RW / 2);
-        for (int x = threadIdx.x; x < ne * (RW / 2); x += kThreads) s_rec2[ns * (RW / 2) + x] = src[x];
+        for (int x = threadIdx.x; x < ne * (RW / 2); x += kThreads) {
+          const int rr = x / (RW / 2), w = x - rr * (RW / 2);
+          const f64x2 v = src[x];
+          s_recd[(ns + rr) * RS + 2 * w] = v.x;
+          s_recd[(ns + rr) * RS + 2 * w + 1] = v.y;
+        }
       } else {
         for (int x = threadIdx.x; x < ni; x += kThreads) s_inc[x] = q.inc[i0 + x];
         const f64x2* src = reinterpret_cast<const f64x2*>(q.rec) + static_cast<long>(e0) * (RW / 2);
-        for (int x = threadIdx.x; x < ne * (RW / 2); x += kThreads) s_rec2[x] = src[x];
+        for (int x = threadIdx.x; x < ne * (RW / 2); x += kThreads) {
+          const int rr = x / (RW / 2), w = x - rr * (RW / 2);
+          const f64x2 v = src[x];
+          s_recd[rr * RS + 2 * w] = v.x;
+          s_recd[rr * RS + 2 * w + 1] = v.y;
+        }
       }
     }
     if constexpr (STAGE) __syncthreads();
     constexpr bool NODIAG = MODE == MODE_QF;
     if (p.ok) {
-      const double* s_rec = reinterpret_cast<const double*>(s_rec2);
+      const double* s_rec = s_recd;
       if constexpr (mode_hess(MODE)) {
         constexpr bool SNAP = mode_snap(MODE);
         if (staged)
