@@ -76,7 +76,7 @@ namespace {
 
 dpgo::QView qview(dpgo_hip_problem h) {
   return dpgo::QView{h->rowptr.p, h->col.p, h->blocks.p, h->inc_ptr.p, h->inc.p, h->rec.p, h->diag.p, h->rec_first.p,
-                     h->sv_ptr.p, h->sv_ids.p, h->inc_sv.p, h->fmt};
+                     h->sv_ptr.p, h->sv_ids.p, h->inc_sv.p, h->fmt, h->tuning};
 }
 
 int check_handle(dpgo_hip_problem h) {
@@ -271,7 +271,7 @@ int sync_q_edges(dpgo_hip_problem h) {
   h->sv_ptr.release();
   h->sv_ids.release();
   h->inc_sv.release();
-  if (dpgo::g_tuning[dpgo::TUNE_SV_STAGE] > 0) {
+  if (h->tuning[dpgo::TUNE_SV_STAGE] > 0) {
     const int T = h->num_tiles;
     std::vector<int> sv_ptr(T + 1, 0), sv_ids;
     std::vector<int2> inc_sv(inc.size());
@@ -867,6 +867,7 @@ int dpgo_hip_problem_create_batch(int num_agents, const int* poses_per_agent, in
     if (poses_per_agent[a] <= 0) return fail(DPGO_HIP_EINVAL, "every agent needs >= 1 pose");
   if (usable_devices() == 0) return fail(DPGO_HIP_ENODEV, "no gfx950 device available (no CPU fallback)");
   auto* h = new dpgo_hip_problem_s();
+  std::memcpy(h->tuning, dpgo::g_tuning, sizeof(h->tuning));
   h->K = num_agents;
   h->d = d;
   h->r = r;
@@ -1177,6 +1178,13 @@ int dpgo_hip_set_tuning(int key, int value) {
   return DPGO_HIP_OK;
 }
 
+int dpgo_hip_problem_set_tuning(dpgo_hip_problem h, int key, int value) {
+  DPGO_TRY(check_handle(h));
+  if (key < 0 || key >= dpgo::TUNE_COUNT) return fail(DPGO_HIP_EINVAL, "bad tuning key");
+  h->tuning[key] = value;
+  return DPGO_HIP_OK;
+}
+
 int dpgo_hip_synchronize(dpgo_hip_problem h) {
   DPGO_TRY(check_handle(h));
   HIP_TRY(hipStreamSynchronize(h->stream));
@@ -1308,7 +1316,7 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
   // agent's arithmetic does not depend on which other agents share its handle.
   // (a first step forced to the full pass reads grad(x1) in that pass already: the merged HESS_QF_M's r_0)
   bool g_valid = !(fused_tcg && single && h->predict_boundary && P.tr_max_inner > 0 &&
-                   dpgo::g_tuning[dpgo::TUNE_FIRST_STEP] != 2);
+                   h->tuning[dpgo::TUNE_FIRST_STEP] != 2);
   if (fused_tcg) {
     const dpgo::FinalizeArgs fin = make_fin(h, dpgo::OP_EVAL_TCG_INIT, h->pa.p, 3, nullptr, 0, &o, en_dev);
     DPGO_TRY(eval_at(h, x1, g_valid ? h->g.p : nullptr, h->S.p, h->pa.p, dpgo::FLAG_NONE, dpgo::MODE_EVAL_TCG,
@@ -1386,7 +1394,7 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     std::vector<int> tags, step_tags;
     // Consumer-side finalize (TUNE_FUSE_TCG): the step test's scalar logic runs in the update kernel's
     // prologue and the stopping test's in the direction update's, three launches per tCG iteration.
-    const bool fuse_tcg = dpgo::g_tuning[dpgo::TUNE_FUSE_TCG] > 0 && !exact;
+    const bool fuse_tcg = h->tuning[dpgo::TUNE_FUSE_TCG] > 0 && !exact;
     // iteration j's step test: Hdelta = Hess[delta] and d_Hd = <delta, Hdelta> (MODE_HESS); for the
     // first step d_Hd by the each-edge-once formula, alone (MODE_QF) or with Hdelta stored (MODE_HESS_QF)
     auto launch_step = [&](int mode) -> int {
@@ -1433,7 +1441,7 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     const bool qf0 = !exact && P.tr_max_inner > 0;
     // When the previous call took CG steps the first step test is the full pass (MODE_HESS_QF): same
     // d_Hd, and Hess[delta] is there for the agents that continue (no second pass over them).
-    const int first_kind = dpgo::g_tuning[dpgo::TUNE_FIRST_STEP];
+    const int first_kind = h->tuning[dpgo::TUNE_FIRST_STEP];
     const bool full0 = qf0 && (first_kind == 2 || (first_kind == 0 && !h->predict_boundary));
     // Single Run, first steps predicted on the boundary: the candidate, f(x2) and the rho test of the
     // agents whose first step already ended tCG are queued right behind the step test, before the host
@@ -1442,12 +1450,12 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     const bool spec = qf0 && single && !full0;
     // PGOAgent status folded into the retraction + rho test of a single Run (no k_sqdiff / OP_STATUS pass);
     // agents that never ran this call (|grad| < tol) are the separate pass's, run only when some did
-    const bool status_fold = st != nullptr && single && dpgo::g_tuning[dpgo::TUNE_STATUS_PASS] == 0;
+    const bool status_fold = st != nullptr && single && h->tuning[dpgo::TUNE_STATUS_PASS] == 0;
     // Merged tCG iteration (the default with block-Jacobi / no preconditioner): HESS_M, one finalize for
     // the step test and the stopping test (OP_TCG_STEP_CHECK), then k_tcg_updir -- three launches per
     // iteration instead of five, no z vector.  The exact preconditioner and TUNE_FUSE_TCG keep the
     // classic sequence (TUNE_CLASSIC_TCG forces it).
-    const bool merged = qf0 && !fuse_tcg && dpgo::g_tuning[dpgo::TUNE_CLASSIC_TCG] == 0;
+    const bool merged = qf0 && !fuse_tcg && h->tuning[dpgo::TUNE_CLASSIC_TCG] == 0;
     auto launch_merged = [&](int j, int mode, int flag, int op, bool publish = true) -> int {
       auto ch = make_ctx(h, flag, h->pa.p);
       const int tag = publish ? next_tag(h) : 0;
@@ -1546,7 +1554,7 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     // Every iteration queued at once, no status published inside tCG (the CG regime, where tCG runs
     // to MAXITER or close: agents that stop skip their tiles, an all-stopped iteration costs three
     // near-empty launches).  Adaptive (default): when the previous call's tCG took CG steps.
-    const int la = dpgo::g_tuning[dpgo::TUNE_TCG_LOOKAHEAD];
+    const int la = h->tuning[dpgo::TUNE_TCG_LOOKAHEAD];
     const bool all_ahead = merged && single && full0 && la != 1 && (la == 2 || !h->predict_boundary);
     const bool split = all_ahead && dpgo::merged_split(h);
     if (split) {
@@ -1557,7 +1565,7 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
       }
       // value 2: the second half starts once the first half's first iteration is done, so the two halves run
       // out of phase (one half's HESS_M beside the other's k_tcg_updir) rather than side by side
-      const bool offset = dpgo::g_tuning[dpgo::TUNE_SPLIT_STREAMS] == 2;
+      const bool offset = h->tuning[dpgo::TUNE_SPLIT_STREAMS] == 2;
       const int am = K / 2;
       if (!offset) {
         HIP_TRY(hipEventRecord(h->split_fork, h->stream));
@@ -1725,7 +1733,7 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
 bool dpgo::merged_split(dpgo_hip_problem h) {
   constexpr int kSplitMaxTiles = 4096;
   return h->K >= 2 && h->num_tiles <= kSplitMaxTiles && h->fuse_finalize == 0 &&
-         dpgo::g_tuning[dpgo::TUNE_SPLIT_STREAMS] > 0;
+         h->tuning[dpgo::TUNE_SPLIT_STREAMS] > 0;
 }
 
 int dpgo::eval_sums_dev(dpgo_hip_problem h, const double* X) {

@@ -103,6 +103,7 @@ struct QView {
   const int* sv_ids;
   const int2* inc_sv;
   int fmt;                // QFormat
+  const int* tuning;      // host only: the handle's tuning keys (launch-time variant choice; kernels never read it)
 };
 
 struct OptScalars {
@@ -242,7 +243,7 @@ enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH =
 // variant of the edge-stream SpMM used unless TUNE_EDGE_VARIANT overrides it (bit 0: XCD-aware
 // tile remap; v >> 1: minimum waves per SIMD the register allocation must allow, none/4/5/6)
 constexpr int kEdgeDefaultVariant = 1;
-extern int g_tuning[TUNE_COUNT];
+extern int g_tuning[TUNE_COUNT];  // process defaults, copied into every handle at creation (dpgo_hip_set_tuning)
 
 bool supported_rb(int r, int b);
 hipError_t launch_gather_poses(int count, int rb, const int* idx, const double* A, const double* Bsrc, double* dst,

@@ -3162,32 +3162,32 @@ hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q
   if (q.fmt == QFMT_EDGES) {
     constexpr bool kPreMode = mode_hess(MODE) || MODE == MODE_QF || MODE == MODE_EVAL_TCG;
     if constexpr (mode_hess(MODE)) {
-      if (r == 5 && b == 4 && g_tuning[TUNE_SV_STAGE] > 0 && g_tuning[TUNE_EDGE_VARIANT] < 0 && q.sv_ptr != nullptr) {
+      if (r == 5 && b == 4 && q.tuning[TUNE_SV_STAGE] > 0 && q.tuning[TUNE_EDGE_VARIANT] < 0 && q.sv_ptr != nullptr) {
         k_spmm<5, 4, MODE, kEdgeDefaultVariant | 8 | 32, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
         return hipSuccess;
       }
     }
     if constexpr (mode_merged(MODE)) {
-      const int mp = g_tuning[TUNE_MERGED_PREFETCH];
-      if (r == 5 && b == 4 && g_tuning[TUNE_EPI_PREFETCH] > 0 && g_tuning[TUNE_EDGE_VARIANT] < 0 && mp > 0) {
+      const int mp = q.tuning[TUNE_MERGED_PREFETCH];
+      if (r == 5 && b == 4 && q.tuning[TUNE_EPI_PREFETCH] > 0 && q.tuning[TUNE_EDGE_VARIANT] < 0 && mp > 0) {
         // (measured slower: occupancy 4 -> 3; the 5-wave register budgets measured spill)
         k_spmm<5, 4, MODE, kEdgeDefaultVariant | 8 | 16, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
         return hipSuccess;
       }
     }
     if constexpr (kPreMode) {
-      if (r == 5 && b == 4 && g_tuning[TUNE_EPI_PREFETCH] > 0 && g_tuning[TUNE_EDGE_VARIANT] < 0) {
+      if (r == 5 && b == 4 && q.tuning[TUNE_EPI_PREFETCH] > 0 && q.tuning[TUNE_EDGE_VARIANT] < 0) {
         k_spmm<5, 4, MODE, kEdgeDefaultVariant | 8, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
         return hipSuccess;
       }
     }
-    const int var = g_tuning[TUNE_EDGE_VARIANT] < 0 ? kEdgeDefaultVariant : g_tuning[TUNE_EDGE_VARIANT];
+    const int var = q.tuning[TUNE_EDGE_VARIANT] < 0 ? kEdgeDefaultVariant : q.tuning[TUNE_EDGE_VARIANT];
     if constexpr (MODE == MODE_XQ) {
       if (r == 5 && b == 4 && var != kEdgeDefaultVariant) return spmm_variant54<QFMT_EDGES>(var, grid, c, q, a);
     }
     return spmm_rb<MODE, kEdgeDefaultVariant, QFMT_EDGES>(r, b, grid, c, q, a);
   }
-  const int var = g_tuning[TUNE_SPMM_VARIANT];
+  const int var = q.tuning[TUNE_SPMM_VARIANT];
   if constexpr (MODE == MODE_XQ) {
     if (r == 5 && b == 4 && var != 0) return spmm_variant54<QFMT_BSR>(var, grid, c, q, a);
   }

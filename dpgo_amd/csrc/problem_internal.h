@@ -65,6 +65,7 @@ struct DevBuf {
 
 struct dpgo_hip_problem_s {
   int K = 0, d = 0, r = 0, b = 0;
+  int tuning[dpgo::TUNE_COUNT] = {};  // this handle's tuning keys (the process defaults at creation)
   long N = 0;  // total poses
   std::vector<int> n_agent;
   std::vector<long> pose_off;

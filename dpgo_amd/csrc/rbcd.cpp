@@ -1036,13 +1036,13 @@ int dpgo_rbcd_bytes(dpgo_rbcd e, double* bytes, double* evaltcg_bytes_per_color)
   double total = e->host_bytes;
   // the merged tCG iteration (capi.cpp optimize_dev_status): HESS_M also reads r and Minv; k_tcg_updir
   // replaces the update / direction pair and no z vector is written or read
-  const bool merged = e->P.precon != DPGO_PRECON_EXACT && g_tuning[TUNE_CLASSIC_TCG] == 0 &&
-                      g_tuning[TUNE_FUSE_TCG] <= 0;
-  const double mx = merged ? P + DW : 0.0;  // HESS_M's extra operands per pose
   for (int c = 0; c < e->ncolors; ++c) {
     dpgo_hip_problem h = e->prob[c];
     if (evaltcg_bytes_per_color) evaltcg_bytes_per_color[c] = 0.0;
     if (!h) continue;
+    const bool merged = e->P.precon != DPGO_PRECON_EXACT && h->tuning[TUNE_CLASSIC_TCG] == 0 &&
+                        h->tuning[TUNE_FUSE_TCG] <= 0;
+    const double mx = merged ? P + DW : 0.0;  // HESS_M's extra operands per pose
     std::vector<int> st(static_cast<size_t>(h->K) * kStatsInts);
     DPGO_TRY(dpgo_hip_stats(h, st.data()));
     double calls_all = 0.0;
@@ -1131,6 +1131,13 @@ int dpgo_rbcd_get_trace(dpgo_rbcd e, int agent, double* out, int max_records, in
     for (int q = e->color_off[c]; q < e->color_off[c + 1]; ++q)
       if (e->owned[q] == agent) return dpgo_hip_get_trace(e->prob[c], q - e->color_off[c], out, max_records, count);
   return fail(DPGO_HIP_EINVAL, "agent not owned by this rank");
+}
+
+int dpgo_rbcd_set_tuning(dpgo_rbcd e, int key, int value) {
+  if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
+  for (auto* h : e->prob)
+    if (h) DPGO_TRY(dpgo_hip_problem_set_tuning(h, key, value));
+  return DPGO_HIP_OK;
 }
 
 int dpgo_rbcd_set_kernel_timing(dpgo_rbcd e, int on) {

@@ -87,6 +87,7 @@ _SIGS = [
                                C.POINTER(OptResult)], C.c_int),
     ("dpgo_hip_synchronize", [C.c_void_p], C.c_int),
     ("dpgo_hip_set_tuning", [C.c_int, C.c_int], C.c_int),
+    ("dpgo_hip_problem_set_tuning", [C.c_void_p, C.c_int, C.c_int], C.c_int),
     ("dpgo_hip_spmm_bytes", [C.c_void_p], C.c_double),
     ("dpgo_hip_bench_spmm", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, _dp], C.c_int),
     ("dpgo_hip_spmm_bytes_bsr", [C.c_void_p], C.c_double),
@@ -162,6 +163,8 @@ def rccl_unique_id() -> bytes:
 
 
 def set_tuning(key: int, value: int):
+    """Process default of a tuning key: handles created afterwards copy it (Problem / Rbcd.set_tuning change
+    an existing one)."""
     _check(lib().dpgo_hip_set_tuning(int(key), int(value)))
 
 
@@ -383,6 +386,10 @@ class Problem:
         _check(lib().dpgo_hip_set_trace(self.h, int(capacity)))
         self._trace_cap = int(capacity)
 
+    def set_tuning(self, key, value):
+        """A tuning key on this handle only (dpgo_hip_problem_set_tuning)."""
+        _check(lib().dpgo_hip_problem_set_tuning(self.h, int(key), int(value)))
+
     def get_trace(self, agent=0):
         """Per-iteration records of one agent: list of dicts (TRACE_FIELDS)."""
         cap = getattr(self, "_trace_cap", 0)
@@ -485,6 +492,7 @@ _SIGS2 = [
     ("dpgo_rbcd_comm_attach", [C.c_void_p, C.c_void_p], C.c_int),
     ("dpgo_rbcd_exchange", [C.c_void_p, C.POINTER(C.c_void_p)], C.c_int),
     ("dpgo_rbcd_set_kernel_timing", [C.c_void_p, C.c_int], C.c_int),
+    ("dpgo_rbcd_set_tuning", [C.c_void_p, C.c_int, C.c_int], C.c_int),
     ("dpgo_rbcd_set_trace", [C.c_void_p, C.c_int], C.c_int),
     ("dpgo_rbcd_get_trace", [C.c_void_p, C.c_int, _dp, C.c_int, _ip], C.c_int),
     ("dpgo_rbcd_kernel_times", [C.c_void_p, _dp, _lp], C.c_int),
@@ -857,6 +865,10 @@ class Rbcd:
 
     def set_kernel_timing(self, on):
         _check(lib().dpgo_rbcd_set_kernel_timing(self.h, int(on)))  # 0 off, k: every k-th launch per mode
+
+    def set_tuning(self, key, value):
+        """A tuning key on this engine's colour problems (A/B timing without rebuilding the engine)."""
+        _check(lib().dpgo_rbcd_set_tuning(self.h, int(key), int(value)))
 
     def kernel_times(self):
         """{mode: (ms summed, launches)} of the timed in-step X.Q launches since the last call."""

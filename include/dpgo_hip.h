@@ -232,9 +232,13 @@ int dpgo_hip_certify(dpgo_hip_problem h, const double* X, int max_iters, double 
  * 1 each-edge-once pass, 2 full pass).  key 5: 1 = the classic five-launch tCG iteration instead of the
  * merged one.  key 6: 1 = HESS_M operands prefetched.  key 7: tCG queueing (0 adaptive, 1 one iteration
  * ahead, 2 all at once).  key 8: 1 = second-visit record staging (set before Q).  key 9: 1 = the agent
- * status by its own pass instead of folded into the rho test.  key 10: 1 = the exact preconditioner
- * level by level (no chained levels).  DESIGN.md records each key's measurement. */
+ * status by its own pass instead of folded into the rho test.  key 10: merged tCG iterations of a small
+ * batch (<= 4,096 tiles) in two agent halves on two streams (1, default; 0 off; 2 the halves out of phase).
+ * DESIGN.md records each key's measurement.  These are the process DEFAULTS: a handle copies them when it is
+ * created, so handles created afterwards follow; dpgo_hip_problem_set_tuning changes one existing handle. */
 int dpgo_hip_set_tuning(int key, int value);
+/* The same keys on one existing handle (A/B timing of variants on one problem without rebuilding it). */
+int dpgo_hip_problem_set_tuning(dpgo_hip_problem h, int key, int value);
 /* Algorithmic HBM bytes of one X.Q SpMM over this handle: BSR blocks + indices + X + Y, or, for
  * an edge-stream Q, every edge record once + 8 B per incidence + pointers + X + Y. */
 double dpgo_hip_spmm_bytes(dpgo_hip_problem h);

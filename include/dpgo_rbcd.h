@@ -225,6 +225,8 @@ int dpgo_rbcd_mode_bytes(dpgo_rbcd e, int color, double* out);
  * dpgo_rbcd_kernel_times synchronises and returns, per SpMM mode (DPGO_SPMM_MODES entries, order above), the
  * summed milliseconds and launch counts of the timed launches since the last call. */
 int dpgo_rbcd_set_kernel_timing(dpgo_rbcd e, int period);
+/* dpgo_hip_problem_set_tuning on every colour problem of the engine (A/B timing on one engine). */
+int dpgo_rbcd_set_tuning(dpgo_rbcd e, int key, int value);
 /* Per-iteration RTR / tCG trace of every owned agent's updates (dpgo_hip_set_trace / _get_trace
  * records, per agent at its global index). */
 int dpgo_rbcd_set_trace(dpgo_rbcd e, int capacity);

@@ -30,10 +30,10 @@ def main():
     res = {v: [] for v in variants}
     for rnd in range(args.rounds):
         for v in variants:
-            H.set_tuning(key, v)
+            eng.set_tuning(key, v)
             b, ms = eng.bench_spmm(0, args.reps)
             res[v].append(ms)
-    H.set_tuning(key, -1 if key == 1 else 0)
+    eng.set_tuning(key, -1 if key == 1 else 0)
     out = {}
     for v in variants:
         t = np.array(res[v])

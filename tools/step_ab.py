@@ -54,7 +54,7 @@ def main():
         fin = {}
         for rnd in range(a.rounds):
             for v in a.values:
-                H.set_tuning(a.key, v)
+                eng.set_tuning(a.key, v)
                 eng.set_X(Xb)
                 step()
                 torch.cuda.synchronize()
