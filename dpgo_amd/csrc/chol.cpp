@@ -262,7 +262,13 @@ int supernodal_cholesky(int n, int b, const std::vector<int>& rowptr, const std:
       for (int u : nodes[c].R) add(u);
     std::sort(R.begin(), R.end(), [&](int p, int q) { return elim[p] < elim[q]; });
     nd.R = std::move(R);
-    total += sn_panel_tiles(static_cast<int>(nd.S.size()) * b, static_cast<int>(nd.R.size()) * b) * kSnTile * kSnTile;
+    const long node_doubles =
+        sn_panel_tiles(static_cast<int>(nd.S.size()) * b, static_cast<int>(nd.R.size()) * b) * kSnTile * kSnTile;
+    if (node_doubles * 8 >= (1L << 32)) {  // the solves address a node's panel with 32-bit buffer offsets
+      err = "exact preconditioner: one supernode's panel would exceed 4 GiB (use DPGO_PRECON_BLOCK_JACOBI)";
+      return -1;
+    }
+    total += node_doubles;
     if (total > max_doubles) {
       err = "exact preconditioner: the supernodal factor panels of Q + 0.1 I would exceed " +
             std::to_string(max_doubles / (1L << 27)) + " GiB (use DPGO_PRECON_BLOCK_JACOBI for this size)";

@@ -2723,12 +2723,31 @@ __device__ __forceinline__ long sn_tile_dev(int ns, int I, int J) {
                 : static_cast<long>(ns) * (ns + 1) / 2 + static_cast<long>(I - ns) * ns + J;
 }
 
-// rows 4 rq .. 4 rq + 3, columns 4 cq .. 4 cq + 3 of a tile
+// Rows 4 rq .. 4 rq + 3, columns 4 cq .. 4 cq + 3 of a tile (plain loads: k_sn_bwd's two-deep pipeline, which
+// measured faster than the three-deep buffer-load one there: 226 vs 253 us per level launch at C5)
 __device__ __forceinline__ void sn_load_tile(const double* __restrict__ tile, int rq, int cq, double (&p)[4][4]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const f64x2* src = reinterpret_cast<const f64x2*>(tile + (rq * 4 + i) * kSnTileDev + cq * 4);
     const f64x2 a = src[0], c = src[1];
+    p[i][0] = a.x;
+    p[i][1] = a.y;
+    p[i][2] = c.x;
+    p[i][3] = c.y;
+  }
+}
+
+// Rows 4 rq .. 4 rq + 3, columns 4 cq .. 4 cq + 3 of a panel tile, by raw buffer loads (byte offset of the
+// tile < 4 GiB: a node's panel is checked
+// on the host): intrinsic loads stay where the software pipeline issues them (plain loads of a loop-carried
+// register set are folded into one load of a phi of the addresses at the point of use)
+__device__ __forceinline__ void sn_load_tile_buf(__amdgpu_buffer_rsrc_t r, unsigned tile_byte, int rq, int cq,
+                                                 double (&p)[4][4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const unsigned o = tile_byte + 8u * static_cast<unsigned>((rq * 4 + i) * kSnTileDev + cq * 4);
+    const f64x2 a = __builtin_bit_cast(f64x2, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0));
+    const f64x2 c = __builtin_bit_cast(f64x2, __builtin_amdgcn_raw_buffer_load_b128(r, o + 16u, 0, 0));
     p[i][0] = a.x;
     p[i][1] = a.y;
     p[i][2] = c.x;
@@ -2780,7 +2799,7 @@ constexpr int kSnVecRegs = (kSnTileDev * 8 + kThreads - 1) / kThreads;  // enoug
 template <int R>
 __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __restrict__ items, int b,
                                                      double* __restrict__ y) {
-  __shared__ double sf[2][kSnTileDev * R];  // double-buffered frontal chunks
+  __shared__ double sf[3][kSnTileDev * R];  // triple-buffered frontal chunks
   const int2 it = items[blockIdx.x];
   const int node = it.x, I = it.y;
   const int s = v.s[node], t = v.t[node], sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), ns = Sp / kSnTileDev;
@@ -2794,9 +2813,9 @@ __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __res
     for (int a = 0; a < R; ++a) acc[i][a] = 0.0;
   const int nJ = I < ns ? I + 1 : ns;
   constexpr int kTileD = kSnTileDev * kSnTileDev, kChunk = kSnTileDev * R;
-  // software pipeline: tile J + 1's panel values and frontal chunk are loaded into registers while tile J
-  // is consumed; the chunk then goes to the other LDS buffer (one barrier per tile)
-  double p[4][4], pn[4][4], fv[kSnVecRegs];
+  // software pipeline: tiles J + 1 and J + 2's panel values are loaded into registers and their frontal chunks
+  // staged in LDS while tile J is consumed (one barrier per tile)
+  double p[4][4], pn[4][4], pm[4][4], fv[kSnVecRegs];
   auto load_chunk = [&](int J) {
 #pragma unroll
     for (int i = 0; i < kSnVecRegs; ++i) {
@@ -2811,19 +2830,8 @@ __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __res
       if (e < kChunk) sf[buf][e] = fv[i];
     }
   };
-  if (nJ > 0) {
-    sn_load_tile(panel + sn_tile_dev(ns, I, 0) * kTileD, rq, cq, p);
-    load_chunk(0);
-    store_chunk(0);
-  }
-  __syncthreads();
-  for (int J = 0; J < nJ; ++J) {
-    const bool more = J + 1 < nJ;
-    if (more) {
-      sn_load_tile(panel + sn_tile_dev(ns, I, J + 1) * kTileD, rq, cq, pn);
-      load_chunk(J + 1);
-    }
-    const double* cf = sf[J & 1];
+  auto consume = [&](const double (&pt)[4][4], int buf) {
+    const double* cf = sf[buf];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       double fc[R];
@@ -2832,14 +2840,39 @@ __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __res
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int a = 0; a < R; ++a) acc[i][a] = fma(p[i][c], fc[a], acc[i][a]);
+        for (int a = 0; a < R; ++a) acc[i][a] = fma(pt[i][c], fc[a], acc[i][a]);
     }
-    if (more) store_chunk((J + 1) & 1);
-    __syncthreads();  // chunk J + 1 visible; every read of chunk J - 1's buffer (rewritten next) done
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) p[i][c] = pn[i][c];
+  };
+  const __amdgpu_buffer_rsrc_t rp = buf_rsrc(panel);
+  auto tile = [&](int J) { return 8u * static_cast<unsigned>(sn_tile_dev(ns, I, J) * kTileD); };
+  // Sub-step J: store chunk J + 1 (loaded one sub-step earlier; its wait is for loads issued before tile J + 1's),
+  // issue chunk J + 2 and tile J + 2, consume tile J: tiles J + 1 and J + 2 stay in flight while tile J is
+  // consumed.  Three register sets (tile J in set J % 3), chunk J in LDS buffer J % 3, one barrier per tile.
+  if (nJ > 0) {
+    load_chunk(0);
+    sn_load_tile_buf(rp, tile(0), rq, cq, p);
+    store_chunk(0);
+  }
+  if (nJ > 1) {
+    load_chunk(1);
+    sn_load_tile_buf(rp, tile(1), rq, cq, pn);
+  }
+  __syncthreads();
+  auto sub_step = [&](int J, const double (&pc)[4][4], double (&pnext)[4][4], int bc, int b1) {
+    if (J + 1 < nJ) store_chunk(b1);
+    if (J + 2 < nJ) {
+      load_chunk(J + 2);
+      sn_load_tile_buf(rp, tile(J + 2), rq, cq, pnext);
+    }
+    consume(pc, bc);
+    __syncthreads();  // chunk J + 1 visible; every read of buffer bc done before chunk J + 3 lands there
+  };
+  for (int J = 0; J < nJ; J += 3) {
+    sub_step(J, p, pm, 0, 1);
+    if (J + 1 >= nJ) break;
+    sub_step(J + 1, pn, p, 1, 2);
+    if (J + 2 >= nJ) break;
+    sub_step(J + 2, pm, pn, 2, 0);
   }
   // sum over the 16 column groups (lanes cq = 0..15 of a 16-lane group, fixed order)
 #pragma unroll
