@@ -1529,11 +1529,14 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
       // double-double partials (exact products, compensated sums): the stopping test combines them as
       // polynomials in alpha whose terms cancel by the residual drop (merged_stop_test)
       // |r_j|^2 and <z_j, r_j> only when no k_tcg_updir left them (args.rz_own: the first iteration)
-      DotAcc rr_, rh_, hh_, zr_, zh_;
+      // <r, Hd> enters only |r'|^2, i.e. the stopping test, whose bar is relative to |r_0| (a plain sum is exact
+      // enough there); <z', r'> (beta, which steers the next direction) keeps every term exact
+      DotAcc rr_, hh_, zr_, zh_;
+      double rh_p = 0.0;
       const bool rz = mode_snap(MODE) || args.rz_own != 0;  // (the first iteration's kernel: always)
 #pragma unroll
       for (int a = 0; a < R; ++a) {
-        rh_.add(rcol[a], hc[a]);
+        rh_p = fma(rcol[a], hc[a], rh_p);
         hh_.add(hc[a], hc[a]);
         zh_.add(zc[a], hc[a]);
       }
@@ -1544,7 +1547,7 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
           zr_.add(zc[a], rcol[a]);
         }
       }
-      const dd rr = rr_.val(), rh = rh_.val(), hh = hh_.val(), zr = zr_.val(), zh = zh_.val();
+      const dd rr = rr_.val(), rh{rh_p, 0.0}, hh = hh_.val(), zr = zr_.val(), zh = zh_.val();
       dd mh{0.0, 0.0};
       if (args.pmode == PRECON_NONE) {
         mh = hh;
