@@ -593,6 +593,10 @@ int sync_chol(dpgo_hip_problem h) {
   DPGO_TRY(up(h->sn_cpos, cpos));
   DPGO_TRY(up(h->sn_contrib, contrib));
   DPGO_TRY(up(h->sn_items, items));
+  std::vector<int> node_agent(base[K]);
+  for (int a = 0; a < K; ++a)
+    for (int g = base[a]; g < base[a + 1]; ++g) node_agent[g] = a;
+  DPGO_TRY(up(h->sn_node_agent, node_agent));
   HIP_TRY(h->sn_F.ensure(std::max<long>(fo, 1)));
   HIP_TRY(h->sn_U.ensure(std::max<long>(uo, 1)));
   h->chol_doubles = po;
@@ -603,7 +607,8 @@ int sync_chol(dpgo_hip_problem h) {
 // z = P_X(in (Q + 0.1 I)^-1) for every agent (QuadraticProblem::PreConditioner, :75-87): the forward sweep
 // up the supernodal trees into tA, the backward sweep down into tB (one launch per level and kernel), then
 // projection + partials <z, rref>, |rref|^2 (pass rref = in).  With a failed factorisation z = in,
-// unprojected, as the reference.
+// unprojected, as the reference.  Agents that `flag` skips (k_precond_finish leaves their z untouched) are skipped
+// by the sweeps too: a tCG iteration streams only the panels of the agents still in tCG.
 int exact_precond(dpgo_hip_problem h, const double* in, double* z_out, double* delta_out, const double* X,
                   const double* rref, double* partials, int flag) {
   DPGO_TRY(sync_chol(h));
@@ -611,7 +616,7 @@ int exact_precond(dpgo_hip_problem h, const double* in, double* z_out, double* d
   if (h->chol_state == 1) {
     const dpgo::SnView v{h->sn_panel.p, h->sn_panel_off.p, h->sn_s.p,    h->sn_t.p,    h->sn_poses_off.p,
                          h->sn_poses.p, h->sn_f_off.p,     h->sn_u_off.p, h->sn_cpos_off.p, h->sn_cpos.p,
-                         h->sn_contrib.p, h->sn_F.p,       h->sn_U.p};
+                         h->sn_contrib.p, h->sn_F.p,       h->sn_U.p,    h->sn_node_agent.p, h->state.p, flag};
     const int2* it = h->sn_items.p;
     const int nl = static_cast<int>(h->sn_levels.size());
     for (int l = nl - 1; l >= 0; --l) {

@@ -202,6 +202,11 @@ struct SnView {
   const int2* contrib;    // per frontal position: (child node, index in the child's R), children in order
   double* F;
   double* U;
+  // per-agent skip (the flag of the launch that consumes the sweep, k_precond_finish): a supernode's workgroups
+  // exit when its agent's flag says so, so stopped agents cost no panel traffic
+  const int* node_agent = nullptr;  // [nodes] batch agent of the node
+  const AgentState* state = nullptr;
+  int flag_kind = 0;
 };
 
 // Loop closures one engine colour class reweights (PGOAgent::updateLoopClosuresWeights,

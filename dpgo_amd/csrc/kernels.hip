@@ -17,19 +17,22 @@
 
 namespace dpgo {
 
-__device__ __forceinline__ bool tile_skipped(const LaunchCtx& c, int agent) {
-  if (c.flag_kind == FLAG_NONE || c.state == nullptr) return false;
-  const AgentState& s = c.state[agent];
-  if (c.flag_kind == FLAG_RUN) return s.run_active == 0;
-  if (c.flag_kind == FLAG_TCG) return s.tcg_active == 0;
-  if (c.flag_kind == FLAG_TCG_MODE) return s.tcg_mode == 2;
-  if (c.flag_kind == FLAG_MOVED) return s.runs > 0 && s.accepted && !s.gave_up;
-  if (c.flag_kind == FLAG_TCG_CG) return s.tcg_mode != 0;
-  if (c.flag_kind == FLAG_RUN_IMPL) return s.run_active == 0 || s.eta_implicit == 0;
-  if (c.flag_kind == FLAG_RUN_EXPL) return s.run_active == 0 || s.eta_implicit != 0;
-  if (c.flag_kind == FLAG_DECIDED)  // accepted / gave up in Run `round`, or never ran (round 0)
-    return !(s.run_active == 0 && (s.runs == c.round + 1 || (c.round == 0 && s.runs == 0)));
+__device__ __forceinline__ bool agent_skipped(const AgentState* state, int flag_kind, int round, int agent) {
+  if (flag_kind == FLAG_NONE || state == nullptr) return false;
+  const AgentState& s = state[agent];
+  if (flag_kind == FLAG_RUN) return s.run_active == 0;
+  if (flag_kind == FLAG_TCG) return s.tcg_active == 0;
+  if (flag_kind == FLAG_TCG_MODE) return s.tcg_mode == 2;
+  if (flag_kind == FLAG_MOVED) return s.runs > 0 && s.accepted && !s.gave_up;
+  if (flag_kind == FLAG_TCG_CG) return s.tcg_mode != 0;
+  if (flag_kind == FLAG_RUN_IMPL) return s.run_active == 0 || s.eta_implicit == 0;
+  if (flag_kind == FLAG_RUN_EXPL) return s.run_active == 0 || s.eta_implicit != 0;
+  if (flag_kind == FLAG_DECIDED)  // accepted / gave up in Run `round`, or never ran (round 0)
+    return !(s.run_active == 0 && (s.runs == round + 1 || (round == 0 && s.runs == 0)));
   return false;
+}
+__device__ __forceinline__ bool tile_skipped(const LaunchCtx& c, int agent) {
+  return agent_skipped(c.state, c.flag_kind, c.round, agent);
 }
 
 template <int R, int B>
@@ -2762,6 +2765,7 @@ template <int R>
 __global__ __launch_bounds__(kThreads) void k_sn_assemble(SnView v, const int2* __restrict__ items, int b,
                                                           const double* __restrict__ rhs) {
   const int2 it = items[blockIdx.x];
+  if (v.node_agent && agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x])) return;
   const int node = it.x, row = it.y * kThreads + static_cast<int>(threadIdx.x);
   const int s = v.s[node], t = v.t[node], sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), Rp = sn_pad_dev(tb);
   if (row >= Sp + Rp) return;
@@ -2804,6 +2808,7 @@ __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __res
                                                      double* __restrict__ y) {
   __shared__ double sf[3][kSnTileDev * R];  // triple-buffered frontal chunks
   const int2 it = items[blockIdx.x];
+  if (v.node_agent && agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x])) return;
   const int node = it.x, I = it.y;
   const int s = v.s[node], t = v.t[node], sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), ns = Sp / kSnTileDev;
   const double* __restrict__ f = v.F + v.f_off[node];
@@ -2911,6 +2916,7 @@ __global__ __launch_bounds__(kThreads) void k_sn_bwd(SnView v, const int2* __res
   __shared__ double sg[2][kSnTileDev * R];  // double-buffered [y_S ; -x_R] chunks
   __shared__ double red[kThreads / 64][16][4 * R];
   const int2 it = items[blockIdx.x];
+  if (v.node_agent && agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x])) return;
   const int node = it.x, J = it.y;
   const int s = v.s[node], t = v.t[node], sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), Rp = sn_pad_dev(tb);
   const int ns = Sp / kSnTileDev, nI = (Sp + Rp) / kSnTileDev;

@@ -117,6 +117,7 @@ struct dpgo_hip_problem_s {
   dpgo::DevBuf<long> sn_panel_off, sn_f_off, sn_u_off;
   dpgo::DevBuf<int> sn_s, sn_t, sn_poses_off, sn_poses, sn_cpos_off, sn_cpos;
   dpgo::DevBuf<int2> sn_contrib, sn_items;
+  dpgo::DevBuf<int> sn_node_agent;  // [nodes] batch agent of each supernode (per-agent skip in the sweeps)
   struct SnLevel {  // item ranges into sn_items of one tree depth
     int asm0 = 0, asm_n = 0, fwd0 = 0, fwd_n = 0, bwd0 = 0, bwd_n = 0;
   };
