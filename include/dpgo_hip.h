@@ -231,7 +231,7 @@ int dpgo_hip_certify(dpgo_hip_problem h, const double* X, int max_iters, double 
  * key 3: consumer-side tCG finalize (classic sequence).  key 4: first tCG step kind (0 predicted,
  * 1 each-edge-once pass, 2 full pass).  key 5: 1 = the classic five-launch tCG iteration instead of the
  * merged one.  key 6: 1 = HESS_M operands prefetched.  key 7: tCG queueing (0 adaptive, 1 one iteration
- * ahead, 2 all at once).  key 8: 1 = second-visit record staging (set before Q).  key 9: 1 = the agent
+ * ahead, 2 all at once; the classic sequence of the exact preconditioner queues all at once only with 2).  key 8: 1 = second-visit record staging (set before Q).  key 9: 1 = the agent
  * status by its own pass instead of folded into the rho test.  key 10: merged tCG iterations of a small
  * batch (<= 4,096 tiles) in two agent halves on two streams (1, default; 0 off; 2 the halves out of phase).
  * DESIGN.md records each key's measurement.  These are the process DEFAULTS: a handle copies them when it is

@@ -131,3 +131,36 @@ def test_single_agent_local_pgo(hip, name):
     assert abs(rh["gradNormOpt"] - res["gradNormOpt"]) <= 1e-9 * max(abs(res["gradNormOpt"]), 1e-12) + 1e-12
     assert rh["outer_iters"] == len(trace)
     assert rh["tCGStatus"] == res["tCGStatus"]
+
+
+def test_exact_lookahead_bitwise(hip):
+    """The classic tCG sequence of the exact preconditioner queued one iteration ahead of a published status
+    (tuning key TUNE_TCG_LOOKAHEAD = 1) or every iteration at once (2; 0 = adaptive): agents that stopped skip
+    their tiles and their supernodes, so the iterates, counters and per-iteration traces are bitwise the same."""
+    g = hip.Graph.grid3d(10, seed=3)
+    aop = g.grid_partition(2)
+    X0, _, _ = g.distributed_init(aop, 5, hip.lifting_matrix(3, 5), gpu=True, rtol=1e-12, dev_layout=True)
+    out = []
+    for la in (1, 2, 0):
+        hip.set_tuning(7, la)
+        try:
+            e = hip.Rbcd(g, aop, np.zeros(8, np.int32), 0, 1,
+                         hip.rbcd_params(r=5, acceleration=1, precon=hip.PRECON_EXACT))
+            e.set_trace(512)
+            e.set_X(X0)
+            for it in range(24):
+                e.pre_exchange(it % e.num_colors)
+                e.update(it % e.num_colors, None)
+            X = np.zeros(X0.size)
+            e.get_X_into(X)
+            out.append((X, e.stats().copy(), [e.get_trace(a) for a in range(8)]))
+        finally:
+            hip.set_tuning(7, 0)
+    for o in out[1:]:
+        assert np.array_equal(out[0][0], o[0])
+        assert np.array_equal(out[0][1][:, :12], o[1][:, :12])
+        for a in range(8):
+            assert len(out[0][2][a]) == len(o[2][a])
+            for x, y in zip(out[0][2][a], o[2][a]):
+                assert x == y
+    assert out[0][1][:, 10].sum() > 0  # CG steps were taken

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--burnin", type=int, default=300)
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--agents-per-axis", type=int, default=4)
+    ap.add_argument("--precon", default="block_jacobi", choices=["block_jacobi", "exact"])
     a = ap.parse_args()
     import torch
     from dpgo_amd import hip as H
@@ -32,7 +33,8 @@ def main():
     g = H.Graph.grid3d(a.k, seed=0)
     A = a.agents_per_axis
     aop = g.grid_partition(A)
-    eng = H.Rbcd(g, aop, np.zeros(A ** 3, np.int32), 0, 1, H.rbcd_params(r=5, acceleration=1))
+    eng = H.Rbcd(g, aop, np.zeros(A ** 3, np.int32), 0, 1, H.rbcd_params(
+        r=5, acceleration=1, precon=H.PRECON_EXACT if a.precon == "exact" else H.PRECON_BLOCK_JACOBI))
     s = torch.cuda.Stream(dev)
     eng.set_stream(s.cuda_stream)
     X0, _, _ = g.distributed_init(aop, 5, H.lifting_matrix(3, 5), gpu=True, rtol=1e-12, max_iters=50000,
