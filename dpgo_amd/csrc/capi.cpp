@@ -1183,6 +1183,12 @@ int dpgo_hip_set_tuning(int key, int value) {
   return DPGO_HIP_OK;
 }
 
+int dpgo_hip_get_tuning(int key, int* value) {
+  if (key < 0 || key >= dpgo::TUNE_COUNT || !value) return fail(DPGO_HIP_EINVAL, "bad tuning key");
+  *value = dpgo::g_tuning[key];
+  return DPGO_HIP_OK;
+}
+
 int dpgo_hip_problem_set_tuning(dpgo_hip_problem h, int key, int value) {
   DPGO_TRY(check_handle(h));
   if (key < 0 || key >= dpgo::TUNE_COUNT) return fail(DPGO_HIP_EINVAL, "bad tuning key");
@@ -1476,7 +1482,7 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
       dpgo::FinalizeArgs fin = make_fin(h, op, h->pa.p, 7, nullptr, 0, &os, nullptr, publish ? 1 : 0, tag);
       fin.pc = h->peh.p;
       fin.nq_c = 1;
-      fin.dd_mask = 0x7E;  // |r|^2 .. <Minv Hd, Hd> are double-double partials (k_spmm MODE_HESS_M)
+      fin.dd_mask = dpgo::merged_dd_mask(h->fmt, h->tuning);  // which merged partials are double-double
       fin.rz_pc = rz_pc ? 1 : 0;
       DPGO_TRY(spmm_then_finalize(h, mode, ch, sa, fin));
       auto cu = make_ctx(h, dpgo::FLAG_TCG_MODE, h->peh.p);
@@ -1538,7 +1544,7 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
       dpgo::FinalizeArgs fin = make_fin(h, op, h->pa.p, 7, nullptr, 0, &os, nullptr, 0, 0);
       fin.pc = h->peh.p;
       fin.nq_c = 1;
-      fin.dd_mask = 0x7E;
+      fin.dd_mask = dpgo::merged_dd_mask(h->fmt, h->tuning);
       fin.rz_pc = rz_pc ? 1 : 0;
       fin.agent_tile_off += a0;  // tile offsets stay global: the partial slots are the unsplit ones
       fin.agent_num_poses += a0;

@@ -120,28 +120,35 @@ __device__ __forceinline__ double wave_sum(double v) {
 // ---- double-double (hi + lo, |lo| <= ulp(hi) / 2): exact products and compensated sums for the merged
 // tCG iteration's one-step polynomials, whose terms cancel by the tCG's residual drop (kernels.hip,
 // merged_stop_test).  Error-free transformations: two_sum (Knuth), two_prod (FMA).  Nothing here may be
-// reassociated; hipcc does not (no fast-math) and contraction cannot touch the add-only sequences.
+// reassociated (hipcc does not: no fast-math).  FP contraction is off in these bodies: hipcc contracts a * b + c into an FMA by default, and inside an
+// error-free transformation that silently changes what the low part measures (a product contracted into
+// two_sum's sum and again into its error term counts the product's rounding error twice).
 struct dd {
   double hi, lo;
 };
 __device__ __forceinline__ dd dd_fast2(double a, double b) {  // |a| >= |b|
+#pragma clang fp contract(off)
   const double s = a + b;
   return {s, b - (s - a)};
 }
 __device__ __forceinline__ dd dd_two_sum(double a, double b) {
+#pragma clang fp contract(off)
   const double s = a + b, bb = s - a;
   return {s, (a - (s - bb)) + (b - bb)};
 }
 __device__ __forceinline__ dd dd_add(dd x, dd y) {
+#pragma clang fp contract(off)
   const dd s = dd_two_sum(x.hi, y.hi);
   return dd_fast2(s.hi, s.lo + (x.lo + y.lo));
 }
 // x + a b with the product exact
 __device__ __forceinline__ dd dd_fma(dd x, double a, double b) {
+#pragma clang fp contract(off)
   const double p = a * b;
   return dd_add(x, {p, __builtin_fma(a, b, -p)});
 }
 __device__ __forceinline__ dd dd_mul_d(dd x, double a) {
+#pragma clang fp contract(off)
   const double p = x.hi * a;
   return dd_fast2(p, __builtin_fma(x.hi, a, -p) + x.lo * a);
 }
@@ -171,6 +178,20 @@ __device__ __forceinline__ void quad_reduce_scatter(const double (&acc)[R][B], i
     const double hA = (odd ? c1 : c0) + dpp_f64<0xB1>(odd ? c0 : c1);
     const double hB = (odd ? c3 : c2) + dpp_f64<0xB1>(odd ? c2 : c3);
     col[a] = (hi ? hB : hA) + dpp_f64<0x4E>(hi ? hA : hB);
+  }
+}
+
+// The same reduce-scatter for an XOR-rotated accumulator (b = 4): lane k keeps column s ^ k of its partial
+// sums in slot s, so the partner k ^ x holds column k in slot x and no lane has to select which column
+// to send: col = (slot 0 + (k^1)'s slot 1) + (k^2)'s (slot 2 + (k^3)'s slot 3).  Those are qsum's pairs in
+// qsum's order, so the result is bitwise quad_reduce_scatter's on the unrotated accumulator.
+template <int R>
+__device__ __forceinline__ void quad_reduce_scatter_rot(const double (&acc)[R][4], double (&col)[R]) {
+#pragma unroll
+  for (int a = 0; a < R; ++a) {
+    const double lo = acc[a][0] + dpp_f64<0xB1>(acc[a][1]);
+    const double hi = acc[a][2] + dpp_f64<0xB1>(acc[a][3]);
+    col[a] = lo + dpp_f64<0x4E>(hi);
   }
 }
 

@@ -24,6 +24,17 @@ __host__ __device__ constexpr bool mode_hess(int m) {
   return m == MODE_HESS || m == MODE_HESS_QF || m == MODE_HESS_M || m == MODE_HESS_QF_M;
 }
 __host__ __device__ constexpr bool mode_snap(int m) { return m == MODE_HESS_QF || m == MODE_HESS_QF_M; }
+// Precision of the merged tCG partials (pa slots of MODE_HESS_M / MODE_HESS_QF_M, FinalizeArgs::dd_mask): bit s set
+// = slot s is double-double.  kMergedDdSlotsV1 is the round-3 epilogue's (every quantity but d_Hd).  The v2
+// epilogue (edge variant bit 6) keeps double-double where a sum cancels across poses and feeds beta: |r_0|^2
+// and <z_0, r_0> (slots 1, 4: first iteration) always, the others as DPGO_MERGED_DD_SLOTS says -- <r,Hd> (2),
+// |Hd|^2 (3), 2<z,Hd> (5), <Minv Hd,Hd> (6).  The default is the one test_rtr_trace_extended_precision and
+// tools/trace_precision.py chose.
+#ifndef DPGO_MERGED_DD_SLOTS
+#define DPGO_MERGED_DD_SLOTS 0x20
+#endif
+constexpr int kMergedDdSlotsV1 = 0x7E;
+constexpr int kMergedDdSlots = 0x12 | (DPGO_MERGED_DD_SLOTS & 0x6C);
 // Per-agent tile gating: RUN skips agents out of the RTR Run, TCG those whose tCG stopped, TCG_MODE
 // those with no tCG step pending, MOVED those whose single-Run candidate was accepted.
 enum FlagKind { FLAG_NONE = 0, FLAG_RUN = 1, FLAG_TCG = 2, FLAG_TCG_MODE = 3, FLAG_MOVED = 4, FLAG_TCG_CG = 5,
@@ -244,7 +255,14 @@ enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH =
                                          // streams (one half's VALU-bound HESS_M beside the other's HBM-bound
                                          // k_tcg_updir); 0 off, 1 on (default: 1M -0.7 %, the 125 k
                                          // share -4.6 % ms/step), 2 the halves out of phase (no gain)
+               TUNE_SPMM_V2 = 11,  // > 0: the merged partials at kMergedDdSlots (edge variant bit 6) and the rotated
+                                   //    accumulator (bit 7) in every mode (1), in none (2), in the merged modes (3);
+                                   //    0: the round-3 kernels
                TUNE_COUNT = 12 };
+// dd_mask of the merged tCG partials for the kernel a handle with these tuning keys and Q format runs
+inline int merged_dd_mask(int fmt, const int* tuning) {
+  return fmt == QFMT_EDGES && tuning[TUNE_SPMM_V2] > 0 ? kMergedDdSlots : kMergedDdSlotsV1;
+}
 // variant of the edge-stream SpMM used unless TUNE_EDGE_VARIANT overrides it (bit 0: XCD-aware
 // tile remap; v >> 1: minimum waves per SIMD the register allocation must allow, none/4/5/6)
 constexpr int kEdgeDefaultVariant = 1;

@@ -172,6 +172,53 @@ __device__ __forceinline__ void block_partials_dd_lds(double v0, dd (&v)[ND], Dd
   if (threadIdx.x == 0) put(0, ((red0[0] + red0[1]) + red0[2]) + red0[3]);
 }
 
+// One plain partial v0 (block_partials' path and order, bitwise what the single-quantity passes write to slot 0)
+// and NQ further quantities v[i] to slot sl[i], double-double where isdd[i] (low part kDdLo slots later), plain
+// otherwise (v[i].lo ignored).  Every lane's values go through `scratch` (the SpMM's record stage, dead after the
+// edge loop) and wave w reduces items w, w + 4, ...: one quantity per wave, each in its own arithmetic (a plain
+// quantity costs a plain wave sum, not a double-double one).  Callers list the double-double items first so
+// they land on different waves.  Fixed order throughout, so the totals are reproducible.
+template <int NQ>
+__device__ __forceinline__ void block_partials_mixed(double v0, const dd (&v)[NQ], const int (&sl)[NQ],
+                                                     const bool (&isdd)[NQ], double* __restrict__ partials, int tile,
+                                                     bool coherent, double* scratch) {
+  __shared__ double red0[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v0 = wave_sum(v0);
+  __syncthreads();  // every wave is past its edge loop: the record stage is free
+  if (lane == 0) red0[wave] = v0;
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    scratch[(2 * i) * kThreads + threadIdx.x] = v[i].hi;
+    if (isdd[i]) scratch[(2 * i + 1) * kThreads + threadIdx.x] = v[i].lo;
+  }
+  __syncthreads();
+  auto put = [&](int s, double t) {
+    if (coherent)
+      __hip_atomic_store(&partials[tile * kPartialStride + s], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      partials[tile * kPartialStride + s] = t;
+  };
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    if (wave != (i & 3)) continue;  // wave-uniform
+    const double* hi = scratch + (2 * i) * kThreads;
+    if (isdd[i]) {
+      const double* lo = scratch + (2 * i + 1) * kThreads;
+      auto at = [&](int t) { return dd{hi[t], lo[t]}; };
+      const dd x = wave_sum_dd(dd_add(dd_add(at(lane), at(lane + 128)), dd_add(at(lane + 64), at(lane + 192))));
+      if (lane == 0) {
+        put(sl[i], x.hi);
+        put(sl[i] + kDdLo, x.lo);
+      }
+    } else {
+      const double x = wave_sum((hi[lane] + hi[lane + 128]) + (hi[lane + 64] + hi[lane + 192]));
+      if (lane == 0) put(sl[i], x);
+    }
+  }
+  if (threadIdx.x == 0) put(0, ((red0[0] + red0[1]) + red0[2]) + red0[3]);
+}
+
 // block_partials_dd's layout from plain partials (v[0] plain, v[1 .. ND] the high parts, low parts zero)
 template <int ND>
 __device__ __forceinline__ void block_partials_lo0(double (&v)[13], double* __restrict__ partials, int tile,
@@ -223,6 +270,22 @@ struct DotAcc {
     return {p, s};
   }
 };
+
+// Column dot product of one lane (R terms): double-double (DotAcc) or a plain FMA chain (low part zero)
+template <bool DD, int R>
+__device__ __forceinline__ dd lane_dot(const double (&u)[R], const double (&v)[R]) {
+  if constexpr (DD) {
+    DotAcc t;
+#pragma unroll
+    for (int a = 0; a < R; ++a) t.add(u[a], v[a]);
+    return t.val();
+  } else {
+    double t = 0.0;
+#pragma unroll
+    for (int a = 0; a < R; ++a) t = fma(u[a], v[a], t);
+    return {t, 0.0};
+  }
+}
 
 struct PoseLane {
   int lane, wave, k, tile, agent, pslot;
@@ -452,6 +515,139 @@ __device__ __forceinline__ void edge_loop(const QView& q, const double* __restri
   }
 }
 
+// edge_loop for b = 4 with the XOR-rotated accumulator (quad_reduce_scatter_rot): lane kc accumulates column
+// s ^ kc in slot s, so it reads the record entries in that order.  Row kc of M (incoming) is at offsets
+// 4 kc + (s ^ kc) = 5 kc ^ s, column kc (outgoing) at kc + 4 (s ^ kc) = 5 kc ^ 4 s.  The stage of incidence z + 1
+// is issued before incidence z is consumed and no branch separates the two (a loop exit between them let the
+// compiler sink the next gather below the FMAs that should hide it); an odd tail is consumed after the loop.
+template <int R, bool INC_LDS, bool REC_LDS>
+__device__ __forceinline__ void edge_loop_rot(const QView& q, const double* __restrict__ in, int kc, int z0, int z1,
+                                              const int2* s_inc, int i0, const double* s_rec, int e0,
+                                              double (&acc)[R][4]) {
+  constexpr int B = 4, RW = edge_rec_width(3);
+  struct Stage {
+    double m[B];
+    double x[R];
+  };
+  const __amdgpu_buffer_rsrc_t rin = buf_rsrc(in), rrec = buf_rsrc(q.rec);
+  const int k5 = 5 * kc;
+  auto fetch = [&](int z, Stage& st) {
+    int2 ie;
+    if constexpr (INC_LDS)
+      ie = s_inc[z - i0];
+    else
+      ie = q.inc[z];
+    const int sh = (ie.x & 1) << 1;  // outgoing: stride 4 between the slots' entries
+    if constexpr (REC_LDS) {
+      const double* mr = s_rec + ((ie.x >> 1) - e0) * lds_rec_stride(B);
+#pragma unroll
+      for (int s = 0; s < B; ++s) st.m[s] = mr[k5 ^ (s << sh)];
+    } else {
+      const unsigned mo = 8u * static_cast<unsigned>(ie.x >> 1) * RW;
+#pragma unroll
+      for (int s = 0; s < B; ++s)
+        st.m[s] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                 rrec, mo + 8u * static_cast<unsigned>(k5 ^ (s << sh)), 0, 0));
+    }
+    buf_load_f64<R>(rin, 8u * (static_cast<unsigned>(ie.y) * (R * B) + kc * R), st.x);
+  };
+  auto consume = [&](const Stage& st) {
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int s = 0; s < B; ++s) acc[a][s] = fma(-st.x[a], st.m[s], acc[a][s]);
+  };
+  if (z0 >= z1) return;
+  Stage sa, sb;
+  fetch(z0, sa);
+  int nz = z0;
+  for (; nz + 1 < z1; nz += 2) {
+    fetch(nz + 1, sb);
+    consume(sa);
+    fetch(min(nz + 2, z1 - 1), sa);
+    consume(sb);
+  }
+  if (nz < z1) consume(sa);
+}
+
+// One pipeline over every incidence of a pose (b = 4, rotated accumulator, staged tile): positions p < L1 are
+// incidences a0 + p, the rest b0 + (p - L1), in that order -- the order of the separate loops it replaces, so the
+// sums are bitwise theirs.  A record whose id is below the tile's first-visit range (a second visit) is read
+// from HBM / L2, the others from the LDS stage; one two-stage pipeline instead of one per record source, so only
+// the pose's first gather waits a full memory latency.
+template <int R>
+__device__ __forceinline__ void edge_loop_uni(const QView& q, const double* __restrict__ in, int kc, int a0, int L1,
+                                              int b0, int L2, const int2* s_inc, int i0, const double* s_rec, int e0,
+                                              double (&acc)[R][4]) {
+  constexpr int B = 4, RW = edge_rec_width(3);
+  struct Stage {
+    double m[B];
+    double x[R];
+  };
+  const __amdgpu_buffer_rsrc_t rin = buf_rsrc(in), rrec = buf_rsrc(q.rec);
+  const int k5 = 5 * kc, n = L1 + L2;
+  auto fetch = [&](int pos, Stage& st) {
+    const int z = pos < L1 ? a0 + pos : b0 + (pos - L1);
+    const int2 ie = s_inc[z - i0];
+    const int sh = (ie.x & 1) << 1;  // outgoing: stride 4 between the slots' entries
+    const int id = ie.x >> 1;
+    if (id >= e0) {
+      const double* mr = s_rec + (id - e0) * lds_rec_stride(B);
+#pragma unroll
+      for (int s = 0; s < B; ++s) st.m[s] = mr[k5 ^ (s << sh)];
+    } else {
+      const unsigned mo = 8u * static_cast<unsigned>(id) * RW;
+#pragma unroll
+      for (int s = 0; s < B; ++s)
+        st.m[s] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                 rrec, mo + 8u * static_cast<unsigned>(k5 ^ (s << sh)), 0, 0));
+    }
+    buf_load_f64<R>(rin, 8u * (static_cast<unsigned>(ie.y) * (R * B) + kc * R), st.x);
+  };
+  auto consume = [&](const Stage& st) {
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int s = 0; s < B; ++s) acc[a][s] = fma(-st.x[a], st.m[s], acc[a][s]);
+  };
+  if (n <= 0) return;
+  Stage sa, sb;
+  fetch(0, sa);
+  int p = 0;
+  for (; p + 1 < n; p += 2) {
+    fetch(p + 1, sb);
+    consume(sa);
+    fetch(min(p + 2, n - 1), sa);
+    consume(sb);
+  }
+  if (p < n) consume(sa);
+}
+
+// Row kc of the pose's packed diagonal block in the rotated slot order (slot s = column s ^ kc), b = 4
+__device__ __forceinline__ void diag_row_rot(const QView& q, long j, int kc, double (&dk)[4]) {
+  constexpr int DW = diag_width(3);
+  const double* dj = q.diag + j * DW;
+  // packed upper-triangle index of (kc, c), c = s ^ kc: sym_index<4> restated without a dynamic table
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int c = s ^ kc;
+    const int u = kc < c ? kc : c, v = kc < c ? c : kc;
+    dk[s] = dj[u * 4 - u * (u - 1) / 2 + (v - u)];
+  }
+}
+
+template <int R, int B, bool INC_LDS, bool REC_LDS, bool ROT>
+__device__ __forceinline__ void edge_loop_any(const QView& q, const double* __restrict__ in, int kc, int z0, int z1,
+                                              const int2* s_inc, int i0, const double* s_rec, int e0,
+                                              double (&acc)[R][B]) {
+  if constexpr (ROT) {
+    static_assert(B == 4, "rotated accumulator: b = 4 only");
+    edge_loop_rot<R, INC_LDS, REC_LDS>(q, in, kc, z0, z1, s_inc, i0, s_rec, e0, acc);
+  } else {
+    edge_loop<R, B, INC_LDS, REC_LDS>(q, in, kc, z0, z1, s_inc, i0, s_rec, e0, acc);
+  }
+}
+
 // Block row j of X.Q for the edge-stream form: off-diagonal incidences (second visits through
 // L2 first, then first visits from the LDS stage), then + X_j[:,k] (x) Q_jj[k,:].  The whole quad
 // runs together; lane 3 of a d = 2 quad mirrors lane 0 and its acc is dropped.
@@ -463,7 +659,7 @@ __device__ __forceinline__ void edge_loop(const QView& q, const double* __restri
 // half the neighbour gathers.
 // NODIAG (the first-step quadratic form, MODE_QF / MODE_HESS_QF): the half sum without the diagonal
 // term (added after the quad reduction, qf_first_step_dhd); the lane-3 mirror of a d = 2 quad is zeroed.
-template <int R, int B, bool STAGED, bool HALF = false, bool NODIAG = false>
+template <int R, int B, bool STAGED, bool HALF = false, bool NODIAG = false, bool ROT = false, bool UNI = false>
 __device__ __forceinline__ void spmm_accumulate_edges(const QView& q, const double* __restrict__ in, long j,
                                                       int k, int beg, int end, const int2* s_inc, int i0,
                                                       const double* s_rec, int e0, double (&acc)[R][B],
@@ -475,32 +671,41 @@ __device__ __forceinline__ void spmm_accumulate_edges(const QView& q, const doub
     if constexpr (STAGED) {
       int mid = end;  // first visits of j are the largest ids of its list
       while (mid > beg && (s_inc[mid - 1 - i0].x >> 1) >= rf) --mid;
-      edge_loop<R, B, true, true>(q, in, kc, mid, end, s_inc, i0, s_rec, e0, acc);
+      edge_loop_any<R, B, true, true, ROT>(q, in, kc, mid, end, s_inc, i0, s_rec, e0, acc);
     } else {
       int mid = end;
       while (mid > beg && (q.inc[mid - 1].x >> 1) >= rf) --mid;
-      edge_loop<R, B, false, false>(q, in, kc, mid, end, s_inc, i0, s_rec, e0, acc);
+      edge_loop_any<R, B, false, false, ROT>(q, in, kc, mid, end, s_inc, i0, s_rec, e0, acc);
     }
+  } else if constexpr (STAGED && UNI && ROT) {  // one pipeline over [beg, end), the record source per incidence
+    edge_loop_uni<R>(q, in, kc, beg, end - beg, beg, 0, s_inc, i0, s_rec, e0, acc);
   } else if constexpr (STAGED) {
     int mid = beg;  // ids ascend: the second visits (ids below the tile's range) come first
     while (mid < end && (s_inc[mid - i0].x >> 1) < e0) ++mid;
-    edge_loop<R, B, true, false>(q, in, kc, beg, mid, s_inc, i0, s_rec, e0, acc);
-    edge_loop<R, B, true, true>(q, in, kc, mid, end, s_inc, i0, s_rec, e0, acc);
+    edge_loop_any<R, B, true, false, ROT>(q, in, kc, beg, mid, s_inc, i0, s_rec, e0, acc);
+    edge_loop_any<R, B, true, true, ROT>(q, in, kc, mid, end, s_inc, i0, s_rec, e0, acc);
   } else {
-    edge_loop<R, B, false, false>(q, in, kc, beg, end, s_inc, i0, s_rec, e0, acc);
+    edge_loop_any<R, B, false, false, ROT>(q, in, kc, beg, end, s_inc, i0, s_rec, e0, acc);
   }
   double xj[R], dk[B];
   const double* pj = in + j * (R * B) + kc * R;
 #pragma unroll
   for (int a = 0; a < R; ++a) xj[a] = pj[a];
-  const double* dj = q.diag + j * DW;
+  if constexpr (ROT) {
+    double d4[4];
+    diag_row_rot(q, j, kc, d4);
 #pragma unroll
-  for (int c = 0; c < B; ++c) {
-    int o = sym_index<B>(0, c);
-    if (kc == 1) o = sym_index<B>(1, c);
-    if (kc == 2) o = sym_index<B>(2, c);
-    if (B > 3 && kc == 3) o = sym_index<B>(B > 3 ? 3 : 0, c);
-    dk[c] = dj[o];
+    for (int c = 0; c < B; ++c) dk[c] = d4[c < 4 ? c : 0];
+  } else {
+    const double* dj = q.diag + j * DW;
+#pragma unroll
+    for (int c = 0; c < B; ++c) {
+      int o = sym_index<B>(0, c);
+      if (kc == 1) o = sym_index<B>(1, c);
+      if (kc == 2) o = sym_index<B>(2, c);
+      if (B > 3 && kc == 3) o = sym_index<B>(B > 3 ? 3 : 0, c);
+      dk[c] = dj[o];
+    }
   }
   const bool act = k < B;
 #pragma unroll
@@ -537,9 +742,18 @@ __device__ __forceinline__ void diag_row(const QView& q, long j, int kc, double 
 
 // column k of the quad-reduced running sum (the lane-3 mirror of a d = 2 quad masked out; for d = 3
 // every lane is active and acc is reduced in place, no copy held across the edge loop)
-template <int R, int B>
+template <int R, int B, bool ROT = false>
 __device__ __forceinline__ void snapshot_half(const double (&acc)[R][B], int k, bool act, double (&qch)[R]) {
-  if constexpr (B == 4) {
+  if constexpr (ROT) {
+    (void)act;
+    (void)k;
+    double a4[R][4];
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) a4[a][c] = acc[a][c < B ? c : 0];
+    quad_reduce_scatter_rot<R>(a4, qch);
+  } else if constexpr (B == 4) {
     (void)act;
     quad_reduce_scatter<R, B>(acc, k, qch);
   } else {
@@ -560,7 +774,7 @@ __device__ __forceinline__ void snapshot_half(const double (&acc)[R][B], int k, 
 // SV (second-visit staging): s_inc holds QView::inc_sv, whose record fields are tile-local LDS slots
 // (second visits 0 .. sv_ns - 1, first visit id -> sv_ns + id - e0), so every incidence reads its record
 // from LDS; the phase boundaries move to slot space and the order of additions is unchanged.
-template <int R, int B, bool STAGED, bool SNAP, bool SV = false>
+template <int R, int B, bool STAGED, bool SNAP, bool SV = false, bool ROT = false, bool UNI = false>
 __device__ __forceinline__ void spmm_accumulate_edges_hq(const QView& q, const double* __restrict__ in, long j,
                                                          int k, int beg, int end, const int2* s_inc, int i0,
                                                          const double* s_rec, int e0, double (&acc)[R][B],
@@ -574,21 +788,38 @@ __device__ __forceinline__ void spmm_accumulate_edges_hq(const QView& q, const d
     int mid = beg;  // second visits (ids below the tile's range) | first visits of earlier poses of the tile
     while (mid < end && (s_inc[mid - i0].x >> 1) < bnd) ++mid;
     while (midh > mid && (s_inc[midh - 1 - i0].x >> 1) >= rf) --midh;
-    edge_loop<R, B, true, true>(q, in, kc, midh, end, s_inc, i0, s_rec, rbase, acc);
-    if constexpr (SNAP) snapshot_half<R, B>(acc, k, act, qch);
-    edge_loop<R, B, true, SV>(q, in, kc, beg, mid, s_inc, i0, s_rec, rbase, acc);
-    edge_loop<R, B, true, true>(q, in, kc, mid, midh, s_inc, i0, s_rec, rbase, acc);
+    if constexpr (UNI && ROT && !SV) {  // one pipeline: own first visits, then [beg, midh)
+      if constexpr (SNAP) {
+        edge_loop_uni<R>(q, in, kc, midh, end - midh, beg, 0, s_inc, i0, s_rec, e0, acc);
+        snapshot_half<R, B, ROT>(acc, k, act, qch);
+        edge_loop_uni<R>(q, in, kc, beg, midh - beg, beg, 0, s_inc, i0, s_rec, e0, acc);
+      } else {
+        edge_loop_uni<R>(q, in, kc, midh, end - midh, beg, midh - beg, s_inc, i0, s_rec, e0, acc);
+      }
+    } else {
+      edge_loop_any<R, B, true, true, ROT>(q, in, kc, midh, end, s_inc, i0, s_rec, rbase, acc);
+      if constexpr (SNAP) snapshot_half<R, B, ROT>(acc, k, act, qch);
+      edge_loop_any<R, B, true, SV, ROT>(q, in, kc, beg, mid, s_inc, i0, s_rec, rbase, acc);
+      edge_loop_any<R, B, true, true, ROT>(q, in, kc, mid, midh, s_inc, i0, s_rec, rbase, acc);
+    }
   } else {
     while (midh > beg && (q.inc[midh - 1].x >> 1) >= rf) --midh;
-    edge_loop<R, B, false, false>(q, in, kc, midh, end, s_inc, i0, s_rec, e0, acc);
-    if constexpr (SNAP) snapshot_half<R, B>(acc, k, act, qch);
-    edge_loop<R, B, false, false>(q, in, kc, beg, midh, s_inc, i0, s_rec, e0, acc);
+    edge_loop_any<R, B, false, false, ROT>(q, in, kc, midh, end, s_inc, i0, s_rec, e0, acc);
+    if constexpr (SNAP) snapshot_half<R, B, ROT>(acc, k, act, qch);
+    edge_loop_any<R, B, false, false, ROT>(q, in, kc, beg, midh, s_inc, i0, s_rec, e0, acc);
   }
   double xj[R], dk[B];
   const double* pj = in + j * (R * B) + kc * R;
 #pragma unroll
   for (int a = 0; a < R; ++a) xj[a] = pj[a];
-  diag_row<B>(q, j, kc, dk);
+  if constexpr (ROT) {
+    double d4[4];
+    diag_row_rot(q, j, kc, d4);
+#pragma unroll
+    for (int c = 0; c < B; ++c) dk[c] = d4[c < 4 ? c : 0];
+  } else {
+    diag_row<B>(q, j, kc, dk);
+  }
 #pragma unroll
   for (int a = 0; a < R; ++a) xown[a] = act ? xj[a] : 0.0;
 #pragma unroll
@@ -644,6 +875,14 @@ constexpr bool evar_pre(int v) { return (v & 8) != 0; }
 constexpr bool evar_pre_r(int v) { return (v & 16) != 0; }
 // bit 5: second-visit records staged in LDS with the first visits (QView::sv_*, the HESS passes)
 constexpr bool evar_sv(int v) { return (v & 32) != 0; }
+// bit 6 (round 4): the merged tCG partials in the precision kMergedDdSlots states, reduced one quantity per wave
+// with plain quantities on plain paths
+constexpr bool evar_v2(int v) { return (v & 64) != 0; }
+// bit 7 (round 4): the XOR-rotated accumulator (quad_reduce_scatter_rot: no column selects in the quad reduction;
+// b = 4), bitwise the plain one
+constexpr bool evar_rot(int v) { return (v & 128) != 0; }
+// bit 8 (round 4, with bit 7): one edge-loop pipeline per pose over both record sources (edge_loop_uni)
+constexpr bool evar_uni(int v) { return (v & 256) != 0; }
 constexpr int kSvStage = 376;  // records staged per tile with second visits: 3 blocks of ~53 KB LDS per CU
 
 
@@ -1187,6 +1426,8 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
   double* __restrict__ S_out = args.S_out;
   constexpr int D = B - 1;
   const PoseLane p = pose_lane<B, FMT == QFMT_EDGES ? evar_xcd(VAR) : var_xcd(VAR)>(c);
+  constexpr bool ROT = FMT == QFMT_EDGES && B == 4 && evar_rot(VAR);
+  constexpr bool UNI = ROT && evar_uni(VAR);
   if (tile_skipped(c, p.agent)) {
     if constexpr (spmm_fusable(MODE)) spmm_arrive(args, p.agent);
     return;
@@ -1293,17 +1534,19 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
       if constexpr (mode_hess(MODE)) {
         constexpr bool SNAP = mode_snap(MODE);
         if (staged)
-          spmm_accumulate_edges_hq<R, B, true, SNAP, SVS>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1],
-                                                          s_inc, i0, s_rec, e0, acc, xin, qch, ns);
+          spmm_accumulate_edges_hq<R, B, true, SNAP, SVS, ROT, UNI>(q, in, p.j, p.k, s_ptr[p.pslot],
+                                                                    s_ptr[p.pslot + 1], s_inc, i0, s_rec, e0, acc,
+                                                                    xin, qch, ns);
         else
-          spmm_accumulate_edges_hq<R, B, false, SNAP>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc,
-                                                      i0, s_rec, e0, acc, xin, qch);
+          spmm_accumulate_edges_hq<R, B, false, SNAP, false, ROT>(q, in, p.j, p.k, s_ptr[p.pslot],
+                                                                  s_ptr[p.pslot + 1], s_inc, i0, s_rec, e0, acc, xin,
+                                                                  qch);
       } else if (staged) {
-        spmm_accumulate_edges<R, B, true, HALF, NODIAG>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc,
-                                                        i0, s_rec, e0, acc, xin);
+        spmm_accumulate_edges<R, B, true, HALF, NODIAG, ROT, UNI>(q, in, p.j, p.k, s_ptr[p.pslot],
+                                                                  s_ptr[p.pslot + 1], s_inc, i0, s_rec, e0, acc, xin);
       } else {
-        spmm_accumulate_edges<R, B, false, HALF, NODIAG>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1], s_inc,
-                                                         i0, s_rec, e0, acc, xin);
+        spmm_accumulate_edges<R, B, false, HALF, NODIAG, ROT>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1],
+                                                              s_inc, i0, s_rec, e0, acc, xin);
       }
     }
   } else {
@@ -1313,7 +1556,16 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
   // lane k keeps column k of the block row only (quad reduce-scatter; same additions, same
   // order as a quad all-reduce, so bitwise identical to it) and the epilogues work column-locally
   double qc[R];
-  quad_reduce_scatter<R, B>(acc, p.k, qc);
+  if constexpr (ROT) {
+    double a4[R][4];
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) a4[a][cc] = acc[a][cc < B ? cc : 0];
+    quad_reduce_scatter_rot<R>(a4, qc);
+  } else {
+    quad_reduce_scatter<R, B>(acc, p.k, qc);
+  }
 
   const long off = p.j * (R * B) + p.k * R;
   const bool own = p.ok && p.k < B;
@@ -1529,6 +1781,65 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
       } else {
         precond_col_mk<R, B>(Xf, mk, p.k, args.pmode, rcol, zc);
       }
+      if constexpr (FMT == QFMT_EDGES && evar_v2(VAR)) {
+        // Per-quantity precision (kMergedDdSlots): double-double (exact products, compensated sums) for the
+        // sums whose terms cancel across poses and feed beta; plain FMA chains for the rest.  |r_j|^2 and
+        // <z_j, r_j> only when no k_tcg_updir left them (args.rz_own: the first iteration).
+        constexpr bool DD_RH = (kMergedDdSlots & 0x04) != 0, DD_HH = (kMergedDdSlots & 0x08) != 0,
+                       DD_ZH = (kMergedDdSlots & 0x20) != 0, DD_MH = (kMergedDdSlots & 0x40) != 0;
+        const bool rz = mode_snap(MODE) || args.rz_own != 0;
+        const dd rh = lane_dot<DD_RH, R>(rcol, hc), hh = lane_dot<DD_HH, R>(hc, hc), zh = lane_dot<DD_ZH, R>(zc, hc);
+        dd mh{0.0, 0.0};
+        if (args.pmode == PRECON_NONE) {
+          mh = DD_MH == DD_HH ? hh : lane_dot<DD_MH, R>(hc, hc);
+        } else {
+          // <Hd Minv, Hd> of the pose, column-locally: lane k adds Minv_kk |h_k|^2 and Minv_{k,k^x} <h_k, h_{k^x}>
+          // for x = 1, 2, 3 (one partner column at a time, no full-pose gather)
+          const int kc = p.k < B ? p.k : 0;
+          const bool act = p.k < B;
+          double mkk = 0.0;
+#pragma unroll
+          for (int u = 0; u < B; ++u) mkk = kc == u ? mk[u] : mkk;
+          const dd h2 = DD_MH == DD_HH ? hh : lane_dot<DD_MH, R>(hc, hc);
+          mh = act ? (DD_MH ? dd_mul_d(h2, mkk) : dd{h2.hi * mkk, 0.0}) : dd{0.0, 0.0};
+          auto pair = [&](int x, const double (&hq)[R]) {
+            const int pk = p.k ^ x;
+            double m = 0.0;
+#pragma unroll
+            for (int u = 0; u < B; ++u) m = pk == u ? mk[u] : m;  // Minv_{pk, k} = column k's entry pk
+            if (pk >= B || !act) m = 0.0;
+            const dd t = lane_dot<DD_MH, R>(hc, hq);
+            mh = DD_MH ? dd_add(mh, dd_mul_d(t, m)) : dd{fma(t.hi, m, mh.hi), 0.0};
+          };
+          double hq[R];
+#pragma unroll
+          for (int a = 0; a < R; ++a) hq[a] = dpp_f64<0xB1>(hc[a]);  // quad_perm [1,0,3,2]: partner k^1
+          pair(1, hq);
+#pragma unroll
+          for (int a = 0; a < R; ++a) hq[a] = dpp_f64<0x4E>(hc[a]);  // [2,3,0,1]: k^2
+          pair(2, hq);
+#pragma unroll
+          for (int a = 0; a < R; ++a) hq[a] = dpp_f64<0x1B>(hc[a]);  // [3,2,1,0]: k^3
+          pair(3, hq);
+        }
+        const dd zero{0.0, 0.0};
+        const dd zh2 = own ? (DD_ZH ? dd{2.0 * zh.hi, 2.0 * zh.lo} : dd{2.0 * zh.hi, 0.0}) : zero;
+        if (rz) {
+          const dd rr = lane_dot<true, R>(rcol, rcol), zr = lane_dot<true, R>(zc, rcol);
+          // double-double items first (one per wave), then the plain ones
+          constexpr int sl[6] = {1, 4, 5, 6, 3, 2};
+          constexpr bool isdd[6] = {true, true, DD_ZH, DD_MH, DD_HH, DD_RH};
+          const dd v[6] = {own ? rr : zero, own ? zr : zero, zh2, own ? mh : zero, own ? hh : zero, own ? rh : zero};
+          block_partials_mixed<6>(own ? dpart : 0.0, v, sl, isdd, c.partials, p.tile, args.fin_mode == 2,
+                                  red_scratch);
+        } else {  // slots 1 and 4 are not read (FinalizeArgs::rz_pc)
+          constexpr int sl[4] = {5, 6, 3, 2};
+          constexpr bool isdd[4] = {DD_ZH, DD_MH, DD_HH, DD_RH};
+          const dd v[4] = {zh2, own ? mh : zero, own ? hh : zero, own ? rh : zero};
+          block_partials_mixed<4>(own ? dpart : 0.0, v, sl, isdd, c.partials, p.tile, args.fin_mode == 2,
+                                  red_scratch);
+        }
+      } else {
       // double-double partials (exact products, compensated sums): the stopping test combines them as
       // polynomials in alpha whose terms cancel by the residual drop (merged_stop_test)
       // |r_j|^2 and <z_j, r_j> only when no k_tcg_updir left them (args.rz_own: the first iteration)
@@ -1611,6 +1922,7 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
         for (int q = 0; q < 6; ++q) pl[1 + q] = parts[q].hi;
         block_partials_lo0<6>(pl, c.partials, p.tile, args.fin_mode == 2);
       }
+      }  // v1 partials
     } else {
       double parts[1] = {own ? dpart : 0.0};
       block_partials<1>(parts, c.partials, p.tile, args.fin_mode == 2);
@@ -3203,6 +3515,42 @@ template <int MODE>
 hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const SpmmArgs& a) {
   if (q.fmt == QFMT_EDGES) {
     constexpr bool kPreMode = mode_hess(MODE) || MODE == MODE_QF || MODE == MODE_EVAL_TCG;
+    const int v2 = q.tuning[TUNE_SPMM_V2];
+    if (v2 > 0) {
+      // round-4 kernels: the merged modes' partials (bit 6) for every shape, since the host's dd_mask follows the
+      // tuning key; the rotated accumulator (bit 7, bitwise the plain one) at the headline shape: v2 = 1 every
+      // mode, 2 none, 3 the merged modes only
+      constexpr int V2 = kEdgeDefaultVariant | (mode_merged(MODE) ? 64 : 0);
+      const bool rot = v2 == 1 || v2 == 5 || ((v2 == 3 || v2 == 4) && mode_merged(MODE));
+      const bool uni = v2 == 5 || (v2 == 4 && mode_merged(MODE));
+      if (uni && r == 5 && b == 4) {
+        if constexpr (kPreMode) {
+          if (q.tuning[TUNE_EPI_PREFETCH] > 0) {
+            k_spmm<5, 4, MODE, V2 | 8 | 128 | 256, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+            return hipSuccess;
+          }
+        }
+        k_spmm<5, 4, MODE, V2 | 128 | 256, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+        return hipSuccess;
+      }
+      if (r == 5 && b == 4 && (q.tuning[TUNE_EDGE_VARIANT] < 0 || mode_merged(MODE))) {
+        if constexpr (kPreMode) {
+          if (q.tuning[TUNE_EPI_PREFETCH] > 0) {
+            if (rot)
+              k_spmm<5, 4, MODE, V2 | 8 | 128, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+            else
+              k_spmm<5, 4, MODE, V2 | 8, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+            return hipSuccess;
+          }
+        }
+        if (rot)
+          k_spmm<5, 4, MODE, V2 | 128, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+        else
+          k_spmm<5, 4, MODE, V2, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+        return hipSuccess;
+      }
+      if constexpr (mode_merged(MODE)) return spmm_rb<MODE, V2, QFMT_EDGES>(r, b, grid, c, q, a);
+    }
     if constexpr (mode_hess(MODE)) {
       if (r == 5 && b == 4 && q.tuning[TUNE_SV_STAGE] > 0 && q.tuning[TUNE_EDGE_VARIANT] < 0 && q.sv_ptr != nullptr) {
         k_spmm<5, 4, MODE, kEdgeDefaultVariant | 8 | 32, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);

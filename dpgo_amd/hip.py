@@ -87,6 +87,7 @@ _SIGS = [
                                C.POINTER(OptResult)], C.c_int),
     ("dpgo_hip_synchronize", [C.c_void_p], C.c_int),
     ("dpgo_hip_set_tuning", [C.c_int, C.c_int], C.c_int),
+    ("dpgo_hip_get_tuning", [C.c_int, C.POINTER(C.c_int)], C.c_int),
     ("dpgo_hip_problem_set_tuning", [C.c_void_p, C.c_int, C.c_int], C.c_int),
     ("dpgo_hip_spmm_bytes", [C.c_void_p], C.c_double),
     ("dpgo_hip_bench_spmm", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, _dp], C.c_int),
@@ -128,6 +129,10 @@ def lib():
             fn.argtypes = args
             fn.restype = res
         _lib = L
+        # DPGO_TUNE="key=value,...": process defaults of tuning keys (A/B and profiling runs of tools/ and bench.py)
+        for kv in filter(None, os.environ.get("DPGO_TUNE", "").split(",")):
+            k, v = kv.split("=")
+            _check(L.dpgo_hip_set_tuning(int(k), int(v)))
     return _lib
 
 
@@ -160,6 +165,13 @@ def rccl_unique_id() -> bytes:
     buf = C.create_string_buffer(128)
     _check(lib().dpgo_rccl_unique_id(buf))
     return buf.raw
+
+
+def get_tuning(key: int) -> int:
+    """Process default of a tuning key."""
+    v = C.c_int()
+    _check(lib().dpgo_hip_get_tuning(int(key), C.byref(v)))
+    return v.value
 
 
 def set_tuning(key: int, value: int):

@@ -237,6 +237,8 @@ int dpgo_hip_certify(dpgo_hip_problem h, const double* X, int max_iters, double 
  * DESIGN.md records each key's measurement.  These are the process DEFAULTS: a handle copies them when it is
  * created, so handles created afterwards follow; dpgo_hip_problem_set_tuning changes one existing handle. */
 int dpgo_hip_set_tuning(int key, int value);
+/* The process default of a tuning key. */
+int dpgo_hip_get_tuning(int key, int* value);
 /* The same keys on one existing handle (A/B timing of variants on one problem without rebuilding it). */
 int dpgo_hip_problem_set_tuning(dpgo_hip_problem h, int key, int value);
 /* Algorithmic HBM bytes of one X.Q SpMM over this handle: BSR blocks + indices + X + Y, or, for

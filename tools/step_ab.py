@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--agents-per-axis", type=int, default=4)
     ap.add_argument("--precon", default="block_jacobi", choices=["block_jacobi", "exact"])
+    ap.add_argument("--kernel-timing", type=int, default=0, help="sample every k-th in-step SpMM launch per mode")
     a = ap.parse_args()
     import torch
     from dpgo_amd import hip as H
@@ -46,6 +47,9 @@ def main():
             eng.pre_exchange(c)
             eng.update(c, None)
 
+    if a.kernel_timing:
+        eng.set_kernel_timing(a.kernel_timing)
+    kt = {v: {} for v in a.values}
     with torch.cuda.stream(s):
         for _ in range(a.burnin):
             step()
@@ -60,11 +64,16 @@ def main():
                 eng.set_X(Xb)
                 step()
                 torch.cuda.synchronize()
+                if a.kernel_timing:
+                    eng.kernel_times()  # drop the warm-up step's samples
                 t0 = time.perf_counter()
                 for _ in range(a.steps):
                     step()
                 torch.cuda.synchronize()
                 ms = 1e3 * (time.perf_counter() - t0) / a.steps
+                if a.kernel_timing:
+                    for m, (tot, cnt) in eng.kernel_times().items():
+                        kt[v].setdefault(m, []).append(1e3 * tot / max(cnt, 1))
                 f, _ = eng.central_eval()
                 hv = eng.bench_hvp(0, 20)
                 res[v].append(ms)
@@ -73,7 +82,9 @@ def main():
                 print(json.dumps({"round": rnd, "value": v, "ms_per_step": ms, "hvp_ms": hv, "f": f}), flush=True)
     print(json.dumps({"key": a.key, "median_ms_per_step": {v: float(np.median(res[v])) for v in a.values},
                       "median_hvp_ms": {v: float(np.median(hvp[v])) for v in a.values},
-                      "f_after": fin}), flush=True)
+                      "f_after": fin,
+                      "median_kernel_us": {v: {m: float(np.median(x)) for m, x in kt[v].items()} for v in a.values}}),
+          flush=True)
 
 
 if __name__ == "__main__":
