@@ -123,6 +123,8 @@ def main():
     if one_device:
         local_rank = 0
     world = max(world, 1)
+    if world != args.gpus:  # the driver's SCALE runs must measure the world they name
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     torch.cuda.set_device(local_rank)
     if world > 1:
         if one_device:
@@ -279,7 +281,7 @@ def main():
         sync()
         elapsed = time.perf_counter() - t0
         eng.set_kernel_timing(0)
-        ktimes = eng.kernel_times()
+        ktimes = eng.kernel_times(batch_equiv=True)
         st1 = eng.stats().copy()
         b1, _ = eng.bytes()
         f_end, gn_end = central()
@@ -316,10 +318,12 @@ def main():
     traffic = measured_traffic() if (args.k == 100 and A == 4 and world == 1) else None
     per_mode = {}
     for m, v in ktimes.items():
-        avg = v[0] / max(v[1], 1)
+        # per full-batch launch equivalent: a half-batch launch of the split merged tCG (small batches, tuning
+        # key 10) moves about half the colour's bytes and counts 0.5 (dpgo_rbcd_kernel_times_ex)
+        avg = v[0] / max(v[2], 1e-12)
         byt = float(np.mean([x.get(m, 0.0) for x in mb]))
-        e = {"ms_total": v[0], "launches": v[1], "avg_ms": avg, "algorithmic_bytes_per_launch": byt,
-             "GBps": byt / (avg * 1e-3) / 1e9 if avg > 0 else 0.0}
+        e = {"ms_total": v[0], "launches": v[1], "batch_equivalents": v[2], "avg_ms": avg,
+             "algorithmic_bytes_per_launch": byt, "GBps": byt / (avg * 1e-3) / 1e9 if avg > 0 else 0.0}
         e["frac"] = e["GBps"] / HBM_PEAK_GBS
         tb = (traffic or {}).get("kernels", {}).get(m, {}).get("traffic_bytes_per_launch")
         if tb:
@@ -335,6 +339,47 @@ def main():
         step_bytes = float(tb.item())
     # the events time every k-th launch of each mode (--kernel-timing k): per-step SpMM time ~ k x the sample's
     spmm_ms_step = max(args.kernel_timing, 1) * sum(v["ms_total"] for v in per_mode.values()) / args.steps
+
+    # ---- what the multi-GPU run actually was (the driver's SCALE runs verify themselves): the collective's world as
+    # the communicator reports it, ranks sharing a device, and per colour this rank's halo bytes and exchange time
+    comm = {"world_size": world, "gpus_arg": args.gpus, "backend": dist.get_backend() if world > 1 else None,
+            "torch_world": dist.get_world_size() if world > 1 else 1}
+    if native:
+        comm["rccl_comm_count"], comm["rccl_comm_rank"] = eng.comm_info()
+        if comm["rccl_comm_count"] != world:
+            raise SystemExit(f"bench.py: RCCL communicator has {comm['rccl_comm_count']} ranks, WORLD_SIZE={world}")
+    if world > 1:
+        import socket
+        who = [None] * world
+        dist.all_gather_object(who, (socket.gethostname(), torch.cuda.current_device()))
+        comm["ranks_per_device"] = max(who.count(w) for w in who)
+        comm["devices"] = len(set(who))
+        xt = []
+        with torch.cuda.stream(stream):
+            for c in range(eng.num_colors):
+                reps = 10
+                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                sync()
+                ev0.record(stream)
+                for _ in range(reps):
+                    if args.halo == "color":
+                        exchange_color(c)
+                    else:
+                        exchange()
+                ev1.record(stream)
+                sync()
+                xt.append(ev0.elapsed_time(ev1) / reps)
+        tx = torch.tensor(xt, dtype=torch.float64, device="cpu" if one_device else dev)
+        dist.all_reduce(tx, op=dist.ReduceOp.MAX)
+        comm["exchange_per_color"] = [
+            {"color": c, "bytes_sent_this_rank": 8.0 * (sum(c_in[c]) if args.halo == "color" else int(eng.send_counts.sum())),
+             "bytes_received_this_rank": 8.0 * (sum(c_out[c]) if args.halo == "color" else int(eng.recv_counts.sum())),
+             "ms_max_over_ranks": float(tx[c]), "what": "pack + all_to_all (or the RCCL group) on the engine stream, "
+                                                          "mean of 10, outside the timed steps"}
+            for c in range(eng.num_colors)]
+    else:
+        comm["ranks_per_device"] = 1
+        comm["devices"] = 1
 
     # ---- the standalone X.Q SpMM over one colour class (the metric's "X.Q SpMM HBM GB/s")
     fmt_bytes, spmm_ms = eng.bench_spmm(0, args.spmm_reps)
@@ -415,6 +460,7 @@ def main():
         "setup_s": setup_s,
         "init": init_info,
     }
+    out["comm"] = comm
     out["halo"] = {"kind": args.halo if world > 1 else "none (one rank)",
                    "bytes_sent_per_step_this_rank": 8.0 * (sum(sum(v) for v in c_in) if args.halo == "color"
                                                            else eng.num_colors * int(eng.send_counts.sum())),

@@ -14,6 +14,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <new>
+#include <stdexcept>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -104,7 +106,8 @@ int dpgo::spmm_launch(dpgo_hip_problem h, int mode, const LaunchCtx& c, const Sp
     HIP_TRY(dpgo::launch_spmm(h->r, h->b, mode, c, qview(h), a));
     return DPGO_HIP_OK;
   }
-  dpgo_hip_problem_s::TimedLaunch t{mode, nullptr, nullptr};
+  dpgo_hip_problem_s::TimedLaunch t{mode, nullptr, nullptr,
+                                    static_cast<double>(c.num_tiles) / std::max(h->num_tiles, 1)};
   HIP_TRY(pooled_event(h, &t.a));
   HIP_TRY(pooled_event(h, &t.b));
   HIP_TRY(hipEventRecord(t.a, c.stream));
@@ -136,6 +139,7 @@ int dpgo::drain_timed(dpgo_hip_problem h, bool wait) {
     if (t.mode >= 0 && t.mode < dpgo::kSpmmModes) {
       h->timed_ms[t.mode] += v;
       h->timed_n[t.mode] += 1;
+      h->timed_frac[t.mode] += t.frac;
     }
     h->ev_pool.push_back(t.a);
     h->ev_pool.push_back(t.b);
@@ -144,13 +148,15 @@ int dpgo::drain_timed(dpgo_hip_problem h, bool wait) {
   return DPGO_HIP_OK;
 }
 
-int dpgo::take_spmm_times(dpgo_hip_problem h, double* ms, long long* launches) {
+int dpgo::take_spmm_times(dpgo_hip_problem h, double* ms, long long* launches, double* batch_equiv) {
   DPGO_TRY(drain_timed(h, true));
   for (int m = 0; m < dpgo::kSpmmModes; ++m) {
     ms[m] += h->timed_ms[m];
     launches[m] += h->timed_n[m];
+    batch_equiv[m] += h->timed_frac[m];
     h->timed_ms[m] = 0.0;
     h->timed_n[m] = 0;
+    h->timed_frac[m] = 0.0;
   }
   return DPGO_HIP_OK;
 }
@@ -323,6 +329,8 @@ int sync_q_edges(dpgo_hip_problem h) {
   HIP_TRY(hipMemcpyAsync(h->rec_first.p, lowcnt.data(), sizeof(int) * (h->N + 1), hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipMemcpyAsync(h->inc.p, inc.data(), sizeof(int2) * inc.size(), hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipMemcpyAsync(h->rec.p, rec.data(), sizeof(double) * rec.size(), hipMemcpyHostToDevice, h->stream));
+  h->h_inc_ptr = deg;  // the device factorisation's assembly tables (sync_chol) index these incidences
+  h->h_inc = inc;
   if (!diag.empty())
     HIP_TRY(hipMemcpyAsync(h->diag.p, diag.data(), sizeof(double) * diag.size(), hipMemcpyHostToDevice, h->stream));
   h->fmt = dpgo::QFMT_EDGES;
@@ -337,6 +345,7 @@ int sync_q_edges(dpgo_hip_problem h) {
 int sync_q(dpgo_hip_problem h) {
   if (!h->q_dirty) return DPGO_HIP_OK;
   h->chol_state = 0;  // the exact preconditioner follows Q (setQ refactorises, :37-41)
+  h->sn_sym_ready = false;  // a new Q may have a new pattern
   const int f0 = h->q_fmt[0];
   for (int a = 1; a < h->K; ++a)
     if (h->q_fmt[a] != f0) return fail(DPGO_HIP_ESTATE, "agents of one handle mix BSR and edge-stream Q");
@@ -425,9 +434,52 @@ int chol_threads(int K) {
   return std::max(1, std::min(t, K));
 }
 
+// The device numeric factorisation: k_sn_factor level by level (deepest first) over the symbolic structure and
+// the current edge-stream Q; a non-positive pivot falls back to the identity as the reference does.
+int device_factor(dpgo_hip_problem h) {
+  const int maxd = static_cast<int>(h->fac_level_off.size()) - 2;
+  HIP_TRY(hipMemsetAsync(h->fac_not_pd.p, 0, sizeof(int), h->stream));
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  HIP_TRY(hipEventCreate(&e0));
+  HIP_TRY(hipEventCreate(&e1));
+  HIP_TRY(hipEventRecord(e0, h->stream));
+  for (int dep = maxd; dep >= 0; --dep) {
+    const int n0 = h->fac_level_off[dep], n1 = h->fac_level_off[dep + 1];
+    dpgo::SnFactorView v{h->fac_nodes.p + n0, h->sn_s.p, h->sn_t.p, h->fac_off.p, h->sn_panel_off.p, h->sn_poses_off.p,
+                         h->sn_poses.p, h->fac_ch_off.p, h->fac_ch.p, h->fac_tp_off.p, h->fac_tp.p, h->fac_ent_off.p,
+                         h->fac_ent.p, h->fac_src.p, h->rec.p, h->diag.p, 0.1, h->fac_F[dep & 1].p,
+                         h->fac_F[(dep + 1) & 1].p, h->sn_panel.p, h->fac_not_pd.p};
+    HIP_TRY(dpgo::launch_sn_factor(h->b, v, n1 - n0, h->stream));
+  }
+  HIP_TRY(hipEventRecord(e1, h->stream));
+  int bad = 0;
+  HIP_TRY(hipMemcpyAsync(&bad, h->fac_not_pd.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  h->chol_factor_ms = ms;
+  h->chol_factor_count += 1;
+  if (std::getenv("DPGO_VERBOSE_CHOL"))
+    std::fprintf(stderr, "[dpgo_hip] exact preconditioner: device factorisation %.2f ms\n", static_cast<double>(ms));
+  if (bad) {
+    // src/QuadraticProblem.cpp:81-86: the solve fails -> "Preconditioner failed", out = in
+    std::printf("[dpgo_hip] Preconditioner failed (Q + 0.1 I not positive definite); using the identity.\n");
+    h->chol_state = 2;
+    return DPGO_HIP_OK;
+  }
+  h->chol_state = 1;
+  return DPGO_HIP_OK;
+}
+
 int sync_chol(dpgo_hip_problem h) {
   if (h->chol_state != 0) return DPGO_HIP_OK;
-  if (h->host_weights_stale) {  // weights changed on the device: bring the host measurement copy up to date
+  bool edges = true;
+  for (int a = 0; a < h->K; ++a) edges = edges && h->q_fmt[a] == dpgo::QFMT_EDGES;
+  const bool device = edges && h->tuning[dpgo::TUNE_DEVICE_CHOL] > 0;
+  if (device && h->sn_sym_ready) return device_factor(h);  // same pattern: only the numeric half again
+  if (!device && h->host_weights_stale) {  // weights changed on the device: bring the host measurement copy up to date
     std::vector<double> w(std::max<long>(h->num_edges, 1));
     HIP_TRY(hipMemcpyAsync(w.data(), h->w_dev_last, sizeof(double) * h->num_edges, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -442,7 +494,7 @@ int sync_chol(dpgo_hip_problem h) {
     h->host_weights_stale = false;
   }
   const int b = h->b, r = h->r, K = h->K;
-  // ---- per-agent factorisations, in parallel host threads
+  // ---- per-agent factor structure (device: symbolic only; host: the whole factorisation), host threads
   std::vector<dpgo::SupernodalFactor> Fs(K);
   std::vector<std::string> errs(K);
   std::vector<int> rcs(K, 0);
@@ -452,10 +504,19 @@ int sync_chol(dpgo_hip_problem h) {
     std::mutex log_mu;
     auto work = [&]() {
       for (int a = next++; a < K; a = next++) {
-        HostBSR Q;
-        agent_bsr(h, a, Q);
-        rcs[a] = dpgo::supernodal_cholesky(h->n_agent[a], b, Q.rowptr, Q.col, Q.blocks, 0.1, kMaxCholDoubles, Fs[a],
-                                           errs[a]);
+        try {
+          HostBSR Q;
+          agent_bsr(h, a, Q);
+          rcs[a] = device ? dpgo::supernodal_symbolic(h->n_agent[a], b, Q.rowptr, Q.col, kMaxCholDoubles, Fs[a], errs[a])
+                          : dpgo::supernodal_cholesky(h->n_agent[a], b, Q.rowptr, Q.col, Q.blocks, 0.1, kMaxCholDoubles,
+                                                      Fs[a], errs[a]);
+        } catch (const std::bad_alloc&) {
+          rcs[a] = -2;
+          errs[a] = "exact preconditioner: out of host memory in the factorisation";
+        } catch (const std::exception& ex) {
+          rcs[a] = -1;
+          errs[a] = std::string("exact preconditioner: ") + ex.what();
+        }
         // a long factorisation reports progress (a silent process looks hung to a supervisor)
         const int k = ++done;
         const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -480,7 +541,7 @@ int sync_chol(dpgo_hip_problem h) {
         h->chol_state = 2;
         return DPGO_HIP_OK;
       }
-      return fail(DPGO_HIP_EINVAL, errs[a]);
+      return fail(rcs[a] == -2 ? DPGO_HIP_ENOMEM : DPGO_HIP_EINVAL, errs[a]);
     }
     total += Fs[a].panel_doubles;
   }
@@ -509,7 +570,7 @@ int sync_chol(dpgo_hip_problem h) {
       s_[g] = s;
       t_[g] = t;
       panel_off[g] = po;
-      po += static_cast<long>(nd.panel.size());
+      po += dpgo::sn_panel_tiles(s * b, t * b) * dpgo::kSnTile * dpgo::kSnTile;
       f_off[g] = fo;
       fo += static_cast<long>(dpgo::sn_pad(s * b) + dpgo::sn_pad(t * b)) * r;
       u_off[g] = uo;
@@ -573,15 +634,15 @@ int sync_chol(dpgo_hip_problem h) {
   };
   HIP_TRY(hipStreamSynchronize(h->stream));
   HIP_TRY(h->sn_panel.ensure(std::max<long>(po, 1)));
-  for (int a = 0; a < K; ++a) {
-    for (size_t x = 0; x < Fs[a].nodes.size(); ++x) {
-      const auto& P = Fs[a].nodes[x].panel;
-      if (!P.empty())
-        HIP_TRY(hipMemcpy(h->sn_panel.p + panel_off[base[a] + x], P.data(), sizeof(double) * P.size(),
-                          hipMemcpyHostToDevice));
-    }
-    dpgo::SupernodalFactor().nodes.swap(Fs[a].nodes);  // release the host panels
-  }
+  if (!device)
+    for (int a = 0; a < K; ++a)
+      for (size_t x = 0; x < Fs[a].nodes.size(); ++x) {
+        const auto& P = Fs[a].nodes[x].panel;
+        if (!P.empty())
+          HIP_TRY(hipMemcpy(h->sn_panel.p + panel_off[base[a] + x], P.data(), sizeof(double) * P.size(),
+                            hipMemcpyHostToDevice));
+        std::vector<double>().swap(Fs[a].nodes[x].panel);  // release the host panel
+      }
   DPGO_TRY(up(h->sn_panel_off, panel_off));
   DPGO_TRY(up(h->sn_f_off, f_off));
   DPGO_TRY(up(h->sn_u_off, u_off));
@@ -600,8 +661,88 @@ int sync_chol(dpgo_hip_problem h) {
   HIP_TRY(h->sn_F.ensure(std::max<long>(fo, 1)));
   HIP_TRY(h->sn_U.ensure(std::max<long>(uo, 1)));
   h->chol_doubles = po;
-  h->chol_state = 1;
-  return DPGO_HIP_OK;
+  if (!device) {
+    h->chol_state = 1;
+    return DPGO_HIP_OK;
+  }
+  // ---- the device factorisation's tables: per tree level its nodes, per node its children, the positions of its R
+  // entries in its parent's frontal order, and the original entries of its S columns from the edge-stream Q
+  std::vector<int> fac_nodes, level_off(maxd + 2, 0), ch_off(nn + 1, 0), ch, tp_off(nn, 0), tp, ent_off(nn + 1, 0),
+      src;
+  std::vector<long> fac_off(nn, 0);
+  std::vector<dpgo::SnEntry> ent;
+  long level_size[2] = {0, 0};
+  for (int dep = 0; dep <= maxd; ++dep) {
+    level_off[dep] = static_cast<int>(fac_nodes.size());
+    long lo = 0;
+    for (int a = 0; a < K; ++a)
+      for (size_t x = 0; x < Fs[a].nodes.size(); ++x)
+        if (Fs[a].nodes[x].depth == dep) {
+          const int g = base[a] + static_cast<int>(x);
+          fac_nodes.push_back(g);
+          const long M = dpgo::sn_pad(s_[g] * b) + dpgo::sn_pad(t_[g] * b);
+          fac_off[g] = lo;
+          lo += M * M;
+        }
+    level_size[dep & 1] = std::max(level_size[dep & 1], lo);
+  }
+  level_off[maxd + 1] = static_cast<int>(fac_nodes.size());
+  std::vector<int> fpos;
+  for (int a = 0; a < K; ++a) {
+    const auto& nodes = Fs[a].nodes;
+    const long off = h->pose_off[a];
+    fpos.assign(h->n_agent[a], -1);
+    for (size_t x = 0; x < nodes.size(); ++x) {
+      const int g = base[a] + static_cast<int>(x);
+      const dpgo::SnNode& nd = nodes[x];
+      for (int c : nd.children) ch.push_back(base[a] + c);
+      ch_off[g + 1] = static_cast<int>(ch.size());
+      tp_off[g] = static_cast<int>(tp.size());
+      tp.insert(tp.end(), nd.to_parent.begin(), nd.to_parent.end());
+      const int s = static_cast<int>(nd.S.size());
+      for (int p = 0; p < s; ++p) fpos[nd.S[p]] = p;
+      for (size_t q = 0; q < nd.R.size(); ++q) fpos[nd.R[q]] = s + static_cast<int>(q);
+      for (int p = 0; p < s; ++p) {
+        ent.push_back(dpgo::SnEntry{p, p, 0, 0});  // the diagonal block (+ shift)
+        const long gv = off + nd.S[p];
+        // incidences of the column's pose (ascending edge id), grouped by the frontal row they land in
+        std::vector<std::pair<int, int>> rows;  // (q, code)
+        for (int k = h->h_inc_ptr[gv]; k < h->h_inc_ptr[gv + 1]; ++k) {
+          const int2 ie = h->h_inc[k];
+          const int q = fpos[ie.y - off];
+          if (q >= p) rows.emplace_back(q, ie.x);  // q < 0: eliminated below; q < p: the upper triangle
+        }
+        std::stable_sort(rows.begin(), rows.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+        for (size_t i = 0; i < rows.size();) {
+          size_t j = i;
+          const int s0 = static_cast<int>(src.size());
+          for (; j < rows.size() && rows[j].first == rows[i].first; ++j) src.push_back(rows[j].second);
+          ent.push_back(dpgo::SnEntry{rows[i].first, p, s0, static_cast<int>(src.size())});
+          i = j;
+        }
+      }
+      ent_off[g + 1] = static_cast<int>(ent.size());
+      for (int v : nd.S) fpos[v] = -1;
+      for (int v : nd.R) fpos[v] = -1;
+    }
+  }
+  if (std::getenv("DPGO_VERBOSE_CHOL"))
+    std::fprintf(stderr, "[dpgo_hip] exact preconditioner: device factorisation, %d levels, frontal buffers %.3f + %.3f GiB\n",
+                 maxd + 1, 8.0 * level_size[0] / (1 << 30), 8.0 * level_size[1] / (1 << 30));
+  h->fac_level_off = level_off;
+  DPGO_TRY(up(h->fac_nodes, fac_nodes));
+  DPGO_TRY(up(h->fac_off, fac_off));
+  DPGO_TRY(up(h->fac_ch_off, ch_off));
+  DPGO_TRY(up(h->fac_ch, ch));
+  DPGO_TRY(up(h->fac_tp_off, tp_off));
+  DPGO_TRY(up(h->fac_tp, tp));
+  DPGO_TRY(up(h->fac_ent_off, ent_off));
+  DPGO_TRY(up(h->fac_ent, ent));
+  DPGO_TRY(up(h->fac_src, src));
+  HIP_TRY(h->fac_not_pd.ensure(1));
+  for (int q = 0; q < 2; ++q) HIP_TRY(h->fac_F[q].ensure(std::max<long>(level_size[q], 1)));
+  h->sn_sym_ready = true;
+  return device_factor(h);
 }
 
 // z = P_X(in (Q + 0.1 I)^-1) for every agent (QuadraticProblem::PreConditioner, :75-87): the forward sweep
@@ -1180,6 +1321,26 @@ int dpgo_hip_polar_combine_dev(dpgo_hip_problem h, const double* A, const double
 int dpgo_hip_set_tuning(int key, int value) {
   if (key < 0 || key >= dpgo::TUNE_COUNT) return fail(DPGO_HIP_EINVAL, "bad tuning key");
   dpgo::g_tuning[key] = value;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_exact_factor_info(dpgo_hip_problem h, long long* nodes, int* levels, int* max_s_tiles,
+                               long long* panel_doubles, double* factor_ms, int* factor_count) {
+  DPGO_TRY(check_handle(h));
+  if (!nodes || !levels || !max_s_tiles || !panel_doubles || !factor_ms || !factor_count)
+    return fail(DPGO_HIP_EINVAL, "null argument");
+  const long nn = static_cast<long>(h->sn_s.n);
+  *nodes = h->chol_doubles > 0 ? nn : 0;
+  *levels = static_cast<int>(h->sn_levels.size());
+  *max_s_tiles = 0;
+  if (*nodes > 0) {
+    std::vector<int> s(nn);
+    HIP_TRY(hipMemcpy(s.data(), h->sn_s.p, sizeof(int) * nn, hipMemcpyDeviceToHost));
+    for (int v : s) *max_s_tiles = std::max(*max_s_tiles, dpgo::sn_pad(v * h->b) / dpgo::kSnTile);
+  }
+  *panel_doubles = h->chol_doubles;
+  *factor_ms = h->chol_factor_ms;
+  *factor_count = h->chol_factor_count;
   return DPGO_HIP_OK;
 }
 

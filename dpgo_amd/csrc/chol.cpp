@@ -206,10 +206,8 @@ void trmm_right_lower(const double* A, int m, int n, long lda, const double* Lin
 
 }  // namespace
 
-int supernodal_cholesky(int n, int b, const std::vector<int>& rowptr, const std::vector<int>& col,
-                        const std::vector<double>& blocks_colmajor, double shift, long max_doubles,
+int supernodal_symbolic(int n, int b, const std::vector<int>& rowptr, const std::vector<int>& col, long max_doubles,
                         SupernodalFactor& F, std::string& err) {
-  const int bb = b * b;
   F = SupernodalFactor{};
   F.n = n;
   F.b = b;
@@ -291,6 +289,18 @@ int supernodal_cholesky(int n, int b, const std::vector<int>& rowptr, const std:
     for (int v : nd.S) fpos[v] = -1;
     for (int v : nd.R) fpos[v] = -1;
   }
+  return 0;
+}
+
+int supernodal_cholesky(int n, int b, const std::vector<int>& rowptr, const std::vector<int>& col,
+                        const std::vector<double>& blocks_colmajor, double shift, long max_doubles,
+                        SupernodalFactor& F, std::string& err) {
+  const int bb = b * b;
+  if (const int rc = supernodal_symbolic(n, b, rowptr, col, max_doubles, F, err)) return rc;
+  if (n == 0) return 0;
+  auto& nodes = F.nodes;
+  const int nn = static_cast<int>(nodes.size());
+  std::vector<int> fpos(n, -1);
   // ---- numeric, multifrontal in postorder
   std::vector<std::vector<double>> upd(nn);  // update matrices waiting for their parent
   std::vector<double> Fm, Linv, M;

@@ -47,6 +47,13 @@ struct SupernodalFactor {
   long panel_doubles = 0;
 };
 
+// The symbolic half of supernodal_cholesky: the nested-dissection tree, every node's S and R (elimination
+// order), the extend-add maps (to_parent) and panel_doubles; no values (the pattern of Q only; blocks unused).
+// Returns 0, or -1 with err set (the panels would exceed max_doubles).  The device factorisation
+// (kernels.hip k_sn_factor) runs its numeric half on this structure.
+int supernodal_symbolic(int n, int b, const std::vector<int>& rowptr, const std::vector<int>& col, long max_doubles,
+                        SupernodalFactor& F, std::string& err);
+
 // Factorise P = Q + shift I, Q given as symmetric block-sparse rows (block (j, col) column-major), over
 // the nested-dissection supernodes of its block graph (multifrontal, dense frontal matrices).  Returns 0,
 // or -1 with err set (not positive definite, or the panels would exceed max_doubles).

@@ -220,6 +220,41 @@ struct SnView {
   int flag_kind = 0;
 };
 
+// Numeric supernodal factorisation of P = Q + shift I on the device (k_sn_factor), over the symbolic structure the
+// host built once (chol_internal.h supernodal_symbolic): one workgroup per supernode, one launch per tree level
+// (deepest first).  Node g's dense frontal matrix (M x M row-major, M = S_pad + R_pad: the S rows padded to a
+// kSnTileDev multiple, then the R rows) lives at F + f_off[g] in its level's buffer; its children's (one level
+// deeper) in Fchild.  Assembly: the original entries of the S columns from the edge-stream Q (rec / diag, the
+// current weights), then the children's update matrices (extend-add); then the blocked right-looking Cholesky
+// over the S tile columns (leaving L_SS, L_RS and the update matrix U = F_RR - L_RS L_RS^T in place) and the
+// panel [L_SS^-1 ; L_RS L_SS^-1] in the solve's tile layout.  Only the lower triangle of F is kept.
+struct SnEntry {
+  int q, p;    // frontal pose positions (row q >= column p; p in S)
+  int s0, s1;  // edge sources src[s0 .. s1) (2 id + 1: block -M^T, 2 id: block -M); q == p: the diagonal block
+};
+struct SnFactorView {
+  const int* nodes;       // this launch's node ids (one level)
+  const int* s;           // [nodes] poses in S
+  const int* t;           // [nodes] poses in R
+  const long* f_off;      // [nodes] frontal offset in its level's buffer
+  const long* panel_off;  // [nodes]
+  const int* poses_off;   // [nodes] into poses: S then R (batch-global)
+  const int* poses;
+  const int* ch_off;      // [nodes + 1] into ch: children
+  const int* ch;
+  const int* tp_off;      // [nodes] into tp: the node's R entries' positions in its parent's frontal order
+  const int* tp;
+  const int* ent_off;     // [nodes + 1] into ent
+  const SnEntry* ent;
+  const int* src;
+  const double* rec;      // edge-stream Q (current weights)
+  const double* diag;
+  double shift;
+  double* F;              // this level's frontal buffer
+  const double* Fchild;   // the level below
+  double* panel;
+  int* not_pd;            // set to 1 when a pivot is not positive
+};
 // Loop closures one engine colour class reweights (PGOAgent::updateLoopClosuresWeights,
 // src/PGOAgent.cpp:1181-1244): pose sources >= 0 index the engine's X buffer, < 0 -> (-1 - s) the
 // received-pose buffer; weights go to the colour problem's edge and, for shared edges, its G entry.
@@ -255,10 +290,12 @@ enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH =
                                          // streams (one half's VALU-bound HESS_M beside the other's HBM-bound
                                          // k_tcg_updir); 0 off, 1 on (default: 1M -0.7 %, the 125 k
                                          // share -4.6 % ms/step), 2 the halves out of phase (no gain)
+               TUNE_DEVICE_CHOL = 12,  // exact preconditioner over an edge-stream Q: 1 numeric factorisation on the
+                                       // device (k_sn_factor), 0 on the host (chol.cpp, panels uploaded)
                TUNE_SPMM_V2 = 11,  // > 0: the merged partials at kMergedDdSlots (edge variant bit 6) and the rotated
                                    //    accumulator (bit 7) in every mode (1), in none (2), in the merged modes (3);
                                    //    0: the round-3 kernels
-               TUNE_COUNT = 12 };
+               TUNE_COUNT = 13 };
 // dd_mask of the merged tCG partials for the kernel a handle with these tuning keys and Q format runs
 inline int merged_dd_mask(int fmt, const int* tuning) {
   return fmt == QFMT_EDGES && tuning[TUNE_SPMM_V2] > 0 ? kMergedDdSlots : kMergedDdSlotsV1;
@@ -329,6 +366,8 @@ hipError_t launch_sn_assemble(int r, int b, const SnView& v, const int2* items, 
 hipError_t launch_sn_fwd(int r, int b, const SnView& v, const int2* items, int count, double* y, hipStream_t stream);
 hipError_t launch_sn_bwd(int r, int b, const SnView& v, const int2* items, int count, const double* y, double* x,
                          hipStream_t stream);
+// numeric factorisation of one tree level's supernodes (count nodes, v.nodes), see SnFactorView
+hipError_t launch_sn_factor(int b, const SnFactorView& v, int count, hipStream_t stream);
 // z = P_X(zraw) (or z = zraw when project == 0); optional z_out / delta_out = -z; partials
 // <z, rref>, |rref|^2 per tile
 hipError_t launch_precond_finish(int r, int b, const LaunchCtx& c, const double* X, const double* zraw,

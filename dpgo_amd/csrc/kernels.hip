@@ -3328,6 +3328,253 @@ __global__ __launch_bounds__(kThreads) void k_sn_bwd(SnView v, const int2* __res
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Numeric supernodal factorisation on the device (SnFactorView): one workgroup per supernode of one tree level.
+// Dense frontal work in 64 x 64 tiles staged in LDS; the tile products run on the fp64 matrix cores
+// (v_mfma_f64_16x16x4f64: A lane l = A[l & 15][k = l >> 4], B lane l = B[k = l >> 4][l & 15], C/D lane l,
+// register q = C[(l >> 4) + 4 q][l & 15]), one 16-row strip of the output tile per wave.
+// ------------------------------------------------------------------------------------------
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+constexpr int kFT = kSnTileDev;  // 64
+constexpr int kFLD = kFT + 1;    // LDS tile stride (doubles)
+
+// acc (rows r0 .. r0 + 15 of a 64 x 64 tile, four 16-column blocks) += sign * A(strip) . op(B): op(B)[k][c] =
+// B[c][k] (BT) or B[k][c]; A and B are LDS tiles
+template <bool BT>
+__device__ __forceinline__ void mfma_strip(f64x4 (&acc)[4], const double* As, const double* Bs, int r0, double sign) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+#pragma unroll 4
+  for (int k0 = 0; k0 < kFT; k0 += 4) {
+    const double a = sign * As[(r0 + lr) * kFLD + k0 + lk];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const int c = cb * 16 + lr;
+      const double bv = BT ? Bs[c * kFLD + k0 + lk] : Bs[(k0 + lk) * kFLD + c];
+      acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc[cb], 0, 0, 0);
+    }
+  }
+}
+
+// global 64 x 64 tile (row-major, leading dimension ld) <-> LDS tile, all threads
+__device__ __forceinline__ void sn_tile_to_lds(double* Ls, const double* __restrict__ g, long ld) {
+  for (int x = threadIdx.x; x < kFT * kFT; x += kThreads) {
+    const int i = x / kFT, j = x % kFT;
+    Ls[i * kFLD + j] = g[i * ld + j];
+  }
+}
+// the wave's strip of a global tile into / out of the MFMA accumulator layout
+__device__ __forceinline__ void sn_strip_load(f64x4 (&acc)[4], const double* __restrict__ g, long ld, int r0) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[cb][q] = g[(r0 + (l >> 4) + 4 * q) * ld + cb * 16 + (l & 15)];
+}
+__device__ __forceinline__ void sn_strip_store(const f64x4 (&acc)[4], double* __restrict__ g, long ld, int r0) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) g[(r0 + (l >> 4) + 4 * q) * ld + cb * 16 + (l & 15)] = acc[cb][q];
+}
+
+// In-place lower Cholesky of the LDS tile (right-looking, one column per step); a non-positive pivot sets *bad
+__device__ void sn_potrf_lds(double* A, int* bad) {
+  const int tid = threadIdx.x;
+  for (int j = 0; j < kFT; ++j) {
+    if (tid == 0) {
+      const double d = A[j * kFLD + j];
+      if (!(d > 0.0)) *bad = 1;
+      A[j * kFLD + j] = sqrt(d > 0.0 ? d : 1.0);
+    }
+    __syncthreads();
+    const double inv = 1.0 / A[j * kFLD + j];
+    if (tid > j && tid < kFT) A[tid * kFLD + j] *= inv;
+    __syncthreads();
+    const int i = tid & 63;
+    if (i > j) {
+      const double lij = A[i * kFLD + j];
+      for (int k = j + 1 + (tid >> 6); k <= i; k += 4) A[i * kFLD + k] -= lij * A[k * kFLD + j];
+    }
+    __syncthreads();
+  }
+}
+// Linv = L^-1 (lower) of the lower LDS tile L, column c by thread c (forward substitution); upper part zeroed
+__device__ void sn_trtri_lds(const double* L, double* Linv) {
+  const int c = threadIdx.x;
+  if (c < kFT) {
+    for (int i = 0; i < c; ++i) Linv[i * kFLD + c] = 0.0;
+    Linv[c * kFLD + c] = 1.0 / L[c * kFLD + c];
+    for (int i = c + 1; i < kFT; ++i) {
+      double acc = 0.0;
+      for (int k = c; k < i; ++k) acc = fma(L[i * kFLD + k], Linv[k * kFLD + c], acc);
+      Linv[i * kFLD + c] = -acc / L[i * kFLD + i];
+    }
+  }
+  __syncthreads();
+}
+
+// frontal row of (pose position pos, component k): S poses first, then R poses after the S padding
+__device__ __forceinline__ int sn_frow(int pos, int k, int s, int b, int Sp) {
+  return pos < s ? pos * b + k : Sp + (pos - s) * b + k;
+}
+
+template <int B>
+__global__ __launch_bounds__(kThreads) void k_sn_factor(SnFactorView v) {
+  constexpr int D = B - 1, RW = edge_rec_width(D), DW = diag_width(D);
+  __shared__ double As[kFT * kFLD], Bs[kFT * kFLD];
+  __shared__ int s_bad;
+  const int g = v.nodes[blockIdx.x];
+  const int s = v.s[g], t = v.t[g], sb = s * B, tb = t * B, Sp = sn_pad_dev(sb), Rp = sn_pad_dev(tb);
+  const int M = Sp + Rp, NT = M / kFT, ns = Sp / kFT;
+  const long ld = M;
+  double* __restrict__ F = v.F + v.f_off[g];
+  double* __restrict__ panel = v.panel + v.panel_off[g];
+  const int tid = threadIdx.x, wave = tid >> 6;
+  if (tid == 0) s_bad = 0;
+  // ---- assembly: zero the lower triangle (identity on the padding rows), original entries, children
+  const int lane = tid & 63;
+  for (int i = wave; i < M; i += 4) {  // a row per wave, its columns over the lanes
+    const bool pad = (i >= sb && i < Sp) || i >= Sp + tb;
+    for (int j = lane; j <= i; j += 64) F[static_cast<long>(i) * ld + j] = (i == j && pad) ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  const int* poses = v.poses + v.poses_off[g];
+  for (int e = v.ent_off[g] + tid; e < v.ent_off[g + 1]; e += kThreads) {
+    const SnEntry en = v.ent[e];
+    double blk[B][B];  // Q block (pose q, pose p)
+    if (en.q == en.p) {
+      const double* dg = v.diag + static_cast<long>(poses[en.p]) * DW;
+#pragma unroll
+      for (int i = 0; i < B; ++i)
+#pragma unroll
+        for (int j = 0; j < B; ++j) blk[i][j] = dg[sym_index<B>(i, j)] + (i == j ? v.shift : 0.0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < B; ++i)
+#pragma unroll
+        for (int j = 0; j < B; ++j) blk[i][j] = 0.0;
+      for (int k = en.s0; k < en.s1; ++k) {  // in source order (duplicate measurements of one pair)
+        const int code = v.src[k];
+        const double* m = v.rec + static_cast<long>(code >> 1) * RW;
+#pragma unroll
+        for (int i = 0; i < B; ++i)
+#pragma unroll
+          for (int j = 0; j < B; ++j) blk[i][j] -= (code & 1) ? m[4 * j + i] : m[4 * i + j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      const long row = sn_frow(en.q, i, s, B, Sp);
+#pragma unroll
+      for (int j = 0; j < B; ++j) {
+        const int col = en.p * B + j;
+        if (row >= col) F[row * ld + col] += blk[i][j];
+      }
+    }
+  }
+  __syncthreads();
+  for (int ci = v.ch_off[g]; ci < v.ch_off[g + 1]; ++ci) {  // children in order, one at a time
+    const int c = v.ch[ci];
+    const int tcb = v.t[c] * B, Spc = sn_pad_dev(v.s[c] * B);
+    const long ldc = Spc + sn_pad_dev(tcb);
+    const double* __restrict__ U = v.Fchild + v.f_off[c] + Spc * ldc + Spc;
+    const int* tp = v.tp + v.tp_off[c];
+    for (int ri = wave; ri < tcb; ri += 4) {
+      const long pr = sn_frow(tp[ri / B], ri % B, s, B, Sp);
+      for (int rj = lane; rj <= ri; rj += 64) {
+        const long pc = sn_frow(tp[rj / B], rj % B, s, B, Sp);
+        F[pr * ld + pc] += U[static_cast<long>(ri) * ldc + rj];
+      }
+    }
+    __syncthreads();
+  }
+  // ---- blocked right-looking Cholesky over the S tile columns
+  for (int K = 0; K < ns; ++K) {
+    sn_tile_to_lds(As, F + static_cast<long>(K) * kFT * ld + K * kFT, ld);
+    __syncthreads();
+    sn_potrf_lds(As, &s_bad);
+    sn_trtri_lds(As, Bs);
+    for (int x = tid; x < kFT * kFT; x += kThreads) {
+      const int i = x / kFT, j = x % kFT;
+      F[(static_cast<long>(K) * kFT + i) * ld + K * kFT + j] = As[i * kFLD + j];
+      // the panel's diagonal tile: L_KK^-1 with the padding zeroed
+      const bool real = K * kFT + i < sb && K * kFT + j < sb;
+      panel[sn_tile_dev(ns, K, K) * kFT * kFT + x] = real ? Bs[i * kFLD + j] : 0.0;
+    }
+    __syncthreads();
+    // L_IK = F_IK L_KK^-T for every tile row below
+    for (int I = K + 1; I < NT; ++I) {
+      double* gt = F + static_cast<long>(I) * kFT * ld + K * kFT;
+      sn_tile_to_lds(As, gt, ld);
+      __syncthreads();
+      f64x4 acc[4] = {};
+      mfma_strip<true>(acc, As, Bs, wave * 16, 1.0);
+      sn_strip_store(acc, gt, ld, wave * 16);
+      __syncthreads();
+    }
+    // trailing update F_IJ -= L_IK L_JK^T, K < J <= I (the R block becomes the update matrix)
+    for (int I = K + 1; I < NT; ++I) {
+      sn_tile_to_lds(As, F + static_cast<long>(I) * kFT * ld + K * kFT, ld);
+      for (int J = K + 1; J <= I; ++J) {
+        sn_tile_to_lds(Bs, F + static_cast<long>(J) * kFT * ld + K * kFT, ld);
+        __syncthreads();
+        double* gt = F + static_cast<long>(I) * kFT * ld + J * kFT;
+        f64x4 acc[4];
+        sn_strip_load(acc, gt, ld, wave * 16);
+        mfma_strip<true>(acc, As, Bs, wave * 16, -1.0);
+        sn_strip_store(acc, gt, ld, wave * 16);
+        __syncthreads();
+      }
+    }
+  }
+  if (tid == 0 && s_bad) *v.not_pd = 1;
+  // ---- panel: Z = [I ; L_RS] L_SS^-1, tile column J from the last: Z_IJ = (B_IJ - sum_{K > J} Z_IK L_KJ) L_JJ^-1,
+  // B_IJ = 0 (S rows, I != J) or L_RS (R rows); Z_IK = 0 for S rows with K > I
+  for (int J = ns - 1; J >= 0; --J) {
+    for (int I = J + 1; I < NT; ++I) {
+      f64x4 acc[4] = {};
+      if (I >= ns) sn_strip_load(acc, F + static_cast<long>(I) * kFT * ld + J * kFT, ld, wave * 16);
+      const int Kmax = I < ns ? I : ns - 1;
+      for (int K = J + 1; K <= Kmax; ++K) {
+        const double* z = panel + sn_tile_dev(ns, I, K) * kFT * kFT;
+        for (int x = tid; x < kFT * kFT; x += kThreads) As[(x / kFT) * kFLD + x % kFT] = z[x];
+        sn_tile_to_lds(Bs, F + static_cast<long>(K) * kFT * ld + J * kFT, ld);
+        __syncthreads();
+        mfma_strip<false>(acc, As, Bs, wave * 16, -1.0);
+        __syncthreads();
+      }
+      // acc L_JJ^-1: acc through LDS into the A-operand layout, L_JJ^-1 from the panel's diagonal tile
+      {
+        const int l = tid & 63;
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) As[(wave * 16 + (l >> 4) + 4 * q) * kFLD + cb * 16 + (l & 15)] = acc[cb][q];
+      }
+      const double* dj = panel + sn_tile_dev(ns, J, J) * kFT * kFT;
+      for (int x = tid; x < kFT * kFT; x += kThreads) Bs[(x / kFT) * kFLD + x % kFT] = dj[x];
+      __syncthreads();
+      f64x4 z[4] = {};
+      mfma_strip<false>(z, As, Bs, wave * 16, 1.0);
+      {
+        const int l = tid & 63;
+        double* out = panel + sn_tile_dev(ns, I, J) * kFT * kFT;
+        const int rbase = I < ns ? I * kFT : (I - ns) * kFT, rlim = I < ns ? sb : tb;
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int rr = wave * 16 + (l >> 4) + 4 * q, cc = cb * 16 + (l & 15);
+            const bool real = rbase + rr < rlim && J * kFT + cc < sb;
+            out[rr * kFT + cc] = real ? z[cb][q] : 0.0;
+          }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 template <int R, int B>
 __global__ __launch_bounds__(kThreads) void k_precond_finish(LaunchCtx c, const double* __restrict__ X,
                                                              const double* __restrict__ zraw,
@@ -3480,7 +3727,7 @@ template <int MODE>
 hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const SpmmArgs& a);
 
 #ifndef DPGO_SPMM_TU
-int g_tuning[TUNE_COUNT] = {0, -1, 1, 0, 0, 0, 0, 0, 0, 0, 1, 0};
+int g_tuning[TUNE_COUNT] = {0, -1, 1, 0, 0, 0, 0, 0, 0, 0, 1, 0, 1};
 
 bool supported_rb(int r, int b) {
   if (b == 3) return r >= 2 && r <= 8;
@@ -3782,6 +4029,17 @@ hipError_t launch_sn_bwd(int r, int b, const SnView& v, const int2* items, int c
                          hipStream_t stream) {
   if (count == 0) return hipSuccess;
   DPGO_DISPATCH_R(r, (k_sn_bwd<R><<<count, kThreads, 0, stream>>>(v, items, b, y, x)));
+  return hipGetLastError();
+}
+
+hipError_t launch_sn_factor(int b, const SnFactorView& v, int count, hipStream_t stream) {
+  if (count == 0) return hipSuccess;
+  if (b == 4)
+    k_sn_factor<4><<<count, kThreads, 0, stream>>>(v);
+  else if (b == 3)
+    k_sn_factor<3><<<count, kThreads, 0, stream>>>(v);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -123,6 +123,19 @@ struct dpgo_hip_problem_s {
   };
   std::vector<SnLevel> sn_levels;  // index = depth (0 = the roots)
   long chol_doubles = 0;
+  // device numeric factorisation (TUNE_DEVICE_CHOL, edge-stream Q): the symbolic structure is built once per Q
+  // pattern (sn_sym_ready); every refresh after a reweighting re-runs only k_sn_factor, level by level
+  bool sn_sym_ready = false;
+  std::vector<int> fac_level_off;  // [depth + 1] into fac_nodes
+  dpgo::DevBuf<int> fac_nodes, fac_ch_off, fac_ch, fac_tp_off, fac_tp, fac_ent_off, fac_src, fac_not_pd;
+  dpgo::DevBuf<long> fac_off;
+  dpgo::DevBuf<dpgo::SnEntry> fac_ent;
+  dpgo::DevBuf<double> fac_F[2];  // frontal matrices of the even / odd tree depths
+  double chol_factor_ms = 0.0;    // the last device factorisation (hipEvent), for the benches
+  int chol_factor_count = 0;
+  // host copy of the edge-stream incidences (sync_q_edges), for the factor's assembly tables
+  std::vector<int> h_inc_ptr;
+  std::vector<int2> h_inc;
 
   // work
   dpgo::DevBuf<double> x1, x2, g, g2, S, S2, eta, rv, z, delta, Hdelta, tA, tB;
@@ -161,12 +174,14 @@ struct dpgo_hip_problem_s {
   struct TimedLaunch {
     int mode;
     hipEvent_t a, b;
+    double frac;  // the launch's tiles / the batch's tiles (a half-batch launch of the split merged tCG: ~0.5)
   };
   std::vector<TimedLaunch> timed;
   std::vector<hipEvent_t> ev_pool;
   // completed timed launches drained out of `timed` (bounded event count on long timed runs)
   double timed_ms[dpgo::kSpmmModes] = {};
   long long timed_n[dpgo::kSpmmModes] = {};
+  double timed_frac[dpgo::kSpmmModes] = {};  // summed TimedLaunch::frac: full-batch launch equivalents
   ~dpgo_hip_problem_s() {
     for (auto& t : timed) {
       (void)hipEventDestroy(t.a);
@@ -205,7 +220,7 @@ int download_sums_public(dpgo_hip_problem h, std::vector<double>& out);
 // X.Q launch with the handle's optional event timing
 int spmm_launch(dpgo_hip_problem h, int mode, const LaunchCtx& c, const SpmmArgs& a);
 // synchronise and add the elapsed ms / launch counts of the timed launches per SpmmMode (kSpmmModes)
-int take_spmm_times(dpgo_hip_problem h, double* ms_per_mode, long long* launches_per_mode);
+int take_spmm_times(dpgo_hip_problem h, double* ms_per_mode, long long* launches_per_mode, double* batch_equiv);
 // fold completed (wait: all) timed launches into the handle's per-mode running totals
 int drain_timed(dpgo_hip_problem h, bool wait);
 }  // namespace dpgo

@@ -1109,12 +1109,6 @@ int dpgo_rbcd_mode_bytes(dpgo_rbcd e, int color, double* out) {
     out[MODE_QF] += half_in + z.n * SW;
     out[MODE_F] += half_in + gread;
   }
-  if (e->prob[color] && merged_split(e->prob[color])) {
-    // the merged tCG iterations run as two launches over the colour's agent halves (TUNE_SPLIT_STREAMS): the
-    // mean bytes of one such launch
-    out[MODE_HESS_M] *= 0.5;
-    out[MODE_HESS_QF_M] *= 0.5;
-  }
   return DPGO_HIP_OK;
 }
 
@@ -1150,17 +1144,23 @@ int dpgo_rbcd_set_kernel_timing(dpgo_rbcd e, int on) {
   return DPGO_HIP_OK;
 }
 
-int dpgo_rbcd_kernel_times(dpgo_rbcd e, double* ms_per_mode, long long* launches_per_mode) {
+int dpgo_rbcd_kernel_times_ex(dpgo_rbcd e, double* ms_per_mode, long long* launches_per_mode, double* batch_equiv) {
   if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
+  double frac[kSpmmModes] = {};
   for (auto* h : e->prob)
-    if (h) DPGO_TRY(take_spmm_times(h, e->spmm_ms, e->spmm_launches));
+    if (h) DPGO_TRY(take_spmm_times(h, e->spmm_ms, e->spmm_launches, frac));
   for (int m = 0; m < kSpmmModes; ++m) {
     if (ms_per_mode) ms_per_mode[m] = e->spmm_ms[m];
     if (launches_per_mode) launches_per_mode[m] = e->spmm_launches[m];
+    if (batch_equiv) batch_equiv[m] = frac[m];
     e->spmm_ms[m] = 0.0;
     e->spmm_launches[m] = 0;
   }
   return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_kernel_times(dpgo_rbcd e, double* ms_per_mode, long long* launches_per_mode) {
+  return dpgo_rbcd_kernel_times_ex(e, ms_per_mode, launches_per_mode, nullptr);
 }
 
 int dpgo_rbcd_bench_spmm(dpgo_rbcd e, int color, int reps, double* bytes, double* ms) {
@@ -1301,6 +1301,31 @@ int dpgo_rbcd_comm_init(dpgo_rbcd e, const void* id) {
   DPGO_TRY(rccl_check(rccl().CommInitRank(&c, e->world, uid, e->rank), "ncclCommInitRank"));
   e->comm = c;
   e->own_comm = true;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_rbcd_exact_factor_info(dpgo_rbcd e, int color, long long* nodes, int* levels, int* max_s_tiles,
+                                long long* panel_doubles, double* factor_ms, int* factor_count) {
+  if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
+  if (!e->prob[color]) {
+    if (nodes) *nodes = 0;
+    if (levels) *levels = 0;
+    if (max_s_tiles) *max_s_tiles = 0;
+    if (panel_doubles) *panel_doubles = 0;
+    if (factor_ms) *factor_ms = 0.0;
+    if (factor_count) *factor_count = 0;
+    return DPGO_HIP_OK;
+  }
+  return dpgo_hip_exact_factor_info(e->prob[color], nodes, levels, max_s_tiles, panel_doubles, factor_ms, factor_count);
+}
+
+int dpgo_rbcd_comm_info(dpgo_rbcd e, int* count, int* rank) {
+  if (!e || !count || !rank) return fail(DPGO_HIP_EINVAL, "null argument");
+  *count = -1;
+  *rank = -1;
+  if (!e->comm) return DPGO_HIP_OK;
+  DPGO_TRY(rccl_check(rccl().CommCount(e->comm, count), "ncclCommCount"));
+  DPGO_TRY(rccl_check(rccl().CommUserRank(e->comm, rank), "ncclCommUserRank"));
   return DPGO_HIP_OK;
 }
 

@@ -88,6 +88,8 @@ _SIGS = [
     ("dpgo_hip_synchronize", [C.c_void_p], C.c_int),
     ("dpgo_hip_set_tuning", [C.c_int, C.c_int], C.c_int),
     ("dpgo_hip_get_tuning", [C.c_int, C.POINTER(C.c_int)], C.c_int),
+    ("dpgo_hip_exact_factor_info", [C.c_void_p, C.POINTER(C.c_longlong), C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                    C.POINTER(C.c_longlong), C.POINTER(C.c_double), C.POINTER(C.c_int)], C.c_int),
     ("dpgo_hip_problem_set_tuning", [C.c_void_p, C.c_int, C.c_int], C.c_int),
     ("dpgo_hip_spmm_bytes", [C.c_void_p], C.c_double),
     ("dpgo_hip_bench_spmm", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, _dp], C.c_int),
@@ -398,6 +400,15 @@ class Problem:
         _check(lib().dpgo_hip_set_trace(self.h, int(capacity)))
         self._trace_cap = int(capacity)
 
+    def exact_factor_info(self):
+        """The exact preconditioner's factor: supernodes, levels, widest separator (64-row tiles), panel doubles,
+        last device factorisation ms, device factorisations so far."""
+        n, lv, mt, pd, ms, cnt = C.c_longlong(), C.c_int(), C.c_int(), C.c_longlong(), C.c_double(), C.c_int()
+        _check(lib().dpgo_hip_exact_factor_info(self.h, C.byref(n), C.byref(lv), C.byref(mt), C.byref(pd), C.byref(ms),
+                                                C.byref(cnt)))
+        return {"nodes": n.value, "levels": lv.value, "max_s_tiles": mt.value, "panel_doubles": pd.value,
+                "factor_ms": ms.value, "factor_count": cnt.value}
+
     def set_tuning(self, key, value):
         """A tuning key on this handle only (dpgo_hip_problem_set_tuning)."""
         _check(lib().dpgo_hip_problem_set_tuning(self.h, int(key), int(value)))
@@ -502,12 +513,17 @@ _SIGS2 = [
     ("dpgo_rccl_unique_id", [C.c_void_p], C.c_int),
     ("dpgo_rbcd_comm_init", [C.c_void_p, C.c_void_p], C.c_int),
     ("dpgo_rbcd_comm_attach", [C.c_void_p, C.c_void_p], C.c_int),
+    ("dpgo_rbcd_comm_info", [C.c_void_p, _ip, _ip], C.c_int),
+    ("dpgo_rbcd_exact_factor_info", [C.c_void_p, C.c_int, C.POINTER(C.c_longlong), C.POINTER(C.c_int),
+                                     C.POINTER(C.c_int), C.POINTER(C.c_longlong), C.POINTER(C.c_double),
+                                     C.POINTER(C.c_int)], C.c_int),
     ("dpgo_rbcd_exchange", [C.c_void_p, C.POINTER(C.c_void_p)], C.c_int),
     ("dpgo_rbcd_set_kernel_timing", [C.c_void_p, C.c_int], C.c_int),
     ("dpgo_rbcd_set_tuning", [C.c_void_p, C.c_int, C.c_int], C.c_int),
     ("dpgo_rbcd_set_trace", [C.c_void_p, C.c_int], C.c_int),
     ("dpgo_rbcd_get_trace", [C.c_void_p, C.c_int, _dp, C.c_int, _ip], C.c_int),
     ("dpgo_rbcd_kernel_times", [C.c_void_p, _dp, _lp], C.c_int),
+    ("dpgo_rbcd_kernel_times_ex", [C.c_void_p, _dp, _lp, _dp], C.c_int),
     ("dpgo_rbcd_plan_color", [C.c_void_p, C.c_int, _ip, _ip, C.c_int, C.c_int, C.c_int, _lp, _lp, _ip, _ip], C.c_int),
     ("dpgo_rbcd_exchange_counts_color", [C.c_void_p, C.c_int, _lp, _lp], C.c_int),
     ("dpgo_rbcd_pack_color", [C.c_void_p, C.c_int, C.c_void_p], C.c_int),
@@ -830,6 +846,20 @@ class Rbcd:
         buf = C.create_string_buffer(bytes(uid), 128)
         _check(lib().dpgo_rbcd_comm_init(self.h, buf))
 
+    def exact_factor_info(self, color):
+        """Problem.exact_factor_info of the colour's batched problem."""
+        n, lv, mt, pd, ms, cnt = C.c_longlong(), C.c_int(), C.c_int(), C.c_longlong(), C.c_double(), C.c_int()
+        _check(lib().dpgo_rbcd_exact_factor_info(self.h, int(color), C.byref(n), C.byref(lv), C.byref(mt), C.byref(pd),
+                                                 C.byref(ms), C.byref(cnt)))
+        return {"nodes": n.value, "levels": lv.value, "max_s_tiles": mt.value, "panel_doubles": pd.value,
+                "factor_ms": ms.value, "factor_count": cnt.value}
+
+    def comm_info(self):
+        """(ncclCommCount, ncclCommUserRank) of the engine's own RCCL communicator, (-1, -1) without one."""
+        n, r = C.c_int(), C.c_int()
+        _check(lib().dpgo_rbcd_comm_info(self.h, C.byref(n), C.byref(r)))
+        return n.value, r.value
+
     def exchange_color(self, color):
         """Per-colour halo by the engine's RCCL group (after pre_exchange(color)); pass the result to
         update_color()."""
@@ -882,11 +912,16 @@ class Rbcd:
         """A tuning key on this engine's colour problems (A/B timing without rebuilding the engine)."""
         _check(lib().dpgo_rbcd_set_tuning(self.h, int(key), int(value)))
 
-    def kernel_times(self):
-        """{mode: (ms summed, launches)} of the timed in-step X.Q launches since the last call."""
+    def kernel_times(self, batch_equiv=False):
+        """{mode: (ms summed, launches)} of the timed in-step X.Q launches since the last call; with batch_equiv,
+        (ms, launches, full-batch launch equivalents) -- the divisor of mode_bytes for a per-launch rate."""
         ms = np.zeros(len(SPMM_MODES))
         n = np.zeros(len(SPMM_MODES), np.int64)
-        _check(lib().dpgo_rbcd_kernel_times(self.h, ms.ctypes.data_as(_dp), n.ctypes.data_as(_lp)))
+        fr = np.zeros(len(SPMM_MODES))
+        _check(lib().dpgo_rbcd_kernel_times_ex(self.h, ms.ctypes.data_as(_dp), n.ctypes.data_as(_lp),
+                                               fr.ctypes.data_as(_dp)))
+        if batch_equiv:
+            return {SPMM_MODES[m]: (float(ms[m]), int(n[m]), float(fr[m])) for m in range(len(SPMM_MODES)) if n[m] > 0}
         return {SPMM_MODES[m]: (float(ms[m]), int(n[m])) for m in range(len(SPMM_MODES)) if n[m] > 0}
 
     def pre_exchange(self, color):

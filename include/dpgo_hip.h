@@ -237,6 +237,11 @@ int dpgo_hip_certify(dpgo_hip_problem h, const double* X, int max_iters, double 
  * DESIGN.md records each key's measurement.  These are the process DEFAULTS: a handle copies them when it is
  * created, so handles created afterwards follow; dpgo_hip_problem_set_tuning changes one existing handle. */
 int dpgo_hip_set_tuning(int key, int value);
+/* The exact preconditioner's factor of the handle (after a solve that used it): supernodes, tree levels, the
+ * widest separator in 64-row tiles, panel doubles, and the last device factorisation's time (ms, 0 when it ran on
+ * the host) with the number of device factorisations so far. */
+int dpgo_hip_exact_factor_info(dpgo_hip_problem h, long long* nodes, int* levels, int* max_s_tiles,
+                               long long* panel_doubles, double* factor_ms, int* factor_count);
 /* The process default of a tuning key. */
 int dpgo_hip_get_tuning(int key, int* value);
 /* The same keys on one existing handle (A/B timing of variants on one problem without rebuilding it). */

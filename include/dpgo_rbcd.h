@@ -209,6 +209,11 @@ int dpgo_rbcd_bytes(dpgo_rbcd e, double* bytes, double* evaltcg_bytes_per_color)
 int dpgo_rccl_unique_id(void* id_out);
 int dpgo_rbcd_comm_init(dpgo_rbcd e, const void* id);
 int dpgo_rbcd_comm_attach(dpgo_rbcd e, void* comm);
+/* dpgo_hip_exact_factor_info of the colour's batched problem (zeros when this rank owns none of its agents) */
+int dpgo_rbcd_exact_factor_info(dpgo_rbcd e, int color, long long* nodes, int* levels, int* max_s_tiles,
+                                long long* panel_doubles, double* factor_ms, int* factor_count);
+/* The engine's RCCL communicator as RCCL sees it (ncclCommCount, ncclCommUserRank); -1, -1 without one. */
+int dpgo_rbcd_comm_info(dpgo_rbcd e, int* count, int* rank);
 int dpgo_rbcd_exchange(dpgo_rbcd e, const double** recv_dev);
 /* the per-colour halo of colour c by the same RCCL group (then dpgo_rbcd_update_color) */
 int dpgo_rbcd_exchange_color(dpgo_rbcd e, int color, const double** recv_dev);
@@ -216,9 +221,9 @@ int dpgo_rbcd_exchange_color(dpgo_rbcd e, int color, const double** recv_dev);
  * HESS_M, HESS_QF_M (the last two: the merged tCG iteration's Hessian passes) */
 #define DPGO_SPMM_MODES 11
 /* Algorithmic bytes of one X.Q launch over every agent of `color`, per SpMM mode (out[DPGO_SPMM_MODES], indexed as
- * dpgo_rbcd_kernel_times; 0 for modes the engine does not launch in a step).  Where the colour's merged tCG runs
- * as two half-batch launches on two streams (small batches, tuning key 10) HESS_M / HESS_QF_M give the mean bytes
- * of one such launch (half the colour's). */
+ * dpgo_rbcd_kernel_times; 0 for modes the engine does not launch in a step).  A launch over part of the batch (the
+ * merged tCG's half-batch launches on two streams, tuning key 10) moves its share of these bytes: divide by
+ * dpgo_rbcd_kernel_times_ex's full-batch equivalents, not by the launch count. */
 int dpgo_rbcd_mode_bytes(dpgo_rbcd e, int color, double* out);
 /* HIP events around in-step X.Q launches (on the launch stream): `period` 0 = off, 1 = every launch, k = every
  * k-th launch of each mode (a sample: an event pair adds a dispatch gap of a few microseconds around its launch);
@@ -232,6 +237,9 @@ int dpgo_rbcd_set_tuning(dpgo_rbcd e, int key, int value);
 int dpgo_rbcd_set_trace(dpgo_rbcd e, int capacity);
 int dpgo_rbcd_get_trace(dpgo_rbcd e, int agent, double* out, int max_records, int* count);
 int dpgo_rbcd_kernel_times(dpgo_rbcd e, double* ms_per_mode, long long* launches_per_mode);
+/* dpgo_rbcd_kernel_times plus, per mode, the timed launches' summed share of their batch's tiles (full-batch launch
+ * equivalents: a launch over every agent counts 1, a half-batch launch about 0.5); any pointer may be null. */
+int dpgo_rbcd_kernel_times_ex(dpgo_rbcd e, double* ms_per_mode, long long* launches_per_mode, double* batch_equiv);
 
 #ifdef __cplusplus
 }

@@ -829,7 +829,8 @@ void* dpgo_cpu_rbcd_create(int d, int r, int m, const int* p1, const int* p2, co
   E->X.assign(L, 0.0);
   E->Y.assign(L, 0.0);
   E->V.assign(L, 0.0);
-  E->work.resize(std::max(1, omp_get_max_threads()));
+  // one workspace per thread of the widest team an iterate may request (a colour's agents: the all-cores leg)
+  E->work.resize(std::max(32, omp_get_max_threads()));
   return E;
 }
 

@@ -170,15 +170,15 @@ def max_threads():
 
 
 def host_cores():
-    """(threads the baseline runs, CPUs this process may run on, OpenMP's default team): the baseline uses
-    OpenMP's team (OMP_NUM_THREADS: on the GPU box the pool's per-GPU host share, 16) capped by the affinity
-    mask, never more than a colour's agents can use."""
+    """(threads of the all-cores leg, CPUs this process may run on, OpenMP's default team).  SURVEY 8d(b): OpenMP
+    over a colour's agents on all host cores, i.e. min(32 = the agents of a colour, CPUs in the affinity mask);
+    the OpenMP team (OMP_NUM_THREADS: on the GPU box the pool's per-GPU host share, 16) is timed as a second leg."""
     try:
         avail = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         avail = os.cpu_count() or 1
     omp = max_threads()
-    return max(1, min(omp, avail, 32)), avail, omp
+    return max(1, min(avail, 32)), avail, omp
 
 
 def engine_baseline(graph, agent_of_pose, X_start, r, accel, num_agents, warmup=3, rounds=20, robust="L2"):
@@ -198,23 +198,31 @@ def engine_baseline(graph, agent_of_pose, X_start, r, accel, num_agents, warmup=
     _, sec = E.iterate(threads=T, timed_serial=ns)  # iteration 0: ns updates serially, the rest in parallel
     serial = [sec[a] for a in range(num_agents) if E.colors[a] == 0 and not np.isnan(sec[a])][:ns]
     one = float(np.median(serial[warmup:])) if len(serial) > warmup else float("nan")
-    walls, sel_counts = [], []
-    for it in range(1, 1 + warmup + rounds):
-        w, s = E.iterate(threads=T)
-        walls.append(w)
-        sel_counts.append(int(np.sum(~np.isnan(s))))
-    med = float(np.median(walls[warmup:]))
-    upd = float(np.median(sel_counts[warmup:]))
+    def leg(threads):
+        walls, sel_counts = [], []
+        for it in range(warmup + rounds):
+            w, s = E.iterate(threads=threads)
+            walls.append(w)
+            sel_counts.append(int(np.sum(~np.isnan(s))))
+        return float(np.median(walls[warmup:])), float(np.median(sel_counts[warmup:]))
+    med, upd = leg(T)
+    T_share = max(1, min(omp, avail, 32))
+    share = None
+    if T_share != T:
+        ms_, us_ = leg(T_share)
+        share = {"value": us_ / ms_, "threads": T_share, "seconds_per_iteration": ms_,
+                 "what": "the OpenMP team (OMP_NUM_THREADS: the GPU box's per-GPU host share)"}
     res = {"value": upd / med, "unit": "RBCD agent-updates/s", "cores": T, "kind": "port",
            "sample": (f"oracle/cpu colour-schedule RBCD ({robust}, Nesterov={bool(accel)}, block-Jacobi on both sides: "
                       f"CHOLMOD absent) from the GPU timed region's start X; {T} OpenMP threads (of {avail} CPUs in "
-                      f"the affinity mask; OMP team {omp}): median of {rounds} colour iterations ({upd:.0f} agent "
+                      f"the affinity mask, capped at a colour's 32 agents; OMP team {omp} timed as omp_team_leg): median of {rounds} colour iterations ({upd:.0f} agent "
                       f"updates each, OpenMP over them) after {warmup} warm-up; one thread: median of "
                       f"{max(len(serial) - warmup, 0)} single agent updates after {warmup}"),
            "threads": T, "affinity_cpus": avail, "omp_max_threads": omp, "isa": ISA,
            "seconds_per_iteration_all_cores": med,
            "single_thread": {"value": 1.0 / one if one > 0 else None, "seconds_per_agent_update": one,
                              "cores": 1},
+           "omp_team_leg": share,
            "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
-    iters = 1 + warmup + rounds
+    iters = 1 + (warmup + rounds) * (2 if share is not None else 1)
     return res, E.get_X(), E.stats(), iters

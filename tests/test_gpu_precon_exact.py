@@ -164,3 +164,107 @@ def test_exact_lookahead_bitwise(hip):
             for x, y in zip(out[0][2][a], o[2][a]):
                 assert x == y
     assert out[0][1][:, 10].sum() > 0  # CG steps were taken
+
+
+def _grid_meas(hip, k, seed):
+    g = hip.Graph.grid3d(k, seed=seed)
+    a = g.arrays()
+    meas = O.Measurements(3, np.zeros(g.m, np.int64), np.zeros(g.m, np.int64), a["p1"].astype(np.int64),
+                          a["p2"].astype(np.int64), a["R"], a["t"], a["kappa"], a["tau"], np.ones(g.m), g.n)
+    return g, meas
+
+
+@pytest.mark.parametrize("k", [12, 20])
+def test_device_factor_large_separator(hip, k):
+    """The exact preconditioner at d = 3, r = 5 on one agent large enough that its top separator spans many 64-row
+    tiles (grid3d k = 20: 8000 poses, a 400-pose top separator = 25 tile rows, the C5 agents' shape at 1/8 the
+    volume), with the numeric factorisation on the device (k_sn_factor, TUNE_DEVICE_CHOL = 1, the default) and on
+    the host (0): single applications against the oracle's sparse LU at 1e-10, and the two factorisations against
+    each other at 1e-12 (the same symbolic structure; only the summation order of the dense steps differs)."""
+    g, meas = _grid_meas(hip, k, 7)
+    d, n, r = 3, g.n, 5
+    Q = O.connection_laplacian(meas, n)
+    P = O.QuadraticProblem(n, d, r)
+    P.set_Q(Q)
+    X = random_point(r, d, n, 61)
+    V = random_tangent(X, d, 62)
+    ref = P.precondition(X, V, O.PRECON_EXACT)
+    got = {}
+    for dev in (1, 0):
+        H = hip.Problem(n, d, r)
+        H.set_tuning(12, dev)
+        H.set_Q_edges(0, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau, meas.weight)
+        H.set_precon(hip.PRECON_EXACT)
+        got[dev] = H.precondition(X, V)
+        info = H.exact_factor_info()
+        assert info["factor_count"] == dev
+        if k == 20:
+            assert info["max_s_tiles"] >= 8, info
+        assert rel(got[dev], ref) <= 1e-10, (dev, rel(got[dev], ref))
+    assert rel(got[1], got[0]) <= 1e-12
+
+
+def test_device_refactor_after_reweighting(hip):
+    """set_edge_weights_dev (the on-device GNC reweighting) leaves the pattern and refreshes only the numeric half:
+    the next application re-runs k_sn_factor on the new weights and matches the oracle's LU of the reweighted Q."""
+    g, meas = _grid_meas(hip, 8, 9)
+    d, n, r = 3, g.n, 5
+    rng = np.random.default_rng(3)
+    w = rng.uniform(0.05, 1.0, g.m)
+    X = random_point(r, d, n, 63)
+    V = random_tangent(X, d, 64)
+    H = hip.Problem(n, d, r)
+    H.set_Q_edges(0, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau, meas.weight)
+    H.set_precon(hip.PRECON_EXACT)
+    H.precondition(X, V)
+    import torch
+    wd = torch.tensor(w, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    H.set_edge_weights_dev(wd.data_ptr())
+    z = H.precondition(X, V)
+    assert H.exact_factor_info()["factor_count"] == 2
+    mw = O.Measurements(3, meas.r1, meas.r2, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau, w, n)
+    P = O.QuadraticProblem(n, d, r)
+    P.set_Q(O.connection_laplacian(mw, n))
+    assert rel(z, P.precondition(X, V, O.PRECON_EXACT)) <= 1e-10
+
+
+@pytest.mark.parametrize("robust", ["L2", "GNC_TLS"])
+def test_engine_exact_matches_oracle(hip, robust):
+    """The engine's colour schedule with the exact preconditioner (the reference's default) on grid3d k = 24 with 8
+    agents of 12^3 poses (L2), and k = 8 with outliers under GNC_TLS (reweighting every 3 iterations: the factor is
+    refreshed on the device after each), against the oracle's PGOAgent colour schedule at 1e-9 with the same
+    solver counters."""
+    k, A, r = (24, 2, 5) if robust == "L2" else (8, 2, 5)
+    iters = 6 if robust == "L2" else 8
+    g, meas = _grid_meas(hip, k, 11)
+    if robust != "L2":
+        a = g.arrays()
+        p1, p2 = a["p1"].astype(np.int64), a["p2"].astype(np.int64)
+        t = a["t"].copy()
+        lc = np.nonzero(np.abs(p2 - p1) != 1)[0]
+        bad = np.random.default_rng(5).choice(lc, size=max(1, len(lc) // 10), replace=False)
+        t[bad] += np.random.default_rng(6).normal(0.0, 5.0, size=(len(bad), 3))
+        g0 = g
+        g = hip.Graph.from_arrays(3, g0.n, p1, p2, a["R"], t, a["kappa"], a["tau"])
+        meas = O.Measurements(3, np.zeros(len(p1), np.int64), np.zeros(len(p1), np.int64), p1, p2, a["R"], t,
+                              a["kappa"], a["tau"], np.ones(len(p1)), g0.n)
+        aop = g0.grid_partition(A)
+        X0 = g0.chain_init(r, O.lifting_matrix(3, r))
+    else:
+        aop = g.grid_partition(A)
+        X0 = g.chain_init(r, O.lifting_matrix(3, r))
+    e = hip.Rbcd(g, aop, np.zeros(A ** 3, np.int32), 0, 1,
+                 hip.rbcd_params(r=r, acceleration=1, robust_cost=hip.ROBUST[robust], robust_opt_inner_iters=3,
+                                 precon=hip.PRECON_EXACT))
+    e.set_X(X0)
+    for it in range(iters):
+        e.pre_exchange(it % e.num_colors)
+        e.update(it % e.num_colors, None)
+    out = np.zeros(X0.size)
+    e.get_X_into(out)
+    Xo, _ = O.colour_rbcd(meas, aop, A ** 3, X0, iters, r, acceleration=True, robust=robust,
+                          robust_opt_inner_iters=3, precon=O.PRECON_EXACT)
+    assert rel(hip.from_dev_layout(out, r), Xo) <= 1e-9
+    if robust != "L2":
+        assert sum(e.exact_factor_info(c)["factor_count"] for c in range(e.num_colors)) >= 3
