@@ -272,6 +272,7 @@ def main():
             torch.empty_like(cx).copy_(cx)
         st0 = eng.stats().copy()
         b0, _ = eng.bytes()
+        fc0 = sum(eng.exact_factor_info(c)["factor_count"] for c in range(eng.num_colors)) if args.precon == "exact" else 0
         eng.kernel_times()  # drop anything recorded so far
         eng.set_kernel_timing(args.kernel_timing)
         sync()
@@ -281,6 +282,8 @@ def main():
         sync()
         elapsed = time.perf_counter() - t0
         eng.set_kernel_timing(0)
+        refactor_in_timed = (sum(eng.exact_factor_info(c)["factor_count"] for c in range(eng.num_colors)) - fc0
+                             if args.precon == "exact" else 0)
         ktimes = eng.kernel_times(batch_equiv=True)
         st1 = eng.stats().copy()
         b1, _ = eng.bytes()
@@ -461,6 +464,11 @@ def main():
         "init": init_info,
     }
     out["comm"] = comm
+    if args.precon == "exact":
+        # the factor of Q + 0.1 I per colour batch: tree, size, and the device numeric factorisation (it re-runs after
+        # every GNC reweighting, inside the timed steps when one falls there)
+        out["exact_factor"] = {f"color{c}": eng.exact_factor_info(c) for c in range(eng.num_colors)}
+        out["exact_factor"]["refactorisations_in_timed_steps"] = refactor_in_timed
     out["halo"] = {"kind": args.halo if world > 1 else "none (one rank)",
                    "bytes_sent_per_step_this_rank": 8.0 * (sum(sum(v) for v in c_in) if args.halo == "color"
                                                            else eng.num_colors * int(eng.send_counts.sum())),

@@ -3727,7 +3727,7 @@ template <int MODE>
 hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const SpmmArgs& a);
 
 #ifndef DPGO_SPMM_TU
-int g_tuning[TUNE_COUNT] = {0, -1, 1, 0, 0, 0, 0, 0, 0, 0, 1, 0, 1};
+int g_tuning[TUNE_COUNT] = {0, -1, 1, 0, 0, 0, 0, 0, 0, 0, 1, 4, 1};
 
 bool supported_rb(int r, int b) {
   if (b == 3) return r >= 2 && r <= 8;

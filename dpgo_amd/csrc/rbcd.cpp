@@ -39,6 +39,8 @@ struct dpgo_rbcd_s {
   hipStream_t side = nullptr;
   hipEvent_t ev_start = nullptr, ev_sel = nullptr;
   bool sel_pending = false;
+  // colour of the last pre_exchange (-1 after set_X): a robust cost over several ranks needs the cyclic schedule
+  int last_color = -1;
   std::vector<dpgo_hip_problem> prob;     // per colour (nullptr if none owned)
   DevBuf<double> X, Y, V, Xprev;
   // exchange: the public poses' X only.  With Nesterov a receiver uses its neighbours' aux poses
@@ -745,8 +747,19 @@ int dpgo_rbcd_exchange_counts(dpgo_rbcd e, long long* send_counts, long long* re
   return DPGO_HIP_OK;
 }
 
+// The selected colour's updateY / XPrev copy / deferred updateV that dpgo_rbcd_pre_exchange queued on the side stream:
+// every entry point that reads or writes Y, V or XPrev joins it first (the launch stream waits on its event).
+static int join_side(dpgo_rbcd e) {
+  if (e->sel_pending) {
+    HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_sel, 0));
+    e->sel_pending = false;
+  }
+  return DPGO_HIP_OK;
+}
+
 int dpgo_rbcd_set_X(dpgo_rbcd e, const double* Xg) {
   if (!e || !Xg) return fail(DPGO_HIP_EINVAL, "null argument");
+  DPGO_TRY(join_side(e));
   const size_t rbs = e->rb();
   std::vector<double> host(std::max<size_t>(static_cast<size_t>(e->Nown) * rbs, 1));
   for (long q = 0; q < e->Nown; ++q)
@@ -763,12 +776,14 @@ int dpgo_rbcd_set_X(dpgo_rbcd e, const double* Xg) {
   e->gamma = 0.0;
   e->alpha = 0.0;
   e->iteration = 0;
+  e->last_color = -1;
   std::fill(e->v_pending.begin(), e->v_pending.end(), 0);
   return DPGO_HIP_OK;
 }
 
 int dpgo_rbcd_get_X(dpgo_rbcd e, double* Xg) {
   if (!e || !Xg) return fail(DPGO_HIP_EINVAL, "null argument");
+  DPGO_TRY(join_side(e));
   const size_t rbs = e->rb();
   std::vector<double> host(std::max<size_t>(static_cast<size_t>(e->Nown) * rbs, 1));
   if (e->Nown) {
@@ -786,6 +801,15 @@ static bool restart_now(dpgo_rbcd e) {
 
 int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color) {
   if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
+  DPGO_TRY(join_side(e));  // a second pre_exchange without an update in between
+  // With a robust cost the non-selected agents' reweighting reads their neighbours' poses: in place on this rank,
+  // from the last halo that carried them across ranks.  Under the cyclic colour schedule (the example driver's,
+  // the bench's) both are the poses of the neighbours' last update, so every rank count and halo kind give bitwise
+  // the same weights; out of order they would differ by the halo's vintage, so that case is refused.
+  if (e->P.robust_cost != DPGO_ROBUST_L2 && e->world > 1 && e->last_color >= 0 &&
+      color != (e->last_color + 1) % e->ncolors)
+    return fail(DPGO_HIP_EINVAL, "a robust cost over several ranks needs the cyclic colour schedule (colour t mod C)");
+  e->last_color = color;
   e->iteration += 1;  // mIterationNumber++ (:643)
   // shouldUpdateLoopClosureWeights (:1174-1179): every agent reweights at the start of its iterate;
   // the non-selected ones here, the selected ones in dpgo_rbcd_update once their neighbours' poses
@@ -865,7 +889,8 @@ int dpgo_rbcd_pack(dpgo_rbcd e, double* send_dev) {
 
 // A per-colour halo refreshes only the RX slots the selected colour reads.  With two colours that is also
 // every slot a non-selected colour's reweighting reads at the next iteration (its neighbours are exactly the
-// poses its own last exchange brought); with more colours and a robust cost the engine keeps the full halo.
+// poses its own last exchange brought) under the cyclic schedule, which dpgo_rbcd_pre_exchange requires of a
+// robust cost over several ranks; with more colours and a robust cost the engine keeps the full halo.
 static bool halo_color_ok(dpgo_rbcd e) { return e->ncolors <= 2 || e->P.robust_cost == DPGO_ROBUST_L2; }
 
 int dpgo_rbcd_pack_color(dpgo_rbcd e, int color, double* send_dev) {
@@ -917,10 +942,7 @@ int dpgo_rbcd_update_color(dpgo_rbcd e, int color, const double* recv_dev, dpgo_
 }
 
 static int update_body(dpgo_rbcd e, int color, dpgo_opt_result* results) {
-  if (e->sel_pending) {  // the selected colour's updateY from the side stream (dpgo_rbcd_pre_exchange)
-    HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_sel, 0));
-    e->sel_pending = false;
-  }
+  DPGO_TRY(join_side(e));  // the selected colour's updateY from the side stream (dpgo_rbcd_pre_exchange)
   const bool restart = restart_now(e);
   if (e->gnc_due) {
     DPGO_TRY(reweight_color(e, color));
@@ -962,6 +984,7 @@ static int update_body(dpgo_rbcd e, int color, dpgo_opt_result* results) {
 }
 
 int dpgo_rbcd_central_eval(dpgo_rbcd e, const double* recv_dev, double* f_out, double* gradnorm_sq) {
+  if (e) DPGO_TRY(join_side(e));
   if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
   if (e->n_recv_poses > 0) {
     if (!recv_dev) return fail(DPGO_HIP_EINVAL, "receive buffer required");
@@ -993,6 +1016,7 @@ int dpgo_rbcd_central_eval(dpgo_rbcd e, const double* recv_dev, double* f_out, d
 }
 
 int dpgo_rbcd_status(dpgo_rbcd e, double* rel_change, int* ready) {
+  if (e) DPGO_TRY(join_side(e));
   if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
   for (int c = 0; c < e->ncolors; ++c) {
     dpgo_hip_problem h = e->prob[c];

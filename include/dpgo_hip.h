@@ -37,9 +37,12 @@ extern "C" {
 #define DPGO_HIP_ESTATE (-5)
 
 /* Preconditioner modes (QuadraticProblem::PreConditioner, src/QuadraticProblem.cpp:75-87).
- * EXACT: the reference's own -- P_X(V (Q + 0.1 I)^-1) with a block Cholesky factor built on the
- * host once per Q (nested dissection order) and level-scheduled triangular solves on the GPU; if
- * Q + 0.1 I is not positive definite it falls back to the identity, as the reference does (:81-86).
+ * EXACT: the reference's own -- P_X(V (Q + 0.1 I)^-1) with a supernodal multifrontal Cholesky factor of
+ * Q + 0.1 I: nested-dissection tree built on the host once per Q pattern, numeric factorisation on the GPU for an
+ * edge-stream Q (per tree level, dense frontal tiles on the fp64 matrix cores; again after every on-device
+ * reweighting) or on the host for a BSR Q; each application is two sweeps of dense panel products
+ * [L_SS^-1 ; L_RS L_SS^-1] per supernode, one launch per tree level and sweep.  If Q + 0.1 I is not positive
+ * definite it falls back to the identity, as the reference does (:81-86).
  * BLOCK_JACOBI: per-pose (Q_jj + 0.1 I)^-1 (the north_star's throughput choice). NONE: identity. */
 #define DPGO_PRECON_EXACT 0
 #define DPGO_PRECON_BLOCK_JACOBI 1

@@ -125,3 +125,48 @@ def test_two_ranks_bitwise_one_rank_and_oracle(accel, robust, halo):
     Xo, _ = O.colour_rbcd(meas, aop, A ** 3, X0, ITERS, R, acceleration=accel, robust=robust,
                           robust_opt_inner_iters=3)
     assert rel(H.from_dev_layout(Xflat, R), Xo) <= 1e-9
+
+
+def _order_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dpgo_amd import hip as H
+        g = H.Graph.grid3d(K, seed=5)
+        aop = g.grid_partition(A)
+        ranks = (np.arange(A ** 3) * world // A ** 3).astype(np.int32)
+        res = []
+        for robust in ("L2", "GNC_TLS"):
+            e = H.Rbcd(g, aop, ranks, rank, world, _params(H, False, robust))
+            e.set_X(g.chain_init(R, O.lifting_matrix(3, R)))
+            e.pre_exchange(0)
+            try:
+                e.pre_exchange(0)  # colour 0 twice in a row: not the cyclic schedule
+                res.append((robust, "ok"))
+            except H.DPGOHipError as exc:
+                res.append((robust, str(exc)))
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_robust_cost_needs_cyclic_order_across_ranks():
+    """with a robust cost the non-selected agents' reweighting reads neighbour poses in place on their rank
+    and from the last halo across ranks; those agree (bitwise, rank-count invariant) under the cyclic colour schedule
+    only, so on several ranks an out-of-order colour is refused, and accepted with the L2 cost."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_order_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=240) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    for _, res in outs:
+        d = dict(res)
+        assert d["L2"] == "ok"
+        assert "cyclic colour schedule" in d["GNC_TLS"]

@@ -57,6 +57,7 @@ def main():
         eng.get_X_into(Xb)
         res = {v: [] for v in a.values}
         hvp = {v: [] for v in a.values}
+        xqs = {}
         fin = {}
         for rnd in range(a.rounds):
             for v in a.values:
@@ -76,12 +77,15 @@ def main():
                         kt[v].setdefault(m, []).append(1e3 * tot / max(cnt, 1))
                 f, _ = eng.central_eval()
                 hv = eng.bench_hvp(0, 20)
+                _, xq = eng.bench_spmm(0, 20)
                 res[v].append(ms)
                 hvp[v].append(hv)
+                xqs.setdefault(v, []).append(xq)
                 fin.setdefault(v, f)
                 print(json.dumps({"round": rnd, "value": v, "ms_per_step": ms, "hvp_ms": hv, "f": f}), flush=True)
     print(json.dumps({"key": a.key, "median_ms_per_step": {v: float(np.median(res[v])) for v in a.values},
                       "median_hvp_ms": {v: float(np.median(hvp[v])) for v in a.values},
+                      "median_xq_ms": {v: float(np.median(xqs[v])) for v in a.values},
                       "f_after": fin,
                       "median_kernel_us": {v: {m: float(np.median(x)) for m, x in kt[v].items()} for v in a.values}}),
           flush=True)
