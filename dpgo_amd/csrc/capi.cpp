@@ -443,14 +443,19 @@ int device_factor(dpgo_hip_problem h) {
   HIP_TRY(hipEventCreate(&e0));
   HIP_TRY(hipEventCreate(&e1));
   HIP_TRY(hipEventRecord(e0, h->stream));
+  const bool verbose = std::getenv("DPGO_VERBOSE_CHOL") != nullptr;
+  std::vector<hipEvent_t> lev(verbose ? maxd + 2 : 0, nullptr);
+  for (auto& ev : lev) HIP_TRY(hipEventCreate(&ev));
   for (int dep = maxd; dep >= 0; --dep) {
     const int n0 = h->fac_level_off[dep], n1 = h->fac_level_off[dep + 1];
     dpgo::SnFactorView v{h->fac_nodes.p + n0, h->sn_s.p, h->sn_t.p, h->fac_off.p, h->sn_panel_off.p, h->sn_poses_off.p,
                          h->sn_poses.p, h->fac_ch_off.p, h->fac_ch.p, h->fac_tp_off.p, h->fac_tp.p, h->fac_ent_off.p,
                          h->fac_ent.p, h->fac_src.p, h->rec.p, h->diag.p, 0.1, h->fac_F[dep & 1].p,
                          h->fac_F[(dep + 1) & 1].p, h->sn_panel.p, h->fac_not_pd.p};
+    if (verbose) HIP_TRY(hipEventRecord(lev[dep + 1], h->stream));
     HIP_TRY(dpgo::launch_sn_factor(h->b, v, n1 - n0, h->stream));
   }
+  if (verbose) HIP_TRY(hipEventRecord(lev[0], h->stream));
   HIP_TRY(hipEventRecord(e1, h->stream));
   int bad = 0;
   HIP_TRY(hipMemcpyAsync(&bad, h->fac_not_pd.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
@@ -461,8 +466,17 @@ int device_factor(dpgo_hip_problem h) {
   (void)hipEventDestroy(e1);
   h->chol_factor_ms = ms;
   h->chol_factor_count += 1;
-  if (std::getenv("DPGO_VERBOSE_CHOL"))
-    std::fprintf(stderr, "[dpgo_hip] exact preconditioner: device factorisation %.2f ms\n", static_cast<double>(ms));
+  if (verbose) {
+    std::fprintf(stderr, "[dpgo_hip] exact preconditioner: device factorisation %.2f ms; per level (depth: nodes ms):",
+                 static_cast<double>(ms));
+    for (int dep = maxd; dep >= 0; --dep) {
+      float lm = 0.f;
+      HIP_TRY(hipEventElapsedTime(&lm, lev[dep + 1], lev[dep]));
+      std::fprintf(stderr, " %d:%d %.1f", dep, h->fac_level_off[dep + 1] - h->fac_level_off[dep], static_cast<double>(lm));
+    }
+    std::fprintf(stderr, "\n");
+    for (auto& ev : lev) (void)hipEventDestroy(ev);
+  }
   if (bad) {
     // src/QuadraticProblem.cpp:81-86: the solve fails -> "Preconditioner failed", out = in
     std::printf("[dpgo_hip] Preconditioner failed (Q + 0.1 I not positive definite); using the identity.\n");
@@ -892,6 +906,8 @@ int download_sums(dpgo_hip_problem h) {
 // agent's flag is set.  Falls back to a stream synchronisation after 20 s (never expected).
 int wait_published(dpgo_hip_problem h, int tag, bool* any, bool* any_cg = nullptr, bool* any_never = nullptr) {
   const auto t0 = std::chrono::steady_clock::now();
+  // DPGO_VERBOSE_WAIT=<ms>: report every wait longer than that (host-side view of GPU idle gaps)
+  static const double verbose_ms = std::getenv("DPGO_VERBOSE_WAIT") ? std::atof(std::getenv("DPGO_VERBOSE_WAIT")) : -1.0;
   for (long spin = 0;; ++spin) {
     bool all = true, a = false, c = false, nv = false;
     for (int k = 0; k < h->K; ++k) {
@@ -908,6 +924,10 @@ int wait_published(dpgo_hip_problem h, int tag, bool* any, bool* any_cg = nullpt
       *any = a;
       if (any_cg) *any_cg = c;
       if (any_never) *any_never = nv;
+      if (verbose_ms >= 0.0) {
+        const double ms = 1e3 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (ms > verbose_ms) std::fprintf(stderr, "[dpgo_hip] waited %.3f ms for status tag %d (%ld polls)\n", ms, tag, spin);
+      }
       return DPGO_HIP_OK;
     }
     if ((spin & 1023) == 1023 &&

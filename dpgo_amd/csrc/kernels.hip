@@ -1235,8 +1235,13 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       s.tcg_active = 0;
       s.tcg_mode = 2;
       if (!s.eta_implicit) s.g_eta = tot[0];
-      s.f2 = sfold ? tot[4] : tot[2];
-      s.ngf2 = sqrt(sfold ? tot[5] : tot[3]);
+      // selects between register copies (pinned by the empty asm): a select between two elements of tot[] is folded
+      // into a dynamically indexed load, which puts tot[] in scratch memory -- and a kernel that needs scratch can
+      // make the queue drain while the runtime sizes its scratch
+      double t2 = tot[2], t3 = tot[3], t4 = tot[4], t5 = tot[5];
+      asm("" : "+v"(t2), "+v"(t3), "+v"(t4), "+v"(t5));
+      s.f2 = sfold ? t4 : t2;
+      s.ngf2 = sqrt(sfold ? t5 : t3);
       const double denom = -s.g_eta - 0.5 * s.eta_Heta;
       s.rho = (s.f1 - s.f2) / denom;
       s.accepted = s.rho > 0.1 ? 1 : 0;
@@ -1257,7 +1262,7 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
       s.st_tcg_iters += s.tcg_iters;
 #pragma unroll
       for (int q = 0; q < 5; ++q)  // static indices: the state stays in registers
-        if (s.tcg_status == q) s.st_status[q] += 1;
+        s.st_status[q] += s.tcg_status == q ? 1 : 0;  // static indices (no scratch, see above)
       if (s.rho < 0.25) {
         s.Delta = 0.25 * s.Delta;
       } else if (s.rho > 0.75 && (s.tcg_status == TCG_EXCREGION || s.tcg_status == TCG_NEGCURVTURE)) {
@@ -1281,7 +1286,7 @@ __device__ __forceinline__ void finalize_scalar(const FinalizeArgs& f, int agent
         }
         // the output is decided (accepted -> x2, gave up -> the input): its status from the retraction's
         // partials (a retry Run decides later)
-        if (sfold && !s.run_active) set_status(f, agent, s.accepted && !s.gave_up ? tot[2] : tot[3], s);
+        if (sfold && !s.run_active) set_status(f, agent, s.accepted && !s.gave_up ? t2 : t3, s);
       } else {
         if (s.accepted) {
           s.f1 = s.f2;

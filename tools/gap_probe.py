@@ -37,6 +37,12 @@ def main():
     launch = {}
     for nm, st, en, corr in c.execute("select name, start, end, corr_id from regions where name like '%Launch%'"):
         launch[corr] = (st, en)
+    if not launch:  # schema / naming check: what the regions table holds
+        cols = [r[1] for r in c.execute("pragma table_info(regions)")]
+        names = Counter(nm for (nm,) in c.execute("select name from regions limit 200000"))
+        print("# no launch regions matched; regions columns:", cols, "top names:", names.most_common(12))
+        kc = [r[1] for r in c.execute("pragma table_info(kernels)")]
+        print("# kernels columns:", kc)
     gaps = []
     for x, y in zip(W, W[1:]):
         g = y[1] - x[2]
