@@ -2092,10 +2092,11 @@ namespace {
 
 // Eigenpairs of the symmetric tridiagonal T (diag a, off-diagonal e[i] between i and i+1) by the
 // implicit QL method; Z (k x k, column-major) receives the eigenvectors.
-void tridiag_eig(std::vector<double> a, std::vector<double> e, std::vector<double>& Z) {
+// vectors = false: eigenvalues only (O(k^2)); Z then holds just the k ascending eigenvalues.
+void tridiag_eig(std::vector<double> a, std::vector<double> e, std::vector<double>& Z, bool vectors = true) {
   const int k = static_cast<int>(a.size());
-  Z.assign(static_cast<size_t>(k) * k, 0.0);
-  for (int i = 0; i < k; ++i) Z[static_cast<size_t>(i) * k + i] = 1.0;
+  Z.assign(vectors ? static_cast<size_t>(k) * k : 0, 0.0);
+  for (int i = 0; i < k && vectors; ++i) Z[static_cast<size_t>(i) * k + i] = 1.0;
   e.resize(k, 0.0);
   for (int l = 0; l < k; ++l) {
     for (int iter = 0; iter < 200; ++iter) {
@@ -2127,7 +2128,7 @@ void tridiag_eig(std::vector<double> a, std::vector<double> e, std::vector<doubl
         p = s * r;
         a[i + 1] = g + p;
         g = c * r - bb;
-        for (int q = 0; q < k; ++q) {
+        for (int q = 0; q < k && vectors; ++q) {
           f = Z[static_cast<size_t>(i + 1) * k + q];
           Z[static_cast<size_t>(i + 1) * k + q] = s * Z[static_cast<size_t>(i) * k + q] + c * f;
           Z[static_cast<size_t>(i) * k + q] = c * Z[static_cast<size_t>(i) * k + q] - s * f;
@@ -2138,6 +2139,11 @@ void tridiag_eig(std::vector<double> a, std::vector<double> e, std::vector<doubl
       e[l] = g;
       e[m] = 0.0;
     }
+  }
+  if (!vectors) {
+    std::sort(a.begin(), a.end());
+    Z = a;
+    return;
   }
   // a now holds the eigenvalues; store them in Z's companion by sorting indices
   std::vector<int> idx(k);
@@ -2151,30 +2157,140 @@ void tridiag_eig(std::vector<double> a, std::vector<double> e, std::vector<doubl
   Z.insert(Z.end(), a.begin(), a.end());  // eigenvalues appended after the k x k vectors
 }
 
+// Unit eigenvector of the tridiagonal T (diag a, off-diagonal e) for its lowest eigenvalue th0 (th1 the next):
+// inverse iteration with the shift th0 - delta below the spectrum, so T - shift is positive definite and the
+// LDL^T (Thomas) solve needs no pivoting; each solve amplifies the wanted component by (th1 - s) / (th0 - s).
+std::vector<double> tridiag_lowest_vector(const std::vector<double>& a, const std::vector<double>& e, double th0,
+                                          double th1, double scale) {
+  const int k = static_cast<int>(a.size());
+  const double delta = std::max(1e-3 * std::max(th1 - th0, 0.0), 1e-13 * scale);
+  const double sh = th0 - delta;
+  std::vector<double> dd(k), l(k, 0.0), x(k, 1.0);
+  dd[0] = a[0] - sh;
+  for (int i = 1; i < k; ++i) {
+    l[i] = e[i - 1] / dd[i - 1];
+    dd[i] = a[i] - sh - l[i] * e[i - 1];
+  }
+  for (int it = 0; it < 4; ++it) {
+    for (int i = 1; i < k; ++i) x[i] -= l[i] * x[i - 1];
+    x[k - 1] /= dd[k - 1];
+    for (int i = k - 2; i >= 0; --i) x[i] = (x[i] - e[i] * x[i + 1]) / dd[i];
+    double nrm = 0.0;
+    for (double v : x) nrm += v * v;
+    nrm = std::sqrt(nrm);
+    for (double& v : x) v /= nrm;
+  }
+  return x;
+}
+
+// Eigenpairs of the dense symmetric m x m matrix A (row-major): Householder reduction to tridiagonal form
+// (A = Q T Q^T, Q accumulated) and tridiag_eig on T; Z as tridiag_eig's (eigenvectors of A, then the
+// ascending eigenvalues).
+void sym_eig(int m, std::vector<double> A, std::vector<double>& Z) {
+  std::vector<double> Q(static_cast<size_t>(m) * m, 0.0), v(m), p(m), wv(m);
+  for (int i = 0; i < m; ++i) Q[static_cast<size_t>(i) * m + i] = 1.0;
+  auto a = [&](int i, int j) -> double& { return A[static_cast<size_t>(i) * m + j]; };
+  for (int k = 0; k + 2 < m; ++k) {
+    double xn = 0.0;
+    for (int i = k + 1; i < m; ++i) xn += a(i, k) * a(i, k);
+    xn = std::sqrt(xn);
+    if (xn == 0.0) continue;
+    const double alpha = a(k + 1, k) > 0.0 ? -xn : xn;
+    std::fill(v.begin(), v.end(), 0.0);
+    for (int i = k + 1; i < m; ++i) v[i] = a(i, k);
+    v[k + 1] -= alpha;
+    double vn2 = 0.0;
+    for (int i = k + 1; i < m; ++i) vn2 += v[i] * v[i];
+    if (vn2 == 0.0) continue;
+    const double bt = 2.0 / vn2;
+    // p = bt A v over rows k.., K = bt / 2 v^T p, w = p - K v; A -= v w^T + w v^T
+    double K = 0.0;
+    for (int i = k; i < m; ++i) {
+      double acc = 0.0;
+      for (int j = k + 1; j < m; ++j) acc += a(i, j) * v[j];
+      p[i] = bt * acc;
+      K += v[i] * p[i];
+    }
+    K *= 0.5 * bt;
+    for (int i = k; i < m; ++i) wv[i] = p[i] - K * v[i];
+    for (int i = k; i < m; ++i)
+      for (int j = k; j < m; ++j) a(i, j) -= v[i] * wv[j] + wv[i] * v[j];
+    // Q <- Q H
+    for (int i = 0; i < m; ++i) {
+      double acc = 0.0;
+      for (int j = k + 1; j < m; ++j) acc += Q[static_cast<size_t>(i) * m + j] * v[j];
+      acc *= bt;
+      for (int j = k + 1; j < m; ++j) Q[static_cast<size_t>(i) * m + j] -= acc * v[j];
+    }
+  }
+  std::vector<double> d(m), e(m, 0.0), Zt;
+  for (int i = 0; i < m; ++i) {
+    d[i] = a(i, i);
+    if (i + 1 < m) e[i] = a(i, i + 1);
+  }
+  tridiag_eig(d, e, Zt);
+  Z.assign(static_cast<size_t>(m) * m + m, 0.0);
+  for (int c = 0; c < m; ++c)
+    for (int i = 0; i < m; ++i) {
+      double acc = 0.0;
+      for (int q = 0; q < m; ++q) acc += Q[static_cast<size_t>(i) * m + q] * Zt[static_cast<size_t>(c) * m + q];
+      Z[static_cast<size_t>(c) * m + i] = acc;
+    }
+  std::copy(Zt.begin() + static_cast<long>(m) * m, Zt.end(), Z.begin() + static_cast<long>(m) * m);
+}
+
 }  // namespace
 
 extern "C" {
 
 int dpgo_hip_certify(dpgo_hip_problem h, const double* X, int max_iters, double tol, double* lambda_min,
                      double* residual, int* iters, double* eigvec) {
+  dpgo_cert_info info;
+  DPGO_TRY(dpgo_hip_certify_ex(h, X, max_iters, 0, 0, tol, lambda_min, eigvec, &info));
+  if (residual) *residual = info.residual;
+  if (iters) *iters = info.iters;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_certify_ex(dpgo_hip_problem h, const double* X, int max_iters, int basis_max, int flags, double tol,
+                        double* lambda_min, double* eigvec, dpgo_cert_info* info) {
   DPGO_TRY(ready(h));
   if (h->K != 1) return fail(DPGO_HIP_EINVAL, "certification needs a single-agent handle");
-  if (!X || !lambda_min || max_iters < 2) return fail(DPGO_HIP_EINVAL, "bad certification arguments");
+  if (!X || !lambda_min || max_iters < 2 || basis_max < 0 || (basis_max > 0 && basis_max < 8))
+    return fail(DPGO_HIP_EINVAL, "bad certification arguments");
   DPGO_TRY(ensure_work(h));
   const long L = static_cast<long>(h->vec_len());
-  const int kmax = static_cast<int>(std::min<long>(max_iters, L));
+  const int r = h->r;
+  const bool seed_x = (flags & DPGO_CERT_SEED_X) != 0;
+  const int nseed = seed_x ? r : 0;
+  // with a seed block everything lives on row 0 of the lifted layout: the basis is stored compact
+  // ((d + 1) n doubles per vector, r x less traffic in the orthogonalisation) and expanded around the operator
+  const long Lc = seed_x ? L / r : L;
+  // Krylov chain basis: every step without a limit, else thick restarts from the lowest `keep` Ritz vectors
+  const int mmax = static_cast<int>(std::min<long>(basis_max > 0 ? basis_max : max_iters, Lc - nseed));
+  if (mmax < 2) return fail(DPGO_HIP_EINVAL, "certification basis too small");
+  const bool dense = basis_max > 0;  // restarts make the projected matrix arrowhead + tridiagonal
+  const int keep = dense ? std::min(mmax / 2, std::max(8, mmax / 4)) : 0;
   HostIO io;
   DPGO_TRY(io.init(h));
   DPGO_TRY(upload(io.a.p, X, L, h->stream));
   // Lambda(X): S_j = sym(Y_j^T (XQ + G)_Y) (the same S the Riemannian Hessian uses)
   DPGO_TRY(eval_at(h, io.a.p, h->tA.p, h->S.p, h->pa.p, dpgo::FLAG_NONE));
-  DevBuf<double> basis, c, part;
-  HIP_TRY(basis.ensure(static_cast<size_t>(kmax + 1) * L));
-  HIP_TRY(c.ensure(kmax + 1));
-  HIP_TRY(part.ensure(static_cast<size_t>(dpgo::kDotBlocks) * (kmax + 1)));
+  const int slots = nseed + mmax + 1;
+  DevBuf<double> V, tmp, c, part, xin, xout;
+  HIP_TRY(V.ensure(static_cast<size_t>(slots) * Lc));
+  if (keep > 0) HIP_TRY(tmp.ensure(static_cast<size_t>(keep) * Lc));
+  if (seed_x) {
+    HIP_TRY(xin.ensure(L));
+    HIP_TRY(xout.ensure(L));
+    HIP_TRY(hipMemsetAsync(xin.p, 0, sizeof(double) * L, h->stream));  // rows 1.. stay zero
+  }
+  HIP_TRY(c.ensure(slots));
+  HIP_TRY(part.ensure(static_cast<size_t>(dpgo::kDotBlocks) * slots));
   double* w = io.b.p;
-  auto dots = [&](const double* vec, const double* B, int k, std::vector<double>& out) -> int {
-    HIP_TRY(dpgo::launch_dot_multi(L, vec, B, k, part.p, h->stream));
+  auto vec = [&](int j) { return V.p + static_cast<long>(j) * Lc; };
+  auto dots = [&](const double* x, const double* B, int k, std::vector<double>& out) -> int {
+    HIP_TRY(dpgo::launch_dot_multi(Lc, x, B, k, part.p, h->stream));
     std::vector<double> hp(static_cast<size_t>(dpgo::kDotBlocks) * k);
     HIP_TRY(hipMemcpyAsync(hp.data(), part.p, sizeof(double) * hp.size(), hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -2183,73 +2299,254 @@ int dpgo_hip_certify(dpgo_hip_problem h, const double* X, int max_iters, double 
       for (int j = 0; j < k; ++j) out[j] += hp[static_cast<size_t>(g) * k + j];
     return DPGO_HIP_OK;
   };
-  // seeded start vector (SplitMix64 uniform in [-1, 1))
-  {
-    std::vector<double> q0(L);
+  // x -= sum_j coef_j B_j (coefficients through the device array c)
+  auto subtract = [&](double* x, const double* B, int k, const std::vector<double>& coef) -> int {
+    if (k == 0) return DPGO_HIP_OK;
+    HIP_TRY(hipMemcpyAsync(c.p, coef.data(), sizeof(double) * k, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(dpgo::launch_axpy_multi(Lc, x, B, k, c.p, h->stream));
+    return DPGO_HIP_OK;
+  };
+  // classical Gram-Schmidt twice against V_0..V_{k-1}; the summed coefficients (= <x, V_j> before) in cs
+  auto orthogonalise = [&](double* x, int k, std::vector<double>& cs) -> int {
+    cs.assign(k, 0.0);
+    for (int pass = 0; pass < 2 && k > 0; ++pass) {
+      std::vector<double> cc;
+      DPGO_TRY(dots(x, V.p, k, cc));
+      for (int j = 0; j < k; ++j) cs[j] += cc[j];
+      DPGO_TRY(subtract(x, V.p, k, cc));
+    }
+    return DPGO_HIP_OK;
+  };
+  auto cert_apply = [&](const double* x, double* y) -> int {
+    const double* xi = x;
+    double* yo = y;
+    if (seed_x) {
+      HIP_TRY(dpgo::launch_strided_copy(Lc, x, 1, xin.p, r, h->stream));
+      xi = xin.p;
+      yo = xout.p;
+    }
+    const dpgo::SpmmArgs sa{xi, nullptr, nullptr, nullptr, h->S.p, yo, nullptr, nullptr, nullptr, dpgo::PRECON_NONE};
+    HIP_TRY(dpgo::launch_spmm(h->r, h->b, dpgo::MODE_CERT, make_ctx(h, dpgo::FLAG_NONE, nullptr), qview(h), sa));
+    if (seed_x) HIP_TRY(dpgo::launch_strided_copy(Lc, xout.p, r, y, 1, h->stream));
+    return DPGO_HIP_OK;
+  };
+  // |S y - th y| / |y| (S y into io.a); project: |P (S y) - th y| for y orthogonal to the first `project` basis
+  // vectors (the locked block: the chain's own operator P S P)
+  auto residual_of = [&](const double* y, double th, double& res, int project) -> int {
+    DPGO_TRY(cert_apply(y, io.a.p));
+    if (project > 0) {
+      std::vector<double> pc;
+      DPGO_TRY(orthogonalise(io.a.p, project, pc));
+    }
+    std::vector<double> yy, ys, ss;
+    DPGO_TRY(dots(y, y, 1, yy));
+    DPGO_TRY(dots(y, io.a.p, 1, ys));
+    DPGO_TRY(dots(io.a.p, io.a.p, 1, ss));
+    res = std::sqrt(std::max(0.0, ss[0] - 2.0 * th * ys[0] + th * th * yy[0]) / std::max(yy[0], 1e-300));
+    return DPGO_HIP_OK;
+  };
+  // seed block U (DPGO_CERT_SEED_X): the rows of X, S(X) X^T ~ 0 at a critical point (the near-null space),
+  // orthonormalised on row 0 of the lifted r x (d+1) n layout (V -> V S acts row by row, so the search
+  // space stays on row 0 and its spectrum is S's).  U is locked: the Krylov chain runs on the complement
+  // (P S P, P = I - U U^T) and U's block is resolved exactly at the end.
+  int nl = 0;
+  std::vector<double> q0(Lc, 0.0), cs, nn;
+  // the principal directions of X's rows (eigenvectors of X X^T with sigma >= 1e-3 sigma_max): a row at the
+  // noise level of a rank-deficient X is in S's null space only to within |RieGrad| / its norm
+  std::vector<double> seedv;
+  if (nseed > 0) {
+    std::vector<double> G(static_cast<size_t>(r) * r, 0.0), Zg;
+    for (long x = 0; x < L / r; ++x)
+      for (int i = 0; i < r; ++i)
+        for (int j = 0; j < r; ++j) G[static_cast<size_t>(i) * r + j] += X[x * r + i] * X[x * r + j];
+    sym_eig(r, G, Zg);
+    const double gmax = Zg[static_cast<size_t>(r) * r + r - 1];
+    for (int e = r - 1; e >= 0; --e)
+      if (Zg[static_cast<size_t>(r) * r + e] >= 1e-6 * gmax)
+        seedv.insert(seedv.end(), Zg.begin() + static_cast<long>(e) * r, Zg.begin() + static_cast<long>(e + 1) * r);
+  }
+  for (int j = 0; j < static_cast<int>(seedv.size()) / std::max(r, 1); ++j) {
+    for (long x = 0; x < L / r; ++x) {
+      double acc = 0.0;
+      for (int i = 0; i < r; ++i) acc += seedv[static_cast<size_t>(j) * r + i] * X[x * r + i];
+      q0[x] = acc;
+    }
+    DPGO_TRY(upload(w, q0.data(), Lc, h->stream));
+    DPGO_TRY(dots(w, w, 1, nn));
+    const double n0 = std::sqrt(nn[0]);
+    DPGO_TRY(orthogonalise(w, nl, cs));
+    DPGO_TRY(dots(w, w, 1, nn));
+    if (!(std::sqrt(nn[0]) > 1e-10 * n0)) continue;  // a row in the span of the previous ones
+    HIP_TRY(dpgo::launch_scale(Lc, w, 1.0 / std::sqrt(nn[0]), vec(nl), h->stream));
+    ++nl;
+  }
+  {  // seeded random start (SplitMix64 uniform in [-1, 1)), on row 0 only with a seed block
     unsigned long long st = 0x5EEDULL;
+    std::fill(q0.begin(), q0.end(), 0.0);
     for (long x = 0; x < L; ++x) {
       st += 0x9E3779B97F4A7C15ULL;
       unsigned long long z = st;
       z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
       z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
       z ^= z >> 31;
-      q0[x] = 2.0 * (static_cast<double>(z >> 11) * (1.0 / 9007199254740992.0)) - 1.0;
+      const double u = 2.0 * (static_cast<double>(z >> 11) * (1.0 / 9007199254740992.0)) - 1.0;
+      if (!seed_x)
+        q0[x] = u;
+      else if (x % r == 0)  // the full layout's row-0 entries of the same stream
+        q0[x / r] = u;
     }
-    DPGO_TRY(upload(w, q0.data(), L, h->stream));
-    std::vector<double> nn;
+    DPGO_TRY(upload(w, q0.data(), Lc, h->stream));
+    DPGO_TRY(orthogonalise(w, nl, cs));
     DPGO_TRY(dots(w, w, 1, nn));
-    HIP_TRY(dpgo::launch_scale(L, w, 1.0 / std::sqrt(nn[0]), basis.p, h->stream));
+    HIP_TRY(dpgo::launch_scale(Lc, w, 1.0 / std::sqrt(nn[0]), vec(nl), h->stream));
   }
-  std::vector<double> alpha, beta, Z;  // beta[j] couples q_j and q_{j+1}
-  double lam = 0.0, res = 0.0;
-  int k = 0;
-  auto ritz = [&](int kk) {
-    tridiag_eig(std::vector<double>(alpha.begin(), alpha.begin() + kk),
-                std::vector<double>(beta.begin(), beta.begin() + kk), Z);
-    lam = Z[static_cast<size_t>(kk) * kk + 0];
-    res = std::fabs(beta[kk - 1] * Z[static_cast<size_t>(0) * kk + (kk - 1)]);
-  };
-  auto c_ctx = make_ctx(h, dpgo::FLAG_NONE, nullptr);
-  for (k = 0; k < kmax; ++k) {
-    const double* qk = basis.p + static_cast<long>(k) * L;
-    const dpgo::SpmmArgs sa{qk, nullptr, nullptr, nullptr, h->S.p, w, nullptr, nullptr, nullptr, dpgo::PRECON_NONE};
-    HIP_TRY(dpgo::launch_spmm(h->r, h->b, dpgo::MODE_CERT, c_ctx, qview(h), sa));
-    // full reorthogonalisation, classical Gram-Schmidt twice; alpha_k from both passes
-    double ak = 0.0;
-    for (int pass = 0; pass < 2; ++pass) {
-      std::vector<double> cc;
-      DPGO_TRY(dots(w, basis.p, k + 1, cc));
-      ak += cc[k];
-      HIP_TRY(hipMemcpyAsync(c.p, cc.data(), sizeof(double) * (k + 1), hipMemcpyHostToDevice, h->stream));
-      HIP_TRY(dpgo::launch_axpy_multi(L, w, basis.p, k + 1, c.p, h->stream));
+  int nb = nl + 1;
+  // Rayleigh-Ritz on the chain's T = V_c^T P S P V_c (tridiagonal: alpha / beta; dense after a restart)
+  std::vector<double> T(static_cast<size_t>(mmax + 1) * (mmax + 1), 0.0);
+  auto Tat = [&](int i, int j) -> double& { return T[static_cast<size_t>(i) * (mmax + 1) + j]; };
+  std::vector<double> alpha, beta, Z, theta;
+  auto rayleigh_ritz = [&](int m) {  // theta ascending, Z column-major m x m
+    if (!dense) {  // eigenvalues, and the lowest one's vector by inverse iteration: O(m^2) at any basis size
+      const std::vector<double> am(alpha.begin(), alpha.begin() + m), em(beta.begin(), beta.begin() + m);
+      tridiag_eig(am, em, Z, false);
+      const double sc = std::max(std::fabs(Z.front()), std::fabs(Z.back()));
+      std::vector<double> z0 = tridiag_lowest_vector(am, em, Z[0], m > 1 ? Z[1] : Z[0], sc);
+      z0.insert(z0.end(), Z.begin(), Z.end());
+      Z.swap(z0);
+    } else {
+      std::vector<double> A(static_cast<size_t>(m) * m);
+      for (int i = 0; i < m; ++i)
+        for (int j = 0; j < m; ++j) A[static_cast<size_t>(i) * m + j] = Tat(i, j);
+      sym_eig(m, A, Z);
     }
-    std::vector<double> nn;
+    const size_t nv = dense ? static_cast<size_t>(m) * m : static_cast<size_t>(m);  // tridiagonal: z_0 only
+    theta.assign(Z.begin() + static_cast<long>(nv), Z.end());
+    Z.resize(nv);
+  };
+  // chain Ritz vector i of the first m chain vectors into y
+  auto ritz_vector = [&](int m, int i, double* y) -> int {
+    std::vector<double> negz(m);
+    for (int j = 0; j < m; ++j) negz[j] = -Z[static_cast<size_t>(i) * m + j];
+    HIP_TRY(hipMemsetAsync(y, 0, sizeof(double) * Lc, h->stream));
+    return subtract(y, vec(nl), m, negz);
+  };
+  double res = 0.0;
+  int k = nl, total = 0, nrestart = 0, m_final = 0;
+  const bool verbose = std::getenv("DPGO_VERBOSE_CERT") != nullptr;
+  while (true) {
+    // expand: S q_k, its column of T against the chain, the next direction orthogonal to U and the chain
+    DPGO_TRY(cert_apply(vec(k), w));
+    std::vector<double> sq;
+    DPGO_TRY(dots(w, w, 1, sq));  // |S q_k| before the projection: the breakdown test is relative to it
+    DPGO_TRY(orthogonalise(w, nb, cs));
+    const int kc = k - nl;
+    for (int j = nl; j < nb; ++j) Tat(j - nl, kc) = Tat(kc, j - nl) = cs[j];
+    ++total;
     DPGO_TRY(dots(w, w, 1, nn));
     const double bk = std::sqrt(nn[0]);
-    alpha.push_back(ak);
-    beta.push_back(bk);
-    if ((k + 1) % 5 == 0 || k + 1 == kmax || bk <= 1e-300) {
-      ritz(k + 1);
-      const double scale = std::max(std::fabs(Z.back()), std::fabs(lam));
-      if (res <= tol * std::max(scale, 1e-300) || bk <= 1e-300) {
-        ++k;
-        break;
-      }
+    if (!dense) {
+      alpha.push_back(cs[k]);
+      beta.push_back(bk);
     }
-    if (k + 1 < kmax + 1) HIP_TRY(dpgo::launch_scale(L, w, 1.0 / bk, basis.p + static_cast<long>(k + 1) * L, h->stream));
+    // an invariant subspace up to rounding (CGS2 leaves ~eps |S q_k| sqrt(k)): the Ritz values are exact
+    const bool breakdown = bk <= 1e-10 * std::sqrt(sq[0]);
+    if (nb - nl <= mmax && !breakdown) {
+      HIP_TRY(dpgo::launch_scale(Lc, w, 1.0 / bk, vec(nb), h->stream));
+      Tat(nb - nl, kc) = Tat(kc, nb - nl) = bk;
+      ++nb;
+    }
+    ++k;
+    const int m = k - nl;
+    const bool full = nb - nl > mmax || breakdown;
+    const bool last = total >= max_iters;
+    // Ritz checks: every 5 steps on the tridiagonal T (every ~2 % of the basis beyond 250); with restarts (a dense O(m^3) eigensolve on the host) at
+    // every 20 steps of a small basis, every 500 of a large one, and at each restart
+    const bool check = dense ? ((m <= 200 && m % 20 == 0) || m % 500 == 0) : m % std::max(5, m / 250 * 5) == 0;
+    if (!(check || full || last)) continue;
+    rayleigh_ritz(m);
+    const double scale = std::max(std::fabs(theta.back()), std::fabs(theta[0]));
+    // the chain's residual estimate |beta z_last| (Lanczos); after a restart the true one
+    if (!dense) {
+      res = std::fabs(bk * Z[static_cast<size_t>(m) - 1]);
+    } else {
+      DPGO_TRY(ritz_vector(m, 0, io.c.p));
+      DPGO_TRY(residual_of(io.c.p, theta[0], res, nl));
+    }
+    m_final = m;
+    if (verbose && (total % 500 < (dense ? 500 : 5) || full || last))
+      std::fprintf(stderr, "certify: %d steps, %d restarts, basis %d, theta0 %.6e, residual %.3e\n", total, nrestart,
+                   m, theta[0], res);
+    if (res <= tol * std::max(scale, 1e-300) || breakdown || last) break;
+    if (!full) continue;
+    if (!dense) break;
+    // thick restart: the lowest `keep` Ritz vectors and the chain's newest direction (orthogonal to them)
+    for (int i = 0; i < keep; ++i) DPGO_TRY(ritz_vector(m, i, tmp.p + static_cast<long>(i) * Lc));
+    HIP_TRY(hipMemcpyAsync(vec(nl + keep), vec(nb - 1), sizeof(double) * Lc, hipMemcpyDeviceToDevice, h->stream));
+    HIP_TRY(hipMemcpyAsync(vec(nl), tmp.p, sizeof(double) * keep * Lc, hipMemcpyDeviceToDevice, h->stream));
+    std::fill(T.begin(), T.end(), 0.0);
+    for (int i = 0; i < keep; ++i) Tat(i, i) = theta[i];
+    nb = nl + keep + 1;
+    k = nl + keep;
+    ++nrestart;
   }
-  if (k > kmax) k = kmax;
-  ritz(k);
+  // the chain's lowest Ritz pair with its true residuals on P S P and on S (y in io.c)
+  DPGO_TRY(ritz_vector(m_final, 0, io.c.p));
+  DPGO_TRY(residual_of(io.c.p, theta[0], res, nl));
+  const double theta_c = theta[0], res_c = res;
+  if (nl > 0) DPGO_TRY(residual_of(io.c.p, theta[0], res, 0));
+  double lam = theta_c, lam_s = NAN, coupling = 0.0;
+  if (nl > 0) {
+    // U's block A_s = U^T S U and the coupling |(I - U U^T) S U|_F: S = [A_s B^T; B C] in (U, U_perp), so
+    // lambda_min(S) >= min(lambda_min(A_s), lambda_min(C)) - |B|
+    std::vector<double> As(static_cast<size_t>(nl) * nl), col, s2, Zs;
+    double c2 = 0.0;
+    for (int j = 0; j < nl; ++j) {
+      DPGO_TRY(cert_apply(vec(j), io.a.p));
+      DPGO_TRY(dots(io.a.p, V.p, nl, col));
+      DPGO_TRY(dots(io.a.p, io.a.p, 1, s2));
+      double cc = 0.0;
+      for (int i = 0; i < nl; ++i) {
+        As[static_cast<size_t>(i) * nl + j] = col[i];
+        cc += col[i] * col[i];
+      }
+      c2 += std::max(0.0, s2[0] - cc);
+    }
+    for (int i = 0; i < nl; ++i)
+      for (int j = 0; j < i; ++j) {
+        const double v = 0.5 * (As[static_cast<size_t>(i) * nl + j] + As[static_cast<size_t>(j) * nl + i]);
+        As[static_cast<size_t>(i) * nl + j] = As[static_cast<size_t>(j) * nl + i] = v;
+      }
+    sym_eig(nl, As, Zs);
+    lam_s = Zs[static_cast<size_t>(nl) * nl];
+    coupling = std::sqrt(c2);
+    if (lam_s < theta_c) {  // the lowest Ritz pair lies in U
+      lam = lam_s;
+      std::vector<double> negz(nl);
+      for (int j = 0; j < nl; ++j) negz[j] = -Zs[j];
+      HIP_TRY(hipMemsetAsync(io.c.p, 0, sizeof(double) * Lc, h->stream));
+      DPGO_TRY(subtract(io.c.p, V.p, nl, negz));
+      DPGO_TRY(residual_of(io.c.p, lam, res, 0));
+    }
+  }
   *lambda_min = lam;
-  if (residual) *residual = res;
-  if (iters) *iters = k;
-  if (eigvec) {  // Ritz vector sum_i z_i q_i (axpy with -z onto zero)
-    std::vector<double> negz(k);
-    for (int i = 0; i < k; ++i) negz[i] = -Z[static_cast<size_t>(0) * k + i];
-    HIP_TRY(hipMemsetAsync(w, 0, sizeof(double) * L, h->stream));
-    HIP_TRY(hipMemcpyAsync(c.p, negz.data(), sizeof(double) * k, hipMemcpyHostToDevice, h->stream));
-    HIP_TRY(dpgo::launch_axpy_multi(L, w, basis.p, k, c.p, h->stream));
-    DPGO_TRY(download(eigvec, w, L, h->stream));
+  if (info) {
+    info->iters = total;
+    info->restarts = nrestart;
+    info->seeds = nl;
+    info->residual = res;
+    info->lambda_seed = lam_s;
+    info->lambda_complement = theta_c;
+    info->residual_complement = res_c;
+    info->coupling = coupling;
+    info->lower_bound = (nl > 0 ? std::min(lam_s, theta_c - res_c) : theta_c - res_c) - coupling;
+    for (int i = 0; i < 8; ++i) info->ritz[i] = i < static_cast<int>(theta.size()) ? theta[i] : NAN;
+  }
+  if (eigvec && !seed_x) DPGO_TRY(download(eigvec, io.c.p, L, h->stream));
+  if (eigvec && seed_x) {  // row 0 of the lifted layout
+    std::vector<double> yc(Lc);
+    DPGO_TRY(download(yc.data(), io.c.p, Lc, h->stream));
+    std::fill(eigvec, eigvec + L, 0.0);
+    for (long x = 0; x < Lc; ++x) eigvec[x * r] = yc[x];
   }
   HIP_TRY(hipStreamSynchronize(h->stream));
   return DPGO_HIP_OK;

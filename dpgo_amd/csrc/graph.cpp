@@ -577,6 +577,17 @@ int dpgo_graph_grid_partition(dpgo_graph g, int A, int* agent_of_pose) {
 int dpgo_graph_certify(dpgo_graph g, int r, const double* X, int max_iters, double tol, double* lambda_min,
                        double* residual, int* iters, double* f_relax, double* f_rounded, double* T_rounded,
                        double* eigvec) {
+  dpgo_cert_info info;
+  DPGO_TRY(dpgo_graph_certify_ex(g, r, X, max_iters, 0, 0, tol, lambda_min, f_relax, f_rounded, T_rounded, eigvec,
+                                 &info));
+  if (residual) *residual = info.residual;
+  if (iters) *iters = info.iters;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_graph_certify_ex(dpgo_graph g, int r, const double* X, int max_iters, int basis_max, int flags, double tol,
+                          double* lambda_min, double* f_relax, double* f_rounded, double* T_rounded, double* eigvec,
+                          dpgo_cert_info* info) {
   if (!g || !X || !lambda_min || r < g->d) return fail(DPGO_HIP_EINVAL, "bad certification arguments");
   const int d = g->d, b = d + 1, n = g->n, m = static_cast<int>(g->p1.size());
   dpgo_hip_problem h = nullptr;
@@ -588,11 +599,7 @@ int dpgo_graph_certify(dpgo_graph g, int r, const double* X, int max_iters, doub
   const std::vector<double> w(static_cast<size_t>(m), 1.0);
   DPGO_TRY(dpgo_hip_set_Q_edges(h, 0, m, g->p1.data(), g->p2.data(), g->R.data(), g->t.data(), g->kappa.data(),
                                 g->tau.data(), w.data()));
-  double res = 0.0;
-  int it = 0;
-  DPGO_TRY(dpgo_hip_certify(h, X, max_iters, tol, lambda_min, &res, &it, eigvec));
-  if (residual) *residual = res;
-  if (iters) *iters = it;
+  DPGO_TRY(dpgo_hip_certify_ex(h, X, max_iters, basis_max, flags, tol, lambda_min, eigvec, info));
   double fx = 0.0;
   DPGO_TRY(dpgo_hip_f(h, X, &fx));
   if (f_relax) *f_relax = fx;

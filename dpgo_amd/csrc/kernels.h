@@ -388,6 +388,9 @@ hipError_t launch_dot_multi(long len, const double* w, const double* basis, int 
                             hipStream_t stream);
 hipError_t launch_axpy_multi(long len, double* w, const double* basis, int k, const double* c, hipStream_t stream);
 hipError_t launch_scale(long len, const double* src, double s, double* dst, hipStream_t stream);
+// dst[x * dst_stride] = src[x * src_stride], x < len (one row of the lifted layout <-> a compact vector)
+hipError_t launch_strided_copy(long len, const double* src, int src_stride, double* dst, int dst_stride,
+                               hipStream_t stream);
 hipError_t launch_bj_inverse_diag(int b, int n, const QView& q, double shift, double* Minv, hipStream_t stream);
 
 // ---- Jacobi-PCG on SPD block-sparse systems with several right-hand sides (GPU chordal

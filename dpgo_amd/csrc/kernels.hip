@@ -4141,6 +4141,21 @@ __global__ __launch_bounds__(kThreads) void k_scale(long len, const double* __re
     dst[x] = src[x] * s;
 }
 
+__global__ __launch_bounds__(kThreads) void k_strided_copy(long len, const double* __restrict__ src, int ss,
+                                                           double* __restrict__ dst, int ds) {
+  for (long x = static_cast<long>(blockIdx.x) * kThreads + threadIdx.x; x < len;
+       x += static_cast<long>(gridDim.x) * kThreads)
+    dst[x * ds] = src[x * ss];
+}
+
+hipError_t launch_strided_copy(long len, const double* src, int src_stride, double* dst, int dst_stride,
+                               hipStream_t stream) {
+  if (len == 0) return hipSuccess;
+  const long blocks = std::min<long>((len + kThreads - 1) / kThreads, 4096);
+  k_strided_copy<<<static_cast<int>(blocks), kThreads, 0, stream>>>(len, src, src_stride, dst, dst_stride);
+  return hipGetLastError();
+}
+
 hipError_t launch_scale(long len, const double* src, double s, double* dst, hipStream_t stream) {
   if (len == 0) return hipSuccess;
   const long blocks = std::min<long>((len + kThreads - 1) / kThreads, 4096);

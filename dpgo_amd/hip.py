@@ -95,6 +95,8 @@ _SIGS = [
     ("dpgo_hip_bench_spmm", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, _dp], C.c_int),
     ("dpgo_hip_spmm_bytes_bsr", [C.c_void_p], C.c_double),
     ("dpgo_hip_certify", [C.c_void_p, _dp, C.c_int, C.c_double, _dp, _dp, _ip, _dp], C.c_int),
+    ("dpgo_hip_certify_ex", [C.c_void_p, _dp, C.c_int, C.c_int, C.c_int, C.c_double, _dp, _dp, C.c_void_p],
+     C.c_int),
     ("dpgo_hip_bench_hvp", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, _dp], C.c_int),
     ("dpgo_hip_stats", [C.c_void_p, _ip], C.c_int),
     ("dpgo_hip_set_trace", [C.c_void_p, C.c_int], C.c_int),
@@ -369,14 +371,18 @@ class Problem:
         _check(lib().dpgo_hip_polar_combine_dev(self.h, C.c_void_p(A_dev), C.c_void_p(B_dev or 0), ap, bp,
                                                 C.c_void_p(out_dev)))
 
-    def certify(self, X, max_iters=300, tol=1e-8, want_vector=False):
-        """lambda_min of S(X) = Q - Lambda(X) (Lanczos on the device): (lambda_min, residual, iters, vec)."""
+    def certify(self, X, max_iters=300, tol=1e-8, want_vector=False, basis=0, seed_x=False):
+        """lambda_min of S(X) = Q - Lambda(X) (Lanczos on the device): (lambda_min, residual, iters, vec).
+        basis > 0: thick restart at that basis size; seed_x: the rows of X in the start block
+        (dpgo_hip_certify_ex)."""
         x, xp = self._in(X)
-        lam, res, it = C.c_double(), C.c_double(), C.c_int()
+        lam, info = C.c_double(), CertInfo()
         v = np.empty(self.vec_len) if want_vector else None
-        _check(lib().dpgo_hip_certify(self.h, xp, int(max_iters), float(tol), C.byref(lam), C.byref(res), C.byref(it),
-                                      v.ctypes.data_as(_dp) if v is not None else None))
-        return lam.value, res.value, it.value, (from_dev_layout(v, self.r) if v is not None else None)
+        _check(lib().dpgo_hip_certify_ex(self.h, xp, int(max_iters), int(basis), 1 if seed_x else 0, float(tol),
+                                         C.byref(lam), v.ctypes.data_as(_dp) if v is not None else None,
+                                         C.byref(info)))
+        self.last_certificate = info.as_dict()
+        return lam.value, info.residual, info.iters, (from_dev_layout(v, self.r) if v is not None else None)
 
     def spmm_bytes(self) -> float:
         return float(lib().dpgo_hip_spmm_bytes(self.h))
@@ -455,6 +461,18 @@ def project_polar(M, d):
 # ----------------------------------------------------------------------------------------
 # Pose graphs + multi-agent RBCD engine (include/dpgo_rbcd.h)
 # ----------------------------------------------------------------------------------------
+class CertInfo(C.Structure):
+    """dpgo_cert_info (include/dpgo_hip.h)."""
+    _fields_ = [("iters", C.c_int), ("restarts", C.c_int), ("seeds", C.c_int), ("residual", C.c_double),
+                ("lambda_seed", C.c_double), ("lambda_complement", C.c_double), ("residual_complement", C.c_double),
+                ("coupling", C.c_double), ("lower_bound", C.c_double), ("ritz", C.c_double * 8)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "ritz"}
+        d["ritz"] = [float(x) for x in self.ritz]
+        return d
+
+
 class RbcdParams(C.Structure):
     _fields_ = [("r", C.c_int), ("acceleration", C.c_int), ("restart_interval", C.c_int),
                 ("max_inner", C.c_int), ("initial_radius", C.c_double), ("tolerance", C.c_double),
@@ -481,6 +499,8 @@ _SIGS2 = [
     ("dpgo_graph_grid_partition", [C.c_void_p, C.c_int, _ip], C.c_int),
     ("dpgo_graph_certify", [C.c_void_p, C.c_int, _dp, C.c_int, C.c_double, _dp, _dp, _ip, _dp, _dp, _dp, _dp],
      C.c_int),
+    ("dpgo_graph_certify_ex", [C.c_void_p, C.c_int, _dp, C.c_int, C.c_int, C.c_int, C.c_double, _dp, _dp, _dp, _dp,
+                               _dp, C.c_void_p], C.c_int),
     ("dpgo_chordal_initialization_gpu", [C.c_int, C.c_int, C.c_int, _ip, _ip, _dp, _dp, _dp, _dp, C.c_double,
                                          C.c_int, _dp, _ip, _dp], C.c_int),
     ("dpgo_graph_chordal_init_gpu", [C.c_void_p, C.c_int, _dp, C.c_double, C.c_int, _dp, _ip, _dp], C.c_int),
@@ -638,7 +658,7 @@ class Graph:
         _check(lib().dpgo_graph_chain_init(self.h, r, Yp, out.ctypes.data_as(_dp)))
         return out
 
-    def certify(self, X, r, max_iters=300, tol=1e-8, want_rounded=False, want_vector=False):
+    def certify(self, X, r, max_iters=300, tol=1e-8, want_rounded=False, want_vector=False, basis=0, seed_x=False):
         """Certified optimality gap of X (flat r x (d+1) n column-major buffer, or the r x (d+1) n
         matrix) for the whole graph: dict(lambda_min, residual, iters, f_relax, f_rounded, gap, rel_gap
         [, T_rounded d x (d+1) n])."""
@@ -646,16 +666,16 @@ class Graph:
         flat = np.ascontiguousarray(X.T).ravel() if X.ndim == 2 else np.ascontiguousarray(X).ravel()
         if flat.size != r * (self.d + 1) * self.n:
             raise DPGOHipError("X has the wrong size")
-        lam, res, fx, fr = C.c_double(), C.c_double(), C.c_double(), C.c_double()
-        it = C.c_int()
+        lam, fx, fr, info = C.c_double(), C.c_double(), C.c_double(), CertInfo()
         T = np.empty(self.d * (self.d + 1) * self.n) if want_rounded else None
         V = np.empty(flat.size) if want_vector else None
-        _check(lib().dpgo_graph_certify(self.h, int(r), flat.ctypes.data_as(_dp), int(max_iters), float(tol),
-                                        C.byref(lam), C.byref(res), C.byref(it), C.byref(fx), C.byref(fr),
-                                        T.ctypes.data_as(_dp) if T is not None else None,
-                                        V.ctypes.data_as(_dp) if V is not None else None))
-        out = dict(lambda_min=lam.value, residual=res.value, iters=it.value, f_relax=fx.value, f_rounded=fr.value,
-                   gap=fr.value - fx.value, rel_gap=(fr.value - fx.value) / fx.value if fx.value else float("nan"))
+        _check(lib().dpgo_graph_certify_ex(self.h, int(r), flat.ctypes.data_as(_dp), int(max_iters), int(basis),
+                                           1 if seed_x else 0, float(tol), C.byref(lam), C.byref(fx), C.byref(fr),
+                                           T.ctypes.data_as(_dp) if T is not None else None,
+                                           V.ctypes.data_as(_dp) if V is not None else None, C.byref(info)))
+        out = dict(lambda_min=lam.value, f_relax=fx.value, f_rounded=fr.value, gap=fr.value - fx.value,
+                   rel_gap=(fr.value - fx.value) / fx.value if fx.value else float("nan"))
+        out.update(info.as_dict())
         if T is not None:
             out["T_rounded"] = from_dev_layout(T, self.d)
         if V is not None:

@@ -85,6 +85,10 @@ int dpgo_graph_distributed_init(dpgo_graph g, int num_agents, const int* agent_o
 int dpgo_graph_certify(dpgo_graph g, int r, const double* X, int max_iters, double tol, double* lambda_min,
                        double* residual, int* iters, double* f_relax, double* f_rounded, double* T_rounded,
                        double* eigvec);
+/* The same through dpgo_hip_certify_ex (thick restart with basis_max, DPGO_CERT_SEED_X, the bound in info). */
+int dpgo_graph_certify_ex(dpgo_graph g, int r, const double* X, int max_iters, int basis_max, int flags, double tol,
+                          double* lambda_min, double* f_relax, double* f_rounded, double* T_rounded, double* eigvec,
+                          dpgo_cert_info* info);
 int dpgo_graph_grid_partition(dpgo_graph g, int agents_per_axis, int* agent_of_pose);
 
 /* ---- RBCD engine ----------------------------------------------------------------------------*/

@@ -143,3 +143,79 @@ def test_graph_certify_certified_gap(hip, name):
     assert c["lambda_min"] >= -1e-6 * lam_bound
     assert c["gap"] >= -1e-9 * abs(c["f_relax"])
     assert abs(c["f_rounded"] - O.central_cost(meas, O.round_to_se(Xo, d))) <= 1e-10 * abs(c["f_rounded"])
+
+
+def _seed_blocks(S, X):
+    """The seed block's exact quantities for row 0 of the lifted layout: U = orthonormal rows of X,
+    lambda_min(U^T S U), lambda_min of S compressed to U's complement, |(I - U U^T) S U|_F."""
+    import scipy.linalg as sl
+    Sd = S.toarray()
+    U, sv, _ = np.linalg.svd(X.T, full_matrices=False)
+    U = U[:, sv >= 1e-3 * sv[0]]  # X's principal row directions, as dpgo_hip_certify_ex seeds them
+    N = sl.null_space(U.T)
+    SU = Sd @ U
+    return (float(np.linalg.eigvalsh(U.T @ SU)[0]), float(np.linalg.eigvalsh(N.T @ Sd @ N)[0]),
+            float(np.linalg.norm(SU - U @ (U.T @ SU))), U.shape[1])
+
+
+@pytest.mark.parametrize("seed_x", [False, True])
+@pytest.mark.parametrize("name,r", [("tinyGrid3D", 3), ("smallGrid3D", 5)])
+def test_certificate_thick_restart(hip, name, r, seed_x):
+    """dpgo_hip_certify_ex with a basis far below the iteration count (thick restarts), optionally with the
+    rows of X as a locked seed block: lambda_min of the explicit matrix (no seeds) or the block quantities
+    of S = [A_s B^T; B C] and the sandwich lower_bound <= lambda_min(S) <= lambda (seeds); true residuals."""
+    meas = load_meas(name)
+    d, n = meas.d, meas.num_poses
+    Q = O.connection_laplacian(meas, n)
+    X = random_point(r, d, n, 62)
+    H = hip.Problem(n, d, r)
+    H.set_Q_edges(0, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau, meas.weight)
+    S = O.certificate_matrix(Q, X, d)
+    ev = np.linalg.eigvalsh(S.toarray())
+    lam_max = float(np.abs(ev).max())
+    lam, res, it, v = H.certify(X, max_iters=4000, tol=1e-10, want_vector=True, basis=40, seed_x=seed_x)
+    info = H.last_certificate
+    assert abs(np.linalg.norm(v) - 1.0) <= 1e-8
+    true_res = np.linalg.norm(np.asarray((S @ v.T).T) - lam * v)
+    assert abs(true_res - res) <= 1e-3 * true_res + 1e-9 * lam_max, (true_res, res)
+    assert info["restarts"] >= 1 or info["iters"] <= 40, info  # tinyGrid3D's row-0 space is exhausted first
+    if not seed_x:
+        assert abs(lam - ev[0]) <= 1e-6 * lam_max, (lam, ev[0], res, it)
+        assert true_res <= 1e-6 * lam_max
+        return
+    lam_s, lam_c, coup, ns = _seed_blocks(S, X)
+    assert info["seeds"] == ns
+    assert abs(info["lambda_seed"] - lam_s) <= 1e-9 * lam_max, (info, lam_s)
+    assert abs(info["lambda_complement"] - lam_c) <= 1e-6 * lam_max, (info, lam_c)
+    assert info["residual_complement"] <= 1e-6 * lam_max
+    assert abs(info["coupling"] - coup) <= 1e-9 * lam_max + 1e-6 * coup, (info, coup)
+    assert info["lower_bound"] <= ev[0] + 1e-9 * lam_max <= lam + 2e-9 * lam_max, (info, ev[0], lam)
+    assert lam == min(info["lambda_seed"], info["lambda_complement"])
+    assert float(np.abs(v[1:]).max()) == 0.0  # the search space lives on row 0 of the lifted layout
+
+
+def test_graph_certify_seeded_at_optimum(hip):
+    """At the RTR optimum of smallGrid3D (S(X) X^T ~ 0) the locked seed block carries the near-null cluster,
+    its coupling to the complement is ~0 and the bound certifies: lower_bound >= -eps, with
+    lower_bound <= lambda_min(S) <= lambda_min (reported)."""
+    meas = load_meas("smallGrid3D")
+    d, n, r = meas.d, meas.num_poses, 5
+    Q = O.connection_laplacian(meas, n)
+    X0 = O.lifting_matrix(d, r) @ O.chordal_initialization(d, n, meas)
+    H = hip.Problem(n, d, r)
+    H.set_Q_scipy(0, Q)
+    Xo, _ = H.optimize(X0, hip.default_params(tr_iterations=100, tr_tolerance=1e-10, tr_max_inner=200,
+                                              precon=hip.PRECON_EXACT))
+    g = hip.Graph.from_arrays(d, n, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau)
+    c = g.certify(Xo, r, max_iters=3000, tol=1e-10, basis=60, seed_x=True)
+    S = O.certificate_matrix(Q, Xo, d)
+    ev = np.linalg.eigvalsh(S.toarray())
+    lam_bound = float(abs(S).sum(axis=1).max())
+    lam_s, lam_c, coup, ns = _seed_blocks(S, Xo)
+    assert c["seeds"] == ns
+    assert abs(c["lambda_complement"] - lam_c) <= 1e-6 * lam_bound, (c, lam_c)
+    assert abs(c["coupling"] - coup) <= 1e-8 * lam_bound + 1e-5 * coup, (c, coup)
+    assert c["coupling"] <= 1e-6 * lam_bound
+    assert c["lower_bound"] <= ev[0] + 1e-9 * lam_bound <= c["lambda_min"] + 2e-9 * lam_bound, (c, ev[:4])
+    assert c["lower_bound"] >= -1e-6 * lam_bound
+    assert c["gap"] >= -1e-9 * abs(c["f_relax"])
