@@ -2262,7 +2262,7 @@ int dpgo_hip_certify_ex(dpgo_hip_problem h, const double* X, int max_iters, int 
   const long L = static_cast<long>(h->vec_len());
   const int r = h->r;
   const bool seed_x = (flags & DPGO_CERT_SEED_X) != 0;
-  const int nseed = seed_x ? r : 0;
+  const int nseed = seed_x ? r + 1 : 0;
   // with a seed block everything lives on row 0 of the lifted layout: the basis is stored compact
   // ((d + 1) n doubles per vector, r x less traffic in the orthogonalisation) and expanded around the operator
   const long Lc = seed_x ? L / r : L;
@@ -2365,10 +2365,16 @@ int dpgo_hip_certify_ex(dpgo_hip_problem h, const double* X, int max_iters, int 
       if (Zg[static_cast<size_t>(r) * r + e] >= 1e-6 * gmax)
         seedv.insert(seedv.end(), Zg.begin() + static_cast<long>(e) * r, Zg.begin() + static_cast<long>(e + 1) * r);
   }
-  for (int j = 0; j < static_cast<int>(seedv.size()) / std::max(r, 1); ++j) {
+  // plus the translation gauge: every pose's translation column = 1 is an exact null vector of S (Q's
+  // translation terms t_j - t_i - R_i t_ij vanish for it, Lambda(X) has no translation part)
+  const int nxs = static_cast<int>(seedv.size()) / std::max(r, 1);
+  for (int j = 0; j < nxs + (seed_x ? 1 : 0); ++j) {
     for (long x = 0; x < L / r; ++x) {
       double acc = 0.0;
-      for (int i = 0; i < r; ++i) acc += seedv[static_cast<size_t>(j) * r + i] * X[x * r + i];
+      if (j < nxs)
+        for (int i = 0; i < r; ++i) acc += seedv[static_cast<size_t>(j) * r + i] * X[x * r + i];
+      else
+        acc = x % h->b == h->b - 1 ? 1.0 : 0.0;
       q0[x] = acc;
     }
     DPGO_TRY(upload(w, q0.data(), Lc, h->stream));
@@ -2538,7 +2544,11 @@ int dpgo_hip_certify_ex(dpgo_hip_problem h, const double* X, int max_iters, int 
     info->lambda_complement = theta_c;
     info->residual_complement = res_c;
     info->coupling = coupling;
-    info->lower_bound = (nl > 0 ? std::min(lam_s, theta_c - res_c) : theta_c - res_c) - coupling;
+    // x = (u, v) in (U, U_perp): x^T S x >= a |u|^2 - 2 beta |u||v| + c |v|^2 with a = lambda_min(A_s),
+    // c = theta_C - residual_C, beta = |B|_2 <= |B|_F: the 2 x 2 form's smallest eigenvalue
+    const double cl = theta_c - res_c;
+    info->lower_bound = nl > 0 ? 0.5 * (lam_s + cl) - std::sqrt(0.25 * (cl - lam_s) * (cl - lam_s) + coupling * coupling)
+                               : cl;
     for (int i = 0; i < 8; ++i) info->ritz[i] = i < static_cast<int>(theta.size()) ? theta[i] : NAN;
   }
   if (eigvec && !seed_x) DPGO_TRY(download(eigvec, io.c.p, L, h->stream));

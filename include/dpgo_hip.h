@@ -227,12 +227,15 @@ int dpgo_hip_certify(dpgo_hip_problem h, const double* X, int max_iters, double 
  * basis restarts from its lowest max(basis_max / 4, 8) Ritz vectors and the newest Krylov direction
  * (Rayleigh-Ritz on the dense projected matrix); max_iters counts operator applications over all
  * restarts.  flags DPGO_CERT_SEED_X: the principal directions of X's rows (S(X) X^T ~ 0 at a critical
- * point: the near-null space; singular values >= 1e-3 of the largest), orthonormalised, form a locked block U; the chain runs on its complement and U's block is
+ * point: the near-null space; singular values >= 1e-3 of the largest) and the translation gauge (every
+ * translation column = 1, an exact null vector), orthonormalised, form a locked block U; the chain runs on its complement and U's block is
  * resolved exactly, S = [A_s B^T; B C] in (U, U_perp).  Everything lives on row 0 of the lifted layout
  * (the operator acts row by row).  lambda_min = the lowest Ritz value found (an upper bound of
  * lambda_min(S)); info (optional) carries the true residual of the returned pair and the bound
- * lower_bound = min(lambda_min(A_s), theta_C - residual_C) - |B|_F, which is rigorous when theta_C is
- * C's lowest eigenvalue to within its residual (Lanczos from a random start: with probability ~1). */
+ * lower_bound = (a + c) / 2 - sqrt(((c - a) / 2)^2 + |B|_F^2), a = lambda_min(A_s), c = theta_C -
+ * residual_C (the smallest eigenvalue of [a -|B|; -|B| c], which bounds x^T S x from below), rigorous when
+ * theta_C is C's lowest eigenvalue to within its residual (Lanczos from a random start: with
+ * probability ~1). */
 #define DPGO_CERT_SEED_X 1
 typedef struct {
   int iters;                  /* operator applications (all restarts) */
@@ -243,7 +246,7 @@ typedef struct {
   double lambda_complement;   /* the chain's lowest Ritz value theta_C */
   double residual_complement; /* |P S y - theta_C y|, P = I - U U^T: its residual on C */
   double coupling;            /* |(I - U U^T) S U|_F (0 without seeds) */
-  double lower_bound;         /* min(lambda_seed, theta_C - residual_C) - coupling */
+  double lower_bound;         /* see above (theta_C - residual_C without seeds) */
   double ritz[8];             /* the chain's lowest Ritz values (NaN-padded) */
 } dpgo_cert_info;
 int dpgo_hip_certify_ex(dpgo_hip_problem h, const double* X, int max_iters, int basis_max, int flags, double tol,

@@ -145,13 +145,17 @@ def test_graph_certify_certified_gap(hip, name):
     assert abs(c["f_rounded"] - O.central_cost(meas, O.round_to_se(Xo, d))) <= 1e-10 * abs(c["f_rounded"])
 
 
-def _seed_blocks(S, X):
-    """The seed block's exact quantities for row 0 of the lifted layout: U = orthonormal rows of X,
+def _seed_blocks(S, X, d=3):
+    """The seed block's exact quantities for row 0 of the lifted layout: U = X's principal row directions and
+    the translation gauge, orthonormalised,
     lambda_min(U^T S U), lambda_min of S compressed to U's complement, |(I - U U^T) S U|_F."""
     import scipy.linalg as sl
     Sd = S.toarray()
     U, sv, _ = np.linalg.svd(X.T, full_matrices=False)
     U = U[:, sv >= 1e-3 * sv[0]]  # X's principal row directions, as dpgo_hip_certify_ex seeds them
+    gauge = np.zeros(X.shape[1])
+    gauge[d::d + 1] = 1.0
+    U, _ = np.linalg.qr(np.column_stack([U, gauge]))  # + the translation gauge (exact null vector)
     N = sl.null_space(U.T)
     SU = Sd @ U
     return (float(np.linalg.eigvalsh(U.T @ SU)[0]), float(np.linalg.eigvalsh(N.T @ Sd @ N)[0]),
@@ -183,7 +187,7 @@ def test_certificate_thick_restart(hip, name, r, seed_x):
         assert abs(lam - ev[0]) <= 1e-6 * lam_max, (lam, ev[0], res, it)
         assert true_res <= 1e-6 * lam_max
         return
-    lam_s, lam_c, coup, ns = _seed_blocks(S, X)
+    lam_s, lam_c, coup, ns = _seed_blocks(S, X, d)
     assert info["seeds"] == ns
     assert abs(info["lambda_seed"] - lam_s) <= 1e-9 * lam_max, (info, lam_s)
     assert abs(info["lambda_complement"] - lam_c) <= 1e-6 * lam_max, (info, lam_c)
@@ -211,7 +215,7 @@ def test_graph_certify_seeded_at_optimum(hip):
     S = O.certificate_matrix(Q, Xo, d)
     ev = np.linalg.eigvalsh(S.toarray())
     lam_bound = float(abs(S).sum(axis=1).max())
-    lam_s, lam_c, coup, ns = _seed_blocks(S, Xo)
+    lam_s, lam_c, coup, ns = _seed_blocks(S, Xo, d)
     assert c["seeds"] == ns
     assert abs(c["lambda_complement"] - lam_c) <= 1e-6 * lam_bound, (c, lam_c)
     assert abs(c["coupling"] - coup) <= 1e-8 * lam_bound + 1e-5 * coup, (c, coup)

@@ -16,6 +16,12 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+CERT_RULE = ("lower_bound >= -eta, eta = 1e-6 |f(X)| / n; lower_bound = (a + c)/2 - sqrt(((c - a)/2)^2 + beta^2), "
+             "a = lambda_min(U^T S U), c = theta_C - residual_C, beta = |(I - U U^T) S U|_F, U = X's principal row "
+             "directions + the translation gauge (orthonormalised), theta_C = the thick-restarted Lanczos Ritz value "
+             "on U's complement (dpgo_hip_certify_ex, DPGO_CERT_SEED_X)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--k", type=int, default=48)
@@ -86,10 +92,7 @@ def main():
         "certify_seconds": cert_s,
         "eta": eta,
         "certified": bool(cert["lower_bound"] >= -eta),
-        "certified_rule": "lower_bound >= -eta, eta = 1e-6 |f(X)| / n; lower_bound = min(lambda_min(U^T S U), "
-                          "theta_C - residual_C) - |(I - U U^T) S U|_F with U the orthonormalised rows of X and "
-                          "theta_C the thick-restarted Lanczos Ritz value on U's complement "
-                          "(dpgo_hip_certify_ex, DPGO_CERT_SEED_X)",
+        "certified_rule": CERT_RULE,
     }
     s = json.dumps(out, indent=1)
     print(s)
