@@ -453,7 +453,13 @@ int device_factor(dpgo_hip_problem h) {
                          h->fac_ent.p, h->fac_src.p, h->rec.p, h->diag.p, 0.1, h->fac_F[dep & 1].p,
                          h->fac_F[(dep + 1) & 1].p, h->sn_panel.p, h->fac_not_pd.p};
     if (verbose) HIP_TRY(hipEventRecord(lev[dep + 1], h->stream));
-    HIP_TRY(dpgo::launch_sn_factor(h->b, v, n1 - n0, h->stream));
+    if (dep < static_cast<int>(h->fac_seq.size()) && !h->fac_seq[dep].empty()) {
+      for (const auto& fl : h->fac_seq[dep])
+        HIP_TRY(dpgo::launch_sn_factor_tiled(h->b, v, fl.kind, fl.param, h->fac_titems.p + fl.off, fl.count,
+                                             h->stream));
+    } else {
+      HIP_TRY(dpgo::launch_sn_factor(h->b, v, n1 - n0, h->stream));
+    }
   }
   if (verbose) HIP_TRY(hipEventRecord(lev[0], h->stream));
   HIP_TRY(hipEventRecord(e1, h->stream));
@@ -740,9 +746,83 @@ int sync_chol(dpgo_hip_problem h) {
       for (int v : nd.R) fpos[v] = -1;
     }
   }
-  if (std::getenv("DPGO_VERBOSE_CHOL"))
+  // tile-parallel levels: at most 4096 supernodes (one workgroup per node would leave CUs idle) with a
+  // frontal matrix of at least 8 tile rows; DPGO_FAC_TILED_MAX_NODES overrides the node limit (0: never)
+  int tiled_max = 4096;
+  if (const char* e = std::getenv("DPGO_FAC_TILED_MAX_NODES")) tiled_max = std::atoi(e);
+  std::vector<int2> titems;
+  h->fac_seq.assign(maxd + 1, {});
+  for (int dep = 0; dep <= maxd; ++dep) {
+    const int n0 = level_off[dep], n1 = level_off[dep + 1];
+    int max_nt = 0, max_ns = 0, max_ch = 0;
+    for (int x = n0; x < n1; ++x) {
+      const int g = fac_nodes[x];
+      const int Sp = dpgo::sn_pad(s_[g] * b), M = Sp + dpgo::sn_pad(t_[g] * b);
+      max_nt = std::max(max_nt, M / dpgo::kSnTile);
+      max_ns = std::max(max_ns, Sp / dpgo::kSnTile);
+      max_ch = std::max(max_ch, ch_off[g + 1] - ch_off[g]);
+    }
+    if (n1 - n0 > tiled_max || max_nt < 8) continue;
+    auto& seq = h->fac_seq[dep];
+    auto launch = [&](int kind, int param, const std::vector<int2>& it) {
+      if (it.empty()) return;
+      seq.push_back({kind, param, static_cast<int>(titems.size()), static_cast<int>(it.size())});
+      titems.insert(titems.end(), it.begin(), it.end());
+    };
+    std::vector<int2> it;
+    for (int phase = 0; phase < 2 + max_ch; ++phase) {  // assembly: zero, entries, children in order
+      it.clear();
+      for (int x = n0; x < n1; ++x) {
+        const int g = fac_nodes[x];
+        long n = 0;
+        if (phase == 0)
+          n = (dpgo::sn_pad(s_[g] * b) + dpgo::sn_pad(t_[g] * b) + dpgo::kSnTile - 1) / dpgo::kSnTile;
+        else if (phase == 1)
+          n = (ent_off[g + 1] - ent_off[g] + dpgo::kThreads - 1) / dpgo::kThreads;
+        else if (phase - 2 < ch_off[g + 1] - ch_off[g])
+          n = (static_cast<long>(t_[ch[ch_off[g] + phase - 2]]) * b + dpgo::kSnTile - 1) / dpgo::kSnTile;
+        for (int y = 0; y < n; ++y) it.push_back(make_int2(g, y));
+      }
+      launch(0, phase, it);
+    }
+    for (int K = 0; K < max_ns; ++K) {
+      std::vector<int2> dg, ts, up;
+      for (int x = n0; x < n1; ++x) {
+        const int g = fac_nodes[x];
+        const int ns = dpgo::sn_pad(s_[g] * b) / dpgo::kSnTile;
+        const int NT = ns + dpgo::sn_pad(t_[g] * b) / dpgo::kSnTile;
+        if (K >= ns) continue;
+        dg.push_back(make_int2(g, 0));
+        for (int I = K + 1; I < NT; ++I) {
+          ts.push_back(make_int2(g, I));
+          for (int J = K + 1; J <= I; ++J) up.push_back(make_int2(g, (I << 16) | J));
+        }
+      }
+      launch(1, K, dg);
+      launch(2, K, ts);
+      launch(3, K, up);
+    }
+    for (int J = max_ns - 1; J >= 0; --J) {
+      it.clear();
+      for (int x = n0; x < n1; ++x) {
+        const int g = fac_nodes[x];
+        const int ns = dpgo::sn_pad(s_[g] * b) / dpgo::kSnTile;
+        const int NT = ns + dpgo::sn_pad(t_[g] * b) / dpgo::kSnTile;
+        if (J >= ns) continue;
+        for (int I = J + 1; I < NT; ++I) it.push_back(make_int2(g, I));
+      }
+      launch(4, J, it);
+    }
+  }
+  DPGO_TRY(up(h->fac_titems, titems));
+  if (std::getenv("DPGO_VERBOSE_CHOL")) {
     std::fprintf(stderr, "[dpgo_hip] exact preconditioner: device factorisation, %d levels, frontal buffers %.3f + %.3f GiB\n",
                  maxd + 1, 8.0 * level_size[0] / (1 << 30), 8.0 * level_size[1] / (1 << 30));
+    std::fprintf(stderr, "[dpgo_hip] exact preconditioner: tile-parallel levels:");
+    for (int dep = 0; dep <= maxd; ++dep)
+      if (!h->fac_seq[dep].empty()) std::fprintf(stderr, " %d (%zu launches)", dep, h->fac_seq[dep].size());
+    std::fprintf(stderr, ", %zu items\n", titems.size());
+  }
   h->fac_level_off = level_off;
   DPGO_TRY(up(h->fac_nodes, fac_nodes));
   DPGO_TRY(up(h->fac_off, fac_off));

@@ -369,6 +369,11 @@ hipError_t launch_sn_bwd(int r, int b, const SnView& v, const int2* items, int c
                          hipStream_t stream);
 // numeric factorisation of one tree level's supernodes (count nodes, v.nodes), see SnFactorView
 hipError_t launch_sn_factor(int b, const SnFactorView& v, int count, hipStream_t stream);
+// the same tile-parallel over a level's nodes, one launch of the sequence (kind 0 assembly phase `param`: 0 zero,
+// 1 entries, 2 + c child c; 1 diagonal tile K = param; 2 L_IK; 3 trailing F_IJ; 4 panel column J = param); items:
+// (node, row block / entry chunk / I / I << 16 | J)
+hipError_t launch_sn_factor_tiled(int b, const SnFactorView& v, int kind, int param, const int2* items, int count,
+                                  hipStream_t stream);
 // z = P_X(zraw) (or z = zraw when project == 0); optional z_out / delta_out = -z; partials
 // <z, rref>, |rref|^2 per tile
 hipError_t launch_precond_finish(int r, int b, const LaunchCtx& c, const double* X, const double* zraw,

@@ -3580,6 +3580,180 @@ __global__ __launch_bounds__(kThreads) void k_sn_factor(SnFactorView v) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// The same factorisation tile-parallel over a level's nodes (levels with few, large supernodes: one workgroup per
+// node leaves most CUs idle there): per launch one row block / entry chunk / tile of every node of the level, the
+// right-looking K loop and the panel's J loop as launch sequences on the stream (FacLaunchKind).  Each tile sees
+// the same operations in the same order as in k_sn_factor, so the factors agree bitwise.
+// ------------------------------------------------------------------------------------------
+template <int B>
+__global__ __launch_bounds__(kThreads) void k_snf_asm(SnFactorView v, const int2* __restrict__ items, int phase) {
+  constexpr int D = B - 1, RW = edge_rec_width(D), DW = diag_width(D);
+  const int2 it = items[blockIdx.x];
+  const int g = it.x;
+  const int s = v.s[g], t = v.t[g], sb = s * B, tb = t * B, Sp = sn_pad_dev(sb), M = Sp + sn_pad_dev(tb);
+  const long ld = M;
+  double* __restrict__ F = v.F + v.f_off[g];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (phase == 0) {  // zero rows 64 it.y .. (identity on the padding rows)
+    const int i1 = min(M, it.y * kFT + kFT);
+    for (int i = it.y * kFT + wave; i < i1; i += 4) {
+      const bool pad = (i >= sb && i < Sp) || i >= Sp + tb;
+      for (int j = lane; j <= i; j += 64) F[static_cast<long>(i) * ld + j] = (i == j && pad) ? 1.0 : 0.0;
+    }
+    return;
+  }
+  const int* poses = v.poses + v.poses_off[g];
+  if (phase == 1) {  // original entries, chunk it.y of 256
+    const int e = v.ent_off[g] + it.y * kThreads + tid;
+    if (e >= v.ent_off[g + 1]) return;
+    const SnEntry en = v.ent[e];
+    double blk[B][B];
+    if (en.q == en.p) {
+      const double* dg = v.diag + static_cast<long>(poses[en.p]) * DW;
+#pragma unroll
+      for (int i = 0; i < B; ++i)
+#pragma unroll
+        for (int j = 0; j < B; ++j) blk[i][j] = dg[sym_index<B>(i, j)] + (i == j ? v.shift : 0.0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < B; ++i)
+#pragma unroll
+        for (int j = 0; j < B; ++j) blk[i][j] = 0.0;
+      for (int k = en.s0; k < en.s1; ++k) {
+        const int code = v.src[k];
+        const double* m = v.rec + static_cast<long>(code >> 1) * RW;
+#pragma unroll
+        for (int i = 0; i < B; ++i)
+#pragma unroll
+          for (int j = 0; j < B; ++j) blk[i][j] -= (code & 1) ? m[4 * j + i] : m[4 * i + j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B; ++i) {
+      const long row = sn_frow(en.q, i, s, B, Sp);
+#pragma unroll
+      for (int j = 0; j < B; ++j) {
+        const int col = en.p * B + j;
+        if (row >= col) F[row * ld + col] += blk[i][j];
+      }
+    }
+    return;
+  }
+  // phase 2 + c: child c's update matrix extend-added, its rows 64 it.y ..
+  const int c = v.ch[v.ch_off[g] + phase - 2];
+  const int tcb = v.t[c] * B, Spc = sn_pad_dev(v.s[c] * B);
+  const long ldc = Spc + sn_pad_dev(tcb);
+  const double* __restrict__ U = v.Fchild + v.f_off[c] + Spc * ldc + Spc;
+  const int* tp = v.tp + v.tp_off[c];
+  const int r1 = min(tcb, it.y * kFT + kFT);
+  for (int ri = it.y * kFT + wave; ri < r1; ri += 4) {
+    const long pr = sn_frow(tp[ri / B], ri % B, s, B, Sp);
+    for (int rj = lane; rj <= ri; rj += 64) {
+      const long pc = sn_frow(tp[rj / B], rj % B, s, B, Sp);
+      F[pr * ld + pc] += U[static_cast<long>(ri) * ldc + rj];
+    }
+  }
+}
+
+// kind 1: the diagonal tile K of every node (POTRF, its inverse into the panel); 2: L_IK = F_IK L_KK^-T, item
+// (node, I); 3: F_IJ -= L_IK L_JK^T, item (node, I << 16 | J); 4: the panel's tile (I, J = param), item (node, I)
+template <int B, int KIND>
+__global__ __launch_bounds__(kThreads) void k_snf_tile(SnFactorView v, const int2* __restrict__ items, int P) {
+  constexpr int kind = KIND;
+  __shared__ double As[kFT * kFLD], Bs[kFT * kFLD];
+  __shared__ int s_bad;
+  const int2 it = items[blockIdx.x];
+  const int g = it.x;
+  const int s = v.s[g], t = v.t[g], sb = s * B, tb = t * B, Sp = sn_pad_dev(sb), M = Sp + sn_pad_dev(tb);
+  const int NT = M / kFT, ns = Sp / kFT;
+  const long ld = M;
+  double* __restrict__ F = v.F + v.f_off[g];
+  double* __restrict__ panel = v.panel + v.panel_off[g];
+  const int tid = threadIdx.x, wave = tid >> 6;
+  if constexpr (kind == 1) {
+    const int K = P;
+    if (tid == 0) s_bad = 0;
+    sn_tile_to_lds(As, F + static_cast<long>(K) * kFT * ld + K * kFT, ld);
+    __syncthreads();
+    sn_potrf_lds(As, &s_bad);
+    sn_trtri_lds(As, Bs);
+    for (int x = tid; x < kFT * kFT; x += kThreads) {
+      const int i = x / kFT, j = x % kFT;
+      F[(static_cast<long>(K) * kFT + i) * ld + K * kFT + j] = As[i * kFLD + j];
+      const bool real = K * kFT + i < sb && K * kFT + j < sb;
+      panel[sn_tile_dev(ns, K, K) * kFT * kFT + x] = real ? Bs[i * kFLD + j] : 0.0;
+    }
+    if (tid == 0 && s_bad) *v.not_pd = 1;
+    return;
+  }
+  if constexpr (kind == 2) {
+    const int K = P, I = it.y;
+    // L_KK^-1 with its padding block (identity there; the panel stores zeros)
+    const double* dk = panel + sn_tile_dev(ns, K, K) * kFT * kFT;
+    for (int x = tid; x < kFT * kFT; x += kThreads) {
+      const int i = x / kFT, j = x % kFT;
+      const bool padi = K * kFT + i >= sb;
+      Bs[i * kFLD + j] = padi ? (i == j ? 1.0 : 0.0) : dk[x];
+    }
+    double* gt = F + static_cast<long>(I) * kFT * ld + K * kFT;
+    sn_tile_to_lds(As, gt, ld);
+    __syncthreads();
+    f64x4 acc[4] = {};
+    mfma_strip<true>(acc, As, Bs, wave * 16, 1.0);
+    sn_strip_store(acc, gt, ld, wave * 16);
+    return;
+  }
+  if constexpr (kind == 3) {
+    const int K = P, I = it.y >> 16, J = it.y & 0xFFFF;
+    sn_tile_to_lds(As, F + static_cast<long>(I) * kFT * ld + K * kFT, ld);
+    sn_tile_to_lds(Bs, F + static_cast<long>(J) * kFT * ld + K * kFT, ld);
+    __syncthreads();
+    double* gt = F + static_cast<long>(I) * kFT * ld + J * kFT;
+    f64x4 acc[4];
+    sn_strip_load(acc, gt, ld, wave * 16);
+    mfma_strip<true>(acc, As, Bs, wave * 16, -1.0);
+    sn_strip_store(acc, gt, ld, wave * 16);
+    return;
+  }
+  // kind 4: Z_IJ = (B_IJ - sum_{K > J} Z_IK L_KJ) L_JJ^-1
+  const int J = P, I = it.y;
+  f64x4 acc[4] = {};
+  if (I >= ns) sn_strip_load(acc, F + static_cast<long>(I) * kFT * ld + J * kFT, ld, wave * 16);
+  const int Kmax = I < ns ? I : ns - 1;
+  for (int K = J + 1; K <= Kmax; ++K) {
+    const double* z = panel + sn_tile_dev(ns, I, K) * kFT * kFT;
+    for (int x = tid; x < kFT * kFT; x += kThreads) As[(x / kFT) * kFLD + x % kFT] = z[x];
+    sn_tile_to_lds(Bs, F + static_cast<long>(K) * kFT * ld + J * kFT, ld);
+    __syncthreads();
+    mfma_strip<false>(acc, As, Bs, wave * 16, -1.0);
+    __syncthreads();
+  }
+  {
+    const int l = tid & 63;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) As[(wave * 16 + (l >> 4) + 4 * q) * kFLD + cb * 16 + (l & 15)] = acc[cb][q];
+  }
+  const double* dj = panel + sn_tile_dev(ns, J, J) * kFT * kFT;
+  for (int x = tid; x < kFT * kFT; x += kThreads) Bs[(x / kFT) * kFLD + x % kFT] = dj[x];
+  __syncthreads();
+  f64x4 z[4] = {};
+  mfma_strip<false>(z, As, Bs, wave * 16, 1.0);
+  const int l = tid & 63;
+  double* out = panel + sn_tile_dev(ns, I, J) * kFT * kFT;
+  const int rbase = I < ns ? I * kFT : (I - ns) * kFT, rlim = I < ns ? sb : tb;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rr = wave * 16 + (l >> 4) + 4 * q, cc = cb * 16 + (l & 15);
+      const bool real = rbase + rr < rlim && J * kFT + cc < sb;
+      out[rr * kFT + cc] = real ? z[cb][q] : 0.0;
+    }
+}
+
 template <int R, int B>
 __global__ __launch_bounds__(kThreads) void k_precond_finish(LaunchCtx c, const double* __restrict__ X,
                                                              const double* __restrict__ zraw,
@@ -3763,6 +3937,12 @@ hipError_t spmm_variant54(int var, dim3 grid, const LaunchCtx& c, const QView& q
 
 }  // namespace
 
+// occupancy hint of the unified-loop HESS_M kernel (evar_waves bits: 0 none, 2 / 4 / 6 = 4 / 5 / 6 waves per SIMD)
+#ifndef DPGO_UNI_WAVES
+#define DPGO_UNI_WAVES 0
+#endif
+constexpr int kUniWaves = DPGO_UNI_WAVES & 6;
+
 template <int MODE>
 hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const SpmmArgs& a) {
   if (q.fmt == QFMT_EDGES) {
@@ -3778,11 +3958,11 @@ hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q
       if (uni && r == 5 && b == 4) {
         if constexpr (kPreMode) {
           if (q.tuning[TUNE_EPI_PREFETCH] > 0) {
-            k_spmm<5, 4, MODE, V2 | 8 | 128 | 256, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+            k_spmm<5, 4, MODE, V2 | (MODE == MODE_HESS_M ? kUniWaves : 0) | 8 | 128 | 256, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
             return hipSuccess;
           }
         }
-        k_spmm<5, 4, MODE, V2 | 128 | 256, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+        k_spmm<5, 4, MODE, V2 | (MODE == MODE_HESS_M ? kUniWaves : 0) | 128 | 256, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
         return hipSuccess;
       }
       if (r == 5 && b == 4 && (q.tuning[TUNE_EDGE_VARIANT] < 0 || mode_merged(MODE))) {
@@ -4045,6 +4225,34 @@ hipError_t launch_sn_factor(int b, const SnFactorView& v, int count, hipStream_t
     k_sn_factor<3><<<count, kThreads, 0, stream>>>(v);
   else
     return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_sn_factor_tiled(int b, const SnFactorView& v, int kind, int param, const int2* items, int count,
+                                  hipStream_t stream) {
+  if (count == 0) return hipSuccess;
+  if (kind == 0) {
+    if (b == 4)
+      k_snf_asm<4><<<count, kThreads, 0, stream>>>(v, items, param);
+    else if (b == 3)
+      k_snf_asm<3><<<count, kThreads, 0, stream>>>(v, items, param);
+    else
+      return hipErrorInvalidValue;
+  } else {
+    if (b != 3 && b != 4) return hipErrorInvalidValue;
+#define DPGO_SNF(K)                                                             \
+  case K:                                                                       \
+    if (b == 4)                                                                 \
+      k_snf_tile<4, K><<<count, kThreads, 0, stream>>>(v, items, param);        \
+    else                                                                        \
+      k_snf_tile<3, K><<<count, kThreads, 0, stream>>>(v, items, param);        \
+    break;
+    switch (kind) {
+      DPGO_SNF(1) DPGO_SNF(2) DPGO_SNF(3) DPGO_SNF(4)
+      default: return hipErrorInvalidValue;
+    }
+#undef DPGO_SNF
+  }
   return hipGetLastError();
 }
 

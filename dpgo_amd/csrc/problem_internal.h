@@ -131,6 +131,13 @@ struct dpgo_hip_problem_s {
   dpgo::DevBuf<long> fac_off;
   dpgo::DevBuf<dpgo::SnEntry> fac_ent;
   dpgo::DevBuf<double> fac_F[2];  // frontal matrices of the even / odd tree depths
+  // tree levels factorised tile-parallel (few, large supernodes): per depth the launch sequence of
+  // launch_sn_factor_tiled over fac_titems (empty: one workgroup per node, k_sn_factor)
+  struct FacLaunch {
+    int kind, param, off, count;
+  };
+  std::vector<std::vector<FacLaunch>> fac_seq;
+  dpgo::DevBuf<int2> fac_titems;
   double chol_factor_ms = 0.0;    // the last device factorisation (hipEvent), for the benches
   int chol_factor_count = 0;
   // host copy of the edge-stream incidences (sync_q_edges), for the factor's assembly tables

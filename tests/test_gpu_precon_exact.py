@@ -204,6 +204,26 @@ def test_device_factor_large_separator(hip, k):
     assert rel(got[1], got[0]) <= 1e-12
 
 
+@pytest.mark.parametrize("k", [12, 20])
+def test_device_factor_tiled_levels_bitwise(hip, k, monkeypatch):
+    """The tile-parallel factorisation of the large top levels (k_snf_asm / k_snf_tile, one launch per step of the
+    right-looking K loop) applies every tile the same operations in the same order as the one-workgroup-per-node
+    kernel: the preconditioner outputs agree bitwise (DPGO_FAC_TILED_MAX_NODES=0 forces k_sn_factor everywhere)."""
+    g, meas = _grid_meas(hip, k, 7)
+    d, n, r = 3, g.n, 5
+    X = random_point(r, d, n, 61)
+    V = random_tangent(X, d, 62)
+    got = {}
+    for lim in ("0", "4096"):
+        monkeypatch.setenv("DPGO_FAC_TILED_MAX_NODES", lim)
+        H = hip.Problem(n, d, r)
+        H.set_tuning(12, 1)
+        H.set_Q_edges(0, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau, meas.weight)
+        H.set_precon(hip.PRECON_EXACT)
+        got[lim] = H.precondition(X, V)
+    assert np.array_equal(got["0"], got["4096"]), float(np.abs(got["0"] - got["4096"]).max())
+
+
 def test_device_refactor_after_reweighting(hip):
     """set_edge_weights_dev (the on-device GNC reweighting) leaves the pattern and refreshes only the numeric half:
     the next application re-runs k_sn_factor on the new weights and matches the oracle's LU of the reweighted Q."""
