@@ -785,22 +785,38 @@ int sync_chol(dpgo_hip_problem h) {
       }
       launch(0, phase, it);
     }
-    for (int K = 0; K < max_ns; ++K) {
-      std::vector<int2> dg, ts, up;
+    // right-looking over blocks of kBK columns: inside a block every K updates only the block's own columns
+    // (the next diagonal tiles and L_IK depend on them); the tiles right of the block take the block's kBK
+    // updates in one pass (kind 5: one load / store of F_IJ instead of kBK, the same MFMA order)
+    constexpr int kBK = 4;  // kSnfBlockK (kernels.hip)
+    for (int KB = 0; KB < max_ns; KB += kBK) {
+      for (int K = KB; K < std::min(KB + kBK, max_ns); ++K) {
+        std::vector<int2> dg, ts, up;
+        for (int x = n0; x < n1; ++x) {
+          const int g = fac_nodes[x];
+          const int ns = dpgo::sn_pad(s_[g] * b) / dpgo::kSnTile;
+          const int NT = ns + dpgo::sn_pad(t_[g] * b) / dpgo::kSnTile;
+          if (K >= ns) continue;
+          dg.push_back(make_int2(g, 0));
+          for (int I = K + 1; I < NT; ++I) {
+            ts.push_back(make_int2(g, I));
+            for (int J = K + 1; J <= std::min(I, KB + kBK - 1); ++J) up.push_back(make_int2(g, (I << 16) | J));
+          }
+        }
+        launch(1, K, dg);
+        launch(2, K, ts);
+        launch(3, K, up);
+      }
+      std::vector<int2> rest;
       for (int x = n0; x < n1; ++x) {
         const int g = fac_nodes[x];
         const int ns = dpgo::sn_pad(s_[g] * b) / dpgo::kSnTile;
         const int NT = ns + dpgo::sn_pad(t_[g] * b) / dpgo::kSnTile;
-        if (K >= ns) continue;
-        dg.push_back(make_int2(g, 0));
-        for (int I = K + 1; I < NT; ++I) {
-          ts.push_back(make_int2(g, I));
-          for (int J = K + 1; J <= I; ++J) up.push_back(make_int2(g, (I << 16) | J));
-        }
+        if (KB >= ns) continue;
+        for (int I = KB + kBK; I < NT; ++I)
+          for (int J = KB + kBK; J <= I; ++J) rest.push_back(make_int2(g, (I << 16) | J));
       }
-      launch(1, K, dg);
-      launch(2, K, ts);
-      launch(3, K, up);
+      launch(5, KB, rest);
     }
     for (int J = max_ns - 1; J >= 0; --J) {
       it.clear();

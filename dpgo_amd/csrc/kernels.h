@@ -370,7 +370,8 @@ hipError_t launch_sn_bwd(int r, int b, const SnView& v, const int2* items, int c
 // numeric factorisation of one tree level's supernodes (count nodes, v.nodes), see SnFactorView
 hipError_t launch_sn_factor(int b, const SnFactorView& v, int count, hipStream_t stream);
 // the same tile-parallel over a level's nodes, one launch of the sequence (kind 0 assembly phase `param`: 0 zero,
-// 1 entries, 2 + c child c; 1 diagonal tile K = param; 2 L_IK; 3 trailing F_IJ; 4 panel column J = param); items:
+// 1 entries, 2 + c child c; 1 diagonal tile K = param; 2 L_IK; 3 trailing F_IJ; 4 panel column J = param; 5 the
+// trailing F_IJ right of the column block starting at K = param, all of the block's K at once); items:
 // (node, row block / entry chunk / I / I << 16 | J)
 hipError_t launch_sn_factor_tiled(int b, const SnFactorView& v, int kind, int param, const int2* items, int count,
                                   hipStream_t stream);

@@ -3656,6 +3656,9 @@ __global__ __launch_bounds__(kThreads) void k_snf_asm(SnFactorView v, const int2
   }
 }
 
+// kind 5 (the blocked trailing update): the tiles right of the current block of kSnfBlockK columns
+constexpr int kSnfBlockK = 4;
+
 // kind 1: the diagonal tile K of every node (POTRF, its inverse into the panel); 2: L_IK = F_IK L_KK^-T, item
 // (node, I); 3: F_IJ -= L_IK L_JK^T, item (node, I << 16 | J); 4: the panel's tile (I, J = param), item (node, I)
 template <int B, int KIND>
@@ -3701,6 +3704,21 @@ __global__ __launch_bounds__(kThreads) void k_snf_tile(SnFactorView v, const int
     __syncthreads();
     f64x4 acc[4] = {};
     mfma_strip<true>(acc, As, Bs, wave * 16, 1.0);
+    sn_strip_store(acc, gt, ld, wave * 16);
+    return;
+  }
+  if constexpr (kind == 5) {  // F_IJ -= sum_{K = P .. P + kSnfBlockK - 1, K < ns} L_IK L_JK^T, K in order
+    const int I = it.y >> 16, J = it.y & 0xFFFF, K1 = min(P + kSnfBlockK, ns);
+    double* gt = F + static_cast<long>(I) * kFT * ld + J * kFT;
+    f64x4 acc[4];
+    sn_strip_load(acc, gt, ld, wave * 16);
+    for (int K = P; K < K1; ++K) {
+      sn_tile_to_lds(As, F + static_cast<long>(I) * kFT * ld + K * kFT, ld);
+      sn_tile_to_lds(Bs, F + static_cast<long>(J) * kFT * ld + K * kFT, ld);
+      __syncthreads();
+      mfma_strip<true>(acc, As, Bs, wave * 16, -1.0);
+      __syncthreads();
+    }
     sn_strip_store(acc, gt, ld, wave * 16);
     return;
   }
@@ -4248,7 +4266,7 @@ hipError_t launch_sn_factor_tiled(int b, const SnFactorView& v, int kind, int pa
       k_snf_tile<3, K><<<count, kThreads, 0, stream>>>(v, items, param);        \
     break;
     switch (kind) {
-      DPGO_SNF(1) DPGO_SNF(2) DPGO_SNF(3) DPGO_SNF(4)
+      DPGO_SNF(1) DPGO_SNF(2) DPGO_SNF(3) DPGO_SNF(4) DPGO_SNF(5)
       default: return hipErrorInvalidValue;
     }
 #undef DPGO_SNF
