@@ -232,3 +232,35 @@ def test_c5_iterations_cpu_parity(hip):
         assert np.array_equal(e.stats()[:, 2:4], cpu.stats()[:, 2:4]), stop
     f1, gn1 = e.central_eval()
     assert f1 < f0 and np.isfinite(f1)
+
+
+def test_c5_burnin_regime_cpu_parity(hip):
+    """The regime bench.py times (C5, Nesterov, 300 untimed steps from the distributed initialisation, then
+    set_X of the burnt-in iterate): from that X the engine and oracle/cpu run the same 24 colour iterations --
+    every update 10 tCG iterations deep -- and end with X equal to 1e-9 and the per-agent Run / tCG counters
+    equal (the bench's like_for_like replay, as a test)."""
+    g, aop, X0 = _setup(hip, 100)
+    e = _engine(hip, g, aop, True)
+    e.set_X(X0)
+    for it in range(600):
+        e.pre_exchange(it % e.num_colors)
+        e.update(it % e.num_colors, None)
+    Xb = np.zeros(X0.size)
+    e.get_X_into(Xb)
+    e.set_X(Xb)  # PGOAgent::setX: Nesterov restarts from the burnt-in iterate
+    s0 = e.stats()[:, :10].copy()
+    iters = 24
+    for it in range(iters):
+        e.pre_exchange(it % e.num_colors)
+        e.update(it % e.num_colors, None)
+    Xg = np.zeros(X0.size)
+    e.get_X_into(Xg)
+    sg = e.stats()[:, :10] - s0
+    cpu = _cpu(g, aop, True)
+    cpu.set_X(Xb)
+    for _ in range(iters):
+        cpu.iterate(threads=16)
+    sc = cpu.stats()
+    assert rel(Xg, cpu.get_X()) <= 1e-9
+    assert np.array_equal(sg[:, 2:4], sc[:, 2:4])
+    assert sg[:, 3].sum() >= 9 * sg[:, 2].sum()  # the CG regime: (nearly) every Run takes 10 tCG iterations
