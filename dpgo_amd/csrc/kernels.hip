@@ -2603,9 +2603,24 @@ __global__ __launch_bounds__(kThreads) void k_accept(LaunchCtx c, const double* 
 static_assert(sizeof(AgentState) % sizeof(double) == 0, "AgentState is staged as doubles");
 // OPC >= 0: specialised for one op (the per-tCG-iteration ones): a few hundred instructions instead of every
 // op's logic -- a launch on a few CUs starts with a cold instruction cache, so the code it walks costs time.
+#ifdef DPGO_FIN_PROBE
+// tools/fin_probe.py (a variant build only): wall-clock marks inside the merged tCG finalize, agent 0's block
+__device__ long long g_fin_probe[256][6];
+__device__ int g_fin_probe_n;
+#define DPGO_FIN_MARK(i) \
+  if (probe) tp[i] = wall_clock64();
+#else
+#define DPGO_FIN_MARK(i)
+#endif
+
 template <int NQ, int OPC = -1>
 __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
   static_assert(NQ <= kMaxTot, "finalize slots");
+#ifdef DPGO_FIN_PROBE
+  long long tp[6] = {};
+  const bool probe = OPC == OP_TCG_STEP_CHECK && blockIdx.x == 0 && threadIdx.x == 0;
+#endif
+  DPGO_FIN_MARK(0)
   constexpr bool kDd = OPC < 0 || OPC == OP_TCG_STEP_CHECK || OPC == OP_TCG_CHECK_M;  // ops with dd partials
   const int agent = blockIdx.x;
   const int t0 = f.agent_tile_off[agent], t1 = f.agent_tile_off[agent + 1];
@@ -2638,6 +2653,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
       }
     }
   }
+  DPGO_FIN_MARK(1)
 #pragma unroll
   for (int q = 0; q < NQ; ++q)
     if (srcs[q] != nullptr) {
@@ -2645,6 +2661,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
       if constexpr (kDd) red_lo[q][threadIdx.x] = accl[q];
     }
   __syncthreads();
+  DPGO_FIN_MARK(2)
   // wave w reduces quantities w and w + 4 (lane 0's halving tree over the same lane pairs as the fused path)
   __shared__ double s_tot[2 * kMaxTot];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -2669,6 +2686,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
     }
   }
   __syncthreads();
+  DPGO_FIN_MARK(3)
   if (threadIdx.x != 0) return;
   double tot[kMaxTot], lo[kMaxTot];
 #pragma unroll
@@ -2679,10 +2697,19 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
   // the scalar logic runs on a register copy: a chain of dependent LDS accesses costs microseconds
   AgentState st = sh_state;
   finalize_scalar<OPC>(f, agent, tot, lo, st);
+  DPGO_FIN_MARK(4)
   double* dst = reinterpret_cast<double*>(&f.state[agent]);
   const double* srcw = reinterpret_cast<const double*>(&st);
 #pragma unroll
   for (int w = 0; w < kStateWords; ++w) dst[w] = srcw[w];
+#ifdef DPGO_FIN_PROBE
+  if (probe) {
+    __builtin_amdgcn_s_waitcnt(0);
+    tp[5] = wall_clock64();
+    const int slot = atomicAdd(&g_fin_probe_n, 1) & 255;
+    for (int m = 0; m < 6; ++m) g_fin_probe[slot][m] = tp[m];
+  }
+#endif
 }
 
 
@@ -4281,6 +4308,16 @@ hipError_t launch_precond_finish(int r, int b, const LaunchCtx& c, const double*
                                                                                       delta_out)));
   return hipGetLastError();
 }
+
+#ifdef DPGO_FIN_PROBE
+}  // namespace dpgo
+extern "C" int dpgo_hip_debug_fin_probe(long long* out, int* n) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(dpgo::g_fin_probe), sizeof(long long) * 256 * 6) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(n, HIP_SYMBOL(dpgo::g_fin_probe_n), sizeof(int)) != hipSuccess) return -1;
+  return 0;
+}
+namespace dpgo {
+#endif
 
 hipError_t launch_finalize(const FinalizeArgs& f, int num_agents, hipStream_t stream) {
   if (num_agents == 0) return hipSuccess;
