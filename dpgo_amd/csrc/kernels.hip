@@ -2603,6 +2603,9 @@ __global__ __launch_bounds__(kThreads) void k_accept(LaunchCtx c, const double* 
 static_assert(sizeof(AgentState) % sizeof(double) == 0, "AgentState is staged as doubles");
 // OPC >= 0: specialised for one op (the per-tCG-iteration ones): a few hundred instructions instead of every
 // op's logic -- a launch on a few CUs starts with a cold instruction cache, so the code it walks costs time.
+// the finalize's stand-in operand for an absent partial quantity
+__device__ const double g_zero_partial = 0.0;
+
 #ifdef DPGO_FIN_PROBE
 // tools/fin_probe.py (a variant build only): wall-clock marks inside the merged tCG finalize, agent 0's block
 __device__ long long g_fin_probe[256][6];
@@ -2640,16 +2643,26 @@ __global__ __launch_bounds__(kThreads) void k_finalize(FinalizeArgs f) {
     srcs[q] = part_src(f, q, qqs[q]);
   }
   for (int t = t0 + threadIdx.x; t < t1; t += kThreads) {
+    // every quantity's loads issued back to back (absent ones read a zero), then the sums: a load inside each
+    // quantity's branch waited for its own round trip before the next load was issued
+    double v[NQ], vl[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const bool have = srcs[q] != nullptr;
+      const double* ph = have ? srcs[q] + t * kPartialStride + qqs[q] : &g_zero_partial;
+      const double* pl = have && kDd && ((f.dd_mask >> q) & 1) ? ph + kDdLo : &g_zero_partial;
+      v[q] = *ph;
+      vl[q] = *pl;
+    }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       if (srcs[q] == nullptr) continue;
-      const double v = srcs[q][t * kPartialStride + qqs[q]];
       if (kDd && ((f.dd_mask >> q) & 1)) {
-        const dd a = dd_add({acc[q], accl[q]}, {v, srcs[q][t * kPartialStride + qqs[q] + kDdLo]});
+        const dd a = dd_add({acc[q], accl[q]}, {v[q], vl[q]});
         acc[q] = a.hi;
         accl[q] = a.lo;
       } else {
-        acc[q] += v;
+        acc[q] += v[q];
       }
     }
   }
