@@ -29,6 +29,9 @@ struct dpgo_rbcd_s {
   std::vector<int> color;                 // per global agent
   std::vector<int> owned;                 // owned global agents, colour-major
   std::vector<int> color_off;             // [ncolors + 1] into owned
+  // dpgo_rbcd_set_selected: per owned agent (colour-major, as `owned`) 1 = optimise when its colour is updated;
+  // empty = every agent of the colour (the colour schedule)
+  std::vector<int> sel_mask;
   std::vector<long> own_pose_off;         // [owned + 1] pose offsets into owned buffers
   long Nown = 0;
   std::vector<int> own_global;            // owned buffer pose index -> global pose id
@@ -228,8 +231,13 @@ int optimize_color(dpgo_rbcd e, int c, const double* Xin, double* Xout, dpgo_opt
   StatusArgs st{status_ref, e->lc[c]->valid ? e->lc[c]->ratio.p : nullptr, e->P.rel_change_tol,
                 e->P.min_convergence_ratio};
   if (!h->predict_boundary) e->g_store_calls[c] += 1;  // EVAL_TCG stores grad(x1) (byte model)
-  DPGO_TRY(optimize_dev_status(h, &p, Xin, Xout, nullptr, results, status_ref ? &st : nullptr));
-  e->agent_updates += h->K;
+  // a selection inside the colour (the example's greedy robot, dpgo_rbcd_set_selected): the others keep X_in, which
+  // is PGOAgent::updateX(false) -- X = Y with acceleration, X unchanged without
+  const int* en = e->sel_mask.empty() ? nullptr : e->sel_mask.data() + e->color_off[c];
+  DPGO_TRY(optimize_dev_status(h, &p, Xin, Xout, en, results, status_ref ? &st : nullptr));
+  int n_up = h->K;
+  if (en) n_up = static_cast<int>(std::count(en, en + h->K, 1));
+  e->agent_updates += n_up;
   return DPGO_HIP_OK;
 }
 
@@ -915,6 +923,17 @@ int dpgo_rbcd_exchange_counts_color(dpgo_rbcd e, int color, long long* send_coun
 }
 
 static int update_body(dpgo_rbcd e, int color, dpgo_opt_result* results);
+
+int dpgo_rbcd_set_selected(dpgo_rbcd e, const int* agent_mask) {
+  if (!e) return fail(DPGO_HIP_EINVAL, "null engine");
+  if (!agent_mask) {
+    e->sel_mask.clear();
+    return DPGO_HIP_OK;
+  }
+  e->sel_mask.assign(e->owned.size(), 0);
+  for (size_t q = 0; q < e->owned.size(); ++q) e->sel_mask[q] = agent_mask[e->owned[q]] != 0 ? 1 : 0;
+  return DPGO_HIP_OK;
+}
 
 int dpgo_rbcd_update(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_result* results) {
   if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");

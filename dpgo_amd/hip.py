@@ -520,6 +520,7 @@ _SIGS2 = [
     ("dpgo_rbcd_pre_exchange", [C.c_void_p, C.c_int], C.c_int),
     ("dpgo_rbcd_pack", [C.c_void_p, C.c_void_p], C.c_int),
     ("dpgo_rbcd_update", [C.c_void_p, C.c_int, C.c_void_p, C.POINTER(OptResult)], C.c_int),
+    ("dpgo_rbcd_set_selected", [C.c_void_p, _ip], C.c_int),
     ("dpgo_rbcd_bench_spmm", [C.c_void_p, C.c_int, C.c_int, _dp, _dp], C.c_int),
     ("dpgo_rbcd_counters", [C.c_void_p, _lp, _lp], C.c_int),
     ("dpgo_rbcd_spmm_bytes", [C.c_void_p, C.c_int, _dp, _dp], C.c_int),
@@ -949,6 +950,16 @@ class Rbcd:
 
     def pack(self, send_ptr):
         _check(lib().dpgo_rbcd_pack(self.h, C.c_void_p(send_ptr or 0)))
+
+    def set_selected(self, agent_mask=None):
+        """Optimise only these agents of the updated colour (None: all; the greedy schedule selects one)."""
+        if agent_mask is None:
+            _check(lib().dpgo_rbcd_set_selected(self.h, None))
+            return
+        m, mp = _i32(np.asarray(agent_mask) != 0)
+        if m.size != self.num_agents:
+            raise ValueError("agent_mask needs one entry per agent")
+        _check(lib().dpgo_rbcd_set_selected(self.h, mp))
 
     def update(self, color, recv_ptr, want_results=False):
         if want_results:

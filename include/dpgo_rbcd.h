@@ -160,6 +160,13 @@ int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color);
  * uses equals the sender's X, which ran iterate(false) this iteration). */
 int dpgo_rbcd_pack(dpgo_rbcd e, double* send_dev);
 /* Phase 2: selected agents of colour c update from the received neighbour poses. */
+/* Restrict the next updates to a subset of the selected colour's agents (agent_mask [num_agents], 1 =
+ * optimise; nullptr = every agent of the colour, the colour schedule).  The others of the colour run
+ * PGOAgent::iterate(false) like every other colour's agents (X = Y with acceleration, X unchanged without), so
+ * selecting one agent per round (colour = its colour) is the example's greedy schedule
+ * (examples/MultiRobotExample.cpp:243-256: the next robot is the argmax of the per-robot |RieGrad|, which
+ * dpgo_rbcd_central_eval returns squared per agent). */
+int dpgo_rbcd_set_selected(dpgo_rbcd e, const int* agent_mask);
 int dpgo_rbcd_update(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_result* results);
 /* Per-colour halo (examples/MultiRobotExample.cpp:188-213: only the selected robot pulls its neighbours'
  * poses): the poses the agents of colour c read this iteration -- about half the full plan with two

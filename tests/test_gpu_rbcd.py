@@ -152,3 +152,40 @@ def test_contiguous_partition_2d_eight_agents(hip, name):
     # measured: X agrees to ~1e-14 relative; the central cost is ill-conditioned in X on kitti_00
     # (translations ~2e3 against f ~ 80: a 2e-11 absolute X difference moves f by ~1e-9 relative)
     assert abs(O.central_cost(meas, Xh) - O.central_cost(meas, Xo)) <= 1e-8 * O.central_cost(meas, Xo)
+
+
+@pytest.mark.parametrize("accel", [False, True])
+def test_greedy_selection_matches_example(hip, accel):
+    """The example's greedy schedule (examples/MultiRobotExample.cpp:243-256) driven through the engine: each round
+    one agent is optimised (dpgo_rbcd_set_selected; every other agent runs iterate(false)), and the next one is the
+    argmax of the per-agent |RieGrad| from dpgo_rbcd_central_eval.  The selected robots, the gradient norms and the
+    final X equal the oracle's serialized restatement of the example (smallGrid3D, 5 contiguous robots, L2,
+    block-Jacobi)."""
+    meas = load_meas("smallGrid3D")
+    r, R, iters = 5, 5, 20
+    n = meas.num_poses
+    X0 = O.lifting_matrix(3, r) @ O.chordal_initialization(3, n, meas)
+    log, Xo = O.multi_robot_example(meas, R, r=r, num_iters=iters, acceleration=accel, robust="L2",
+                                    precon=O.PRECON_BLOCK_JACOBI, X_init=X0)
+    _, robot_of, _, _ = O.partition_contiguous(meas, n, R)
+    g = _graph_from_meas(hip, meas)
+    e = hip.Rbcd(g, robot_of.astype(np.int32), np.zeros(R, np.int32), 0, 1,
+                 hip.rbcd_params(r=r, acceleration=int(accel), precon=hip.PRECON_BLOCK_JACOBI))
+    e.set_X(X0)
+    sel, got = 0, []
+    for it in range(len(log)):
+        mask = np.zeros(R, np.int32)
+        mask[sel] = 1
+        e.set_selected(mask)
+        c = int(e.color_of_agent[sel])
+        e.pre_exchange(c)
+        e.update(c, None)
+        _, gn2 = e.central_eval()
+        got.append((sel, float(np.sqrt(gn2.sum()))))
+        sel = int(np.argmax(gn2))
+    assert [s for s, _ in got] == [s for _, s, _, _ in log]
+    for (_, gg), (_, _, _, go) in zip(got, log):
+        assert abs(gg - go) <= 1e-8 * max(go, 1.0), (gg, go)
+    Xd = np.zeros(X0.size)
+    e.get_X_into(Xd)
+    assert rel(hip.from_dev_layout(Xd, r), Xo) <= 1e-9
