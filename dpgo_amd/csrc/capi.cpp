@@ -2537,14 +2537,33 @@ int dpgo_hip_certify_ex(dpgo_hip_problem h, const double* X, int max_iters, int 
   const bool verbose = std::getenv("DPGO_VERBOSE_CERT") != nullptr;
   while (true) {
     // expand: S q_k, its column of T against the chain, the next direction orthogonal to U and the chain
-    DPGO_TRY(cert_apply(vec(k), w));
-    std::vector<double> sq;
-    DPGO_TRY(dots(w, w, 1, sq));  // |S q_k| before the projection: the breakdown test is relative to it
-    DPGO_TRY(orthogonalise(w, nb, cs));
+    // w = S q_k, straight into the next basis slot when there is one: its dots against the basis then carry
+    // |w|^2 too (the breakdown test is relative to |S q_k|)
+    const bool slot = nb - nl <= mmax;
+    double* wk = slot ? vec(nb) : w;
+    DPGO_TRY(cert_apply(vec(k), wk));
+    std::vector<double> c1, sq;
+    DPGO_TRY(dots(wk, V.p, slot ? nb + 1 : nb, c1));
+    if (slot)
+      sq.assign(1, c1[nb]);
+    else
+      DPGO_TRY(dots(wk, wk, 1, sq));
+    cs.assign(c1.begin(), c1.begin() + nb);
+    DPGO_TRY(subtract(wk, V.p, nb, cs));
+    // classical Gram-Schmidt with the DGKS criterion: a second pass when the first removed more than half of
+    // |w|^2 (where rounding can leave components along the basis), otherwise one pass
+    double kept = sq[0];
+    for (int j = 0; j < nb; ++j) kept -= cs[j] * cs[j];
+    if (kept < 0.5 * sq[0]) {
+      std::vector<double> c2;
+      DPGO_TRY(dots(wk, V.p, nb, c2));
+      DPGO_TRY(subtract(wk, V.p, nb, c2));
+      for (int j = 0; j < nb; ++j) cs[j] += c2[j];
+    }
     const int kc = k - nl;
     for (int j = nl; j < nb; ++j) Tat(j - nl, kc) = Tat(kc, j - nl) = cs[j];
     ++total;
-    DPGO_TRY(dots(w, w, 1, nn));
+    DPGO_TRY(dots(wk, wk, 1, nn));
     const double bk = std::sqrt(nn[0]);
     if (!dense) {
       alpha.push_back(cs[k]);
@@ -2552,8 +2571,8 @@ int dpgo_hip_certify_ex(dpgo_hip_problem h, const double* X, int max_iters, int 
     }
     // an invariant subspace up to rounding (CGS2 leaves ~eps |S q_k| sqrt(k)): the Ritz values are exact
     const bool breakdown = bk <= 1e-10 * std::sqrt(sq[0]);
-    if (nb - nl <= mmax && !breakdown) {
-      HIP_TRY(dpgo::launch_scale(Lc, w, 1.0 / bk, vec(nb), h->stream));
+    if (slot && !breakdown) {
+      HIP_TRY(dpgo::launch_scale(Lc, wk, 1.0 / bk, vec(nb), h->stream));
       Tat(nb - nl, kc) = Tat(kc, nb - nl) = bk;
       ++nb;
     }
