@@ -31,8 +31,8 @@ def main():
     ap.add_argument("--check", type=int, default=250, help="steps between central evaluations")
     ap.add_argument("--max-seconds", type=float, default=600.0)
     ap.add_argument("--precon", default="block_jacobi", choices=["block_jacobi", "exact"])
-    ap.add_argument("--lanczos-iters", type=int, default=3000, help="total Lanczos steps over all restarts")
-    ap.add_argument("--lanczos-basis", type=int, default=400, help="basis size before a thick restart")
+    ap.add_argument("--lanczos-iters", type=int, default=30000, help="total Lanczos steps over all restarts")
+    ap.add_argument("--lanczos-basis", type=int, default=500, help="basis size before a thick restart")
     ap.add_argument("--lanczos-tol", type=float, default=1e-8, help="stop at |S y - theta y| <= tol |theta|max")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
