@@ -504,7 +504,7 @@ def main():
             t_c = time.time()
             # thick-restarted Lanczos with X's near-null block locked (dpgo_graph_certify_ex): a lower bound on
             # lambda_min(S(X)), not only a Ritz value (tools/certify_c4.py runs it on converged iterates)
-            c = g.certify(Xc, args.r, max_iters=args.certify_iters, tol=1e-8, basis=min(500, args.certify_iters),
+            c = g.certify(Xc, args.r, max_iters=args.certify_iters, tol=1e-8, basis=500 if args.certify_iters > 500 else 0,
                           seed_x=True)
             c["seconds"] = time.time() - t_c
             eta = 1e-6 * abs(c["f_relax"]) / max(g.n, 1)
