@@ -748,8 +748,9 @@ int sync_chol(dpgo_hip_problem h) {
   }
   // tile-parallel levels: at most 4096 supernodes (one workgroup per node would leave CUs idle) with a
   // frontal matrix of at least 8 tile rows; DPGO_FAC_TILED_MAX_NODES overrides the node limit (0: never)
-  int tiled_max = 4096;
+  int tiled_max = 4096, tiled_min_rows = 8;
   if (const char* e = std::getenv("DPGO_FAC_TILED_MAX_NODES")) tiled_max = std::atoi(e);
+  if (const char* e = std::getenv("DPGO_FAC_TILED_MIN_TILES")) tiled_min_rows = std::atoi(e);  // tests: small graphs
   std::vector<int2> titems;
   h->fac_seq.assign(maxd + 1, {});
   for (int dep = 0; dep <= maxd; ++dep) {
@@ -762,7 +763,7 @@ int sync_chol(dpgo_hip_problem h) {
       max_ns = std::max(max_ns, Sp / dpgo::kSnTile);
       max_ch = std::max(max_ch, ch_off[g + 1] - ch_off[g]);
     }
-    if (n1 - n0 > tiled_max || max_nt < 8) continue;
+    if (n1 - n0 > tiled_max || max_nt < tiled_min_rows) continue;
     auto& seq = h->fac_seq[dep];
     auto launch = [&](int kind, int param, const std::vector<int2>& it) {
       if (it.empty()) return;

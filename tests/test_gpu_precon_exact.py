@@ -224,6 +224,33 @@ def test_device_factor_tiled_levels_bitwise(hip, k, monkeypatch):
     assert np.array_equal(got["0"], got["4096"]), float(np.abs(got["0"] - got["4096"]).max())
 
 
+@pytest.mark.parametrize("name,r", [("input_INTEL_g2o", 3), ("sphere2500", 3), ("smallGrid3D", 5)])
+def test_device_factor_tiled_every_level_bitwise(hip, name, r, monkeypatch):
+    """Every tree level forced through the tile-parallel kernels (DPGO_FAC_TILED_MIN_TILES=1), for d = 2 (b = 3) and
+    d = 3: the preconditioner equals the one-workgroup-per-node factor's bitwise and the oracle's sparse LU to
+    1e-10."""
+    meas = load_meas(name)
+    d, n = meas.d, meas.num_poses
+    Q = O.connection_laplacian(meas, n)
+    P = O.QuadraticProblem(n, d, r)
+    P.set_Q(Q)
+    X = random_point(r, d, n, 71)
+    V = random_tangent(X, d, 72)
+    ref = P.precondition(X, V, O.PRECON_EXACT)
+    got = {}
+    for lim in ("0", "1000000"):
+        monkeypatch.setenv("DPGO_FAC_TILED_MAX_NODES", lim)
+        monkeypatch.setenv("DPGO_FAC_TILED_MIN_TILES", "1")
+        H = hip.Problem(n, d, r)
+        H.set_tuning(12, 1)
+        H.set_Q_edges(0, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau, meas.weight)
+        H.set_precon(hip.PRECON_EXACT)
+        got[lim] = H.precondition(X, V)
+        assert H.exact_factor_info()["factor_count"] == 1
+    assert np.array_equal(got["0"], got["1000000"]), float(np.abs(got["0"] - got["1000000"]).max())
+    assert rel(got["1000000"], ref) <= 1e-10
+
+
 def test_device_refactor_after_reweighting(hip):
     """set_edge_weights_dev (the on-device GNC reweighting) leaves the pattern and refreshes only the numeric half:
     the next application re-runs k_sn_factor on the new weights and matches the oracle's LU of the reweighted Q."""
