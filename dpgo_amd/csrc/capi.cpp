@@ -2581,8 +2581,8 @@ int dpgo_hip_certify_ex(dpgo_hip_problem h, const double* X, int max_iters, int 
     const int m = k - nl;
     const bool full = nb - nl > mmax || breakdown;
     const bool last = total >= max_iters;
-    // Ritz checks: every 5 steps on the tridiagonal T (every ~2 % of the basis beyond 250); with restarts (a dense O(m^3) eigensolve on the host) at
-    // every 20 steps of a small basis, every 500 of a large one, and at each restart
+    // Ritz checks: every 5 steps on the tridiagonal T (every ~2 % of the basis beyond 250); with restarts (a dense
+    // O(m^3) eigensolve on the host) every 20 steps of a small basis, every 500 of a large one, and at each restart
     const bool check = dense ? ((m <= 200 && m % 20 == 0) || m % 500 == 0) : m % std::max(5, m / 250 * 5) == 0;
     if (!(check || full || last)) continue;
     rayleigh_ritz(m);
@@ -2618,8 +2618,8 @@ int dpgo_hip_certify_ex(dpgo_hip_problem h, const double* X, int max_iters, int 
   if (nl > 0) DPGO_TRY(residual_of(io.c.p, theta[0], res, 0));
   double lam = theta_c, lam_s = NAN, coupling = 0.0;
   if (nl > 0) {
-    // U's block A_s = U^T S U and the coupling |(I - U U^T) S U|_F: S = [A_s B^T; B C] in (U, U_perp), so
-    // lambda_min(S) >= min(lambda_min(A_s), lambda_min(C)) - |B|
+    // U's block A_s = U^T S U and the coupling |(I - U U^T) S U|_F: S = [A_s B^T; B C] in (U, U_perp), and
+    // lambda_min(S) is bounded below by the 2 x 2 form of the info's lower_bound
     std::vector<double> As(static_cast<size_t>(nl) * nl), col, s2, Zs;
     double c2 = 0.0;
     for (int j = 0; j < nl; ++j) {
