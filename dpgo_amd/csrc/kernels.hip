@@ -3400,6 +3400,28 @@ __device__ __forceinline__ void mfma_strip(f64x4 (&acc)[4], const double* As, co
   }
 }
 
+// The A operand of mfma_strip read straight from a global tile into registers (the wave's strip: row r0 + (l & 15),
+// columns 4 i + (l >> 4)), so a kernel needs only B's LDS tile: half the LDS, twice the resident workgroups
+__device__ __forceinline__ void sn_strip_a(double (&a)[kFT / 4], const double* __restrict__ Ag, long ld, int r0) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < kFT / 4; ++i) a[i] = Ag[(r0 + (l & 15)) * ld + 4 * i + (l >> 4)];
+}
+// acc += sign * A(strip, registers) . B^T (B an LDS tile): the same MFMA sequence as mfma_strip<true>
+__device__ __forceinline__ void mfma_strip_ra(f64x4 (&acc)[4], const double (&a)[kFT / 4], const double* Bs,
+                                              double sign) {
+  const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
+#pragma unroll
+  for (int k0 = 0; k0 < kFT; k0 += 4) {
+    const double av = sign * a[k0 / 4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const int c = cb * 16 + lr;
+      acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Bs[c * kFLD + k0 + lk], acc[cb], 0, 0, 0);
+    }
+  }
+}
+
 // global 64 x 64 tile (row-major, leading dimension ld) <-> LDS tile, all threads
 __device__ __forceinline__ void sn_tile_to_lds(double* Ls, const double* __restrict__ g, long ld) {
   for (int x = threadIdx.x; x < kFT * kFT; x += kThreads) {
@@ -3732,6 +3754,9 @@ __global__ __launch_bounds__(kThreads) void k_snf_tile(SnFactorView v, const int
   }
   if constexpr (kind == 2) {
     const int K = P, I = it.y;
+    double* gt = F + static_cast<long>(I) * kFT * ld + K * kFT;
+    double a[kFT / 4];
+    sn_strip_a(a, gt, ld, wave * 16);
     // L_KK^-1 with its padding block (identity there; the panel stores zeros)
     const double* dk = panel + sn_tile_dev(ns, K, K) * kFT * kFT;
     for (int x = tid; x < kFT * kFT; x += kThreads) {
@@ -3739,11 +3764,9 @@ __global__ __launch_bounds__(kThreads) void k_snf_tile(SnFactorView v, const int
       const bool padi = K * kFT + i >= sb;
       Bs[i * kFLD + j] = padi ? (i == j ? 1.0 : 0.0) : dk[x];
     }
-    double* gt = F + static_cast<long>(I) * kFT * ld + K * kFT;
-    sn_tile_to_lds(As, gt, ld);
     __syncthreads();
     f64x4 acc[4] = {};
-    mfma_strip<true>(acc, As, Bs, wave * 16, 1.0);
+    mfma_strip_ra(acc, a, Bs, 1.0);
     sn_strip_store(acc, gt, ld, wave * 16);
     return;
   }
@@ -3753,10 +3776,11 @@ __global__ __launch_bounds__(kThreads) void k_snf_tile(SnFactorView v, const int
     f64x4 acc[4];
     sn_strip_load(acc, gt, ld, wave * 16);
     for (int K = P; K < K1; ++K) {
-      sn_tile_to_lds(As, F + static_cast<long>(I) * kFT * ld + K * kFT, ld);
+      double a[kFT / 4];
+      sn_strip_a(a, F + static_cast<long>(I) * kFT * ld + K * kFT, ld, wave * 16);
       sn_tile_to_lds(Bs, F + static_cast<long>(J) * kFT * ld + K * kFT, ld);
       __syncthreads();
-      mfma_strip<true>(acc, As, Bs, wave * 16, -1.0);
+      mfma_strip_ra(acc, a, Bs, -1.0);
       __syncthreads();
     }
     sn_strip_store(acc, gt, ld, wave * 16);
@@ -3764,13 +3788,14 @@ __global__ __launch_bounds__(kThreads) void k_snf_tile(SnFactorView v, const int
   }
   if constexpr (kind == 3) {
     const int K = P, I = it.y >> 16, J = it.y & 0xFFFF;
-    sn_tile_to_lds(As, F + static_cast<long>(I) * kFT * ld + K * kFT, ld);
+    double a[kFT / 4];
+    sn_strip_a(a, F + static_cast<long>(I) * kFT * ld + K * kFT, ld, wave * 16);
     sn_tile_to_lds(Bs, F + static_cast<long>(J) * kFT * ld + K * kFT, ld);
     __syncthreads();
     double* gt = F + static_cast<long>(I) * kFT * ld + J * kFT;
     f64x4 acc[4];
     sn_strip_load(acc, gt, ld, wave * 16);
-    mfma_strip<true>(acc, As, Bs, wave * 16, -1.0);
+    mfma_strip_ra(acc, a, Bs, -1.0);
     sn_strip_store(acc, gt, ld, wave * 16);
     return;
   }
