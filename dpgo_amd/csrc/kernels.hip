@@ -3407,7 +3407,8 @@ __device__ __forceinline__ void sn_strip_a(double (&a)[kFT / 4], const double* _
 #pragma unroll
   for (int i = 0; i < kFT / 4; ++i) a[i] = Ag[(r0 + (l & 15)) * ld + 4 * i + (l >> 4)];
 }
-// acc += sign * A(strip, registers) . B^T (B an LDS tile): the same MFMA sequence as mfma_strip<true>
+// acc += sign * A(strip, registers) . op(B) (B an LDS tile): the same MFMA sequence as mfma_strip<BT>
+template <bool BT = true>
 __device__ __forceinline__ void mfma_strip_ra(f64x4 (&acc)[4], const double (&a)[kFT / 4], const double* Bs,
                                               double sign) {
   const int l = threadIdx.x & 63, lr = l & 15, lk = l >> 4;
@@ -3417,7 +3418,8 @@ __device__ __forceinline__ void mfma_strip_ra(f64x4 (&acc)[4], const double (&a)
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       const int c = cb * 16 + lr;
-      acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, Bs[c * kFLD + k0 + lk], acc[cb], 0, 0, 0);
+      const double bv = BT ? Bs[c * kFLD + k0 + lk] : Bs[(k0 + lk) * kFLD + c];
+      acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[cb], 0, 0, 0);
     }
   }
 }
@@ -3799,32 +3801,36 @@ __global__ __launch_bounds__(kThreads) void k_snf_tile(SnFactorView v, const int
     sn_strip_store(acc, gt, ld, wave * 16);
     return;
   }
-  // kind 4: Z_IJ = (B_IJ - sum_{K > J} Z_IK L_KJ) L_JJ^-1
+  // kind 4: Z_IJ = (B_IJ - sum_{K > J} Z_IK L_KJ) L_JJ^-1 (A strips in registers: one LDS tile)
   const int J = P, I = it.y;
   f64x4 acc[4] = {};
   if (I >= ns) sn_strip_load(acc, F + static_cast<long>(I) * kFT * ld + J * kFT, ld, wave * 16);
   const int Kmax = I < ns ? I : ns - 1;
   for (int K = J + 1; K <= Kmax; ++K) {
-    const double* z = panel + sn_tile_dev(ns, I, K) * kFT * kFT;
-    for (int x = tid; x < kFT * kFT; x += kThreads) As[(x / kFT) * kFLD + x % kFT] = z[x];
+    double a[kFT / 4];
+    sn_strip_a(a, panel + sn_tile_dev(ns, I, K) * kFT * kFT, kFT, wave * 16);
     sn_tile_to_lds(Bs, F + static_cast<long>(K) * kFT * ld + J * kFT, ld);
     __syncthreads();
-    mfma_strip<false>(acc, As, Bs, wave * 16, -1.0);
+    mfma_strip_ra<false>(acc, a, Bs, -1.0);
     __syncthreads();
   }
-  {
-    const int l = tid & 63;
+  const int l = tid & 63;
+  double a[kFT / 4];
+  {  // acc into the A-operand layout through the LDS tile (the wave's own 16 rows)
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) As[(wave * 16 + (l >> 4) + 4 * q) * kFLD + cb * 16 + (l & 15)] = acc[cb][q];
+      for (int q = 0; q < 4; ++q) Bs[(wave * 16 + (l >> 4) + 4 * q) * kFLD + cb * 16 + (l & 15)] = acc[cb][q];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kFT / 4; ++i) a[i] = Bs[(wave * 16 + (l & 15)) * kFLD + 4 * i + (l >> 4)];
+    __syncthreads();
   }
   const double* dj = panel + sn_tile_dev(ns, J, J) * kFT * kFT;
   for (int x = tid; x < kFT * kFT; x += kThreads) Bs[(x / kFT) * kFLD + x % kFT] = dj[x];
   __syncthreads();
   f64x4 z[4] = {};
-  mfma_strip<false>(z, As, Bs, wave * 16, 1.0);
-  const int l = tid & 63;
+  mfma_strip_ra<false>(z, a, Bs, 1.0);
   double* out = panel + sn_tile_dev(ns, I, J) * kFT * kFT;
   const int rbase = I < ns ? I * kFT : (I - ns) * kFT, rlim = I < ns ? sb : tb;
 #pragma unroll
