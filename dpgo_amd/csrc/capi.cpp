@@ -746,9 +746,9 @@ int sync_chol(dpgo_hip_problem h) {
       for (int v : nd.R) fpos[v] = -1;
     }
   }
-  // tile-parallel levels: at most 4096 supernodes (one workgroup per node would leave CUs idle) with a
-  // frontal matrix of at least 8 tile rows; DPGO_FAC_TILED_MAX_NODES overrides the node limit (0: never)
-  int tiled_max = 4096, tiled_min_rows = 8;
+  // tile-parallel levels: every level by default (with the A strips in registers the tile kernels beat one workgroup
+  // per node at every depth: C5 151 -> 142 ms); DPGO_FAC_TILED_MAX_NODES / _MIN_TILES restrict them (0: never)
+  int tiled_max = 1 << 30, tiled_min_rows = 1;
   if (const char* e = std::getenv("DPGO_FAC_TILED_MAX_NODES")) tiled_max = std::atoi(e);
   if (const char* e = std::getenv("DPGO_FAC_TILED_MIN_TILES")) tiled_min_rows = std::atoi(e);  // tests: small graphs
   std::vector<int2> titems;
