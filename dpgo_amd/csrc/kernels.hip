@@ -3744,12 +3744,26 @@ __global__ __launch_bounds__(kThreads) void k_snf_tile(SnFactorView v, const int
     sn_tile_to_lds(As, F + static_cast<long>(K) * kFT * ld + K * kFT, ld);
     __syncthreads();
     sn_potrf_lds(As, &s_bad);
-    sn_trtri_lds(As, Bs);
+    // L^-1 by sn_trtri_lds's recurrence, kept in the same tile: its strict lower part transposed into the (unused)
+    // strict upper triangle, its diagonal in s_dinv -- one LDS tile instead of two
+    __shared__ double s_dinv[kFT];
+    if (tid < kFT) {
+      const int c = tid;
+      const double dc = 1.0 / As[c * kFLD + c];
+      s_dinv[c] = dc;
+      for (int i = c + 1; i < kFT; ++i) {
+        double acc = 0.0;
+        for (int k = c; k < i; ++k) acc = fma(As[i * kFLD + k], k == c ? dc : As[c * kFLD + k], acc);
+        As[c * kFLD + i] = -acc / As[i * kFLD + i];
+      }
+    }
+    __syncthreads();
     for (int x = tid; x < kFT * kFT; x += kThreads) {
       const int i = x / kFT, j = x % kFT;
-      F[(static_cast<long>(K) * kFT + i) * ld + K * kFT + j] = As[i * kFLD + j];
+      if (j <= i) F[(static_cast<long>(K) * kFT + i) * ld + K * kFT + j] = As[i * kFLD + j];  // L (upper unchanged)
       const bool real = K * kFT + i < sb && K * kFT + j < sb;
-      panel[sn_tile_dev(ns, K, K) * kFT * kFT + x] = real ? Bs[i * kFLD + j] : 0.0;
+      const double li = j < i ? As[j * kFLD + i] : j == i ? s_dinv[i] : 0.0;
+      panel[sn_tile_dev(ns, K, K) * kFT * kFT + x] = real ? li : 0.0;
     }
     if (tid == 0 && s_bad) *v.not_pd = 1;
     return;
