@@ -62,6 +62,62 @@ def super_cube_ranks(A, world):
     return ranks
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` with no WORLD_SIZE in the environment: start N rank processes of this same
+    command (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on 127.0.0.1) and relay rank 0's JSON line.
+    This parent makes no GPU call (it does not even import torch) and starts the ranks as child processes, so the
+    command runs the same whether or not a launcher wraps it."""
+    import signal
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port, DPGO_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      text=True, start_new_session=True))
+    import threading
+
+    def watchdog():  # a rank that fails leaves the others blocked in a collective: end the whole job
+        while procs[0].poll() is None:
+            if any(p.poll() not in (None, 0) for p in procs[1:]):
+                for p in procs:
+                    if p.poll() is None:
+                        os.killpg(p.pid, signal.SIGKILL)
+                return
+            time.sleep(1.0)
+    threading.Thread(target=watchdog, daemon=True).start()
+    line = None
+    for ln in procs[0].stdout:  # rank 0 prints exactly one JSON line; anything else goes to stderr
+        if ln.lstrip().startswith("{"):
+            line = ln.strip()
+        else:
+            sys.stderr.write(ln)
+    rcs = [p.wait() for p in procs[:1]]
+    # rank 0 is done: the others have passed the final barrier or failed; never leave one behind
+    for p in procs[1:]:
+        try:
+            rcs.append(p.wait(timeout=120))
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            rcs.append(p.wait())
+    bad = [(r, rc) for r, rc in enumerate(rcs) if rc != 0]
+    if bad or line is None:
+        for p in procs:
+            if p.poll() is None:
+                os.killpg(p.pid, signal.SIGKILL)
+        raise SystemExit(f"bench.py: spawned ranks failed {bad or 'without a JSON line'}")
+    print(line, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -105,14 +161,29 @@ def main():
                          "known read/write bytes for the FETCH_SIZE calibration)")
     ap.add_argument("--precon", default="block_jacobi", choices=["block_jacobi", "exact"],
                     help="block_jacobi: per-pose (Q_jj + 0.1 I)^-1 (throughput setting, CPU baseline too); exact: the "
-                         "reference's factor of Q + 0.1 I (host Cholesky per agent, GPU triangular solves)")
+                         "reference's factor of Q + 0.1 I (nested-dissection tree on the host once per pattern, "
+                         "supernodal numeric factorisation and panel sweeps on the device)")
     ap.add_argument("--robust", default="L2", choices=["L2", "GNC_TLS", "TLS", "Huber", "GM", "L1"],
                     help="robust cost (L2: throughput setting; GNC_TLS: the reference default, "
                          "reweighting every 30 iterations on the device)")
+    ap.add_argument("--spawn-selftest", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args.gpus)  # before torch is imported: this process never touches the GPU
 
     import torch
     import torch.distributed as dist
+    if args.spawn_selftest:  # the launch path alone, on the CPU (tests/test_distributed.py): gloo, no device
+        dist.init_process_group("gloo")
+        t = torch.tensor([float(dist.get_rank())])
+        dist.all_reduce(t)
+        if dist.get_rank() == 0:
+            print(json.dumps({"world": dist.get_world_size(), "rank_sum": float(t.item()),
+                              "spawned": os.environ.get("DPGO_BENCH_SPAWNED") == "1"}), flush=True)
+        dist.barrier()
+        dist.destroy_process_group()
+        return None
     from dpgo_amd import hip as H
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -347,7 +418,9 @@ def main():
     # ---- what the multi-GPU run actually was (the driver's SCALE runs verify themselves): the collective's world as
     # the communicator reports it, ranks sharing a device, and per colour this rank's halo bytes and exchange time
     comm = {"world_size": world, "gpus_arg": args.gpus, "backend": dist.get_backend() if world > 1 else None,
-            "torch_world": dist.get_world_size() if world > 1 else 1}
+            "torch_world": dist.get_world_size() if world > 1 else 1,
+            "launcher": ("bench.py spawn (one child process per rank)" if os.environ.get("DPGO_BENCH_SPAWNED")
+                         else "external (torchrun or equivalent)" if world > 1 else None)}
     if native:
         comm["rccl_comm_count"], comm["rccl_comm_rank"] = eng.comm_info()
         if comm["rccl_comm_count"] != world:

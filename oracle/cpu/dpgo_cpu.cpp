@@ -3,7 +3,8 @@
 // A plain single-threaded C++ restatement (no Eigen / CHOLMOD / ROPTLIB: absent) of
 //   PGOAgent::iterate(true) + iterate(false)     src/PGOAgent.cpp:642-718, 1033-1165
 //   constructQMatrix / constructGMatrix          src/PGOAgent.cpp:720-859
-//   QuadraticProblem f / EucGrad / HVP / precond src/QuadraticProblem.cpp:50-101 (block-Jacobi)
+//   QuadraticProblem f / EucGrad / HVP / precond src/QuadraticProblem.cpp:31-42, 50-101 (block-Jacobi, or the
+//                                                exact factor of Q + 0.1 I: RCM + envelope Cholesky)
 //   QuadraticOptimizer RTR (1 outer, tCG)        src/QuadraticOptimizer.cpp:34-122 + SURVEY A.4
 //   LiftedSEManifold project (one-sided Jacobi)  src/manifold/LiftedSEManifold.cpp:34-45
 // Only bench.py's cpu_baseline leg and tests/ use it (via oracle/cpu_port.py): it is the
@@ -20,6 +21,19 @@
 
 namespace {
 
+// The reference's preconditioner, P = Q + 0.1 I factorised once per Q (src/QuadraticProblem.cpp:31-42, CHOLMOD
+// there) and applied as P_X(V P^-1) (:75-87), restated independently of the GPU library's supernodal code: a
+// reverse Cuthill-McKee pose order and a dense-row envelope (profile) Cholesky, L's row i stored contiguously from
+// its first nonzero column to the diagonal.  Fill stays inside the envelope, so the factor is exact up to rounding.
+struct Envelope {
+  int N = 0;
+  bool ok = false;                 // false: P not positive definite -> the reference's unprojected fallback
+  std::vector<int> pose_new;       // old pose -> RCM position
+  std::vector<int> first;          // per row: first stored column
+  std::vector<size_t> start;       // per row: offset of L(i, first[i])
+  std::vector<double> val;
+};
+
 struct Agent {
   int d, r, b, n;
   std::vector<int> rowptr, col;      // BSR of Q (block (j,i) column-major)
@@ -27,8 +41,152 @@ struct Agent {
   std::vector<int> gpose;            // poses with a G block
   std::vector<double> gblk;          // r*b per entry (column-major)
   std::vector<int> gslot;            // pose -> slot or -1
+  bool exact = false;                // precondition with the envelope factor instead of block-Jacobi
+  Envelope env;
   size_t L() const { return static_cast<size_t>(n) * r * b; }
 };
+
+// Reverse Cuthill-McKee over the pose graph of the BSR pattern: per connected component a BFS from a
+// pseudo-peripheral pose (repeated BFS from the last level's minimum-degree pose), neighbours in increasing degree.
+std::vector<int> rcm_order(const Agent& A) {
+  const int n = A.n;
+  std::vector<int> deg(n), order, level(n, -1);
+  for (int j = 0; j < n; ++j) deg[j] = A.rowptr[j + 1] - A.rowptr[j];
+  std::vector<char> placed(n, 0);
+  order.reserve(n);
+  auto bfs = [&](int s, std::vector<int>& lv, std::vector<int>& seq) {
+    seq.clear();
+    lv[s] = 0;
+    seq.push_back(s);
+    for (size_t h = 0; h < seq.size(); ++h) {
+      const int u = seq[h];
+      for (int k = A.rowptr[u]; k < A.rowptr[u + 1]; ++k) {
+        const int v = A.col[k];
+        if (lv[v] < 0 && !placed[v]) {
+          lv[v] = lv[u] + 1;
+          seq.push_back(v);
+        }
+      }
+    }
+  };
+  std::vector<int> seq;
+  for (int s0 = 0; s0 < n; ++s0) {
+    if (placed[s0]) continue;
+    int s = s0, ecc = -1;
+    for (int pass = 0; pass < 8; ++pass) {  // pseudo-peripheral start
+      bfs(s, level, seq);
+      const int e = level[seq.back()];
+      int best = seq.back();
+      for (int v : seq)
+        if (level[v] == e && deg[v] < deg[best]) best = v;
+      for (int v : seq) level[v] = -1;
+      if (e <= ecc) break;
+      ecc = e;
+      s = best;
+    }
+    // Cuthill-McKee from s
+    const size_t base = order.size();
+    order.push_back(s);
+    placed[s] = 1;
+    for (size_t h = base; h < order.size(); ++h) {
+      const int u = order[h];
+      std::vector<int> nb;
+      for (int k = A.rowptr[u]; k < A.rowptr[u + 1]; ++k)
+        if (!placed[A.col[k]]) {
+          nb.push_back(A.col[k]);
+          placed[A.col[k]] = 1;
+        }
+      std::stable_sort(nb.begin(), nb.end(), [&](int x, int y) { return deg[x] < deg[y]; });
+      order.insert(order.end(), nb.begin(), nb.end());
+    }
+  }
+  std::reverse(order.begin(), order.end());
+  std::vector<int> pos(n);
+  for (int q = 0; q < n; ++q) pos[order[q]] = q;
+  return pos;
+}
+
+// P = Q + 0.1 I = L L^T in the envelope of the RCM-ordered pattern (row-oriented, dot products over contiguous rows)
+void envelope_factor(Agent& A) {
+  Envelope& E = A.env;
+  const int b = A.b, bb = b * b, n = A.n;
+  E.N = n * b;
+  E.pose_new = rcm_order(A);
+  E.first.assign(E.N, 0);
+  E.start.assign(E.N + 1, 0);
+  for (int j = 0; j < n; ++j) {
+    int lo = E.pose_new[j];
+    for (int k = A.rowptr[j]; k < A.rowptr[j + 1]; ++k) lo = std::min(lo, E.pose_new[A.col[k]]);
+    for (int c = 0; c < b; ++c) E.first[E.pose_new[j] * b + c] = lo * b;
+  }
+  for (int i = 0; i < E.N; ++i) E.start[i + 1] = E.start[i] + static_cast<size_t>(i - E.first[i] + 1);
+  E.val.assign(E.start[E.N], 0.0);
+  for (int j = 0; j < n; ++j)  // scatter the lower triangle: entry (j b + c, i b + u) = blk[k][u b + c]
+    for (int k = A.rowptr[j]; k < A.rowptr[j + 1]; ++k) {
+      const int i = A.col[k];
+      for (int c = 0; c < b; ++c)
+        for (int u = 0; u < b; ++u) {
+          const int rn = E.pose_new[j] * b + c, cn = E.pose_new[i] * b + u;
+          if (cn <= rn) E.val[E.start[rn] + (cn - E.first[rn])] = A.blk[static_cast<size_t>(k) * bb + u * b + c];
+        }
+    }
+  for (int i = 0; i < E.N; ++i) E.val[E.start[i] + (i - E.first[i])] += 0.1;
+  E.ok = true;
+  for (int i = 0; i < E.N && E.ok; ++i) {
+    double* Li = &E.val[E.start[i]];
+    const int fi = E.first[i];
+    for (int j = fi; j < i; ++j) {
+      const double* Lj = &E.val[E.start[j]];
+      const int fj = E.first[j], k0 = std::max(fi, fj);
+      double s = Li[j - fi];
+      const double* a = Li + (k0 - fi);
+      const double* c = Lj + (k0 - fj);
+      for (int k = 0; k < j - k0; ++k) s -= a[k] * c[k];
+      Li[j - fi] = s / Lj[j - fj];
+    }
+    double s = Li[i - fi];
+    for (int k = 0; k < i - fi; ++k) s -= Li[k] * Li[k];
+    if (!(s > 0.0)) {
+      E.ok = false;
+      break;
+    }
+    Li[i - fi] = std::sqrt(s);
+  }
+}
+
+// Z = V P^-1 for the r rows of V at once (pose-major layout), by L y = v, L^T x = y
+void envelope_solve(const Agent& A, const double* V, double* Z) {
+  const Envelope& E = A.env;
+  const int r = A.r, b = A.b, rb = r * b;
+  std::vector<double> y(static_cast<size_t>(E.N) * r);
+  for (int j = 0; j < A.n; ++j)
+    for (int c = 0; c < b; ++c)
+      for (int a = 0; a < r; ++a) y[static_cast<size_t>(E.pose_new[j] * b + c) * r + a] = V[static_cast<size_t>(j) * rb + c * r + a];
+  for (int i = 0; i < E.N; ++i) {
+    const double* Li = &E.val[E.start[i]];
+    double acc[8] = {0};
+    for (int k = E.first[i]; k < i; ++k) {
+      const double l = Li[k - E.first[i]];
+      for (int a = 0; a < r; ++a) acc[a] += l * y[static_cast<size_t>(k) * r + a];
+    }
+    const double inv = 1.0 / Li[i - E.first[i]];
+    for (int a = 0; a < r; ++a) y[static_cast<size_t>(i) * r + a] = (y[static_cast<size_t>(i) * r + a] - acc[a]) * inv;
+  }
+  for (int i = E.N - 1; i >= 0; --i) {
+    const double* Li = &E.val[E.start[i]];
+    const double inv = 1.0 / Li[i - E.first[i]];
+    double x[8];
+    for (int a = 0; a < r; ++a) x[a] = y[static_cast<size_t>(i) * r + a] * inv;
+    for (int a = 0; a < r; ++a) y[static_cast<size_t>(i) * r + a] = x[a];
+    for (int k = E.first[i]; k < i; ++k) {
+      const double l = Li[k - E.first[i]];
+      for (int a = 0; a < r; ++a) y[static_cast<size_t>(k) * r + a] -= l * x[a];
+    }
+  }
+  for (int j = 0; j < A.n; ++j)
+    for (int c = 0; c < b; ++c)
+      for (int a = 0; a < r; ++a) Z[static_cast<size_t>(j) * rb + c * r + a] = y[static_cast<size_t>(E.pose_new[j] * b + c) * r + a];
+}
 
 inline double dot(const std::vector<double>& a, const std::vector<double>& c) {
   double s = 0.0;
@@ -205,6 +363,15 @@ void hess(const Agent& A, const double* X, const double* S, const double* V, dou
 
 void precond(const Agent& A, const double* X, const double* V, double* Z) {
   const int r = A.r, d = A.d, b = A.b, rb = r * b;
+  if (A.exact) {
+    if (!A.env.ok) {  // src/QuadraticProblem.cpp:84-85: factorisation failed -> V itself, unprojected
+      std::memcpy(Z, V, sizeof(double) * A.L());
+      return;
+    }
+    envelope_solve(A, V, Z);
+    for (int j = 0; j < A.n; ++j) project_pose(r, d, X + static_cast<size_t>(j) * rb, Z + static_cast<size_t>(j) * rb);
+    return;
+  }
   for (int j = 0; j < A.n; ++j) {
     const double* M = &A.minv[static_cast<size_t>(j) * b * b];
     const double* Vj = V + static_cast<size_t>(j) * rb;
@@ -491,6 +658,9 @@ struct CpuAgent {
   double status_rel = 0.0;
   double conv_ratio = 1.0;  // computeConvergedLoopClosureRatio (GNC_TLS)
   int ready = 0;
+  bool factored = false;    // exact preconditioner: P = Q + 0.1 I factorised for the current Q
+  double factor_sec = 0.0;  // wall seconds of this agent's factorisations
+  int factor_count = 0;
 };
 
 struct CpuEngine {
@@ -508,6 +678,7 @@ struct CpuEngine {
   std::vector<double> R, t, kappa, tau;
   // robust cost (0: L2, 1: GNC_TLS; RobustCostParameters / PGOAgentParameters defaults)
   int robust = 0, inner_iters = 30, gnc_max_iters = 100, gnc_iter = 0;
+  int precon_exact = 0;  // the reference's preconditioner (envelope factor of Q + 0.1 I) instead of block-Jacobi
   double mu = 1e-4, mu_step = 1.4, barc = 10.0, min_ratio = 0.8;
   size_t rb() const { return static_cast<size_t>(r) * b; }
 };
@@ -707,6 +878,18 @@ void reweight_agent(CpuEngine& E, int a) {
   c.conv_ratio = lc ? static_cast<double>(conv) / static_cast<double>(lc) : std::nan("");
   build_agent(E.d, E.r, E.m, E.p1.data(), E.p2.data(), E.R.data(), E.t.data(), E.kappa.data(), E.tau.data(),
               E.agent_of.data(), E.local, a, c.edges, c, c.w.data());
+  c.A.exact = E.precon_exact != 0;  // setQ refactorises P = Q + 0.1 I (src/QuadraticProblem.cpp:31-42): at the
+  c.factored = false;                // agent's next optimize (ensure_factor), the only place the factor is read
+}
+
+// The factor of the agent's current Q, computed when an optimize call first needs it (timed per agent)
+void ensure_factor(CpuAgent& c) {
+  if (!c.A.exact || c.factored) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  envelope_factor(c.A);
+  c.factor_sec += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  c.factor_count += 1;
+  c.factored = true;
 }
 
 // PGOAgent::iterate for agent a (selected or not) on the global state; gamma / alpha already updated
@@ -722,6 +905,7 @@ void iterate_agent(CpuEngine& E, int a, bool selected, bool restart, Work& w, bo
       }
   }
   if (selected && w.x1.size() != c.A.L()) w.init(c.A.L(), static_cast<size_t>(c.A.n) * E.d * E.d);
+  if (selected) ensure_factor(c);
   std::vector<double> X, Y, V, XP;
   gather(c, E.X, X, rb);
   XP = X;  // XPrev = X (:673)
@@ -768,10 +952,13 @@ extern "C" {
 
 // robust: 0 = L2, 1 = GNC_TLS (reweighting every robust_inner_iters iterations, mu from 1e-4 by 1.4 per
 // reweighting for at most 100, barc 10, converged-ratio threshold 0.8: the PGOAgentParameters defaults)
+// precon_exact: 1 = the reference's preconditioner (factor of Q + 0.1 I, refactorised whenever Q changes), 0 =
+// block-Jacobi
 void* dpgo_cpu_rbcd_create(int d, int r, int m, const int* p1, const int* p2, const double* R, const double* t,
                            const double* kappa, const double* tau, long n, const int* agent_of_pose, int num_agents,
-                           int accel, int restart_interval, int robust, int robust_inner_iters) {
+                           int accel, int restart_interval, int robust, int robust_inner_iters, int precon_exact) {
   auto* E = new CpuEngine();
+  E->precon_exact = precon_exact;
   E->robust = robust;
   E->inner_iters = robust_inner_iters > 0 ? robust_inner_iters : 30;
   E->m = m;
@@ -824,6 +1011,7 @@ void* dpgo_cpu_rbcd_create(int d, int r, int m, const int* p1, const int* p2, co
     E->ag[a].edges = edges[a];
     E->ag[a].w.assign(edges[a].size(), 1.0);
     build_agent(d, r, m, p1, p2, R, t, kappa, tau, agent_of_pose, local, a, edges[a], E->ag[a]);
+    E->ag[a].A.exact = precon_exact != 0;
   }
   const size_t L = static_cast<size_t>(n) * E->rb();
   E->X.assign(L, 0.0);
@@ -918,6 +1106,41 @@ void dpgo_cpu_rbcd_status(void* h, double* rel, int* ready) {
 }
 
 int dpgo_cpu_rbcd_color(void* h, int agent) { return static_cast<CpuEngine*>(h)->color[agent]; }
+
+// Bounded timing sample (bench.py's cpu_baseline of the exact-preconditioner legs): the listed agents, OpenMP over
+// them with `threads` threads, each first factorised (if its Q has no factor yet) and then updated `reps` times as
+// selected agents (iterate(true) at the current Nesterov coefficients, neighbours' poses fixed).  factor_sec /
+// update_sec [count]: per agent wall seconds of the factorisation and of one update (mean of reps).  Returns the wall
+// seconds of the update phase (after every listed agent's factor is in place).
+double dpgo_cpu_rbcd_time_sample(void* h, const int* agents, int count, int threads, int reps, double* factor_sec,
+                                 double* update_sec) {
+  auto* E = static_cast<CpuEngine*>(h);
+  const int T = std::max(1, std::min(threads, static_cast<int>(E->work.size())));
+#pragma omp parallel for num_threads(T) schedule(dynamic)
+  for (int q = 0; q < count; ++q) {
+    CpuAgent& c = E->ag[agents[q]];
+    const double before = c.factor_sec;
+    ensure_factor(c);
+    factor_sec[q] = c.factor_sec - before;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+#pragma omp parallel for num_threads(T) schedule(dynamic)
+  for (int q = 0; q < count; ++q) {
+    const auto u0 = std::chrono::steady_clock::now();
+    for (int k = 0; k < reps; ++k) iterate_agent(*E, agents[q], true, false, E->work[omp_get_thread_num()]);
+    update_sec[q] = std::chrono::duration<double>(std::chrono::steady_clock::now() - u0).count() / std::max(reps, 1);
+  }
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// per agent: factorisations of the exact preconditioner and their total wall seconds
+void dpgo_cpu_rbcd_factor_info(void* h, int* count, double* sec) {
+  auto* E = static_cast<CpuEngine*>(h);
+  for (int a = 0; a < E->K; ++a) {
+    count[a] = E->ag[a].factor_count;
+    sec[a] = E->ag[a].factor_sec;
+  }
+}
 int dpgo_cpu_max_threads(void) { return omp_get_max_threads(); }
 
 }  // extern "C"

@@ -98,12 +98,12 @@ class CpuRbcd:
     restart), OpenMP over the agents of a colour class.  TEST / BASELINE INFRASTRUCTURE."""
 
     def __init__(self, d, r, arrays, n, agent_of_pose, num_agents, accel, restart_interval=30, robust="L2",
-                 robust_opt_inner_iters=30):
+                 robust_opt_inner_iters=30, precon="block_jacobi"):
         L = lib()
         dp, ip, vp = C.POINTER(C.c_double), C.POINTER(C.c_int), C.c_void_p
         if not hasattr(L, "_rbcd_bound"):
             L.dpgo_cpu_rbcd_create.argtypes = [C.c_int, C.c_int, C.c_int, ip, ip, dp, dp, dp, dp, C.c_long, ip, C.c_int,
-                                               C.c_int, C.c_int, C.c_int, C.c_int]
+                                               C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
             L.dpgo_cpu_rbcd_create.restype = vp
             L.dpgo_cpu_rbcd_destroy.argtypes = [vp]
             L.dpgo_cpu_rbcd_set_X.argtypes = [vp, dp]
@@ -114,6 +114,9 @@ class CpuRbcd:
             L.dpgo_cpu_rbcd_status.argtypes = [vp, dp, ip]
             L.dpgo_cpu_rbcd_color.argtypes = [vp, C.c_int]
             L.dpgo_cpu_max_threads.restype = C.c_int
+            L.dpgo_cpu_rbcd_time_sample.argtypes = [vp, ip, C.c_int, C.c_int, C.c_int, dp, dp]
+            L.dpgo_cpu_rbcd_time_sample.restype = C.c_double
+            L.dpgo_cpu_rbcd_factor_info.argtypes = [vp, ip, dp]
             L._rbcd_bound = True
         self._keep = [np.ascontiguousarray(arrays["p1"], np.int32), np.ascontiguousarray(arrays["p2"], np.int32),
                       np.ascontiguousarray(arrays["R"], np.float64).ravel(),
@@ -126,7 +129,7 @@ class CpuRbcd:
                                         R.ctypes.data_as(dp), t.ctypes.data_as(dp), k.ctypes.data_as(dp),
                                         ta.ctypes.data_as(dp), int(n), aop.ctypes.data_as(ip), int(num_agents),
                                         int(accel), int(restart_interval), {"L2": 0, "GNC_TLS": 1}[robust],
-                                        int(robust_opt_inner_iters))
+                                        int(robust_opt_inner_iters), {"block_jacobi": 0, "exact": 1}[precon])
         self.colors = [L.dpgo_cpu_rbcd_color(self.h, a) for a in range(self.K)]
 
     def close(self):
@@ -152,6 +155,23 @@ class CpuRbcd:
         w = lib().dpgo_cpu_rbcd_iterate(self.h, int(threads), sec.ctypes.data_as(C.POINTER(C.c_double)),
                                         int(timed_serial))
         return w, sec
+
+    def time_sample(self, agents, threads, reps):
+        """Factorise (if needed) then update each listed agent `reps` times, OpenMP over them: (update-phase wall
+        seconds, per-agent factor seconds, per-agent seconds per update)."""
+        a = np.ascontiguousarray(agents, np.int32)
+        fs, us = np.zeros(len(a)), np.zeros(len(a))
+        w = lib().dpgo_cpu_rbcd_time_sample(self.h, a.ctypes.data_as(C.POINTER(C.c_int)), len(a), int(threads),
+                                            int(reps), fs.ctypes.data_as(C.POINTER(C.c_double)),
+                                            us.ctypes.data_as(C.POINTER(C.c_double)))
+        return w, fs, us
+
+    def factor_info(self):
+        cnt = np.zeros(self.K, np.int32)
+        sec = np.zeros(self.K)
+        lib().dpgo_cpu_rbcd_factor_info(self.h, cnt.ctypes.data_as(C.POINTER(C.c_int)),
+                                        sec.ctypes.data_as(C.POINTER(C.c_double)))
+        return cnt, sec
 
     def stats(self):
         out = np.zeros(self.K * 10, np.int32)

@@ -76,6 +76,24 @@ def test_exchange_plan_all_to_all(world):
     assert all(n > 0 for _, _, n in res)
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_spawns_ranks_without_launcher(world):
+    """`python bench.py --gpus N` with no WORLD_SIZE starts N rank processes itself (the parent makes no GPU call)
+    and relays rank 0's single JSON line: the launch path the driver's SCALE run uses when it does not wrap the
+    command in torchrun."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--spawn-selftest"],
+                         env=env, capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d == {"world": world, "rank_sum": float(world * (world - 1) // 2), "spawned": True}
+
+
 def test_super_cube_assignment():
     import sys
     sys.path.insert(0, ROOT)

@@ -42,15 +42,17 @@ def _setup(hip, k):
     return _CACHE[k]
 
 
-def _engine(hip, g, aop, accel, robust="L2", ranks=None, rank=0, world=1):
+def _engine(hip, g, aop, accel, robust="L2", ranks=None, rank=0, world=1, exact=False):
     ranks = np.zeros(64, np.int32) if ranks is None else ranks
-    return hip.Rbcd(g, aop, ranks, rank, world, hip.rbcd_params(r=R, acceleration=int(accel),
-                                                                robust_cost=hip.ROBUST[robust]))
+    return hip.Rbcd(g, aop, ranks, rank, world, hip.rbcd_params(
+        r=R, acceleration=int(accel), robust_cost=hip.ROBUST[robust],
+        precon=hip.PRECON_EXACT if exact else hip.PRECON_BLOCK_JACOBI))
 
 
-def _cpu(g, aop, accel):
+def _cpu(g, aop, accel, robust="L2", exact=False):
     from oracle import cpu_port
-    return cpu_port.CpuRbcd(3, R, g.arrays(), g.n, aop, 64, accel)
+    return cpu_port.CpuRbcd(3, R, g.arrays(), g.n, aop, 64, accel, robust=robust,
+                            precon="exact" if exact else "block_jacobi")
 
 
 @pytest.mark.parametrize("k", [48, 100])
@@ -121,6 +123,41 @@ def test_c4_nesterov_restart_cpu_parity(hip):
     # the restart re-ran updateX from XPrev for the selected colour: one extra optimize call each
     calls = e.stats()[:, 0]
     assert calls.sum() == 32 * iters + 32
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("accel", [False, True])
+def test_c4_exact_precon_cpu_parity(hip, accel):
+    """C4 (110,592 poses, 64 agents of 12^3) with the reference's default preconditioner: the engine's supernodal
+    factor of Q + 0.1 I (nested-dissection tree on the host, numeric factorisation and panel sweeps on the device)
+    against oracle/cpu's independent exact mode (reverse Cuthill-McKee envelope Cholesky on the host,
+    tests/test_host_native.py pins it to the numpy oracle's sparse LU): 36 colour iterations from the multi-robot
+    initialisation (with Nesterov: through the restart at iteration 29), X to 1e-9, Runs and tCG iterations per
+    agent equal."""
+    g, aop, X0 = _setup(hip, 48)
+    e = _engine(hip, g, aop, accel, exact=True)
+    e.set_X(X0)
+    iters = 36
+    for it in range(iters):
+        e.pre_exchange(it % e.num_colors)
+        e.update(it % e.num_colors, None)
+    Xg = np.zeros(X0.size)
+    e.get_X_into(Xg)
+    cpu = _cpu(g, aop, accel, exact=True)
+    cpu.set_X(X0)
+    for _ in range(iters):
+        cpu.iterate(threads=16)
+    err = rel(Xg, cpu.get_X())
+    print(f"C4 exact accel={accel}: |X_gpu - X_cpu| / |X| = {err:.2e}")
+    assert err <= 1e-9
+    st_g, st_c = e.stats()[:, :10], cpu.stats()
+    assert np.array_equal(st_g[:, 2:4], st_c[:, 2:4])
+    assert st_c[:, 3].sum() > st_c[:, 2].sum()  # CG steps beyond the first were taken
+    bj = _cpu(g, aop, accel)  # and the preconditioner matters on this trajectory
+    bj.set_X(X0)
+    for _ in range(iters):
+        bj.iterate(threads=16)
+    assert rel(bj.get_X(), cpu.get_X()) > 1e-6
 
 
 def test_c4_gnc_default_cadence(hip):

@@ -101,12 +101,23 @@ def _rtr_trace_case(hip, name, r, iters, tol, radius, inner, precon, merged, edg
     exp = _expected_records(trace)
     assert len(exp) > 3
     assert len(got) == len(exp)
-    # Tolerance: 1e-10 relative with block-Jacobi; 1e-7 with the exact factor, whose single
-    # applications already agree with the oracle's sparse LU only to ~1e-10 (cond(Q + 0.1 I) eps).
+    # Tolerance: 1e-10 relative with block-Jacobi.  With the exact factor the bar is derived the same way as the
+    # merged sequence's below: max(1e-10, 2 x the float64 oracle's own distance from the extended-precision Run of
+    # the same settings (its exact branch: (Q + 0.1 I)^-1 by sparse LU refined in extended precision)).  That is
+    # 1e-10 on smallGrid3D, ~2.5e-10 on sphere2500 and ~1.3e-7 on tinyGrid3D, whose exact-preconditioned trajectory
+    # amplifies rounding ~1e5-fold from the second Run on (a 1e-16 perturbation of X0 moves the extended-precision
+    # Run itself by 7e-11; every float64 implementation sits 6e-8 from it).
     # Quantities that shrink inside one tCG (d_Hd, alpha, |r|, <z, r>, beta, tau) are measured against
     # their largest magnitude in that tCG: their terms cancel, so their rounding floor is set by it.
     # rho = (f1 - f2) / model decrease: f1 - f2 loses the digits |f1| / |f1 - f2|.
-    tol = 1e-7 if precon == "exact" else 1e-10
+    tol = 1e-10
+    if precon == "exact":
+        ext = _rtr_extended(Q, X0, d, rtr_tol, radius, 5.0 * radius, iters, inner, precon="exact")
+        assert [e["op"] for e in ext] == [e["op"] for e in exp]
+        tol = max(1e-10, 2.0 * _trace_deviation(exp, ext))
+        print(f"{name} r={r} exact: oracle vs extended-precision Run {_trace_deviation(exp, ext):.2e}, "
+              f"device vs extended {_trace_deviation(got, ext):.2e}, device vs oracle {_trace_deviation(got, exp):.2e}; "
+              f"bar {tol:.2e}")
     if precon == "none":
         # unpreconditioned tCG: 50 inner iterations on smallGrid3D amplify the summation-order rounding
         # (the classic sequence, the oracle's own operations, differs by 1.6e-9 of |r| at iteration 8 and
@@ -172,31 +183,55 @@ def _rtr_trace_case(hip, name, r, iters, tol, radius, inner, precon, merged, edg
     assert rel(Xh, Xo) <= max(1e-8, tol)
 
 
-def _rtr_extended(Q, X0, d, tol, Delta0, Delta_max, max_iter, max_inner):
-    """ROPTLIB RTR Run (A.4: tCG from eta = 0 with block-Jacobi, QF retraction, rho test, radius update;
-    G = 0) in extended precision (np.longdouble, 64-bit mantissa): the record sequence of
-    _expected_records, as the reference trajectory the float64 implementations are measured against."""
+def _rtr_extended(Q, X0, d, tol, Delta0, Delta_max, max_iter, max_inner, precon="bj"):
+    """ROPTLIB RTR Run (A.4: tCG from eta = 0, QF retraction, rho test, radius update; G = 0) in extended precision
+    (np.longdouble, 64-bit mantissa): the record sequence of _expected_records, as the reference trajectory the
+    float64 implementations are measured against.  Q is applied as a sparse product in extended precision.
+    precon "bj": per-pose (Q_jj + 0.1 I)^-1 by Gauss-Jordan in extended precision; "exact": (Q + 0.1 I)^-1
+    (src/QuadraticProblem.cpp:31-42, 75-87) by a float64 sparse LU refined in extended precision until the residual
+    is at the extended rounding level (each refinement step gains ~ -log10(cond * eps64) digits)."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
     L = np.longdouble
     r = X0.shape[0]
     b = d + 1
     n = X0.shape[1] // b
-    Qd = Q.toarray().astype(L)
+    Qc = sp.csr_matrix(Q)
+    Qc.sort_indices()
+    q_val, q_idx, q_ptr = Qc.data.astype(L), Qc.indices, Qc.indptr
+    assert np.all(np.diff(q_ptr) > 0)  # reduceat needs no empty row (a Laplacian has its diagonal)
+
+    def qmul(V):  # (Q V^T)^T, r x N, every product and sum in extended precision
+        return np.add.reduceat(V[:, q_idx] * q_val[None, :], q_ptr[:-1], axis=1)
     P = lambda V: V.reshape(r, n, b).transpose(1, 0, 2)  # noqa: E731  pose blocks (n, r, b)
     U = lambda Pb: Pb.transpose(1, 0, 2).reshape(r, n * b)  # noqa: E731
     ip = lambda A_, B_: np.sum(A_ * B_, dtype=L)  # noqa: E731
     sym = lambda M: 0.5 * (M + np.swapaxes(M, 1, 2))  # noqa: E731
-    Minv = np.zeros((n, b, b), L)  # (Q_jj + 0.1 I)^-1 by Gauss-Jordan in extended precision
-    for j in range(n):
-        A = np.concatenate([Qd[j * b:(j + 1) * b, j * b:(j + 1) * b] + L(0.1) * np.eye(b, dtype=L),
-                            np.eye(b, dtype=L)], axis=1)
-        for c in range(b):
-            piv = c + int(np.argmax(np.abs(A[c:, c])))
-            A[[c, piv]] = A[[piv, c]]
-            A[c] /= A[c, c]
-            for u in range(b):
-                if u != c:
-                    A[u] -= A[u, c] * A[c]
-        Minv[j] = A[:, b:]
+    if precon == "exact":
+        lu = spla.splu((Qc + 0.1 * sp.identity(Qc.shape[0], format="csr")).tocsc())
+
+        def psolve(V):  # V (Q + 0.1 I)^-1 with iterative refinement in extended precision
+            Z = lu.solve(np.ascontiguousarray(V.astype(np.float64).T)).T.astype(L)
+            for _ in range(6):
+                Res = V - (qmul(Z) + L(0.1) * Z)
+                if np.max(np.abs(Res)) <= L(1e-19) * max(np.max(np.abs(V)), L(1e-300)):
+                    break
+                Z = Z + lu.solve(np.ascontiguousarray(Res.astype(np.float64).T)).T.astype(L)
+            return Z
+    else:
+        Minv = np.zeros((n, b, b), L)  # (Q_jj + 0.1 I)^-1 by Gauss-Jordan in extended precision
+        for j in range(n):
+            A = np.concatenate([Qc[j * b:(j + 1) * b, j * b:(j + 1) * b].toarray().astype(L) +
+                                L(0.1) * np.eye(b, dtype=L), np.eye(b, dtype=L)], axis=1)
+            for c in range(b):
+                piv = c + int(np.argmax(np.abs(A[c:, c])))
+                A[[c, piv]] = A[[piv, c]]
+                A[c] /= A[c, c]
+                for u in range(b):
+                    if u != c:
+                        A[u] -= A[u, c] * A[c]
+            Minv[j] = A[:, b:]
+        psolve = lambda V: U(P(V) @ Minv)  # noqa: E731
 
     def proj(X, V):
         Y = P(X)[:, :, :d]
@@ -217,7 +252,7 @@ def _rtr_extended(Q, X0, d, tol, Delta0, Delta_max, max_iter, max_inner):
             Pp[j, :, :d] = M
         return U(Pp)
 
-    egrad = lambda X: (Qd @ X.T).T  # noqa: E731
+    egrad = qmul
     fval = lambda X: L(0.5) * ip(egrad(X), X)  # noqa: E731
     x1 = X0.astype(L)
     EG = egrad(x1)
@@ -233,7 +268,7 @@ def _rtr_extended(Q, X0, d, tol, Delta0, Delta_max, max_iter, max_inner):
             H_[:, :, :d] -= P(V)[:, :, :d] @ S
             return proj(x1, U(H_))
 
-        prec = lambda V: proj(x1, U(P(V) @ Minv))  # noqa: E731
+        prec = lambda V: proj(x1, psolve(V))  # noqa: E731
         eta = np.zeros_like(x1)
         Heta = np.zeros_like(x1)
         rv = g.copy()
@@ -358,6 +393,41 @@ def test_rtr_trace_extended_precision(hip, name, r):
     for m in ("merged", "merged_edges"):
         assert dev[m] <= 1e-10 or dev[m] <= 1.5 * max(dev["oracle"], dev["classic"]), dev
     assert dev["classic"] <= 1e-10 or dev["classic"] <= 1.5 * dev["oracle"], dev
+
+
+@pytest.mark.parametrize("name,r", [("tinyGrid3D", 3), ("smallGrid3D", 5), ("sphere2500", 3)])
+def test_rtr_trace_extended_precision_exact(hip, name, r):
+    """The reference's default preconditioner (exact factor of Q + 0.1 I, the classic tCG sequence) over BSR and
+    edge-stream Q, localPoseGraphOptimization settings, against the extended-precision Run with the same
+    preconditioner: the device trace within 1e-10 of it or within 2x the float64 oracle's own distance from it
+    (the bar test_rtr_trace_matches_oracle derives for the exact cases)."""
+    meas = load_meas(name)
+    d, n = meas.d, meas.num_poses
+    Q = O.connection_laplacian(meas, n)
+    P_ = O.QuadraticProblem(n, d, r)
+    P_.set_Q(Q)
+    P_.precon_mode = O.PRECON_EXACT
+    X0 = O.lifting_matrix(d, r) @ O.chordal_initialization(d, n, meas)
+    trace = []
+    O.optimize(P_, X0, O.OptParams(tr_iterations=10, tr_tolerance=1e-1, tr_initial_radius=10.0, tr_max_inner=50),
+               trace)
+    ora = _expected_records(trace)
+    ext = _rtr_extended(Q, X0, d, 1e-1, 10.0, 50.0, 10, 50, precon="exact")
+    assert [e["op"] for e in ext] == [e["op"] for e in ora]
+    dev = {"oracle": _trace_deviation(ora, ext)}
+    for label, edges in (("bsr", False), ("edges", True)):
+        H = hip.Problem(n, d, r)
+        _set_Q(H, meas, Q, edges)
+        H.set_trace(4096)
+        H.optimize(X0, hip.default_params(tr_iterations=10, tr_tolerance=1e-1, tr_initial_radius=10.0,
+                                          tr_max_inner=50, precon=hip.PRECON_EXACT))
+        got = H.get_trace(0)
+        assert [int(g["op"]) for g in got] == [e["op"] for e in ext]
+        dev[label] = _trace_deviation(got, ext)
+    print(f"{name} exact: max deviation from the extended-precision Run: " +
+          ", ".join(f"{k} {v:.2e}" for k, v in dev.items()))
+    for m in ("bsr", "edges"):
+        assert dev[m] <= max(1e-10, 2.0 * dev["oracle"]), dev
 
 
 @pytest.mark.parametrize("batched", [False, True])

@@ -251,6 +251,55 @@ def test_cpu_engine_gnc_tls_matches_oracle(accel):
     assert min(ag.converged_loop_closure_ratio() for ag in agents) < 1.0  # the reweighting decided some
 
 
+@pytest.mark.parametrize("accel,robust", [(False, "L2"), (True, "L2"), (True, "GNC_TLS")])
+def test_cpu_engine_exact_precon_matches_oracle(accel, robust):
+    """oracle/cpu's exact preconditioner (P = Q + 0.1 I factorised per Q, src/QuadraticProblem.cpp:31-42, 75-87;
+    a reverse Cuthill-McKee envelope Cholesky that shares no code with the GPU library's supernodal factor) vs the
+    numpy restatement's sparse LU inside the same colour schedule: X to 1e-10 over 12 iterations (L2; the trajectory
+    from the odometry chain amplifies rounding ~10x per 4 iterations, so 31 iterations sit at 1e-9..1e-8 for either
+    side's arithmetic), GNC_TLS with a refactorisation after every reweighting (every 3 iterations) to 1e-9."""
+    from oracle import cpu_port
+    k, A, r = 6, 2, 5
+    g = O.grid3d(k, seed=3)
+    s = k // A
+    aop = np.array([(c[0] // s) + A * ((c[1] // s) + A * (c[2] // s)) for c in g.extra["coords"]], np.int32)
+    if robust != "L2":
+        rng = np.random.default_rng(7)
+        lc = np.nonzero(np.abs(g.p2 - g.p1) != 1)[0]
+        bad = rng.choice(lc, size=max(1, len(lc) // 10), replace=False)
+        g.t = g.t.copy()
+        g.t[bad] += rng.normal(0.0, 5.0, size=(len(bad), 3))
+    X0 = O.lifting_matrix(3, r) @ O.chain_initialization(3, g.num_poses, g)
+    arrays = dict(p1=g.p1, p2=g.p2, R=g.R, t=g.t, kappa=g.kappa, tau=g.tau)
+    E = cpu_port.CpuRbcd(3, r, arrays, g.num_poses, aop, A ** 3, accel, robust=robust, robust_opt_inner_iters=3,
+                         precon="exact")
+    E.set_X(O.to_dev(X0))
+    iters = 12 if robust == "L2" else 8
+    for _ in range(iters):
+        E.iterate(threads=4)
+    agents, trace = [], []
+    Xo, _ = O.colour_rbcd(g, aop, A ** 3, X0, iters, r, acceleration=accel, robust=robust, robust_opt_inner_iters=3,
+                          agents_out=agents, trace=trace, precon=O.PRECON_EXACT)
+    assert rel(O.from_dev(E.get_X(), r), Xo) <= (1e-10 if robust == "L2" else 1e-9)
+    runs = np.zeros(A ** 3, int)
+    pending = []
+    for t in trace:
+        if isinstance(t, tuple):
+            runs[t[1]] += len(pending)
+            pending = []
+        else:
+            pending.append(t)
+    assert list(E.stats()[:, 2]) == list(runs)
+    cnt, _ = E.factor_info()
+    assert cnt.min() >= 1 and (robust == "L2") == (cnt.max() == 1)  # refactorised after the reweightings
+    # the block-Jacobi schedule is a different trajectory: the exact factor is what ran
+    Eb = cpu_port.CpuRbcd(3, r, arrays, g.num_poses, aop, A ** 3, accel, robust=robust, robust_opt_inner_iters=3)
+    Eb.set_X(O.to_dev(X0))
+    for _ in range(iters):
+        Eb.iterate(threads=4)
+    assert rel(Eb.get_X(), E.get_X()) > 1e-3
+
+
 def build_abi_check(tmp_path):
     """tests/c/abi_check.c compiled against include/*.h and linked to the in-tree libdpgo_hip.so."""
     exe = str(tmp_path / "abi_check")
