@@ -258,6 +258,11 @@ struct SnFactorView {
 // Loop closures one engine colour class reweights (PGOAgent::updateLoopClosuresWeights,
 // src/PGOAgent.cpp:1181-1244): pose sources >= 0 index the engine's X buffer, < 0 -> (-1 - s) the
 // received-pose buffer; weights go to the colour problem's edge and, for shared edges, its G entry.
+// A shared loop closure reads the neighbour's pose from the agent's neighborPoseDict as the agent last received it
+// (:1201-1235): `dict` holds that pose per entry (r b doubles), `dict_ok` whether the agent has received it yet (the
+// reference skips an edge whose neighbour pose it does not have, weight unchanged); k_gnc_snapshot fills them when
+// the agent is selected (the example delivers neighbour poses to the selected robot only,
+// examples/MultiRobotExample.cpp:188-213).
 struct GncEntries {
   int n;
   const int* prob_edge;
@@ -268,6 +273,10 @@ struct GncEntries {
   const double* t;
   const double* kappa;
   const double* tau;
+  const int* agent;    // agent of the entry (index inside the colour problem)
+  const int* nbr_end;  // shared entries: 1 if p2 is the neighbour's pose, 0 if p1; -1 private
+  double* dict;        // per entry: the neighbour pose of the agent's dictionary
+  int* dict_ok;
 };
 // RobustCost::weight (src/DPGO_robust.cpp:23-67) parameters; type = DPGO_ROBUST_*
 struct RobustParams {
@@ -385,6 +394,8 @@ hipError_t launch_bj_inverse(int b, int n, const QView& q, double shift, double*
 hipError_t launch_edge_reweight(int d, int m, int n, const double* raw, const int* slot_of_edge, const double* w,
                                 const int* dinc_ptr, const int* dinc, double* wslot, double* rec, double* diag,
                                 hipStream_t stream);
+hipError_t launch_gnc_snapshot(int r, int b, const GncEntries& g, const double* X, const double* RX, const int* mask,
+                               hipStream_t stream);
 hipError_t launch_gnc_weights(int r, int b, const GncEntries& g, const double* X, const double* RX,
                               const RobustParams& rp, double* w_prob, double* w_g, hipStream_t stream);
 // Lanczos helpers over flat vectors of length len: partial[g * k + j] = sum over grid block g's

@@ -3002,9 +3002,11 @@ __global__ __launch_bounds__(kThreads) void k_gnc_weights(GncEntries g, const do
   constexpr int B = D + 1;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= g.n) return;
-  const int s1 = g.src1[e], s2 = g.src2[e];
-  const double* P1 = s1 >= 0 ? X + static_cast<long>(s1) * (R * B) : RX + static_cast<long>(-1 - s1) * (R * B);
-  const double* P2 = s2 >= 0 ? X + static_cast<long>(s2) * (R * B) : RX + static_cast<long>(-1 - s2) * (R * B);
+  const int s1 = g.src1[e], s2 = g.src2[e], ne = g.nbr_end[e];
+  if (ne >= 0 && g.dict_ok[e] == 0) return;  // no neighbour pose received yet: weight unchanged (:1208-1212)
+  const double* D_ = ne >= 0 ? g.dict + static_cast<long>(e) * (R * B) : nullptr;
+  const double* P1 = ne == 0 ? D_ : s1 >= 0 ? X + static_cast<long>(s1) * (R * B) : RX + static_cast<long>(-1 - s1) * (R * B);
+  const double* P2 = ne == 1 ? D_ : s2 >= 0 ? X + static_cast<long>(s2) * (R * B) : RX + static_cast<long>(-1 - s2) * (R * B);
   const double* Rm = g.R + static_cast<long>(e) * D * D;
   const double* tv = g.t + static_cast<long>(e) * D;
   double rot = 0.0, tra = 0.0;
@@ -3028,6 +3030,23 @@ __global__ __launch_bounds__(kThreads) void k_gnc_weights(GncEntries g, const do
   const double w = robust_weight(rp, sqrt(err));
   w_prob[g.prob_edge[e]] = w;
   if (g.g_entry[e] >= 0) w_g[g.g_entry[e]] = w;
+}
+
+// The selected agents receive their neighbours' poses (updateNeighborPoses): every shared entry of a selected agent
+// (mask[agent] != 0, or every agent without a mask) copies the neighbour's current pose into its dictionary slot.
+// One thread per (entry, double).
+template <int R, int B>
+__global__ __launch_bounds__(kThreads) void k_gnc_snapshot(GncEntries g, const double* __restrict__ X,
+                                                           const double* __restrict__ RX, const int* __restrict__ mask) {
+  const long x = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int e = static_cast<int>(x / (R * B)), q = static_cast<int>(x % (R * B));
+  if (e >= g.n) return;
+  const int ne = g.nbr_end[e];
+  if (ne < 0 || (mask != nullptr && mask[g.agent[e]] == 0)) return;
+  const int s = ne ? g.src2[e] : g.src1[e];
+  const double* P = s >= 0 ? X + static_cast<long>(s) * (R * B) : RX + static_cast<long>(-1 - s) * (R * B);
+  g.dict[static_cast<long>(e) * (R * B) + q] = P[q];
+  if (q == 0) g.dict_ok[e] = 1;
 }
 
 // One block per agent: converged (w == 1 or w == 0) over all loop closures of the agent.
@@ -4414,6 +4433,15 @@ hipError_t launch_edge_reweight(int d, int m, int n, const double* raw, const in
     else
       k_edge_diag<2><<<gn, kThreads, 0, stream>>>(n, raw, nullptr, wslot, dinc_ptr, dinc, diag);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_gnc_snapshot(int r, int b, const GncEntries& g, const double* X, const double* RX, const int* mask,
+                               hipStream_t stream) {
+  if (g.n == 0) return hipSuccess;
+  const long total = static_cast<long>(g.n) * r * b;
+  const int grid = static_cast<int>((total + kThreads - 1) / kThreads);
+  DPGO_DISPATCH(r, b, (k_gnc_snapshot<R, B><<<grid, kThreads, 0, stream>>>(g, X, RX, mask)));
   return hipGetLastError();
 }
 

@@ -32,6 +32,7 @@ struct dpgo_rbcd_s {
   // dpgo_rbcd_set_selected: per owned agent (colour-major, as `owned`) 1 = optimise when its colour is updated;
   // empty = every agent of the colour (the colour schedule)
   std::vector<int> sel_mask;
+  DevBuf<int> sel_mask_dev;  // sel_mask on the device (the neighbour-pose snapshot of the selected agents)
   std::vector<long> own_pose_off;         // [owned + 1] pose offsets into owned buffers
   long Nown = 0;
   std::vector<int> own_global;            // owned buffer pose index -> global pose id
@@ -42,8 +43,7 @@ struct dpgo_rbcd_s {
   hipStream_t side = nullptr;
   hipEvent_t ev_start = nullptr, ev_sel = nullptr;
   bool sel_pending = false;
-  // colour of the last pre_exchange (-1 after set_X): a robust cost over several ranks needs the cyclic schedule
-  int last_color = -1;
+  int last_color = -1;  // colour of the last pre_exchange (-1 after set_X)
   std::vector<dpgo_hip_problem> prob;     // per colour (nullptr if none owned)
   DevBuf<double> X, Y, V, Xprev;
   // exchange: the public poses' X only.  With Nesterov a receiver uses its neighbours' aux poses
@@ -90,8 +90,8 @@ struct dpgo_rbcd_s {
   std::vector<GTab*> gt;
   // robust cost: per colour, the loop closures its agents reweight and the colour problem's weights
   struct Gnc {
-    DevBuf<int> prob_edge, g_entry, src1, src2;
-    DevBuf<double> R, t, kappa, tau, w_prob;
+    DevBuf<int> prob_edge, g_entry, src1, src2, agent, nbr_end, dict_ok;
+    DevBuf<double> R, t, kappa, tau, w_prob, dict;  // dict: the agents' neighborPoseDict entries (GncEntries)
     int n = 0;
   };
   std::vector<Gnc*> gnc;
@@ -201,8 +201,8 @@ int reweight_color(dpgo_rbcd e, int c) {
   dpgo_hip_problem h = e->prob[c];
   if (!h) return DPGO_HIP_OK;
   auto* g = e->gnc[c];
-  const GncEntries ge{g->n, g->prob_edge.p, g->g_entry.p, g->src1.p, g->src2.p,
-                      g->R.p, g->t.p, g->kappa.p, g->tau.p};
+  const GncEntries ge{g->n, g->prob_edge.p, g->g_entry.p, g->src1.p, g->src2.p, g->R.p, g->t.p, g->kappa.p,
+                      g->tau.p, g->agent.p, g->nbr_end.p, g->dict.p, g->dict_ok.p};
   const RobustParams rp{e->P.robust_cost, e->mu, e->P.gnc_barc, e->P.huber_threshold, e->P.tls_threshold};
   HIP_TRY(launch_gnc_weights(e->r, e->b, ge, e->X.p, e->RX.p, rp, g->w_prob.p, e->gt[c]->w.p, e->stream));
   DPGO_TRY(dpgo_hip_set_edge_weights_dev(h, g->w_prob.p));
@@ -211,6 +211,20 @@ int reweight_color(dpgo_rbcd e, int c) {
     HIP_TRY(launch_conv_ratio(h->K, l->off.p, l->idx.p, g->w_prob.p, l->ratio.p, e->stream));
     l->valid = true;
   }
+  return DPGO_HIP_OK;
+}
+
+// updateNeighborPoses for the selected agents of colour c (examples/MultiRobotExample.cpp:188-213): each shared loop
+// closure they reweight records the neighbour pose they now hold (this iteration's halo / same-rank X), which their
+// updateLoopClosuresWeights reads at any later reweighting (src/PGOAgent.cpp:1201-1235), whichever colour order
+// and whichever rank count: no reweighting reads a received pose older than the agent's own last selection.
+int snapshot_neighbors(dpgo_rbcd e, int c) {
+  auto* g = e->gnc[c];
+  if (!e->prob[c] || g->n == 0) return DPGO_HIP_OK;
+  const GncEntries ge{g->n, g->prob_edge.p, g->g_entry.p, g->src1.p, g->src2.p, g->R.p, g->t.p, g->kappa.p,
+                      g->tau.p, g->agent.p, g->nbr_end.p, g->dict.p, g->dict_ok.p};
+  const int* mask = e->sel_mask.empty() ? nullptr : e->sel_mask_dev.p + e->color_off[c];
+  HIP_TRY(launch_gnc_snapshot(e->r, e->b, ge, e->X.p, e->RX.p, mask, e->stream));
   return DPGO_HIP_OK;
 }
 
@@ -537,7 +551,7 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
     // loop closures this colour reweights (PGOAgent::updateLoopClosuresWeights): private ones that
     // are not odometry (local p2 != p1 + 1, as the partition's split), and shared ones whose other
     // agent has the larger ID (only the lower-ID agent updates its copy)
-    std::vector<int> gn_pe, gn_ge, gn_s1, gn_s2;
+    std::vector<int> gn_pe, gn_ge, gn_s1, gn_s2, gn_agent, gn_nbr;
     std::vector<double> gn_R, gn_t, gn_k, gn_tau;
     long prob_edges = 0;
     if (a1 == a0) continue;
@@ -644,6 +658,8 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
         };
         gn_pe.push_back(static_cast<int>(prob_edges + static_cast<long>(x)));
         gn_ge.push_back(ge);
+        gn_agent.push_back(q - a0);
+        gn_nbr.push_back(ge < 0 ? -1 : own_i ? 1 : 0);  // a shared edge: the endpoint this agent does not own
         gn_s1.push_back(src_of(i));
         gn_s2.push_back(src_of(j));
         gn_R.insert(gn_R.end(), &g->R[k * d * d], &g->R[k * d * d] + d * d);
@@ -687,6 +703,11 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
     if (rc == DPGO_HIP_OK) rc = upload_vec(gc->t, gn_t, e->stream);
     if (rc == DPGO_HIP_OK) rc = upload_vec(gc->kappa, gn_k, e->stream);
     if (rc == DPGO_HIP_OK) rc = upload_vec(gc->tau, gn_tau, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(gc->agent, gn_agent, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(gc->nbr_end, gn_nbr, e->stream);
+    if (rc == DPGO_HIP_OK) rc = upload_vec(gc->dict_ok, std::vector<int>(std::max<size_t>(gn_pe.size(), 1), 0), e->stream);
+    if (rc == DPGO_HIP_OK && gc->dict.ensure(std::max<size_t>(gn_pe.size(), 1) * e->rb()) != hipSuccess)
+      rc = fail(DPGO_HIP_ENOMEM, "GNC neighbour dictionary");
     if (rc == DPGO_HIP_OK) rc = upload_vec(gc->w_prob, std::vector<double>(std::max<long>(prob_edges, 1), 1.0), e->stream);
     if (rc == DPGO_HIP_OK && hipStreamSynchronize(e->stream) != hipSuccess) rc = fail(DPGO_HIP_EDEVICE, "sync");
     if (rc != DPGO_HIP_OK) return bail(rc);
@@ -810,13 +831,10 @@ static bool restart_now(dpgo_rbcd e) {
 int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color) {
   if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
   DPGO_TRY(join_side(e));  // a second pre_exchange without an update in between
-  // With a robust cost the non-selected agents' reweighting reads their neighbours' poses: in place on this rank,
-  // from the last halo that carried them across ranks.  Under the cyclic colour schedule (the example driver's,
-  // the bench's) both are the poses of the neighbours' last update, so every rank count and halo kind give bitwise
-  // the same weights; out of order they would differ by the halo's vintage, so that case is refused.
-  if (e->P.robust_cost != DPGO_ROBUST_L2 && e->world > 1 && e->last_color >= 0 &&
-      color != (e->last_color + 1) % e->ncolors)
-    return fail(DPGO_HIP_EINVAL, "a robust cost over several ranks needs the cyclic colour schedule (colour t mod C)");
+  // With a robust cost the non-selected agents' reweighting reads their own X and, for shared loop closures, the
+  // neighbour poses of their dictionaries (snapshot_neighbors at their last selection): nothing here reads the
+  // halo, so every colour order (the cyclic schedule, the example's greedy robot) and every rank count give
+  // bitwise the same weights.
   e->last_color = color;
   e->iteration += 1;  // mIterationNumber++ (:643)
   // shouldUpdateLoopClosureWeights (:1174-1179): every agent reweights at the start of its iterate;
@@ -895,15 +913,11 @@ int dpgo_rbcd_pack(dpgo_rbcd e, double* send_dev) {
   return DPGO_HIP_OK;
 }
 
-// A per-colour halo refreshes only the RX slots the selected colour reads.  With two colours that is also
-// every slot a non-selected colour's reweighting reads at the next iteration (its neighbours are exactly the
-// poses its own last exchange brought) under the cyclic schedule, which dpgo_rbcd_pre_exchange requires of a
-// robust cost over several ranks; with more colours and a robust cost the engine keeps the full halo.
-static bool halo_color_ok(dpgo_rbcd e) { return e->ncolors <= 2 || e->P.robust_cost == DPGO_ROBUST_L2; }
+// A per-colour halo refreshes only the RX slots the selected colour reads: every read of the halo is the selected
+// colour's (its G, its agents' neighbour-pose snapshot; a reweighting reads the dictionaries, not the halo).
 
 int dpgo_rbcd_pack_color(dpgo_rbcd e, int color, double* send_dev) {
   if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
-  if (!halo_color_ok(e)) return dpgo_rbcd_pack(e, send_dev);
   const auto* H = e->halo[color];
   if (H->n_send == 0) return DPGO_HIP_OK;
   HIP_TRY(launch_gather_poses(static_cast<int>(H->n_send), static_cast<int>(e->rb()), H->pack_idx.p, e->X.p, e->X.p,
@@ -914,7 +928,6 @@ int dpgo_rbcd_pack_color(dpgo_rbcd e, int color, double* send_dev) {
 
 int dpgo_rbcd_exchange_counts_color(dpgo_rbcd e, int color, long long* send_counts, long long* recv_counts) {
   if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
-  if (!halo_color_ok(e)) return dpgo_rbcd_exchange_counts(e, send_counts, recv_counts);
   for (int p = 0; p < e->world; ++p) {
     if (send_counts) send_counts[p] = e->halo[color]->send_counts[p];
     if (recv_counts) recv_counts[p] = e->halo[color]->recv_counts[p];
@@ -932,6 +945,11 @@ int dpgo_rbcd_set_selected(dpgo_rbcd e, const int* agent_mask) {
   }
   e->sel_mask.assign(e->owned.size(), 0);
   for (size_t q = 0; q < e->owned.size(); ++q) e->sel_mask[q] = agent_mask[e->owned[q]] != 0 ? 1 : 0;
+  // the device copy feeds the next update's neighbour snapshot; earlier launches may still read the old one
+  DPGO_TRY(join_side(e));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  DPGO_TRY(upload_vec(e->sel_mask_dev, e->sel_mask, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
   return DPGO_HIP_OK;
 }
 
@@ -949,7 +967,6 @@ int dpgo_rbcd_update(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_re
 
 int dpgo_rbcd_update_color(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_result* results) {
   if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
-  if (!halo_color_ok(e)) return dpgo_rbcd_update(e, color, recv_dev, results);
   const auto* H = e->halo[color];
   if (H->n_recv > 0) {
     if (!recv_dev) return fail(DPGO_HIP_EINVAL, "receive buffer required");
@@ -963,6 +980,8 @@ int dpgo_rbcd_update_color(dpgo_rbcd e, int color, const double* recv_dev, dpgo_
 static int update_body(dpgo_rbcd e, int color, dpgo_opt_result* results) {
   DPGO_TRY(join_side(e));  // the selected colour's updateY from the side stream (dpgo_rbcd_pre_exchange)
   const bool restart = restart_now(e);
+  // the selected agents now hold their neighbours' poses of this iteration (the halo has arrived)
+  if (e->P.robust_cost != DPGO_ROBUST_L2) DPGO_TRY(snapshot_neighbors(e, color));
   if (e->gnc_due) {
     DPGO_TRY(reweight_color(e, color));
     // RobustCost::update (src/DPGO_robust.cpp:86-103): every agent once per reweighting iteration
@@ -1418,7 +1437,6 @@ int dpgo_rbcd_exchange(dpgo_rbcd e, const double** recv_dev) {
 
 int dpgo_rbcd_exchange_color(dpgo_rbcd e, int color, const double** recv_dev) {
   if (!e || !recv_dev || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad argument");
-  if (!halo_color_ok(e)) return dpgo_rbcd_exchange(e, recv_dev);
   if (e->world > 1 && !e->comm) return fail(DPGO_HIP_ESTATE, "no communicator (dpgo_rbcd_comm_init / _attach)");
   const auto* H = e->halo[color];
   HIP_TRY(e->xsend.ensure(std::max<long long>(e->send_off[e->world], 1)));  // the full plan bounds every colour's

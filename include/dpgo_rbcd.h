@@ -151,10 +151,10 @@ int dpgo_rbcd_exchange_counts(dpgo_rbcd e, long long* send_counts, long long* re
 int dpgo_rbcd_set_X(dpgo_rbcd e, const double* X_global);
 /* write the owned poses into a global host array (other poses untouched) */
 int dpgo_rbcd_get_X(dpgo_rbcd e, double* X_global);
-/* Phase 1 of iteration with selected colour c: every non-selected agent runs iterate(false).  With a robust cost
- * on several ranks the colours must follow the cyclic schedule (c = t mod C, as the example driver and the bench):
- * the non-selected agents' reweighting reads neighbour poses in place on their rank and from the last halo across
- * ranks, which agree only then; an out-of-order colour returns DPGO_HIP_EINVAL. */
+/* Phase 1 of iteration with selected colour c: every non-selected agent runs iterate(false).  Any colour order:
+ * a robust cost's reweighting (src/PGOAgent.cpp:1174-1244) reads the agent's own X and, for shared loop closures,
+ * its neighborPoseDict -- the neighbour poses it received when it was last selected (the engine snapshots them in
+ * dpgo_rbcd_update*), so results do not depend on the rank count or on the halo kind. */
 int dpgo_rbcd_pre_exchange(dpgo_rbcd e, int color);
 /* Pack the public poses peers need into send_dev (their X: with Nesterov the aux pose a receiver
  * uses equals the sender's X, which ran iterate(false) this iteration). */
@@ -162,7 +162,8 @@ int dpgo_rbcd_pack(dpgo_rbcd e, double* send_dev);
 /* Phase 2: selected agents of colour c update from the received neighbour poses. */
 /* Restrict the next updates to a subset of the selected colour's agents (agent_mask [num_agents], 1 =
  * optimise; nullptr = every agent of the colour, the colour schedule).  The others of the colour run
- * PGOAgent::iterate(false) like every other colour's agents (X = Y with acceleration, X unchanged without), so
+ * PGOAgent::iterate(false) like every other colour's agents (X = Y with acceleration, X unchanged without) and
+ * do not receive neighbour poses (their reweighting keeps reading their older dictionaries), so
  * selecting one agent per round (colour = its colour) is the example's greedy schedule
  * (examples/MultiRobotExample.cpp:243-256: the next robot is the argmax of the per-robot |RieGrad|, which
  * dpgo_rbcd_central_eval returns squared per agent). */
@@ -172,10 +173,9 @@ int dpgo_rbcd_update(dpgo_rbcd e, int color, const double* recv_dev, dpgo_opt_re
  * poses): the poses the agents of colour c read this iteration -- about half the full plan with two
  * colours.  Same call order as the full halo: dpgo_rbcd_pre_exchange(c), dpgo_rbcd_pack_color(c) into a
  * buffer laid out by dpgo_rbcd_exchange_counts_color(c) (peer-major, ascending global pose id), the
- * exchange, dpgo_rbcd_update_color(c).  Results are bitwise those of the full halo (the cyclic schedule, which a
- * robust cost on several ranks requires, dpgo_rbcd_pre_exchange).  With more than two
- * colours and a robust cost (whose reweighting of the other colours reads their neighbours too) these
- * fall back to the full plan and layout.  dpgo_rbcd_central_eval always takes the full plan. */
+ * exchange, dpgo_rbcd_update_color(c).  Results are bitwise those of the full halo, in any colour order and with
+ * any robust cost (nothing but the selected colour reads the halo).  dpgo_rbcd_central_eval always takes the full
+ * plan. */
 int dpgo_rbcd_plan_color(dpgo_graph g, int num_agents, const int* agent_of_pose, const int* agent_rank, int color,
                          int rank, int world, long long* send_counts, long long* recv_counts, int* send_poses,
                          int* recv_poses);

@@ -1302,7 +1302,7 @@ def _split(meas, robot_of, local, num_robots):
 
 
 def multi_robot_example(meas: Measurements, num_robots, r=5, num_iters=100, acceleration=True,
-                        robust="GNC_TLS", precon=PRECON_EXACT, X_init=None, verbose=False):
+                        robust="GNC_TLS", precon=PRECON_EXACT, X_init=None, verbose=False, robust_opt_inner_iters=30):
     """Serialized greedy RBCD (examples/MultiRobotExample.cpp:21-282) with the App. B fixes.
     Returns a per-iteration log [(iter, robot, 2f, gradnorm)] and the final X."""
     d = meas.d
@@ -1314,7 +1314,7 @@ def multi_robot_example(meas: Measurements, num_robots, r=5, num_iters=100, acce
     agents = []
     for rb in range(num_robots):
         ag = Agent(rb, AgentParams(d, r, num_robots, acceleration=acceleration, robust=robust,
-                                   precon=precon))
+                                   precon=precon, robust_opt_inner_iters=robust_opt_inner_iters))
         ag.set_pose_graph(*parts[rb], n=int(start[rb + 1] - start[rb]))
         agents.append(ag)
     if X_init is None:

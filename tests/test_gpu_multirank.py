@@ -127,7 +127,53 @@ def test_two_ranks_bitwise_one_rank_and_oracle(accel, robust, halo):
     assert rel(H.from_dev_layout(Xflat, R), Xo) <= 1e-9
 
 
-def _order_worker(rank, world, port, q):
+# a non-cyclic schedule: the example's greedy pattern (one robot per round, colours in any order; None = the whole
+# colour) over 12 iterations, reweighting every 3 (GNC_TLS, robust_opt_inner_iters = 3)
+ORDER = [(0, 0), (0, 3), (1, None), (1, 1), (0, 5), (1, 6), (1, 2), (0, None), (0, 3), (1, 7), (0, 0), (1, 4)]
+
+
+def _run_order(H, e, world, rank, halo="color"):
+    """Drive `e` through ORDER; on several ranks each iteration's halo goes over gloo through host copies, ordered
+    with the engine's launches by running both on one stream."""
+    s = torch.cuda.Stream()
+    e.set_stream(s.cuda_stream)
+    with torch.cuda.stream(s):
+        _run_order_on(H, e, world, halo)
+    torch.cuda.synchronize()
+
+
+def _run_order_on(H, e, world, halo):
+    send = torch.zeros(max(int(e.send_counts.sum()), 1), dtype=torch.float64, device="cuda")
+    recv = torch.zeros(max(int(e.recv_counts.sum()), 1), dtype=torch.float64, device="cuda")
+    for c, sel in ORDER:
+        mask = None
+        if sel is not None:
+            mask = np.zeros(A ** 3, np.int32)
+            mask[sel] = 1
+            c = int(e.color_of_agent[sel])
+        e.set_selected(mask)
+        e.pre_exchange(c)
+        if world == 1:
+            e.update(c, None)
+            continue
+        if halo == "color":
+            rs_c = [int(x) for x in e.recv_counts_color[c]]
+            ss_c = [int(x) for x in e.send_counts_color[c]]
+            e.pack_color(c, send.data_ptr())
+            hr = torch.empty(sum(rs_c), dtype=torch.float64)
+            dist.all_to_all_single(hr, send[:sum(ss_c)].cpu(), rs_c, ss_c)
+            recv[:sum(rs_c)].copy_(hr)
+            e.update_color(c, recv.data_ptr())
+        else:
+            e.pack(send.data_ptr())
+            hr = torch.empty(recv.shape, dtype=torch.float64)
+            dist.all_to_all_single(hr, send.cpu(), [int(x) for x in e.recv_counts], [int(x) for x in e.send_counts])
+            recv.copy_(hr)
+            e.update(c, recv.data_ptr())
+    e.set_selected(None)
+
+
+def _order_worker(rank, world, port, accel, halo, q):
     import sys
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -138,35 +184,46 @@ def _order_worker(rank, world, port, q):
         g = H.Graph.grid3d(K, seed=5)
         aop = g.grid_partition(A)
         ranks = (np.arange(A ** 3) * world // A ** 3).astype(np.int32)
-        res = []
-        for robust in ("L2", "GNC_TLS"):
-            e = H.Rbcd(g, aop, ranks, rank, world, _params(H, False, robust))
-            e.set_X(g.chain_init(R, O.lifting_matrix(3, R)))
-            e.pre_exchange(0)
-            try:
-                e.pre_exchange(0)  # colour 0 twice in a row: not the cyclic schedule
-                res.append((robust, "ok"))
-            except H.DPGOHipError as exc:
-                res.append((robust, str(exc)))
-        q.put((rank, res))
+        e = H.Rbcd(g, aop, ranks, rank, world, _params(H, accel, "GNC_TLS"))
+        X0 = g.chain_init(R, O.lifting_matrix(3, R))
+        e.set_X(X0)
+        _run_order(H, e, world, rank, halo=halo)
+        out = np.zeros(X0.size)
+        e.get_X_into(out)
+        rc, rd = e.status()
+        q.put((rank, out, rc, rd))
     finally:
         dist.destroy_process_group()
 
 
-def test_robust_cost_needs_cyclic_order_across_ranks():
-    """with a robust cost the non-selected agents' reweighting reads neighbour poses in place on their rank
-    and from the last halo across ranks; those agree (bitwise, rank-count invariant) under the cyclic colour schedule
-    only, so on several ranks an out-of-order colour is refused, and accepted with the L2 cost."""
+@pytest.mark.parametrize("halo", ["color", "full"])
+@pytest.mark.parametrize("accel", [False, True])
+def test_robust_cost_any_colour_order_across_ranks(accel, halo):
+    """GNC_TLS (PGOAgent::updateLoopClosuresWeights, src/PGOAgent.cpp:1174-1244) under a non-cyclic schedule -- the
+    example's greedy single-robot rounds (examples/MultiRobotExample.cpp:243-256) mixed with whole colours in any
+    order -- on two ranks: every reweighting reads the agent's own X and its neighborPoseDict (the poses it received
+    when last selected), never the halo's vintage, so the result is bitwise the one-rank engine's with either halo."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_order_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_order_worker, args=(r, 2, port, accel, halo, q)) for r in range(2)]
     for p in procs:
         p.start()
-    outs = [q.get(timeout=240) for _ in range(2)]
+    outs = sorted([q.get(timeout=240) for _ in range(2)], key=lambda o: o[0])
     for p in procs:
         p.join(timeout=60)
-    for _, res in outs:
-        d = dict(res)
-        assert d["L2"] == "ok"
-        assert "cyclic colour schedule" in d["GNC_TLS"]
+    from dpgo_amd import hip as H
+    g = H.Graph.grid3d(K, seed=5)
+    aop = g.grid_partition(A)
+    X0 = g.chain_init(R, O.lifting_matrix(3, R))
+    e1 = H.Rbcd(g, aop, np.zeros(A ** 3, np.int32), 0, 1, _params(H, accel, "GNC_TLS"))
+    e1.set_X(X0)
+    _run_order(H, e1, 1, 0)
+    X1 = np.zeros(X0.size)
+    e1.get_X_into(X1)
+    assert np.array_equal(outs[0][1] + outs[1][1], X1)
+    rc1, rd1 = e1.status()
+    ranks = (np.arange(A ** 3) * 2 // A ** 3)
+    for a in range(A ** 3):
+        assert outs[ranks[a]][2][a] == rc1[a] and outs[ranks[a]][3][a] == rd1[a]
+    assert not np.array_equal(X1, X0)

@@ -154,23 +154,27 @@ def test_contiguous_partition_2d_eight_agents(hip, name):
     assert abs(O.central_cost(meas, Xh) - O.central_cost(meas, Xo)) <= 1e-8 * O.central_cost(meas, Xo)
 
 
-@pytest.mark.parametrize("accel", [False, True])
-def test_greedy_selection_matches_example(hip, accel):
+@pytest.mark.parametrize("accel,robust", [(False, "L2"), (True, "L2"), (False, "GNC_TLS"), (True, "GNC_TLS")])
+def test_greedy_selection_matches_example(hip, accel, robust):
     """The example's greedy schedule (examples/MultiRobotExample.cpp:243-256) driven through the engine: each round
     one agent is optimised (dpgo_rbcd_set_selected; every other agent runs iterate(false)), and the next one is the
     argmax of the per-agent |RieGrad| from dpgo_rbcd_central_eval.  The selected robots, the gradient norms and the
-    final X equal the oracle's serialized restatement of the example (smallGrid3D, 5 contiguous robots, L2,
-    block-Jacobi)."""
+    final X equal the oracle's serialized restatement of the example (smallGrid3D, 5 contiguous robots,
+    block-Jacobi).  GNC_TLS (reweighting every 3 iterations): only the selected robot receives its neighbours'
+    poses, so every other robot's reweighting of a shared loop closure reads the pose it received when it was last
+    selected (PGOAgent::updateLoopClosuresWeights, src/PGOAgent.cpp:1201-1235) -- the engine's neighbour
+    dictionaries."""
     meas = load_meas("smallGrid3D")
     r, R, iters = 5, 5, 20
     n = meas.num_poses
     X0 = O.lifting_matrix(3, r) @ O.chordal_initialization(3, n, meas)
-    log, Xo = O.multi_robot_example(meas, R, r=r, num_iters=iters, acceleration=accel, robust="L2",
-                                    precon=O.PRECON_BLOCK_JACOBI, X_init=X0)
+    log, Xo = O.multi_robot_example(meas, R, r=r, num_iters=iters, acceleration=accel, robust=robust,
+                                    precon=O.PRECON_BLOCK_JACOBI, X_init=X0, robust_opt_inner_iters=3)
     _, robot_of, _, _ = O.partition_contiguous(meas, n, R)
     g = _graph_from_meas(hip, meas)
     e = hip.Rbcd(g, robot_of.astype(np.int32), np.zeros(R, np.int32), 0, 1,
-                 hip.rbcd_params(r=r, acceleration=int(accel), precon=hip.PRECON_BLOCK_JACOBI))
+                 hip.rbcd_params(r=r, acceleration=int(accel), precon=hip.PRECON_BLOCK_JACOBI,
+                                 robust_cost=hip.ROBUST[robust], robust_opt_inner_iters=3))
     e.set_X(X0)
     sel, got = 0, []
     for it in range(len(log)):
