@@ -50,6 +50,21 @@ def measured_traffic():
         return None
 
 
+def fp64_peak():
+    """The fp64 ceilings measured on this pool (tools/fp64_peak.hip), newest committed profiles/*_fp64_peak.json."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_fp64_peak.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            t = json.load(f)
+        t["source"] = os.path.relpath(files[-1], ROOT)
+        return t
+    except (OSError, ValueError):
+        return None
+
+
 def super_cube_ranks(A, world):
     """Agents -> ranks: 2x2x2 super-cubes of agents (8 groups), merged for world < 8."""
     ranks = np.zeros(A ** 3, np.int32)
@@ -332,8 +347,7 @@ def main():
                 Xb = tx.cpu().numpy()
             eng.set_X(Xb)  # PGOAgent::setX: Nesterov restarts from the burnt-in iterate
         X_start = None
-        if rank == 0 and world == 1 and args.cpu_baseline and args.precon == "block_jacobi" and \
-                args.robust in ("L2", "GNC_TLS"):
+        if rank == 0 and world == 1 and args.cpu_baseline and args.robust in ("L2", "GNC_TLS"):
             X_start = np.zeros(X0.size)
             eng.get_X_into(X_start)
         f_start, gn_start = central()
@@ -540,14 +554,48 @@ def main():
     out["comm"] = comm
     if args.precon == "exact":
         # the factor of Q + 0.1 I per colour batch: tree, size, and the device numeric factorisation (it re-runs after
-        # every GNC reweighting, inside the timed steps when one falls there)
+        # every GNC reweighting, inside the timed steps when one falls there), its flops and TFLOP/s against the
+        # measured fp64 matrix-core ceiling (tools/fp64_peak.hip, profiles/*_fp64_peak.json)
         out["exact_factor"] = {f"color{c}": eng.exact_factor_info(c) for c in range(eng.num_colors)}
         out["exact_factor"]["refactorisations_in_timed_steps"] = refactor_in_timed
+        peak = fp64_peak()
+        if peak:
+            out["exact_factor"]["fp64_ceiling"] = peak
+            for c in range(eng.num_colors):
+                fi = out["exact_factor"][f"color{c}"]
+                if fi.get("factor_tflops"):
+                    fi["factor_frac_of_mfma_f64"] = fi["factor_tflops"] / peak["mfma_f64_16x16x4_tflops"]
+        # the solves' roofline: each sweep streams every stored panel once (HBM-bound; HIP events around the sweeps of
+        # standalone applications over colour 0, outside the timed steps)
+        with torch.cuda.stream(stream):
+            mf, mb, pb = eng.bench_precond(0, 5)
+        out["exact_roofline"] = {
+            "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "panel_bytes_per_sweep": pb,
+            "forward": {"ms": mf, "GBps": pb / (mf * 1e-3) / 1e9 if mf > 0 else 0.0,
+                        "frac": pb / (mf * 1e-3) / 1e9 / HBM_PEAK_GBS if mf > 0 else 0.0,
+                        "kernels": "every level's k_sn_assemble + k_sn_fwd"},
+            "backward": {"ms": mb, "GBps": pb / (mb * 1e-3) / 1e9 if mb > 0 else 0.0,
+                         "frac": pb / (mb * 1e-3) / 1e9 / HBM_PEAK_GBS if mb > 0 else 0.0,
+                         "kernels": "every level's k_sn_bwd"},
+            "what": "one full application over every agent of colour 0 (no tCG skip), mean of 5 after 3 untimed; "
+                    "bytes = the stored panels (64 x 64 tiles, padding included), read once per sweep"}
     out["halo"] = {"kind": args.halo if world > 1 else "none (one rank)",
                    "bytes_sent_per_step_this_rank": 8.0 * (sum(sum(v) for v in c_in) if args.halo == "color"
                                                            else eng.num_colors * int(eng.send_counts.sum())),
                    "full_plan_bytes_per_exchange": 8.0 * int(eng.send_counts.sum())}
-    if X_start is not None:
+    if X_start is not None and args.precon == "exact":
+        try:
+            from oracle import cpu_port
+            # the GPU timed region's mix: every agent update, and every agent factorisation its refactorisations ran
+            per_color = max(int(eng.agents_per_color[0]), 1)
+            cb = cpu_port.exact_sample_baseline(g, aop, X_start, args.r, bool(args.accel), num_agents,
+                                                robust=args.robust, updates=agent_updates,
+                                                agent_factorisations=refactor_in_timed * per_color)
+            out["cpu_baseline"] = cb
+            out["speedup_vs_cpu_baseline"] = value / cb["value"]
+        except Exception as exc:  # reported, never silently replaced
+            out["cpu_baseline"] = {"error": repr(exc)}
+    elif X_start is not None:
         try:
             from oracle import cpu_port
             cb, Xc, stc, iters = cpu_port.engine_baseline(g, aop, X_start, args.r, bool(args.accel), num_agents,

@@ -580,6 +580,7 @@ int sync_chol(dpgo_hip_problem h) {
   std::vector<int2> contrib;
   int maxd = 0;
   long fo = 0, uo = 0, po = 0;
+  double flops = 0.0, inv_flops = 0.0;
   for (int a = 0; a < K; ++a) {
     const auto& nodes = Fs[a].nodes;
     const long off = h->pose_off[a];
@@ -589,6 +590,11 @@ int sync_chol(dpgo_hip_problem h) {
       const int s = static_cast<int>(nd.S.size()), t = static_cast<int>(nd.R.size());
       s_[g] = s;
       t_[g] = t;
+      {  // scalars: POTRF of the frontal S block, TRSM of the R rows, the update of the R x R frontal block
+        const double ss = static_cast<double>(s) * b, ts = static_cast<double>(t) * b;
+        flops += ss * ss * ss / 3.0 + ss * ss * ts + ss * ts * ts;
+        inv_flops += ss * ss * ss / 3.0 + ss * ss * ts;
+      }
       panel_off[g] = po;
       po += dpgo::sn_panel_tiles(s * b, t * b) * dpgo::kSnTile * dpgo::kSnTile;
       f_off[g] = fo;
@@ -681,6 +687,9 @@ int sync_chol(dpgo_hip_problem h) {
   HIP_TRY(h->sn_F.ensure(std::max<long>(fo, 1)));
   HIP_TRY(h->sn_U.ensure(std::max<long>(uo, 1)));
   h->chol_doubles = po;
+  h->sn_nodes = nn;
+  h->chol_flops = flops;
+  h->chol_inv_flops = inv_flops;
   if (!device) {
     h->chol_state = 1;
     return DPGO_HIP_OK;
@@ -1446,7 +1455,7 @@ int dpgo_hip_exact_factor_info(dpgo_hip_problem h, long long* nodes, int* levels
   DPGO_TRY(check_handle(h));
   if (!nodes || !levels || !max_s_tiles || !panel_doubles || !factor_ms || !factor_count)
     return fail(DPGO_HIP_EINVAL, "null argument");
-  const long nn = static_cast<long>(h->sn_s.n);
+  const long nn = h->sn_nodes;
   *nodes = h->chol_doubles > 0 ? nn : 0;
   *levels = static_cast<int>(h->sn_levels.size());
   *max_s_tiles = 0;
@@ -1458,6 +1467,14 @@ int dpgo_hip_exact_factor_info(dpgo_hip_problem h, long long* nodes, int* levels
   *panel_doubles = h->chol_doubles;
   *factor_ms = h->chol_factor_ms;
   *factor_count = h->chol_factor_count;
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_exact_factor_flops(dpgo_hip_problem h, double* cholesky_flops, double* inverse_flops) {
+  DPGO_TRY(check_handle(h));
+  if (!cholesky_flops || !inverse_flops) return fail(DPGO_HIP_EINVAL, "null argument");
+  *cholesky_flops = h->chol_doubles > 0 ? h->chol_flops : 0.0;
+  *inverse_flops = h->chol_doubles > 0 ? h->chol_inv_flops : 0.0;
   return DPGO_HIP_OK;
 }
 
@@ -2761,6 +2778,51 @@ int dpgo_hip_bench_hvp(dpgo_hip_problem h, const double* X_dev, double* V_dev, d
   *ms = static_cast<double>(t) / reps;
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_bench_precond(dpgo_hip_problem h, const double* V_dev, int reps, double* ms_fwd, double* ms_bwd,
+                           double* panel_bytes) {
+  DPGO_TRY(ready(h));
+  DPGO_TRY(ensure_work(h));
+  if (reps <= 0 || !ms_fwd || !ms_bwd || !panel_bytes) return fail(DPGO_HIP_EINVAL, "bad argument");
+  DPGO_TRY(sync_chol(h));
+  *ms_fwd = *ms_bwd = 0.0;
+  *panel_bytes = 8.0 * static_cast<double>(h->chol_doubles);
+  if (h->chol_state != 1) return DPGO_HIP_OK;
+  const dpgo::SnView v{h->sn_panel.p, h->sn_panel_off.p, h->sn_s.p,    h->sn_t.p,    h->sn_poses_off.p,
+                       h->sn_poses.p, h->sn_f_off.p,     h->sn_u_off.p, h->sn_cpos_off.p, h->sn_cpos.p,
+                       h->sn_contrib.p, h->sn_F.p,       h->sn_U.p,    h->sn_node_agent.p, h->state.p, dpgo::FLAG_NONE};
+  const int2* it = h->sn_items.p;
+  const int nl = static_cast<int>(h->sn_levels.size());
+  hipEvent_t ev[3];
+  for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
+  double tf = 0.0, tb = 0.0;
+  for (int i = 0; i < kBenchWarmup + reps; ++i) {  // untimed applications first (see dpgo_hip_bench_hvp)
+    HIP_TRY(hipEventRecord(ev[0], h->stream));
+    for (int l = nl - 1; l >= 0; --l) {
+      const auto& L = h->sn_levels[l];
+      HIP_TRY(dpgo::launch_sn_assemble(h->r, h->b, v, it + L.asm0, L.asm_n, V_dev, h->stream));
+      HIP_TRY(dpgo::launch_sn_fwd(h->r, h->b, v, it + L.fwd0, L.fwd_n, h->tA.p, h->stream));
+    }
+    HIP_TRY(hipEventRecord(ev[1], h->stream));
+    for (int l = 0; l < nl; ++l) {
+      const auto& L = h->sn_levels[l];
+      HIP_TRY(dpgo::launch_sn_bwd(h->r, h->b, v, it + L.bwd0, L.bwd_n, h->tA.p, h->tB.p, h->stream));
+    }
+    HIP_TRY(hipEventRecord(ev[2], h->stream));
+    HIP_TRY(hipEventSynchronize(ev[2]));
+    if (i >= kBenchWarmup) {
+      float a = 0.f, b = 0.f;
+      HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
+      HIP_TRY(hipEventElapsedTime(&b, ev[1], ev[2]));
+      tf += a;
+      tb += b;
+    }
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  *ms_fwd = tf / reps;
+  *ms_bwd = tb / reps;
   return DPGO_HIP_OK;
 }
 

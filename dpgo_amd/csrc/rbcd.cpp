@@ -1381,6 +1381,27 @@ int dpgo_rbcd_exact_factor_info(dpgo_rbcd e, int color, long long* nodes, int* l
   return dpgo_hip_exact_factor_info(e->prob[color], nodes, levels, max_s_tiles, panel_doubles, factor_ms, factor_count);
 }
 
+int dpgo_rbcd_bench_precond(dpgo_rbcd e, int color, int reps, double* ms_fwd, double* ms_bwd, double* panel_bytes) {
+  if (!e || color < 0 || color >= e->ncolors) return fail(DPGO_HIP_EINVAL, "bad colour");
+  if (!e->prob[color]) {
+    if (ms_fwd) *ms_fwd = 0.0;
+    if (ms_bwd) *ms_bwd = 0.0;
+    if (panel_bytes) *panel_bytes = 0.0;
+    return DPGO_HIP_OK;
+  }
+  DPGO_TRY(join_side(e));
+  return dpgo_hip_bench_precond(e->prob[color], color_ptr(e, e->X, color), reps, ms_fwd, ms_bwd, panel_bytes);
+}
+
+int dpgo_rbcd_exact_factor_flops(dpgo_rbcd e, int color, double* cholesky_flops, double* inverse_flops) {
+  if (!e || color < 0 || color >= e->ncolors || !cholesky_flops || !inverse_flops) return fail(DPGO_HIP_EINVAL, "bad argument");
+  if (!e->prob[color]) {
+    *cholesky_flops = *inverse_flops = 0.0;
+    return DPGO_HIP_OK;
+  }
+  return dpgo_hip_exact_factor_flops(e->prob[color], cholesky_flops, inverse_flops);
+}
+
 int dpgo_rbcd_comm_info(dpgo_rbcd e, int* count, int* rank) {
   if (!e || !count || !rank) return fail(DPGO_HIP_EINVAL, "null argument");
   *count = -1;

@@ -90,6 +90,8 @@ _SIGS = [
     ("dpgo_hip_get_tuning", [C.c_int, C.POINTER(C.c_int)], C.c_int),
     ("dpgo_hip_exact_factor_info", [C.c_void_p, C.POINTER(C.c_longlong), C.POINTER(C.c_int), C.POINTER(C.c_int),
                                     C.POINTER(C.c_longlong), C.POINTER(C.c_double), C.POINTER(C.c_int)], C.c_int),
+    ("dpgo_hip_exact_factor_flops", [C.c_void_p, _dp, _dp], C.c_int),
+    ("dpgo_hip_bench_precond", [C.c_void_p, C.c_void_p, C.c_int, _dp, _dp, _dp], C.c_int),
     ("dpgo_hip_problem_set_tuning", [C.c_void_p, C.c_int, C.c_int], C.c_int),
     ("dpgo_hip_spmm_bytes", [C.c_void_p], C.c_double),
     ("dpgo_hip_bench_spmm", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, _dp], C.c_int),
@@ -412,8 +414,11 @@ class Problem:
         n, lv, mt, pd, ms, cnt = C.c_longlong(), C.c_int(), C.c_int(), C.c_longlong(), C.c_double(), C.c_int()
         _check(lib().dpgo_hip_exact_factor_info(self.h, C.byref(n), C.byref(lv), C.byref(mt), C.byref(pd), C.byref(ms),
                                                 C.byref(cnt)))
+        fl, ifl = C.c_double(), C.c_double()
+        _check(lib().dpgo_hip_exact_factor_flops(self.h, C.byref(fl), C.byref(ifl)))
         return {"nodes": n.value, "levels": lv.value, "max_s_tiles": mt.value, "panel_doubles": pd.value,
-                "factor_ms": ms.value, "factor_count": cnt.value}
+                "factor_ms": ms.value, "factor_count": cnt.value, "cholesky_flops": fl.value,
+                "inverse_flops": ifl.value}
 
     def set_tuning(self, key, value):
         """A tuning key on this handle only (dpgo_hip_problem_set_tuning)."""
@@ -538,6 +543,8 @@ _SIGS2 = [
     ("dpgo_rbcd_exact_factor_info", [C.c_void_p, C.c_int, C.POINTER(C.c_longlong), C.POINTER(C.c_int),
                                      C.POINTER(C.c_int), C.POINTER(C.c_longlong), C.POINTER(C.c_double),
                                      C.POINTER(C.c_int)], C.c_int),
+    ("dpgo_rbcd_exact_factor_flops", [C.c_void_p, C.c_int, _dp, _dp], C.c_int),
+    ("dpgo_rbcd_bench_precond", [C.c_void_p, C.c_int, C.c_int, _dp, _dp, _dp], C.c_int),
     ("dpgo_rbcd_exchange", [C.c_void_p, C.POINTER(C.c_void_p)], C.c_int),
     ("dpgo_rbcd_set_kernel_timing", [C.c_void_p, C.c_int], C.c_int),
     ("dpgo_rbcd_set_tuning", [C.c_void_p, C.c_int, C.c_int], C.c_int),
@@ -872,8 +879,20 @@ class Rbcd:
         n, lv, mt, pd, ms, cnt = C.c_longlong(), C.c_int(), C.c_int(), C.c_longlong(), C.c_double(), C.c_int()
         _check(lib().dpgo_rbcd_exact_factor_info(self.h, int(color), C.byref(n), C.byref(lv), C.byref(mt), C.byref(pd),
                                                  C.byref(ms), C.byref(cnt)))
-        return {"nodes": n.value, "levels": lv.value, "max_s_tiles": mt.value, "panel_doubles": pd.value,
-                "factor_ms": ms.value, "factor_count": cnt.value}
+        fl, ifl = C.c_double(), C.c_double()
+        _check(lib().dpgo_rbcd_exact_factor_flops(self.h, int(color), C.byref(fl), C.byref(ifl)))
+        out = {"nodes": n.value, "levels": lv.value, "max_s_tiles": mt.value, "panel_doubles": pd.value,
+               "factor_ms": ms.value, "factor_count": cnt.value, "cholesky_flops": fl.value, "inverse_flops": ifl.value}
+        if ms.value > 0:
+            out["factor_tflops"] = fl.value / (ms.value * 1e-3) / 1e12
+            out["factor_tflops_with_inverse"] = (fl.value + ifl.value) / (ms.value * 1e-3) / 1e12
+        return out
+
+    def bench_precond(self, color, reps):
+        """The exact preconditioner's forward / backward sweeps over colour class c: (ms_fwd, ms_bwd, panel bytes)."""
+        f, b, p = C.c_double(), C.c_double(), C.c_double()
+        _check(lib().dpgo_rbcd_bench_precond(self.h, int(color), int(reps), C.byref(f), C.byref(b), C.byref(p)))
+        return f.value, b.value, p.value
 
     def comm_info(self):
         """(ncclCommCount, ncclCommUserRank) of the engine's own RCCL communicator, (-1, -1) without one."""

@@ -273,6 +273,17 @@ int dpgo_hip_set_tuning(int key, int value);
  * the host) with the number of device factorisations so far. */
 int dpgo_hip_exact_factor_info(dpgo_hip_problem h, long long* nodes, int* levels, int* max_s_tiles,
                                long long* panel_doubles, double* factor_ms, int* factor_count);
+/* Flop counts of one numeric factorisation of that factor (the roofline of dpgo_hip_exact_factor_info's factor_ms):
+ * the classic supernodal Cholesky count sum_nodes s^3/3 + s^2 t + s t^2 (s, t = the node's S and R scalars; the
+ * work CHOLMOD does for src/QuadraticProblem.cpp:37-41), and the extra flops of the panels' inverse blocks
+ * [L_SS^-1; L_RS L_SS^-1] (s^3/3 + s^2 t per node) that make the solves dense products.  Zeros before a factor. */
+int dpgo_hip_exact_factor_flops(dpgo_hip_problem h, double* cholesky_flops, double* inverse_flops);
+/* The exact preconditioner's two sweeps over every agent of the handle (right-hand side V_dev, the handle's layout),
+ * `reps` applications after 3 untimed ones, each timed with HIP events on the handle's stream: the forward sweep
+ * (every level's k_sn_assemble + k_sn_fwd) and the backward sweep (every level's k_sn_bwd), ms per application, and
+ * the bytes of the stored panels, which each sweep streams once (64 x 64 tiles, padding included). */
+int dpgo_hip_bench_precond(dpgo_hip_problem h, const double* V_dev, int reps, double* ms_fwd, double* ms_bwd,
+                           double* panel_bytes);
 /* The process default of a tuning key. */
 int dpgo_hip_get_tuning(int key, int* value);
 /* The same keys on one existing handle (A/B timing of variants on one problem without rebuilding it). */

@@ -246,3 +246,47 @@ def engine_baseline(graph, agent_of_pose, X_start, r, accel, num_agents, warmup=
            "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
     iters = 1 + (warmup + rounds) * (2 if share is not None else 1)
     return res, E.get_X(), E.stats(), iters
+
+
+def exact_sample_baseline(graph, agent_of_pose, X_start, r, accel, num_agents, robust="L2", reps=2, sample=None,
+                          updates=None, agent_factorisations=0):
+    """CPU baseline of the exact-preconditioner legs (bench.py --precon exact): oracle/cpu's exact mode (reverse
+    Cuthill-McKee envelope Cholesky of Q + 0.1 I per agent, no code shared with the GPU library) on a BOUNDED sample of
+    the workload: `sample` agents of colour 0 (default: as many as the OpenMP team has threads, at most a colour's),
+    OpenMP over them, each factorised once and then updated `reps` times from the GPU timed region's start X.  The
+    two measured rates -- agent factorisations / s and agent updates / s -- are combined for the GPU run's own mix:
+    `updates` agent updates and `agent_factorisations` agent factorisations (the L2 leg refactorises nothing inside
+    the timed steps; GNC_TLS refactorises every agent after each reweighting).  The reference itself refactorises at
+    EVERY update under a robust cost (constructQMatrix -> setQ in PGOAgent::updateX, src/PGOAgent.cpp:1110-1112;
+    src/QuadraticProblem.cpp:37-41), which this baseline does not charge."""
+    import time as _time
+    arrays = graph.arrays()
+    t0 = _time.time()
+    E = CpuRbcd(graph.d, r, arrays, graph.n, agent_of_pose, num_agents, accel, robust=robust, precon="exact")
+    E.set_X(X_start)
+    setup = _time.time() - t0
+    T, avail, omp = host_cores()
+    T = max(1, min(omp, avail, T))
+    col0 = [a for a in range(num_agents) if E.colors[a] == 0]
+    S = min(len(col0), sample or T)
+    agents = col0[:S]
+    wall_upd, fsec, usec = E.time_sample(agents, T, reps)
+    # the factor phase's wall time: S factorisations over min(S, T) threads
+    waves = -(-S // T)
+    fac_wall = float(np.max(fsec)) * waves
+    upd_rate = S * reps / wall_upd
+    fac_rate = S / fac_wall
+    U = updates if updates is not None else S * reps
+    t_model = U / upd_rate + agent_factorisations / fac_rate
+    E.close()
+    return {"value": U / t_model, "unit": "RBCD agent-updates/s", "cores": T, "kind": "port",
+            "sample": (f"oracle/cpu exact mode (RCM envelope Cholesky of Q + 0.1 I, {robust}, Nesterov={bool(accel)}) "
+                       f"from the GPU timed region's start X: {S} agents of colour 0 on {T} OpenMP threads, each "
+                       f"factorised once and updated {reps} times; combined for the GPU run's {U} agent updates and "
+                       f"{agent_factorisations} agent factorisations"),
+            "agent_updates_per_s": upd_rate, "seconds_per_update_median": float(np.median(usec)),
+            "agent_factorisations_per_s": fac_rate, "seconds_per_factorisation_median": float(np.median(fsec)),
+            "setup_s": setup, "threads": T, "affinity_cpus": avail, "omp_max_threads": omp, "isa": ISA,
+            "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
+            "note": "the reference refactorises at every update under a robust cost (src/PGOAgent.cpp:1110-1112); "
+                    "not charged here"}
