@@ -69,6 +69,8 @@ dpgo::LaunchCtx make_ctx(dpgo_hip_problem h, int flag_kind, double* partials) {
   c.partials = partials;
   c.stream = h->stream;
   c.round = 0;
+  c.tile_meta = h->fmt == dpgo::QFMT_EDGES && h->tile_meta.n >= static_cast<size_t>(h->num_tiles) ? h->tile_meta.p
+                                                                                                  : nullptr;
   return c;
 }
 
@@ -316,6 +318,16 @@ int sync_q_edges(dpgo_hip_problem h) {
     if (static_cast<double>(rec.size()) * 8.0 >= lim || static_cast<double>(ymax) * h->r * b * 8.0 >= lim)
       return fail(DPGO_HIP_EINVAL, "edge-stream Q: records or the pose vector exceed the 4 GiB range of the SpMM's "
                                    "buffer gathers (split the poses over more handles / ranks)");
+  }
+  {  // per tile: incidence range and first-visit record range (LaunchCtx::tile_meta)
+    const int T = h->num_tiles;
+    std::vector<int4> meta(std::max(T, 1));
+    for (int t = 0; t < T; ++t) {
+      const int j0 = h->h_tile_start[t], j1 = j0 + h->h_tile_count[t];
+      meta[t] = make_int4(deg[j0], deg[j1] - deg[j0], lowcnt[j0], lowcnt[j1] - lowcnt[j0]);
+    }
+    HIP_TRY(h->tile_meta.ensure(meta.size()));
+    HIP_TRY(hipMemcpy(h->tile_meta.p, meta.data(), sizeof(int4) * meta.size(), hipMemcpyHostToDevice));
   }
   h->nnz_inc = deg[h->N];
   h->num_edges = m;
@@ -1826,6 +1838,7 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
         c.tile_agent += t0;
         c.tile_start += t0;
         c.tile_count += t0;
+        if (c.tile_meta) c.tile_meta += t0;
         c.num_tiles = t1 - t0;
         c.stream = on;
         return c;

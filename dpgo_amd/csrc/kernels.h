@@ -80,6 +80,10 @@ struct LaunchCtx {
   double* partials;       // [num_tiles * kPartialStride]
   hipStream_t stream;
   int round;              // FLAG_DECIDED: the RTR Run index (0-based)
+  // edge-stream Q only (else null): per tile {first incidence, incidences, first first-visit record, records}, so a
+  // launch issues the tile's stage loads right after the tile's scalar header instead of after a round trip
+  // through its poses' incidence pointers
+  const int4* tile_meta;
 };
 
 enum QFormat { QFMT_BSR = 0, QFMT_EDGES = 1 };

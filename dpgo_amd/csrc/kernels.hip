@@ -1433,7 +1433,14 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
   const PoseLane p = pose_lane<B, FMT == QFMT_EDGES ? evar_xcd(VAR) : var_xcd(VAR)>(c);
   constexpr bool ROT = FMT == QFMT_EDGES && B == 4 && evar_rot(VAR);
   constexpr bool UNI = ROT && evar_uni(VAR);
-  if (tile_skipped(c, p.agent)) {
+  // A staged edge-stream tile with its descriptor (LaunchCtx::tile_meta) decides its skip only after its stage loads
+  // are issued: the agent's flag (a scalar load that depends on the tile's agent) then waits in parallel with them
+  // instead of ahead of them.  A skipped tile's stage is read and dropped.
+  constexpr bool kStageFmt = FMT == QFMT_EDGES && !(MODE == MODE_F || MODE == MODE_QF) &&
+                             !(mode_hess(MODE) && evar_sv(VAR));
+  const bool skip = tile_skipped(c, p.agent);
+  const bool late_skip = kStageFmt && c.tile_meta != nullptr;
+  if (skip && !late_skip) {
     if constexpr (spmm_fusable(MODE)) spmm_arrive(args, p.agent);
     return;
   }
@@ -1496,11 +1503,24 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
       red_scratch = s_recd;
     }
     const int t0 = c.tile_start[p.tile], cnt = c.tile_count[p.tile];
-    if (static_cast<int>(threadIdx.x) <= cnt) s_ptr[threadIdx.x] = q.inc_ptr[t0 + threadIdx.x];
-    if (threadIdx.x < 2) s_e[threadIdx.x] = q.rec_first[t0 + (threadIdx.x ? cnt : 0)];
-    if (SVS && threadIdx.x >= 2 && threadIdx.x < 4) s_e[threadIdx.x] = q.sv_ptr[p.tile + threadIdx.x - 2];
-    __syncthreads();
-    const int i0 = s_ptr[0], ni = s_ptr[cnt] - i0, e0 = s_e[0], ne = s_e[1] - e0;
+    int i0, ni, e0, ne;
+    if (late_skip) {  // the stage ranges from the tile descriptor: the pointers below load in parallel with them
+      const int4 tm = c.tile_meta[p.tile];
+      i0 = tm.x;
+      ni = tm.y;
+      e0 = tm.z;
+      ne = tm.w;
+      if (static_cast<int>(threadIdx.x) <= cnt) s_ptr[threadIdx.x] = q.inc_ptr[t0 + threadIdx.x];
+    } else {
+      if (static_cast<int>(threadIdx.x) <= cnt) s_ptr[threadIdx.x] = q.inc_ptr[t0 + threadIdx.x];
+      if (threadIdx.x < 2) s_e[threadIdx.x] = q.rec_first[t0 + (threadIdx.x ? cnt : 0)];
+      if (SVS && threadIdx.x >= 2 && threadIdx.x < 4) s_e[threadIdx.x] = q.sv_ptr[p.tile + threadIdx.x - 2];
+      __syncthreads();
+      i0 = s_ptr[0];
+      ni = s_ptr[cnt] - i0;
+      e0 = s_e[0];
+      ne = s_e[1] - e0;
+    }
     const int sv0 = SVS ? s_e[2] : 0, ns = SVS ? s_e[3] - s_e[2] : 0;
     const bool staged = STAGE && ni <= NINC && ns + ne <= NREC;
     if (staged) {
@@ -1522,17 +1542,48 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
           s_recd[(ns + rr) * RS + 2 * w + 1] = v.y;
         }
       } else {
-        for (int x = threadIdx.x; x < ni; x += kThreads) s_inc[x] = q.inc[i0 + x];
+        // two phases: every stage load of the thread in flight at once, then the LDS writes (a load / wait / write
+        // loop costs one memory latency per trip: up to 2 + 7 of them per tile)
+        constexpr int KI = (NINC + kThreads - 1) / kThreads, KR = (NREC * (RW / 2) + kThreads - 1) / kThreads;
+        int2 iv[KI];
+        f64x2 rv[KR];
         const f64x2* src = reinterpret_cast<const f64x2*>(q.rec) + static_cast<long>(e0) * (RW / 2);
-        for (int x = threadIdx.x; x < ne * (RW / 2); x += kThreads) {
-          const int rr = x / (RW / 2), w = x - rr * (RW / 2);
-          const f64x2 v = src[x];
-          s_recd[rr * RS + 2 * w] = v.x;
-          s_recd[rr * RS + 2 * w + 1] = v.y;
+        const int nr = ne * (RW / 2);
+#pragma unroll
+        for (int u = 0; u < KI; ++u) {
+          const int x = static_cast<int>(threadIdx.x) + u * kThreads;
+          if (x < ni) iv[u] = q.inc[i0 + x];
+        }
+#pragma unroll
+        for (int u = 0; u < KR; ++u) {
+          const int x = static_cast<int>(threadIdx.x) + u * kThreads;
+          if (x < nr) rv[u] = src[x];
+        }
+#pragma unroll
+        for (int u = 0; u < KI; ++u) {
+          const int x = static_cast<int>(threadIdx.x) + u * kThreads;
+          if (x < ni) s_inc[x] = iv[u];
+        }
+#pragma unroll
+        for (int u = 0; u < KR; ++u) {
+          const int x = static_cast<int>(threadIdx.x) + u * kThreads;
+          if (x < nr) {
+            const int rr = x / (RW / 2), w = x - rr * (RW / 2);
+            s_recd[rr * RS + 2 * w] = rv[u].x;
+            s_recd[rr * RS + 2 * w + 1] = rv[u].y;
+          }
         }
       }
     }
-    if constexpr (STAGE) __syncthreads();
+    if (late_skip && skip) {  // uniform over the block: every thread leaves here
+      if constexpr (spmm_fusable(MODE)) spmm_arrive(args, p.agent);
+      return;
+    }
+    if constexpr (STAGE) {
+      __syncthreads();
+    } else {
+      if (late_skip) __syncthreads();  // (never: late_skip needs the stage) s_ptr written above
+    }
     constexpr bool NODIAG = MODE == MODE_QF;
     if (p.ok) {
       const double* s_rec = s_recd;

@@ -123,6 +123,7 @@ struct dpgo_hip_problem_s {
   };
   std::vector<SnLevel> sn_levels;  // index = depth (0 = the roots)
   long chol_doubles = 0;
+  dpgo::DevBuf<int4> tile_meta;  // edge-stream Q: per tile stage ranges (LaunchCtx::tile_meta); empty otherwise
   long sn_nodes = 0;             // supernodes of the current symbolic structure (sn_s may be larger: capacity)
   double chol_flops = 0.0;       // the factorisation's classic flop count: sum over supernodes s^3/3 + s^2 t + s t^2
   double chol_inv_flops = 0.0;   // the panels' extra: L_SS^-1 (s^3/3) and L_RS L_SS^-1 (s^2 t) per supernode
