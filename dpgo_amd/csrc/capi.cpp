@@ -79,8 +79,10 @@ dpgo::LaunchCtx make_ctx(dpgo_hip_problem h, int flag_kind, double* partials) {
 namespace {
 
 dpgo::QView qview(dpgo_hip_problem h) {
-  return dpgo::QView{h->rowptr.p, h->col.p, h->blocks.p, h->inc_ptr.p, h->inc.p, h->rec.p, h->diag.p, h->rec_first.p,
-                     h->sv_ptr.p, h->sv_ids.p, h->inc_sv.p, h->fmt, h->tuning};
+  const bool unit = h->central_unit && h->rec_unit.p != nullptr;
+  return dpgo::QView{h->rowptr.p, h->col.p, h->blocks.p, h->inc_ptr.p, h->inc.p, unit ? h->rec_unit.p : h->rec.p,
+                     unit ? h->diag_unit.p : h->diag.p, h->rec_first.p, h->sv_ptr.p, h->sv_ids.p, h->inc_sv.p, h->fmt,
+                     h->tuning};
 }
 
 int check_handle(dpgo_hip_problem h) {
@@ -2073,6 +2075,23 @@ int dpgo::eval_sums_dev(dpgo_hip_problem h, const double* X) {
   DPGO_TRY(ensure_work(h));
   DPGO_TRY(eval_at(h, X, nullptr, nullptr, h->pa.p, dpgo::FLAG_NONE));
   return finalize(h, dpgo::OP_SUM, h->pa.p, 3, nullptr, 0);
+}
+
+int dpgo::keep_unit_q(dpgo_hip_problem h) {
+  DPGO_TRY(ready(h));
+  if (h->fmt != dpgo::QFMT_EDGES) return DPGO_HIP_OK;
+  HIP_TRY(h->rec_unit.ensure(h->rec.n));
+  HIP_TRY(h->diag_unit.ensure(h->diag.n));
+  HIP_TRY(hipMemcpyAsync(h->rec_unit.p, h->rec.p, sizeof(double) * h->rec.n, hipMemcpyDeviceToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(h->diag_unit.p, h->diag.p, sizeof(double) * h->diag.n, hipMemcpyDeviceToDevice, h->stream));
+  return DPGO_HIP_OK;
+}
+
+int dpgo::eval_sums_unit_dev(dpgo_hip_problem h, const double* X) {
+  h->central_unit = true;
+  const int rc = eval_sums_dev(h, X);
+  h->central_unit = false;
+  return rc;
 }
 
 int dpgo::download_sums_public(dpgo_hip_problem h, std::vector<double>& out) {

@@ -196,7 +196,7 @@ struct GEdges {
   const double* t;       // [d]
   const double* kappa;
   const double* tau;
-  const double* w;
+  const double* w;       // per entry weight, or null: 1
 };
 
 // The exact preconditioner's supernodal factor on the device (chol_internal.h: per supernode the panel

@@ -404,6 +404,11 @@ __device__ __forceinline__ void spmm_accumulate(const QView& q, const double* __
 // leaves HBM at full occupancy-independent MLP instead of one dependent miss per incidence.
 // Tiles whose lists do not fit fall back to global loads.
 constexpr int kIncStage = 512;
+// round 5's SpMM prologue: tile descriptors (LaunchCtx::tile_meta) and the stage loads issued together
+#ifndef DPGO_STAGE_V5
+#define DPGO_STAGE_V5 1
+#endif
+constexpr bool kStageV5 = DPGO_STAGE_V5 != 0;
 #ifndef DPGO_BUFFER_GATHER
 #define DPGO_BUFFER_GATHER 1
 #endif
@@ -1439,7 +1444,7 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
   constexpr bool kStageFmt = FMT == QFMT_EDGES && !(MODE == MODE_F || MODE == MODE_QF) &&
                              !(mode_hess(MODE) && evar_sv(VAR));
   const bool skip = tile_skipped(c, p.agent);
-  const bool late_skip = kStageFmt && c.tile_meta != nullptr;
+  const bool late_skip = kStageFmt && kStageV5 && c.tile_meta != nullptr;
   if (skip && !late_skip) {
     if constexpr (spmm_fusable(MODE)) spmm_arrive(args, p.agent);
     return;
@@ -1540,6 +1545,15 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
           const f64x2 v = src[x];
           s_recd[(ns + rr) * RS + 2 * w] = v.x;
           s_recd[(ns + rr) * RS + 2 * w + 1] = v.y;
+        }
+      } else if constexpr (!kStageV5) {  // round 4's stage loop (A/B builds only, -DDPGO_STAGE_V5=0)
+        for (int x = threadIdx.x; x < ni; x += kThreads) s_inc[x] = q.inc[i0 + x];
+        const f64x2* src = reinterpret_cast<const f64x2*>(q.rec) + static_cast<long>(e0) * (RW / 2);
+        for (int x = threadIdx.x; x < ne * (RW / 2); x += kThreads) {
+          const int rr = x / (RW / 2), w = x - rr * (RW / 2);
+          const f64x2 v = src[x];
+          s_recd[rr * RS + 2 * w] = v.x;
+          s_recd[rr * RS + 2 * w + 1] = v.y;
         }
       } else {
         // two phases: every stage load of the thread in flight at once, then the LDS writes (a load / wait / write
@@ -4013,7 +4027,8 @@ __global__ __launch_bounds__(kThreads) void k_assemble_G(GEdges e, int nslots, c
 #pragma unroll
     for (int v = 0; v < D; ++v) Y[v] = P[v * R + a];
     p = P[D * R + a];
-    const double k = e.w[q] * e.kappa[q], ta = e.w[q] * e.tau[q];
+    const double wq = e.w != nullptr ? e.w[q] : 1.0;  // null: unit weights (the central evaluation)
+    const double k = wq * e.kappa[q], ta = wq * e.tau[q];
     const double* Rm = e.R + static_cast<long>(q) * D * D;  // row-major
     const double* tv = e.t + static_cast<long>(q) * D;
     if (e.outgoing[q]) {

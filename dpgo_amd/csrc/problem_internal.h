@@ -123,7 +123,11 @@ struct dpgo_hip_problem_s {
   };
   std::vector<SnLevel> sn_levels;  // index = depth (0 = the roots)
   long chol_doubles = 0;
-  dpgo::DevBuf<int4> tile_meta;  // edge-stream Q: per tile stage ranges (LaunchCtx::tile_meta); empty otherwise
+  dpgo::DevBuf<int4> tile_meta;
+  // edge-stream records and diagonal blocks at unit weights (kept by the engine under a robust cost): the central
+  // evaluation of examples/MultiRobotExample.cpp:229-235 reads the dataset's Q, not the reweighted one
+  dpgo::DevBuf<double> rec_unit, diag_unit;
+  bool central_unit = false;  // qview() serves rec_unit / diag_unit  // edge-stream Q: per tile stage ranges (LaunchCtx::tile_meta); empty otherwise
   long sn_nodes = 0;             // supernodes of the current symbolic structure (sn_s may be larger: capacity)
   double chol_flops = 0.0;       // the factorisation's classic flop count: sum over supernodes s^3/3 + s^2 t + s t^2
   double chol_inv_flops = 0.0;   // the panels' extra: L_SS^-1 (s^3/3) and L_RS L_SS^-1 (s^2 t) per supernode
@@ -226,6 +230,9 @@ int optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params, const
 // f / |grad|^2 / <G, X> per agent at X into the handle's sums (OP_SUM, nq 3): asynchronous
 bool merged_split(dpgo_hip_problem h);  // TUNE_SPLIT_STREAMS applies to this batch (capi.cpp)
 int eval_sums_dev(dpgo_hip_problem h, const double* X);
+// the same with the edge-stream Q at unit weights (keep_unit_q: the copy taken before any reweighting)
+int eval_sums_unit_dev(dpgo_hip_problem h, const double* X);
+int keep_unit_q(dpgo_hip_problem h);
 // copy the per-agent sums (4 per agent) to the host (synchronises)
 int download_sums_public(dpgo_hip_problem h, std::vector<double>& out);
 // X.Q launch with the handle's optional event timing

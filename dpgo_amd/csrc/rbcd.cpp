@@ -182,11 +182,12 @@ int copy_poses(dpgo_rbcd e, double* dst, const double* src, long first_pose, lon
 // constructGMatrix (src/PGOAgent.cpp:783-859) for colour c from in-place neighbours (X) and received
 // ones (Rx).  In-place neighbours are never in colour c, so they ran iterate(false) this iteration
 // and their aux pose equals X (see dpgo_rbcd_pre_exchange): X serves both dictionaries.
-int assemble_G(dpgo_rbcd e, int c, const double* Rx) {
+int assemble_G(dpgo_rbcd e, int c, const double* Rx, bool unit_weights = false) {
   dpgo_hip_problem h = e->prob[c];
   if (!h || e->gt[c]->nslots == 0) return DPGO_HIP_OK;
   auto* t = e->gt[c];
-  GEdges ge{t->slot_off.p, t->src.p, t->outgoing.p, t->R.p, t->t.p, t->kappa.p, t->tau.p, t->w.p};
+  GEdges ge{t->slot_off.p, t->src.p, t->outgoing.p, t->R.p, t->t.p, t->kappa.p, t->tau.p,
+            unit_weights ? nullptr : t->w.p};
   HIP_TRY(launch_assemble_G(e->r, e->b, ge, t->nslots, e->X.p, Rx, h->gblk.p, e->stream));
   // per entry: neighbour pose + measurement (R, t, kappa, tau, w, src, outgoing); per slot: G block
   const double d = e->d;
@@ -673,6 +674,7 @@ int dpgo_rbcd_create(dpgo_graph g, int num_agents, const int* agent_of_pose, con
       if (rc != DPGO_HIP_OK) return bail(rc);
     }
     rc = problem_ready(h);  // uploads Q, block-Jacobi inverses, G slot map
+    if (rc == DPGO_HIP_OK && e->P.robust_cost != DPGO_ROBUST_L2) rc = keep_unit_q(h);  // the central evaluation's Q
     if (rc != DPGO_HIP_OK) return bail(rc);
     auto* t = e->gt[c];
     t->nslots = static_cast<int>(slot_off.size()) - 1;
@@ -1029,11 +1031,17 @@ int dpgo_rbcd_central_eval(dpgo_rbcd e, const double* recv_dev, double* f_out, d
     HIP_TRY(launch_gather_poses(static_cast<int>(e->n_recv_poses), static_cast<int>(e->rb()), e->unpack_x.p, recv_dev,
                                 recv_dev, e->RXc.p, e->stream));
   }
-  // per colour: G from the current neighbour poses, then f / |P_X(XQ + G)|^2 / <G, X> per agent
+  // per colour: G from the current neighbour poses, then f / |P_X(XQ + G)|^2 / <G, X> per agent.  The example's
+  // central evaluation uses the dataset's Q (QCentral, unit weights): under a robust cost the reweighted colour
+  // problems evaluate on their unit-weight copy of Q and G is assembled with unit weights.
+  const bool unit = e->P.robust_cost != DPGO_ROBUST_L2;
   for (int c = 0; c < e->ncolors; ++c) {
     if (!e->prob[c]) continue;
-    DPGO_TRY(assemble_G(e, c, e->RXc.p));
-    DPGO_TRY(eval_sums_dev(e->prob[c], color_ptr(e, e->X, c)));
+    DPGO_TRY(assemble_G(e, c, e->RXc.p, unit));
+    if (unit)
+      DPGO_TRY(eval_sums_unit_dev(e->prob[c], color_ptr(e, e->X, c)));
+    else
+      DPGO_TRY(eval_sums_dev(e->prob[c], color_ptr(e, e->X, c)));
   }
   double f = 0.0;
   if (gradnorm_sq)

@@ -194,7 +194,8 @@ int dpgo_rbcd_bench_hvp(dpgo_rbcd e, int color, int reps, double* ms);
 int dpgo_rbcd_counters(dpgo_rbcd e, long long* agent_updates, long long* iterations);
 
 /* Central evaluation (examples/MultiRobotExample.cpp:229-235): this rank's share of the whole-graph
- * cost f(X) = 1/2 <X Q, X> (sum over ranks = the central cost; with robust costs the current weights)
+ * cost f(X) = 1/2 <X Q, X> (sum over ranks = the central cost; Q is the dataset's, unit weights, as the
+ * example's QCentral -- with a robust cost the reweighted Q of the solve is not what is evaluated)
  * and, per owned agent, |RieGrad|^2 of its block (the greedy selection / stop test, :243-256).
  * Call between iterations; recv_dev: the public poses of a dpgo_rbcd_pack + exchange done after the
  * last update (required when world > 1).  gradnorm_sq[num_agents]: 0 for agents of other ranks.
