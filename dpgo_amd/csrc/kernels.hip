@@ -580,6 +580,11 @@ __device__ __forceinline__ void edge_loop_rot(const QView& q, const double* __re
 // sums are bitwise theirs.  A record whose id is below the tile's first-visit range (a second visit) is read
 // from HBM / L2, the others from the LDS stage; one two-stage pipeline instead of one per record source, so only
 // the pose's first gather waits a full memory latency.
+#ifndef DPGO_UNI_UNROLLED
+#define DPGO_UNI_UNROLLED 1
+#endif
+constexpr bool kUniUnrolled = DPGO_UNI_UNROLLED != 0;
+constexpr int kUniMax = 8;  // incidences per pose handled straight-line (a 3D lattice pose has at most 6)
 template <int R>
 __device__ __forceinline__ void edge_loop_uni(const QView& q, const double* __restrict__ in, int kc, int a0, int L1,
                                               int b0, int L2, const int2* s_inc, int i0, const double* s_rec, int e0,
@@ -616,6 +621,22 @@ __device__ __forceinline__ void edge_loop_uni(const QView& q, const double* __re
       for (int s = 0; s < B; ++s) acc[a][s] = fma(-st.x[a], st.m[s], acc[a][s]);
   };
   if (n <= 0) return;
+  if (kUniUnrolled && n <= kUniMax) {
+    // Straight-line for the usual degrees: every stage its own registers, each written once and read once.  In the
+    // two-stage loop the fetch into the reused stage is a phi of its LDS and global branches, and the register
+    // allocator copies it at the back edge -- a copy that waits for the next incidence's record loads, so the
+    // second-visit gathers never overlapped the loop's FMAs.
+    Stage st[kUniMax];
+    fetch(0, st[0]);
+#pragma unroll
+    for (int q = 0; q < kUniMax; ++q) {
+      if (q + 1 < kUniMax) {
+        if (q + 1 < n) fetch(q + 1, st[q + 1 < kUniMax ? q + 1 : q]);
+      }
+      if (q < n) consume(st[q]);
+    }
+    return;
+  }
   Stage sa, sb;
   fetch(0, sa);
   int p = 0;
