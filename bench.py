@@ -631,6 +631,10 @@ def main():
             eta = 1e-6 * abs(c["f_relax"]) / max(g.n, 1)
             c["eta"] = eta
             c["certified"] = bool(c["lower_bound"] >= -eta)
+            # the bound takes theta_C as the complement's lowest eigenvalue (Ritz value minus its
+            # residual); a thick-restarted Lanczos from one random start could in principle miss a lower one
+            c["certified_assumes"] = ("theta_C (thick-restarted Lanczos, one seeded random start) is the lowest "
+                                      "eigenvalue of the complement block; a missed lower eigenvalue voids the bound")
             out["certificate"] = c
     if args.boundary_leg:
         # The same engine and step from the odometry chain (no burn-in): every update's tCG stops at its

@@ -453,9 +453,9 @@ int chol_threads(int K) {
 int device_factor(dpgo_hip_problem h) {
   const int maxd = static_cast<int>(h->fac_level_off.size()) - 2;
   HIP_TRY(hipMemsetAsync(h->fac_not_pd.p, 0, sizeof(int), h->stream));
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  HIP_TRY(hipEventCreate(&e0));
-  HIP_TRY(hipEventCreate(&e1));
+  for (auto& ev : h->fac_ev)
+    if (!ev) HIP_TRY(hipEventCreate(&ev));  // owned by the handle: no leak on an early error return
+  hipEvent_t e0 = h->fac_ev[0], e1 = h->fac_ev[1];
   HIP_TRY(hipEventRecord(e0, h->stream));
   const bool verbose = std::getenv("DPGO_VERBOSE_CHOL") != nullptr;
   std::vector<hipEvent_t> lev(verbose ? maxd + 2 : 0, nullptr);
@@ -482,8 +482,6 @@ int device_factor(dpgo_hip_problem h) {
   HIP_TRY(hipStreamSynchronize(h->stream));
   float ms = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   h->chol_factor_ms = ms;
   h->chol_factor_count += 1;
   if (verbose) {

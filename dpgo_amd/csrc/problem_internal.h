@@ -197,7 +197,10 @@ struct dpgo_hip_problem_s {
   double timed_ms[dpgo::kSpmmModes] = {};
   long long timed_n[dpgo::kSpmmModes] = {};
   double timed_frac[dpgo::kSpmmModes] = {};  // summed TimedLaunch::frac: full-batch launch equivalents
+  hipEvent_t fac_ev[2] = {nullptr, nullptr};  // the device factorisation's timing (created once per handle)
   ~dpgo_hip_problem_s() {
+    for (auto e : fac_ev)
+      if (e) (void)hipEventDestroy(e);
     for (auto& t : timed) {
       (void)hipEventDestroy(t.a);
       (void)hipEventDestroy(t.b);
