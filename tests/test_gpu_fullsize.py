@@ -131,33 +131,43 @@ def test_c4_exact_precon_cpu_parity(hip, accel):
     """C4 (110,592 poses, 64 agents of 12^3) with the reference's default preconditioner: the engine's supernodal
     factor of Q + 0.1 I (nested-dissection tree on the host, numeric factorisation and panel sweeps on the device)
     against oracle/cpu's independent exact mode (reverse Cuthill-McKee envelope Cholesky on the host,
-    tests/test_host_native.py pins it to the numpy oracle's sparse LU): 36 colour iterations from the multi-robot
-    initialisation (with Nesterov: through the restart at iteration 29), X to 1e-9, Runs and tCG iterations per
-    agent equal."""
+    tests/test_host_native.py pins it to the numpy oracle's sparse LU), in lockstep over 36 colour iterations from the
+    multi-robot initialisation (with Nesterov: through the restart at iteration 29).  Every agent's Run and tCG
+    counters are equal after every iteration, and X agrees to 1e-12 through iteration 12.  Later the trajectory itself
+    amplifies rounding (~1.75x per iteration without acceleration: a smooth geometric rise with identical solver
+    decisions, profiles/r05b_exact_probe_c4.log), so the final bar is derived like the trace tests': max(1e-9, 10 x the
+    distance between two runs of the port itself whose starting points differ by 1e-15 relative)."""
     g, aop, X0 = _setup(hip, 48)
     e = _engine(hip, g, aop, accel, exact=True)
     e.set_X(X0)
+    cpu = _cpu(g, aop, accel, exact=True)
+    cpu.set_X(X0)
     iters = 36
+    Xg = np.zeros(X0.size)
     for it in range(iters):
         e.pre_exchange(it % e.num_colors)
         e.update(it % e.num_colors, None)
-    Xg = np.zeros(X0.size)
-    e.get_X_into(Xg)
-    cpu = _cpu(g, aop, accel, exact=True)
-    cpu.set_X(X0)
-    for _ in range(iters):
         cpu.iterate(threads=16)
-    err = rel(Xg, cpu.get_X())
-    print(f"C4 exact accel={accel}: |X_gpu - X_cpu| / |X| = {err:.2e}")
-    assert err <= 1e-9
-    st_g, st_c = e.stats()[:, :10], cpu.stats()
-    assert np.array_equal(st_g[:, 2:4], st_c[:, 2:4])
-    assert st_c[:, 3].sum() > st_c[:, 2].sum()  # CG steps beyond the first were taken
+        assert np.array_equal(e.stats()[:, 2:4], cpu.stats()[:, 2:4]), it  # Runs and tCG iterations per agent
+        if it == 12:
+            e.get_X_into(Xg)
+            assert rel(Xg, cpu.get_X()) <= 1e-12, (it, rel(Xg, cpu.get_X()))
+    e.get_X_into(Xg)
+    Xc = cpu.get_X()
+    err = rel(Xg, Xc)
+    twin = _cpu(g, aop, accel, exact=True)  # the trajectory's own amplification of a 1e-15 difference
+    twin.set_X(X0 * (1.0 + 1e-15 * np.random.default_rng(1).standard_normal(X0.size)))
+    for _ in range(iters):
+        twin.iterate(threads=16)
+    floor = rel(twin.get_X(), Xc)
+    print(f"C4 exact accel={accel}: |X_gpu - X_cpu| / |X| = {err:.2e}, port vs its 1e-15-perturbed twin {floor:.2e}")
+    assert err <= max(1e-9, 10.0 * floor)
+    assert cpu.stats()[:, 3].sum() > cpu.stats()[:, 2].sum()  # CG steps beyond the first were taken
     bj = _cpu(g, aop, accel)  # and the preconditioner matters on this trajectory
     bj.set_X(X0)
     for _ in range(iters):
         bj.iterate(threads=16)
-    assert rel(bj.get_X(), cpu.get_X()) > 1e-6
+    assert rel(bj.get_X(), Xc) > 1e-6
 
 
 def test_c4_gnc_default_cadence(hip):
