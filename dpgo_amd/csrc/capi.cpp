@@ -644,23 +644,39 @@ int sync_chol(dpgo_hip_problem h) {
           for (int blk = 0; blk * dpgo::kThreads < rows; ++blk) items.push_back(make_int2(g, blk));
         }
     L.asm_n = static_cast<int>(items.size()) - L.asm0;
+    // The sweeps' work items, longest first: a workgroup streams one row (forward: min(I + 1, ns) tiles) or one
+    // column (backward: nI - J tiles) of a panel, and a level's launch lasts as long as its last workgroup, so the
+    // long rows of the separators start first instead of last (their order changes no result: every item writes
+    // its own rows).
+    auto push_sorted = [&](std::vector<std::pair<int, int2>>& w) {
+      std::stable_sort(w.begin(), w.end(), [](const std::pair<int, int2>& x, const std::pair<int, int2>& y) {
+        return x.first > y.first;
+      });
+      for (const auto& e : w) items.push_back(e.second);
+    };
+    std::vector<std::pair<int, int2>> work;
     L.fwd0 = static_cast<int>(items.size());
     for (int a = 0; a < K; ++a)
       for (size_t x = 0; x < Fs[a].nodes.size(); ++x)
         if (Fs[a].nodes[x].depth == dep) {
           const int g = base[a] + static_cast<int>(x);
+          const int ns = dpgo::sn_pad(s_[g] * b) / dpgo::kSnTile;
           const int nI = (dpgo::sn_pad(s_[g] * b) + dpgo::sn_pad(t_[g] * b)) / dpgo::kSnTile;
-          for (int I = 0; I < nI; ++I) items.push_back(make_int2(g, I));
+          for (int I = 0; I < nI; ++I) work.push_back({std::min(I + 1, ns), make_int2(g, I)});
         }
+    push_sorted(work);
     L.fwd_n = static_cast<int>(items.size()) - L.fwd0;
     L.bwd0 = static_cast<int>(items.size());
+    work.clear();
     for (int a = 0; a < K; ++a)
       for (size_t x = 0; x < Fs[a].nodes.size(); ++x)
         if (Fs[a].nodes[x].depth == dep) {
           const int g = base[a] + static_cast<int>(x);
           const int nJ = dpgo::sn_pad(s_[g] * b) / dpgo::kSnTile;
-          for (int J = 0; J < nJ; ++J) items.push_back(make_int2(g, J));
+          const int nI = (dpgo::sn_pad(s_[g] * b) + dpgo::sn_pad(t_[g] * b)) / dpgo::kSnTile;
+          for (int J = 0; J < nJ; ++J) work.push_back({nI - J, make_int2(g, J)});
         }
+    push_sorted(work);
     L.bwd_n = static_cast<int>(items.size()) - L.bwd0;
   }
   // ---- upload
