@@ -307,8 +307,9 @@ enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH =
                                        // device (k_sn_factor), 0 on the host (chol.cpp, panels uploaded)
                TUNE_SPMM_V2 = 11,  // > 0: the merged partials at kMergedDdSlots (edge variant bit 6) and the rotated
                                    //    accumulator (bit 7) in every mode (1), in none (2), in the merged modes (3);
-                                   //    4 (default): 3 + one edge-loop pipeline per pose in the merged modes (bit 8);
-                                   //    5: rotated + one pipeline in every mode; 0: the round-3 kernels
+                                   //    4: 3 + one edge-loop pipeline per pose in the merged modes (bit 8);
+                                   //    5: rotated + one pipeline in every mode; 6 (default since round 5): 5 but the
+                                   //    half passes (F, QF) plain; 0: the round-3 kernels
                TUNE_COUNT = 13 };
 // dd_mask of the merged tCG partials for the kernel a handle with these tuning keys and Q format runs
 inline int merged_dd_mask(int fmt, const int* tuning) {

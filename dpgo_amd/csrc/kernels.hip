@@ -4115,7 +4115,7 @@ template <int MODE>
 hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const SpmmArgs& a);
 
 #ifndef DPGO_SPMM_TU
-int g_tuning[TUNE_COUNT] = {0, -1, 1, 0, 0, 0, 0, 0, 0, 0, 1, 4, 1};
+int g_tuning[TUNE_COUNT] = {0, -1, 1, 0, 0, 0, 0, 0, 0, 0, 1, 6, 1};
 
 bool supported_rb(int r, int b) {
   if (b == 3) return r >= 2 && r <= 8;
@@ -4162,8 +4162,11 @@ hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q
       // tuning key; the rotated accumulator (bit 7, bitwise the plain one) at the headline shape: v2 = 1 every
       // mode, 2 none, 3 the merged modes only
       constexpr int V2 = kEdgeDefaultVariant | (mode_merged(MODE) ? 64 : 0);
-      const bool rot = v2 == 1 || v2 == 5 || ((v2 == 3 || v2 == 4) && mode_merged(MODE));
-      const bool uni = v2 == 5 || (v2 == 4 && mode_merged(MODE));
+      // 6 (default): rotated + one pipeline in every mode that stages its records (X.Q, EVAL_TCG, HESS*; the half
+      // passes F / QF keep the plain accumulator: rotated measured +3.6 us on F, profiles/r05c_ab_v2.log)
+      constexpr bool kHalfMode = MODE == MODE_F || MODE == MODE_QF;
+      const bool rot = v2 == 1 || v2 == 5 || (v2 == 6 && !kHalfMode) || ((v2 == 3 || v2 == 4) && mode_merged(MODE));
+      const bool uni = v2 == 5 || (v2 == 6 && !kHalfMode) || (v2 == 4 && mode_merged(MODE));
       if (uni && r == 5 && b == 4) {
         if constexpr (kPreMode) {
           if (q.tuning[TUNE_EPI_PREFETCH] > 0) {
