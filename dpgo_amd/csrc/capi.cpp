@@ -505,6 +505,12 @@ int device_factor(dpgo_hip_problem h) {
   return DPGO_HIP_OK;
 }
 
+// DPGO_SN_ITEM_ORDER=0: the sweeps' items in node / tile order (round 4), for A/B runs (tools/sweep_ab.py)
+bool sn_longest_first() {
+  const char* v = std::getenv("DPGO_SN_ITEM_ORDER");
+  return !(v && v[0] == '0');
+}
+
 int sync_chol(dpgo_hip_problem h) {
   if (h->chol_state != 0) return DPGO_HIP_OK;
   bool edges = true;
@@ -649,9 +655,10 @@ int sync_chol(dpgo_hip_problem h) {
     // long rows of the separators start first instead of last (their order changes no result: every item writes
     // its own rows).
     auto push_sorted = [&](std::vector<std::pair<int, int2>>& w) {
-      std::stable_sort(w.begin(), w.end(), [](const std::pair<int, int2>& x, const std::pair<int, int2>& y) {
-        return x.first > y.first;
-      });
+      if (sn_longest_first())
+        std::stable_sort(w.begin(), w.end(), [](const std::pair<int, int2>& x, const std::pair<int, int2>& y) {
+          return x.first > y.first;
+        });
       for (const auto& e : w) items.push_back(e.second);
     };
     std::vector<std::pair<int, int2>> work;

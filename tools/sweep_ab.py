@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""A/B of the exact preconditioner's sweep work-item order (DPGO_SN_ITEM_ORDER: 1 longest-first, 0 node / tile order):
+two engines on the same grid, one per order, standalone full applications over colour 0 alternated between them
+(dpgo_rbcd_bench_precond, HIP events).  Prints one JSON line.  A/B probe only."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--k", type=int, default=100)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    from dpgo_amd import hip as H
+    g = H.Graph.grid3d(a.k, seed=0)
+    aop = g.grid_partition(4)
+    X0 = g.chain_init_dev_layout(5, H.lifting_matrix(3, 5))
+    engs = {}
+    for order in ("1", "0"):
+        os.environ["DPGO_SN_ITEM_ORDER"] = order
+        e = H.Rbcd(g, aop, np.zeros(64, np.int32), 0, 1, H.rbcd_params(r=5, acceleration=1, precon=H.PRECON_EXACT))
+        e.set_X(X0)
+        e.pre_exchange(0)
+        e.update(0, None)  # builds colour 0's factor with this order
+        engs[order] = e
+    res = {o: {"fwd": [], "bwd": []} for o in engs}
+    pb = 0.0
+    for _ in range(a.rounds):
+        for o, e in engs.items():
+            f, b, pb = e.bench_precond(0, a.reps)
+            res[o]["fwd"].append(f)
+            res[o]["bwd"].append(b)
+    out = {o: {k: float(np.median(v)) for k, v in d.items()} for o, d in res.items()}
+    for o in out:
+        out[o]["fwd_GBps"] = pb / (out[o]["fwd"] * 1e-3) / 1e9
+        out[o]["bwd_GBps"] = pb / (out[o]["bwd"] * 1e-3) / 1e9
+    print(json.dumps({"k": a.k, "panel_bytes": pb, "ms": out}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
