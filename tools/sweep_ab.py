@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A/B of the exact preconditioner's sweep work-item order (DPGO_SN_ITEM_ORDER: 1 longest-first, 0 node / tile order):
+"""A/B of the exact preconditioner's sweep work-item orders (DPGO_SN_ITEM_ORDER, SWEEP_ORDERS="2,0" by default):
 two engines on the same grid, one per order, standalone full applications over colour 0 alternated between them
 (dpgo_rbcd_bench_precond, HIP events).  Prints one JSON line.  A/B probe only."""
 import argparse
@@ -23,7 +23,7 @@ def main():
     aop = g.grid_partition(4)
     X0 = g.chain_init_dev_layout(5, H.lifting_matrix(3, 5))
     engs = {}
-    for order in ("1", "0"):
+    for order in [o for o in os.environ.get("SWEEP_ORDERS", "2,0").split(",")]:
         os.environ["DPGO_SN_ITEM_ORDER"] = order
         e = H.Rbcd(g, aop, np.zeros(64, np.int32), 0, 1, H.rbcd_params(r=5, acceleration=1, precon=H.PRECON_EXACT))
         e.set_X(X0)
