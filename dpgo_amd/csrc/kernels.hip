@@ -437,7 +437,10 @@ __host__ __device__ constexpr int minv_index(int u, int v) { return sym_index<B>
 // drains in-flight global loads).  REC_LDS: records from the LDS stage (id - e0), else global.
 // LDS stride of a staged edge record: one double of padding, so the records the 16 poses of a wave read at
 // once start on different banks (a 128-byte stride put all of them on two bank offsets: 4-way conflicts)
-__host__ __device__ constexpr int lds_rec_stride(int b) { return edge_rec_width(b - 1) + 1; }
+#ifndef DPGO_LDS_REC_PAD
+#define DPGO_LDS_REC_PAD 1
+#endif
+__host__ __device__ constexpr int lds_rec_stride(int b) { return edge_rec_width(b - 1) + DPGO_LDS_REC_PAD; }
 
 // Raw buffer loads for the edge loop's gathers.  They are intrinsic calls, not IR loads: plain loads feeding
 // the loop-carried register stage are folded by the optimizer into ONE load of a phi of the two addresses,
@@ -4151,6 +4154,13 @@ hipError_t spmm_variant54(int var, dim3 grid, const LaunchCtx& c, const QView& q
 #define DPGO_UNI_WAVES 0
 #endif
 constexpr int kUniWaves = DPGO_UNI_WAVES & 6;
+// occupancy hint of the X.Q kernel (A/B builds: -DDPGO_XQ_WAVES=6 asks for 6 waves per SIMD)
+#ifndef DPGO_XQ_WAVES
+#define DPGO_XQ_WAVES 0
+#endif
+constexpr int kXqWaves = DPGO_XQ_WAVES & 6;
+template <int MODE>
+constexpr int mode_waves() { return MODE == MODE_HESS_M ? kUniWaves : MODE == MODE_XQ ? kXqWaves : 0; }
 
 template <int MODE>
 hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q, const SpmmArgs& a) {
@@ -4170,11 +4180,11 @@ hipError_t spmm_mode(int r, int b, dim3 grid, const LaunchCtx& c, const QView& q
       if (uni && r == 5 && b == 4) {
         if constexpr (kPreMode) {
           if (q.tuning[TUNE_EPI_PREFETCH] > 0) {
-            k_spmm<5, 4, MODE, V2 | (MODE == MODE_HESS_M ? kUniWaves : 0) | 8 | 128 | 256, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+            k_spmm<5, 4, MODE, V2 | mode_waves<MODE>() | 8 | 128 | 256, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
             return hipSuccess;
           }
         }
-        k_spmm<5, 4, MODE, V2 | (MODE == MODE_HESS_M ? kUniWaves : 0) | 128 | 256, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
+        k_spmm<5, 4, MODE, V2 | mode_waves<MODE>() | 128 | 256, QFMT_EDGES><<<grid, kThreads, 0, c.stream>>>(c, q, a);
         return hipSuccess;
       }
       if (r == 5 && b == 4 && (q.tuning[TUNE_EDGE_VARIANT] < 0 || mode_merged(MODE))) {
