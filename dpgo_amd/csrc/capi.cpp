@@ -505,13 +505,6 @@ int device_factor(dpgo_hip_problem h) {
   return DPGO_HIP_OK;
 }
 
-// The sweeps' item order (DPGO_SN_ITEM_ORDER, A/B runs: tools/sweep_ab.py): 0 node / tile order (round 4); 1 every
-// level's items longest first; 2 (default) node order, each node's forward rows last to first
-int sn_item_order() {
-  const char* v = std::getenv("DPGO_SN_ITEM_ORDER");
-  return v && (v[0] == '0' || v[0] == '1') ? v[0] - '0' : 2;
-}
-
 int sync_chol(dpgo_hip_problem h) {
   if (h->chol_state != 0) return DPGO_HIP_OK;
   bool edges = true;
@@ -651,50 +644,26 @@ int sync_chol(dpgo_hip_problem h) {
           for (int blk = 0; blk * dpgo::kThreads < rows; ++blk) items.push_back(make_int2(g, blk));
         }
     L.asm_n = static_cast<int>(items.size()) - L.asm0;
-    // The sweeps' work items: a workgroup streams one row (forward: min(I + 1, ns) tiles) or one column (backward:
-    // nI - J tiles) of a panel, and a level's launch lasts as long as its last workgroup, so a node's long rows should
-    // start first; a global longest-first sort lost the forward sweep's locality (4.05 vs 3.86 ms per application at
-    // C5, profiles/r05e_sweep_ab.log).  The order changes no result: every item writes its own rows.
-    const int order = sn_item_order();
-    auto push_sorted = [&](std::vector<std::pair<int, int2>>& w, bool fwd) {
-      if (order == 1) {
-        std::stable_sort(w.begin(), w.end(), [](const std::pair<int, int2>& x, const std::pair<int, int2>& y) {
-          return x.first > y.first;
-        });
-      } else if (order == 2 && fwd) {  // per node, its rows last to first (the longest first), nodes in order
-        size_t i = 0;
-        while (i < w.size()) {
-          size_t j = i;
-          while (j < w.size() && w[j].second.x == w[i].second.x) ++j;
-          std::reverse(w.begin() + static_cast<long>(i), w.begin() + static_cast<long>(j));
-          i = j;
-        }
-      }
-      for (const auto& e : w) items.push_back(e.second);
-    };
-    std::vector<std::pair<int, int2>> work;
+    // The sweeps' work items, nodes in order: forward one per row tile I of a node (it streams the row's
+    // min(I + 1, ns) tiles), backward one per column tile J (nI - J tiles).  (Runs of a narrow node's row tiles in
+    // one workgroup measured slower: 3.76 vs 3.48 ms per C5 forward sweep.)
     L.fwd0 = static_cast<int>(items.size());
     for (int a = 0; a < K; ++a)
       for (size_t x = 0; x < Fs[a].nodes.size(); ++x)
         if (Fs[a].nodes[x].depth == dep) {
           const int g = base[a] + static_cast<int>(x);
-          const int ns = dpgo::sn_pad(s_[g] * b) / dpgo::kSnTile;
           const int nI = (dpgo::sn_pad(s_[g] * b) + dpgo::sn_pad(t_[g] * b)) / dpgo::kSnTile;
-          for (int I = 0; I < nI; ++I) work.push_back({std::min(I + 1, ns), make_int2(g, I)});
+          for (int I = 0; I < nI; ++I) items.push_back(make_int2(g, I));
         }
-    push_sorted(work, true);
     L.fwd_n = static_cast<int>(items.size()) - L.fwd0;
     L.bwd0 = static_cast<int>(items.size());
-    work.clear();
     for (int a = 0; a < K; ++a)
       for (size_t x = 0; x < Fs[a].nodes.size(); ++x)
         if (Fs[a].nodes[x].depth == dep) {
           const int g = base[a] + static_cast<int>(x);
           const int nJ = dpgo::sn_pad(s_[g] * b) / dpgo::kSnTile;
-          const int nI = (dpgo::sn_pad(s_[g] * b) + dpgo::sn_pad(t_[g] * b)) / dpgo::kSnTile;
-          for (int J = 0; J < nJ; ++J) work.push_back({nI - J, make_int2(g, J)});
+          for (int J = 0; J < nJ; ++J) items.push_back(make_int2(g, J));
         }
-    push_sorted(work, false);
     L.bwd_n = static_cast<int>(items.size()) - L.bwd0;
   }
   // ---- upload

@@ -3271,21 +3271,33 @@ constexpr int kSnVecRegs = (kSnTileDev * 8 + kThreads - 1) / kThreads;  // enoug
 template <int R>
 __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __restrict__ items, int b,
                                                      double* __restrict__ y) {
-  __shared__ double sf[3][kSnTileDev * R];  // triple-buffered frontal chunks
+  __shared__ double sfl[4 * kSnTileDev * R];  // triple-buffered frontal chunks, then the row tile's f rows (f_R)
+  __shared__ int spz[kSnTileDev];                // the row tile's pose ids (S rows)
   const int2 it = items[blockIdx.x];
   if (v.node_agent && agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x])) return;
+  constexpr int kTileD = kSnTileDev * kSnTileDev, kChunk = kSnTileDev * R;
+  double (*sf)[kChunk] = reinterpret_cast<double (*)[kChunk]>(sfl);
+  double* __restrict__ sfr = sfl + 3 * kChunk;
   const int node = it.x, I = it.y;
   const int s = v.s[node], t = v.t[node], sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), ns = Sp / kSnTileDev;
   const double* __restrict__ f = v.F + v.f_off[node];
   const double* __restrict__ panel = v.panel + v.panel_off[node];
+  const int* __restrict__ pz = v.poses + v.poses_off[node];
   const int tid = static_cast<int>(threadIdx.x), rq = tid >> 4, cq = tid & 15;
+  // the epilogue's operands (the S rows' pose ids, or the R rows' f values) staged into LDS with chunk 0: the
+  // workgroup's outputs then wait on no load after the sweep
+  if (I < ns) {
+    const int row = I * kSnTileDev + tid;
+    if (tid < kSnTileDev && row < sb) spz[tid] = pz[row / b];
+  } else {
+    for (int e = tid; e < kChunk; e += kThreads) sfr[e] = f[static_cast<long>(I) * kChunk + e];
+  }
   double acc[4][R];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int a = 0; a < R; ++a) acc[i][a] = 0.0;
   const int nJ = I < ns ? I + 1 : ns;
-  constexpr int kTileD = kSnTileDev * kSnTileDev, kChunk = kSnTileDev * R;
   // software pipeline: tiles J + 1 and J + 2's panel values are loaded into registers and their frontal chunks
   // staged in LDS while tile J is consumed (one barrier per tile)
   double p[4][4], pn[4][4], pm[4][4], fv[kSnVecRegs];
@@ -3363,11 +3375,11 @@ __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __res
     const int row = I * kSnTileDev + rq * 4 + i;
     if (row < sb) {  // y_S
       const int pos = row / b, k = row - pos * b;
-      double* dst = y + (static_cast<long>(v.poses[v.poses_off[node] + pos]) * b + k) * R;
+      double* dst = y + (static_cast<long>(spz[rq * 4 + i]) * b + k) * R;
 #pragma unroll
       for (int a = 0; a < R; ++a) dst[a] = acc[i][a];
     } else if (row >= Sp && row - Sp < tb) {  // update u = f_R - M f_S
-      const double* fr = f + static_cast<long>(row) * R;
+      const double* fr = sfr + (rq * 4 + i) * R;
       double* dst = v.U + v.u_off[node] + static_cast<long>(row - Sp) * R;
 #pragma unroll
       for (int a = 0; a < R; ++a) dst[a] = fr[a] - acc[i][a];

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""A/B of the exact preconditioner's sweep work-item orders (DPGO_SN_ITEM_ORDER, SWEEP_ORDERS="2,0" by default):
-two engines on the same grid, one per order, standalone full applications over colour 0 alternated between them
+"""A/B of the exact preconditioner's sweeps under an environment switch read when the factor is built (SWEEP_ENV
+names it, SWEEP_ORDERS="a,b" its values; unset: one engine, no switch): one engine per value on the same grid, standalone full applications over colour 0 alternated between them
 (dpgo_rbcd_bench_precond, HIP events).  Prints one JSON line.  A/B probe only."""
 import argparse
 import json
@@ -23,8 +23,9 @@ def main():
     aop = g.grid_partition(4)
     X0 = g.chain_init_dev_layout(5, H.lifting_matrix(3, 5))
     engs = {}
-    for order in [o for o in os.environ.get("SWEEP_ORDERS", "2,0").split(",")]:
-        os.environ["DPGO_SN_ITEM_ORDER"] = order
+    for order in [o for o in os.environ.get("SWEEP_ORDERS", "default").split(",")]:
+        if os.environ.get("SWEEP_ENV"):
+            os.environ[os.environ["SWEEP_ENV"]] = order
         e = H.Rbcd(g, aop, np.zeros(64, np.int32), 0, 1, H.rbcd_params(r=5, acceleration=1, precon=H.PRECON_EXACT))
         e.set_X(X0)
         e.pre_exchange(0)
