@@ -588,6 +588,10 @@ __device__ __forceinline__ void edge_loop_rot(const QView& q, const double* __re
 #endif
 constexpr bool kUniUnrolled = DPGO_UNI_UNROLLED != 0;
 constexpr int kUniMax = 8;  // incidences per pose handled straight-line (a 3D lattice pose has at most 6)
+#ifndef DPGO_UNI_AHEAD
+#define DPGO_UNI_AHEAD 1
+#endif
+constexpr int kUniAhead = DPGO_UNI_AHEAD;  // straight-line loop: incidences fetched ahead of the one consumed
 template <int R>
 __device__ __forceinline__ void edge_loop_uni(const QView& q, const double* __restrict__ in, int kc, int a0, int L1,
                                               int b0, int L2, const int2* s_inc, int i0, const double* s_rec, int e0,
@@ -630,11 +634,13 @@ __device__ __forceinline__ void edge_loop_uni(const QView& q, const double* __re
     // allocator copies it at the back edge -- a copy that waits for the next incidence's record loads, so the
     // second-visit gathers never overlapped the loop's FMAs.
     Stage st[kUniMax];
-    fetch(0, st[0]);
+#pragma unroll
+    for (int q = 0; q < kUniAhead; ++q)
+      if (q < n) fetch(q, st[q]);
 #pragma unroll
     for (int q = 0; q < kUniMax; ++q) {
-      if (q + 1 < kUniMax) {
-        if (q + 1 < n) fetch(q + 1, st[q + 1 < kUniMax ? q + 1 : q]);
+      if (q + kUniAhead < kUniMax) {
+        if (q + kUniAhead < n) fetch(q + kUniAhead, st[q + kUniAhead < kUniMax ? q + kUniAhead : q]);
       }
       if (q < n) consume(st[q]);
     }
