@@ -505,6 +505,12 @@ int device_factor(dpgo_hip_problem h) {
   return DPGO_HIP_OK;
 }
 
+// DPGO_SN_FWD_SMALL=0: every forward item through k_sn_fwd (round 4's one kernel per level), for A/B runs
+bool sn_fwd_small_on() {
+  const char* e = std::getenv("DPGO_SN_FWD_SMALL");
+  return !(e && e[0] == '0');
+}
+
 int sync_chol(dpgo_hip_problem h) {
   if (h->chol_state != 0) return DPGO_HIP_OK;
   bool edges = true;
@@ -645,16 +651,32 @@ int sync_chol(dpgo_hip_problem h) {
         }
     L.asm_n = static_cast<int>(items.size()) - L.asm0;
     // The sweeps' work items, nodes in order: forward one per row tile I of a node (it streams the row's
-    // min(I + 1, ns) tiles), backward one per column tile J (nI - J tiles).  (Runs of a narrow node's row tiles in
-    // one workgroup measured slower: 3.76 vs 3.48 ms per C5 forward sweep.)
-    L.fwd0 = static_cast<int>(items.size());
-    for (int a = 0; a < K; ++a)
+    // min(I + 1, ns) tiles) -- on a level of narrow nodes only (ns <= kSnSmallNs) through k_sn_fwd_small, else k_sn_fwd;
+    // backward one per column tile J (nI - J tiles).  (Runs of a narrow node's row tiles in one workgroup measured
+    // slower: 3.76 vs 3.48 ms per C5 forward sweep.)
+    // (a level with both kinds runs every item through k_sn_fwd: a second launch there cost more than the narrow
+    // nodes' items gained, profiles/r05k_levels.txt)
+    bool small = sn_fwd_small_on();
+    for (int a = 0; a < K && small; ++a)
       for (size_t x = 0; x < Fs[a].nodes.size(); ++x)
-        if (Fs[a].nodes[x].depth == dep) {
-          const int g = base[a] + static_cast<int>(x);
-          const int nI = (dpgo::sn_pad(s_[g] * b) + dpgo::sn_pad(t_[g] * b)) / dpgo::kSnTile;
-          for (int I = 0; I < nI; ++I) items.push_back(make_int2(g, I));
+        if (Fs[a].nodes[x].depth == dep && dpgo::sn_pad(s_[base[a] + static_cast<int>(x)] * b) / dpgo::kSnTile > dpgo::kSnSmallNs) {
+          small = false;
+          break;
         }
+    for (int pass = 0; pass < 2; ++pass) {
+      (pass == 0 ? L.fws0 : L.fwd0) = static_cast<int>(items.size());
+      for (int a = 0; a < K; ++a)
+        for (size_t x = 0; x < Fs[a].nodes.size(); ++x)
+          if (Fs[a].nodes[x].depth == dep) {
+            const int g = base[a] + static_cast<int>(x);
+            const int ns = dpgo::sn_pad(s_[g] * b) / dpgo::kSnTile;
+            const bool narrow = small && ns <= dpgo::kSnSmallNs;
+            if (narrow != (pass == 0)) continue;
+            const int nI = (dpgo::sn_pad(s_[g] * b) + dpgo::sn_pad(t_[g] * b)) / dpgo::kSnTile;
+            for (int I = 0; I < nI; ++I) items.push_back(make_int2(g, I));
+          }
+      if (pass == 0) L.fws_n = static_cast<int>(items.size()) - L.fws0;
+    }
     L.fwd_n = static_cast<int>(items.size()) - L.fwd0;
     L.bwd0 = static_cast<int>(items.size());
     for (int a = 0; a < K; ++a)
@@ -898,6 +920,7 @@ int exact_precond(dpgo_hip_problem h, const double* in, double* z_out, double* d
     for (int l = nl - 1; l >= 0; --l) {
       const auto& L = h->sn_levels[l];
       HIP_TRY(dpgo::launch_sn_assemble(h->r, h->b, v, it + L.asm0, L.asm_n, in, h->stream));
+      HIP_TRY(dpgo::launch_sn_fwd_small(h->r, h->b, v, it + L.fws0, L.fws_n, h->tA.p, h->stream));
       HIP_TRY(dpgo::launch_sn_fwd(h->r, h->b, v, it + L.fwd0, L.fwd_n, h->tA.p, h->stream));
     }
     for (int l = 0; l < nl; ++l) {
@@ -2836,6 +2859,7 @@ int dpgo_hip_bench_precond(dpgo_hip_problem h, const double* V_dev, int reps, do
     for (int l = nl - 1; l >= 0; --l) {
       const auto& L = h->sn_levels[l];
       HIP_TRY(dpgo::launch_sn_assemble(h->r, h->b, v, it + L.asm0, L.asm_n, V_dev, h->stream));
+      HIP_TRY(dpgo::launch_sn_fwd_small(h->r, h->b, v, it + L.fws0, L.fws_n, h->tA.p, h->stream));
       HIP_TRY(dpgo::launch_sn_fwd(h->r, h->b, v, it + L.fwd0, L.fwd_n, h->tA.p, h->stream));
     }
     HIP_TRY(hipEventRecord(ev[1], h->stream));

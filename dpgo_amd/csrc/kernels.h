@@ -203,6 +203,7 @@ struct GEdges {
 // [L_SS^-1 ; L_RS L_SS^-1] in kSnTileDev-square tiles), batch-global pose ids.  Frontal vectors F
 // ((S_pad + R_pad) scalar rows x r) and update vectors U (t b rows x r) are work space.
 constexpr int kSnTileDev = 64;
+constexpr int kSnSmallNs = 2;  // k_sn_fwd_small: nodes of at most this many S column tiles
 struct SnView {
   const double* panel;
   const long* panel_off;  // [nodes] first double of the node's panel
@@ -379,6 +380,9 @@ hipError_t launch_finalize(const FinalizeArgs& f, int num_agents, hipStream_t st
 hipError_t launch_sn_assemble(int r, int b, const SnView& v, const int2* items, int count, const double* rhs,
                               hipStream_t stream);
 hipError_t launch_sn_fwd(int r, int b, const SnView& v, const int2* items, int count, double* y, hipStream_t stream);
+// the forward sweep's items of nodes with at most kSnSmallNs S column tiles (k_sn_fwd_small)
+hipError_t launch_sn_fwd_small(int r, int b, const SnView& v, const int2* items, int count, double* y,
+                               hipStream_t stream);
 hipError_t launch_sn_bwd(int r, int b, const SnView& v, const int2* items, int count, const double* y, double* x,
                          hipStream_t stream);
 // numeric factorisation of one tree level's supernodes (count nodes, v.nodes), see SnFactorView

@@ -3393,6 +3393,101 @@ __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __res
   }
 }
 
+// Forward sweep, narrow supernodes (ns <= kSnSmallNs S column tiles: the deep levels' many small separators, whose
+// row tiles are one or two panel tiles long): the same item (node, row tile I), products and order as k_sn_fwd, but
+// with no pipeline to fill -- every load of the workgroup (epilogue operands, the <= 2 frontal chunks, the <= 2
+// tiles) is issued at once and waited for once -- in about half k_sn_fwd's registers, so more workgroups (and bytes)
+// are in flight per CU on the levels where each streams only 32-64 KB.
+#ifndef DPGO_SNF_SMALL_WAVES
+#define DPGO_SNF_SMALL_WAVES 1  // k_sn_fwd_small's occupancy hint (waves per SIMD; 1 = none)
+#endif
+template <int R>
+__global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small(SnView v, const int2* __restrict__ items, int b,
+                                                           double* __restrict__ y) {
+  constexpr int kTileD = kSnTileDev * kSnTileDev, kChunk = kSnTileDev * R;
+  constexpr int KV = (kSnSmallNs * kChunk + kThreads - 1) / kThreads;
+  __shared__ double sf[kSnSmallNs * kChunk];  // frontal chunks 0 .. nJ - 1
+  __shared__ double sfr[kChunk];               // the row tile's f rows (f_R)
+  __shared__ int spz[kSnTileDev];              // the row tile's pose ids (S rows)
+  const int2 it = items[blockIdx.x];
+  if (v.node_agent && agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x])) return;
+  const int node = it.x, I = it.y;
+  const int s = v.s[node], t = v.t[node], sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), ns = Sp / kSnTileDev;
+  const double* __restrict__ f = v.F + v.f_off[node];
+  const double* __restrict__ panel = v.panel + v.panel_off[node];
+  const int* __restrict__ pz = v.poses + v.poses_off[node];
+  const int tid = static_cast<int>(threadIdx.x), rq = tid >> 4, cq = tid & 15;
+  const int nJ = I < ns ? I + 1 : ns;  // <= kSnSmallNs (host: ns <= kSnSmallNs)
+  if (I < ns) {
+    const int row = I * kSnTileDev + tid;
+    if (tid < kSnTileDev && row < sb) spz[tid] = pz[row / b];
+  } else {
+    for (int e = tid; e < kChunk; e += kThreads) sfr[e] = f[static_cast<long>(I) * kChunk + e];
+  }
+  double fv[KV];
+#pragma unroll
+  for (int i = 0; i < KV; ++i) {
+    const int e = tid + i * kThreads;
+    if (e < nJ * kChunk) fv[i] = f[e];
+  }
+  const __amdgpu_buffer_rsrc_t rp = buf_rsrc(panel);
+  double p[kSnSmallNs][4][4];
+#pragma unroll
+  for (int J = 0; J < kSnSmallNs; ++J)
+    if (J < nJ) sn_load_tile_buf(rp, 8u * static_cast<unsigned>(sn_tile_dev(ns, I, J) * kTileD), rq, cq, p[J]);
+#pragma unroll
+  for (int i = 0; i < KV; ++i) {
+    const int e = tid + i * kThreads;
+    if (e < nJ * kChunk) sf[e] = fv[i];
+  }
+  __syncthreads();
+  double acc[4][R];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int a = 0; a < R; ++a) acc[i][a] = 0.0;
+#pragma unroll
+  for (int J = 0; J < kSnSmallNs; ++J) {
+    if (J >= nJ) break;
+    const double* cf = sf + J * kChunk;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      double fc[R];
+#pragma unroll
+      for (int a = 0; a < R; ++a) fc[a] = cf[(cq * 4 + c) * R + a];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int a = 0; a < R; ++a) acc[i][a] = fma(p[J][i][c], fc[a], acc[i][a]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int a = 0; a < R; ++a) {
+      double x = acc[i][a];
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) x += __shfl_xor(x, off, 64);
+      acc[i][a] = x;
+    }
+  if (cq != 0) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = I * kSnTileDev + rq * 4 + i;
+    if (row < sb) {
+      const int pos = row / b, k = row - pos * b;
+      double* dst = y + (static_cast<long>(spz[rq * 4 + i]) * b + k) * R;
+#pragma unroll
+      for (int a = 0; a < R; ++a) dst[a] = acc[i][a];
+    } else if (row >= Sp && row - Sp < tb) {
+      const double* fr = sfr + (rq * 4 + i) * R;
+      double* dst = v.U + v.u_off[node] + static_cast<long>(row - Sp) * R;
+#pragma unroll
+      for (int a = 0; a < R; ++a) dst[a] = fr[a] - acc[i][a];
+    }
+  }
+}
+
 template <int R>
 __global__ __launch_bounds__(kThreads) void k_sn_bwd(SnView v, const int2* __restrict__ items, int b,
                                                      const double* __restrict__ y, double* __restrict__ x) {
@@ -4447,6 +4542,12 @@ hipError_t launch_sn_assemble(int r, int b, const SnView& v, const int2* items, 
 hipError_t launch_sn_fwd(int r, int b, const SnView& v, const int2* items, int count, double* y, hipStream_t stream) {
   if (count == 0) return hipSuccess;
   DPGO_DISPATCH_R(r, (k_sn_fwd<R><<<count, kThreads, 0, stream>>>(v, items, b, y)));
+  return hipGetLastError();
+}
+hipError_t launch_sn_fwd_small(int r, int b, const SnView& v, const int2* items, int count, double* y,
+                               hipStream_t stream) {
+  if (count == 0) return hipSuccess;
+  DPGO_DISPATCH_R(r, (k_sn_fwd_small<R><<<count, kThreads, 0, stream>>>(v, items, b, y)));
   return hipGetLastError();
 }
 

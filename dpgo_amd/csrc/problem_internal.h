@@ -119,7 +119,7 @@ struct dpgo_hip_problem_s {
   dpgo::DevBuf<int2> sn_contrib, sn_items;
   dpgo::DevBuf<int> sn_node_agent;  // [nodes] batch agent of each supernode (per-agent skip in the sweeps)
   struct SnLevel {  // item ranges into sn_items of one tree depth
-    int asm0 = 0, asm_n = 0, fwd0 = 0, fwd_n = 0, bwd0 = 0, bwd_n = 0;
+    int asm0 = 0, asm_n = 0, fws0 = 0, fws_n = 0, fwd0 = 0, fwd_n = 0, bwd0 = 0, bwd_n = 0;  // fws: k_sn_fwd_small's
   };
   std::vector<SnLevel> sn_levels;  // index = depth (0 = the roots)
   long chol_doubles = 0;

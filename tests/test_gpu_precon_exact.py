@@ -228,6 +228,30 @@ def test_device_factor_tiled_levels_bitwise(hip, k, monkeypatch):
     assert np.array_equal(got["0"], got["4096"]), float(np.abs(got["0"] - got["4096"]).max())
 
 
+@pytest.mark.parametrize("k,r", [(12, 5), (20, 5), (16, 3)])
+def test_forward_small_nodes_bitwise(hip, k, r, monkeypatch):
+    """The narrow supernodes' forward items (at most kSnSmallNs S column tiles) through k_sn_fwd_small: the same
+    products in the same order as k_sn_fwd, so the preconditioner outputs agree bitwise (DPGO_SN_FWD_SMALL=0 sends
+    every item through k_sn_fwd), and both equal the oracle's sparse LU to 1e-10."""
+    g, meas = _grid_meas(hip, k, 7)
+    d, n = 3, g.n
+    Q = O.connection_laplacian(meas, n)
+    P = O.QuadraticProblem(n, d, r)
+    P.set_Q(Q)
+    X = random_point(r, d, n, 81)
+    V = random_tangent(X, d, 82)
+    ref = P.precondition(X, V, O.PRECON_EXACT)
+    got = {}
+    for small in ("0", "1"):
+        monkeypatch.setenv("DPGO_SN_FWD_SMALL", small)
+        H = hip.Problem(n, d, r)
+        H.set_Q_edges(0, meas.p1, meas.p2, meas.R, meas.t, meas.kappa, meas.tau, meas.weight)
+        H.set_precon(hip.PRECON_EXACT)
+        got[small] = H.precondition(X, V)
+    assert np.array_equal(got["0"], got["1"]), float(np.abs(got["0"] - got["1"]).max())
+    assert rel(got["1"], ref) <= 1e-10
+
+
 @pytest.mark.parametrize("name,r", [("input_INTEL_g2o", 3), ("sphere2500", 3), ("smallGrid3D", 5)])
 def test_device_factor_tiled_every_level_bitwise(hip, name, r, monkeypatch):
     """Every tree level forced through the tile-parallel kernels (DPGO_FAC_TILED_MIN_TILES=1), for d = 2 (b = 3) and
