@@ -23,18 +23,29 @@ def main():
     aop = g.grid_partition(4)
     X0 = g.chain_init_dev_layout(5, H.lifting_matrix(3, 5))
     engs = {}
-    for order in [o for o in os.environ.get("SWEEP_ORDERS", "default").split(",")]:
+    dummy = None
+    if os.environ.get("SWEEP_DUMMY_K"):  # a small engine built (and kept) first: tells a first-engine effect apart
+        gd = H.Graph.grid3d(int(os.environ["SWEEP_DUMMY_K"]), seed=0)
+        ad = gd.grid_partition(2)
+        dummy = H.Rbcd(gd, ad, np.zeros(8, np.int32), 0, 1, H.rbcd_params(r=5, acceleration=1, precon=H.PRECON_EXACT))
+        dummy.set_X(gd.chain_init_dev_layout(5, H.lifting_matrix(3, 5)))
+        dummy.pre_exchange(0)
+        dummy.update(0, None)
+    for idx, order in enumerate(os.environ.get("SWEEP_ORDERS", "default").split(",")):
         if os.environ.get("SWEEP_ENV"):
             os.environ[os.environ["SWEEP_ENV"]] = order
         e = H.Rbcd(g, aop, np.zeros(64, np.int32), 0, 1, H.rbcd_params(r=5, acceleration=1, precon=H.PRECON_EXACT))
         e.set_X(X0)
         e.pre_exchange(0)
         e.update(0, None)  # builds colour 0's factor with this order
-        engs[order] = e
+        engs[f"{order}#{idx}"] = e  # a value may repeat (engine-order checks)
     res = {o: {"fwd": [], "bwd": []} for o in engs}
     pb = 0.0
     for _ in range(a.rounds):
-        for o, e in engs.items():
+        items = list(engs.items())
+        if os.environ.get("SWEEP_REVERSE"):  # measure the engines last-built first (order-effect checks)
+            items.reverse()
+        for o, e in items:
             f, b, pb = e.bench_precond(0, a.reps)
             res[o]["fwd"].append(f)
             res[o]["bwd"].append(b)
