@@ -592,7 +592,11 @@ constexpr int kUniMax = 8;  // incidences per pose handled straight-line (a 3D l
 #define DPGO_UNI_AHEAD 1
 #endif
 constexpr int kUniAhead = DPGO_UNI_AHEAD;  // straight-line loop: incidences fetched ahead of the one consumed
-template <int R>
+#ifndef DPGO_XQ_AHEAD
+#define DPGO_XQ_AHEAD 3
+#endif
+constexpr int kXqAhead = DPGO_XQ_AHEAD;  // the same for the standalone X.Q (MODE_XQ / MODE_XQ_G)
+template <int R, int AHEAD = kUniAhead>
 __device__ __forceinline__ void edge_loop_uni(const QView& q, const double* __restrict__ in, int kc, int a0, int L1,
                                               int b0, int L2, const int2* s_inc, int i0, const double* s_rec, int e0,
                                               double (&acc)[R][4]) {
@@ -635,12 +639,12 @@ __device__ __forceinline__ void edge_loop_uni(const QView& q, const double* __re
     // second-visit gathers never overlapped the loop's FMAs.
     Stage st[kUniMax];
 #pragma unroll
-    for (int q = 0; q < kUniAhead; ++q)
+    for (int q = 0; q < AHEAD; ++q)
       if (q < n) fetch(q, st[q]);
 #pragma unroll
     for (int q = 0; q < kUniMax; ++q) {
-      if (q + kUniAhead < kUniMax) {
-        if (q + kUniAhead < n) fetch(q + kUniAhead, st[q + kUniAhead < kUniMax ? q + kUniAhead : q]);
+      if (q + AHEAD < kUniMax) {
+        if (q + AHEAD < n) fetch(q + AHEAD, st[q + AHEAD < kUniMax ? q + AHEAD : q]);
       }
       if (q < n) consume(st[q]);
     }
@@ -694,7 +698,8 @@ __device__ __forceinline__ void edge_loop_any(const QView& q, const double* __re
 // half the neighbour gathers.
 // NODIAG (the first-step quadratic form, MODE_QF / MODE_HESS_QF): the half sum without the diagonal
 // term (added after the quad reduction, qf_first_step_dhd); the lane-3 mirror of a d = 2 quad is zeroed.
-template <int R, int B, bool STAGED, bool HALF = false, bool NODIAG = false, bool ROT = false, bool UNI = false>
+template <int R, int B, bool STAGED, bool HALF = false, bool NODIAG = false, bool ROT = false, bool UNI = false,
+          int AHEAD = kUniAhead>
 __device__ __forceinline__ void spmm_accumulate_edges(const QView& q, const double* __restrict__ in, long j,
                                                       int k, int beg, int end, const int2* s_inc, int i0,
                                                       const double* s_rec, int e0, double (&acc)[R][B],
@@ -713,7 +718,7 @@ __device__ __forceinline__ void spmm_accumulate_edges(const QView& q, const doub
       edge_loop_any<R, B, false, false, ROT>(q, in, kc, mid, end, s_inc, i0, s_rec, e0, acc);
     }
   } else if constexpr (STAGED && UNI && ROT) {  // one pipeline over [beg, end), the record source per incidence
-    edge_loop_uni<R>(q, in, kc, beg, end - beg, beg, 0, s_inc, i0, s_rec, e0, acc);
+    edge_loop_uni<R, AHEAD>(q, in, kc, beg, end - beg, beg, 0, s_inc, i0, s_rec, e0, acc);
   } else if constexpr (STAGED) {
     int mid = beg;  // ids ascend: the second visits (ids below the tile's range) come first
     while (mid < end && (s_inc[mid - i0].x >> 1) < e0) ++mid;
@@ -1642,7 +1647,11 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
                                                                   s_ptr[p.pslot + 1], s_inc, i0, s_rec, e0, acc, xin,
                                                                   qch);
       } else if (staged) {
-        spmm_accumulate_edges<R, B, true, HALF, NODIAG, ROT, UNI>(q, in, p.j, p.k, s_ptr[p.pslot],
+        // the standalone X.Q gathers three incidences ahead (135 VGPRs, 3 waves): 97.8-97.9 us against 98.2-99.5 (two
+        // ahead, 4 waves) and 98.8-99.2 (one ahead, 4 waves), profiles/r05o_xq_*.json -- about 1 %; the in-step modes
+        // (HESS_M: a wave lost for the deeper prefetch costs more, profiles/r05i_ab_uni_ahead*.json) one ahead
+        constexpr int kAhead = (MODE == MODE_XQ || MODE == MODE_XQ_G) ? kXqAhead : kUniAhead;
+        spmm_accumulate_edges<R, B, true, HALF, NODIAG, ROT, UNI, kAhead>(q, in, p.j, p.k, s_ptr[p.pslot],
                                                                   s_ptr[p.pslot + 1], s_inc, i0, s_rec, e0, acc, xin);
       } else {
         spmm_accumulate_edges<R, B, false, HALF, NODIAG, ROT>(q, in, p.j, p.k, s_ptr[p.pslot], s_ptr[p.pslot + 1],
