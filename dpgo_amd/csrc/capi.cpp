@@ -696,7 +696,14 @@ int sync_chol(dpgo_hip_problem h) {
     return DPGO_HIP_OK;
   };
   HIP_TRY(hipStreamSynchronize(h->stream));
-  HIP_TRY(h->sn_panel.ensure(std::max<long>(po, 1)));
+  // DPGO_PANEL_GUARD=1 (debug runs, tools/panel_guard_probe.py): 1 Mi doubles of all-ones bytes (NaN) after the
+  // panels; exact_precond reports any guard value that changed (an out-of-bounds write), and a guard value read
+  // into a product makes the result NaN (an out-of-bounds read)
+  static const bool guard = std::getenv("DPGO_PANEL_GUARD") != nullptr;
+  constexpr long kGuard = 1L << 20;
+  HIP_TRY(h->sn_panel.ensure(std::max<long>(po, 1) + (guard ? kGuard : 0)));
+  if (guard) HIP_TRY(hipMemset(h->sn_panel.p + std::max<long>(po, 1), 0xFF, sizeof(double) * kGuard));
+  h->sn_guard_at = guard ? std::max<long>(po, 1) : -1;
   if (!device)
     for (int a = 0; a < K; ++a)
       for (size_t x = 0; x < Fs[a].nodes.size(); ++x) {
@@ -928,6 +935,19 @@ int exact_precond(dpgo_hip_problem h, const double* in, double* z_out, double* d
       HIP_TRY(dpgo::launch_sn_bwd(h->r, h->b, v, it + L.bwd0, L.bwd_n, h->tA.p, h->tB.p, h->stream));
     }
     zraw = h->tB.p;
+    if (h->sn_guard_at >= 0) {  // DPGO_PANEL_GUARD: the guard after the panels untouched?
+      std::vector<unsigned long long> gbuf(1L << 20);
+      HIP_TRY(hipStreamSynchronize(h->stream));
+      HIP_TRY(hipMemcpy(gbuf.data(), h->sn_panel.p + h->sn_guard_at, sizeof(double) * gbuf.size(), hipMemcpyDeviceToHost));
+      long bad = 0, first = -1;
+      for (size_t i = 0; i < gbuf.size(); ++i)
+        if (gbuf[i] != ~0ULL) {
+          ++bad;
+          if (first < 0) first = static_cast<long>(i);
+        }
+      std::fprintf(stderr, "[dpgo_hip] panel guard: %ld of %zu guard doubles changed (first at +%ld)\n", bad,
+                   gbuf.size(), first);
+    }
   }
   auto c = make_ctx(h, flag, partials);
   HIP_TRY(dpgo::launch_precond_finish(h->r, h->b, c, X, zraw, rref, h->chol_state == 1 ? 1 : 0, z_out, delta_out));
