@@ -34,20 +34,26 @@ STATS = ["calls", "early", "runs", "tcg_iters", "NEGCURVTURE", "EXCREGION", "LCO
          "gave_up", "cg_steps", "implicit", "first_full"]
 
 
-def measured_traffic():
-    """HBM bytes per launch from the newest committed PMC summary (profiles/*_pmc_traffic.json,
-    produced by tools/pmc_traffic.py), or None."""
+def measured_traffic(build_id):
+    """HBM bytes per launch from a committed PMC summary of THIS library build (profiles/*_pmc_traffic.json, written
+    by tools/pmc_step.py, which records the profiled library's dpgo_hip_build_id): the newest file whose build id
+    equals the loaded library's.  (None, reason) when there is none -- a summary of other kernels is never reported
+    as this build's traffic."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
-    if not files:
-        return None
-    try:
-        with open(files[-1]) as f:
-            t = json.load(f)
-        t["source"] = os.path.relpath(files[-1], ROOT)
-        return t
-    except (OSError, ValueError):
-        return None
+    stale = []
+    for path in reversed(files):
+        try:
+            with open(path) as f:
+                t = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if t.get("build_id") == build_id and t.get("kernels"):
+            t["source"] = os.path.relpath(path, ROOT)
+            return t, None
+        stale.append(os.path.relpath(path, ROOT))
+    return None, ("no PMC summary of this build (" + build_id[:12] + "); newest of another build: " +
+                  (stale[0] if stale else "none"))
 
 
 def fp64_peak():
@@ -404,7 +410,8 @@ def main():
     mb = [eng.mode_bytes(c) for c in range(eng.num_colors)]
     step_ms = 1e3 * elapsed / args.steps
     # the committed PMC figures are per launch of the 1M-pose, 64-agent, one-GPU workload only
-    traffic = measured_traffic() if (args.k == 100 and A == 4 and world == 1) else None
+    traffic, traffic_note = (measured_traffic(H.build_id()) if (args.k == 100 and A == 4 and world == 1)
+                             else (None, "PMC summaries cover the one-GPU 1M-pose, 64-agent workload only"))
     per_mode = {}
     for m, v in ktimes.items():
         # per full-batch launch equivalent: a half-batch launch of the split merged tCG (small batches, tuning
@@ -529,7 +536,9 @@ def main():
                                     "frac": step_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                     "definition": "all in-step kernels: SURVEY 8d bytes x exact per-agent launch "
                                                   "counts (dpgo_rbcd_bytes)"},
-                     "traffic_source": traffic["source"] if traffic else None},
+                     "traffic_source": traffic["source"] if traffic else None,
+                     "traffic_build_id": traffic.get("build_id") if traffic else None,
+                     "traffic_note": traffic_note},
         "xq_spmm": {"kernel": "k_spmm<5,4,MODE_XQ,edge-stream> over colour class 0 (standalone reps)",
                     "avg_launch_ms": spmm_ms, "algorithmic_bytes_per_launch": bsr_bytes,
                     "GBps": bsr_bytes / (spmm_ms * 1e-3) / 1e9 if spmm_ms > 0 else 0.0,

@@ -37,6 +37,19 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+bool poison_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DPGO_POISON");
+    return e && e[0] && e[0] != '0';
+  }();
+  return on;
+}
+
+hipError_t poison_fill(void* p, size_t bytes, hipStream_t stream) {
+  if (!p || bytes == 0) return hipSuccess;
+  return hipMemsetAsync(p, 0xFF, bytes, stream);
+}
+
 int g_devices = -1;
 
 int usable_devices() {
@@ -329,7 +342,9 @@ int sync_q_edges(dpgo_hip_problem h) {
       meta[t] = make_int4(deg[j0], deg[j1] - deg[j0], lowcnt[j0], lowcnt[j1] - lowcnt[j0]);
     }
     HIP_TRY(h->tile_meta.ensure(meta.size()));
-    HIP_TRY(hipMemcpy(h->tile_meta.p, meta.data(), sizeof(int4) * meta.size(), hipMemcpyHostToDevice));
+    // stream-ordered like every other table here: SpMM launches still queued on h->stream read the old descriptors
+    HIP_TRY(hipMemcpyAsync(h->tile_meta.p, meta.data(), sizeof(int4) * meta.size(), hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));  // `meta` dies here
   }
   h->nnz_inc = deg[h->N];
   h->num_edges = m;
@@ -448,25 +463,63 @@ int chol_threads(int K) {
   return std::max(1, std::min(t, K));
 }
 
+// Events created for one scope and destroyed on every exit from it (an early HIP_TRY return included)
+struct ScopedEvents {
+  std::vector<hipEvent_t> ev;
+  explicit ScopedEvents(size_t n) : ev(n, nullptr) {}
+  ~ScopedEvents() {
+    for (auto e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
+  hipError_t create() {
+    for (auto& e : ev)
+      if (!e) {
+        const hipError_t r = hipEventCreate(&e);
+        if (r != hipSuccess) return r;
+      }
+    return hipSuccess;
+  }
+};
+
+// The last device factorisation's time (fac_ev pair): resolved when it is asked for, so a refactorisation inside
+// the solve loop never waits for the GPU
+int resolve_factor_ms(dpgo_hip_problem h) {
+  if (!h->chol_factor_pending) return DPGO_HIP_OK;
+  HIP_TRY(hipEventSynchronize(h->fac_ev[1]));
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, h->fac_ev[0], h->fac_ev[1]));
+  h->chol_factor_ms = ms;
+  h->chol_factor_pending = false;
+  return DPGO_HIP_OK;
+}
+
 // The device numeric factorisation: k_sn_factor level by level (deepest first) over the symbolic structure and
-// the current edge-stream Q; a non-positive pivot falls back to the identity as the reference does.
+// the current edge-stream Q.  A non-positive pivot marks its agent in fac_not_pd ([K], reset here); that agent's
+// sweeps are skipped and its preconditioner output is its input, unprojected -- the reference's fallback per
+// QuadraticProblem (src/QuadraticProblem.cpp:81-86), so the other agents of the batch keep their factors.  Nothing
+// here waits for the GPU: the flags are read on the device by the sweeps, and by the host only when asked
+// (dpgo_hip_exact_fallback_agents).
 int device_factor(dpgo_hip_problem h) {
   const int maxd = static_cast<int>(h->fac_level_off.size()) - 2;
-  HIP_TRY(hipMemsetAsync(h->fac_not_pd.p, 0, sizeof(int), h->stream));
+  HIP_TRY(hipMemsetAsync(h->fac_not_pd.p, 0, sizeof(int) * h->K, h->stream));
+  if (dpgo::poison_enabled()) {  // debug: the frontal matrices and panels as nothing-written NaN before each factor
+    for (auto& F : h->fac_F) HIP_TRY(dpgo::poison_fill(F.p, sizeof(double) * F.n, h->stream));
+    HIP_TRY(dpgo::poison_fill(h->sn_panel.p, sizeof(double) * h->chol_doubles, h->stream));
+  }
   for (auto& ev : h->fac_ev)
     if (!ev) HIP_TRY(hipEventCreate(&ev));  // owned by the handle: no leak on an early error return
   hipEvent_t e0 = h->fac_ev[0], e1 = h->fac_ev[1];
   HIP_TRY(hipEventRecord(e0, h->stream));
   const bool verbose = std::getenv("DPGO_VERBOSE_CHOL") != nullptr;
-  std::vector<hipEvent_t> lev(verbose ? maxd + 2 : 0, nullptr);
-  for (auto& ev : lev) HIP_TRY(hipEventCreate(&ev));
+  ScopedEvents lev(verbose ? maxd + 2 : 0);
+  HIP_TRY(lev.create());
   for (int dep = maxd; dep >= 0; --dep) {
     const int n0 = h->fac_level_off[dep], n1 = h->fac_level_off[dep + 1];
     dpgo::SnFactorView v{h->fac_nodes.p + n0, h->sn_s.p, h->sn_t.p, h->fac_off.p, h->sn_panel_off.p, h->sn_poses_off.p,
                          h->sn_poses.p, h->fac_ch_off.p, h->fac_ch.p, h->fac_tp_off.p, h->fac_tp.p, h->fac_ent_off.p,
                          h->fac_ent.p, h->fac_src.p, h->rec.p, h->diag.p, 0.1, h->fac_F[dep & 1].p,
-                         h->fac_F[(dep + 1) & 1].p, h->sn_panel.p, h->fac_not_pd.p};
-    if (verbose) HIP_TRY(hipEventRecord(lev[dep + 1], h->stream));
+                         h->fac_F[(dep + 1) & 1].p, h->sn_panel.p, h->sn_node_agent.p, h->fac_not_pd.p};
+    if (verbose) HIP_TRY(hipEventRecord(lev.ev[dep + 1], h->stream));
     if (dep < static_cast<int>(h->fac_seq.size()) && !h->fac_seq[dep].empty()) {
       for (const auto& fl : h->fac_seq[dep])
         HIP_TRY(dpgo::launch_sn_factor_tiled(h->b, v, fl.kind, fl.param, h->fac_titems.p + fl.off, fl.count,
@@ -475,33 +528,22 @@ int device_factor(dpgo_hip_problem h) {
       HIP_TRY(dpgo::launch_sn_factor(h->b, v, n1 - n0, h->stream));
     }
   }
-  if (verbose) HIP_TRY(hipEventRecord(lev[0], h->stream));
+  if (verbose) HIP_TRY(hipEventRecord(lev.ev[0], h->stream));
   HIP_TRY(hipEventRecord(e1, h->stream));
-  int bad = 0;
-  HIP_TRY(hipMemcpyAsync(&bad, h->fac_not_pd.p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
-  HIP_TRY(hipStreamSynchronize(h->stream));
-  float ms = 0.f;
-  HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
-  h->chol_factor_ms = ms;
   h->chol_factor_count += 1;
+  h->chol_factor_pending = true;
+  h->chol_state = 1;
   if (verbose) {
+    DPGO_TRY(resolve_factor_ms(h));
     std::fprintf(stderr, "[dpgo_hip] exact preconditioner: device factorisation %.2f ms; per level (depth: nodes ms):",
-                 static_cast<double>(ms));
+                 h->chol_factor_ms);
     for (int dep = maxd; dep >= 0; --dep) {
       float lm = 0.f;
-      HIP_TRY(hipEventElapsedTime(&lm, lev[dep + 1], lev[dep]));
+      HIP_TRY(hipEventElapsedTime(&lm, lev.ev[dep + 1], lev.ev[dep]));
       std::fprintf(stderr, " %d:%d %.1f", dep, h->fac_level_off[dep + 1] - h->fac_level_off[dep], static_cast<double>(lm));
     }
     std::fprintf(stderr, "\n");
-    for (auto& ev : lev) (void)hipEventDestroy(ev);
   }
-  if (bad) {
-    // src/QuadraticProblem.cpp:81-86: the solve fails -> "Preconditioner failed", out = in
-    std::printf("[dpgo_hip] Preconditioner failed (Q + 0.1 I not positive definite); using the identity.\n");
-    h->chol_state = 2;
-    return DPGO_HIP_OK;
-  }
-  h->chol_state = 1;
   return DPGO_HIP_OK;
 }
 
@@ -571,15 +613,22 @@ int sync_chol(dpgo_hip_problem h) {
     for (auto& t : pool) t.join();
   }
   long total = 0;
+  std::vector<int> host_ident(K, 0);  // host factorisation: agents whose Q + 0.1 I met a non-positive pivot
   for (int a = 0; a < K; ++a) {
     if (rcs[a] != 0) {
-      if (errs[a].find("positive definite") != std::string::npos) {
-        // src/QuadraticProblem.cpp:81-86: the solve fails -> "Preconditioner failed", out = in
-        std::printf("[dpgo_hip] Preconditioner failed (agent %d: %s); using the identity.\n", a, errs[a].c_str());
-        h->chol_state = 2;
-        return DPGO_HIP_OK;
-      }
-      return fail(rcs[a] == -2 ? DPGO_HIP_ENOMEM : DPGO_HIP_EINVAL, errs[a]);
+      if (errs[a].find("positive definite") == std::string::npos)
+        return fail(rcs[a] == -2 ? DPGO_HIP_ENOMEM : DPGO_HIP_EINVAL, errs[a]);
+      // src/QuadraticProblem.cpp:81-86, per QuadraticProblem: this agent's solves fail -> "Preconditioner failed",
+      // out = in; the batch's other agents keep their factors.  The agent keeps its symbolic structure (its
+      // supernodes are skipped by the sweeps, so its panels are never read).
+      std::printf("[dpgo_hip] Preconditioner failed (agent %d: %s); using the identity for it.\n", a, errs[a].c_str());
+      host_ident[a] = 1;
+      HostBSR Q;
+      agent_bsr(h, a, Q);
+      std::string e2;
+      Fs[a] = dpgo::SupernodalFactor();
+      if (dpgo::supernodal_symbolic(h->n_agent[a], b, Q.rowptr, Q.col, kMaxCholDoubles, Fs[a], e2) != 0)
+        return fail(DPGO_HIP_EINVAL, e2);
     }
     total += Fs[a].panel_doubles;
   }
@@ -689,10 +738,13 @@ int sync_chol(dpgo_hip_problem h) {
     L.bwd_n = static_cast<int>(items.size()) - L.bwd0;
   }
   // ---- upload
+  // every upload is ordered on h->stream (the handle's stream is non-blocking: a copy on the null stream is not
+  // ordered before the sweeps and factor kernels queued after it); the host vectors live until the stream
+  // synchronisation at the end of this function (host path) or in device_factor
   auto up = [&](auto& d, const auto& v) -> int {
     using T = typename std::decay_t<decltype(v)>::value_type;
     HIP_TRY(d.ensure(std::max<size_t>(v.size(), 1)));
-    if (!v.empty()) HIP_TRY(hipMemcpy(d.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
+    if (!v.empty()) HIP_TRY(hipMemcpyAsync(d.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, h->stream));
     return DPGO_HIP_OK;
   };
   HIP_TRY(hipStreamSynchronize(h->stream));
@@ -702,17 +754,20 @@ int sync_chol(dpgo_hip_problem h) {
   static const bool guard = std::getenv("DPGO_PANEL_GUARD") != nullptr;
   constexpr long kGuard = 1L << 20;
   HIP_TRY(h->sn_panel.ensure(std::max<long>(po, 1) + (guard ? kGuard : 0)));
-  if (guard) HIP_TRY(hipMemset(h->sn_panel.p + std::max<long>(po, 1), 0xFF, sizeof(double) * kGuard));
+  if (guard) HIP_TRY(hipMemsetAsync(h->sn_panel.p + std::max<long>(po, 1), 0xFF, sizeof(double) * kGuard, h->stream));
   h->sn_guard_at = guard ? std::max<long>(po, 1) : -1;
+  if (device && dpgo::poison_enabled()) HIP_TRY(dpgo::poison_fill(h->sn_panel.p, sizeof(double) * po, h->stream));
   if (!device)
-    for (int a = 0; a < K; ++a)
+    for (int a = 0; a < K; ++a) {
       for (size_t x = 0; x < Fs[a].nodes.size(); ++x) {
         const auto& P = Fs[a].nodes[x].panel;
         if (!P.empty())
-          HIP_TRY(hipMemcpy(h->sn_panel.p + panel_off[base[a] + x], P.data(), sizeof(double) * P.size(),
-                            hipMemcpyHostToDevice));
-        std::vector<double>().swap(Fs[a].nodes[x].panel);  // release the host panel
+          HIP_TRY(hipMemcpyAsync(h->sn_panel.p + panel_off[base[a] + x], P.data(), sizeof(double) * P.size(),
+                                 hipMemcpyHostToDevice, h->stream));
       }
+      HIP_TRY(hipStreamSynchronize(h->stream));  // then release the agent's host panels
+      for (auto& nd : Fs[a].nodes) std::vector<double>().swap(nd.panel);
+    }
   DPGO_TRY(up(h->sn_panel_off, panel_off));
   DPGO_TRY(up(h->sn_f_off, f_off));
   DPGO_TRY(up(h->sn_u_off, u_off));
@@ -728,6 +783,7 @@ int sync_chol(dpgo_hip_problem h) {
   for (int a = 0; a < K; ++a)
     for (int g = base[a]; g < base[a + 1]; ++g) node_agent[g] = a;
   DPGO_TRY(up(h->sn_node_agent, node_agent));
+  if (!device) DPGO_TRY(up(h->fac_not_pd, host_ident));
   HIP_TRY(h->sn_F.ensure(std::max<long>(fo, 1)));
   HIP_TRY(h->sn_U.ensure(std::max<long>(uo, 1)));
   h->chol_doubles = po;
@@ -735,6 +791,7 @@ int sync_chol(dpgo_hip_problem h) {
   h->chol_flops = flops;
   h->chol_inv_flops = inv_flops;
   if (!device) {
+    HIP_TRY(hipStreamSynchronize(h->stream));  // the uploaded host tables die with this frame
     h->chol_state = 1;
     return DPGO_HIP_OK;
   }
@@ -903,7 +960,7 @@ int sync_chol(dpgo_hip_problem h) {
   DPGO_TRY(up(h->fac_ent_off, ent_off));
   DPGO_TRY(up(h->fac_ent, ent));
   DPGO_TRY(up(h->fac_src, src));
-  HIP_TRY(h->fac_not_pd.ensure(1));
+  HIP_TRY(h->fac_not_pd.ensure(K));
   for (int q = 0; q < 2; ++q) HIP_TRY(h->fac_F[q].ensure(std::max<long>(level_size[q], 1)));
   h->sn_sym_ready = true;
   return device_factor(h);
@@ -921,9 +978,12 @@ int exact_precond(dpgo_hip_problem h, const double* in, double* z_out, double* d
   if (h->chol_state == 1) {
     const dpgo::SnView v{h->sn_panel.p, h->sn_panel_off.p, h->sn_s.p,    h->sn_t.p,    h->sn_poses_off.p,
                          h->sn_poses.p, h->sn_f_off.p,     h->sn_u_off.p, h->sn_cpos_off.p, h->sn_cpos.p,
-                         h->sn_contrib.p, h->sn_F.p,       h->sn_U.p,    h->sn_node_agent.p, h->state.p, flag};
+                         h->sn_contrib.p, h->sn_F.p,       h->sn_U.p,    h->sn_node_agent.p, h->state.p, flag,
+                         h->fac_not_pd.p};
     const int2* it = h->sn_items.p;
     const int nl = static_cast<int>(h->sn_levels.size());
+    if (dpgo::poison_enabled())  // debug: frontal / update / sweep vectors as nothing-written NaN
+      for (auto* B : {&h->sn_F, &h->sn_U, &h->tA, &h->tB}) HIP_TRY(dpgo::poison_fill(B->p, sizeof(double) * B->n, h->stream));
     for (int l = nl - 1; l >= 0; --l) {
       const auto& L = h->sn_levels[l];
       HIP_TRY(dpgo::launch_sn_assemble(h->r, h->b, v, it + L.asm0, L.asm_n, in, h->stream));
@@ -950,7 +1010,8 @@ int exact_precond(dpgo_hip_problem h, const double* in, double* z_out, double* d
     }
   }
   auto c = make_ctx(h, flag, partials);
-  HIP_TRY(dpgo::launch_precond_finish(h->r, h->b, c, X, zraw, rref, h->chol_state == 1 ? 1 : 0, z_out, delta_out));
+  HIP_TRY(dpgo::launch_precond_finish(h->r, h->b, c, X, zraw, in, h->chol_state == 1 ? h->fac_not_pd.p : nullptr, rref,
+                                      h->chol_state == 1 ? 1 : 0, z_out, delta_out));
   return DPGO_HIP_OK;
 }
 
@@ -1242,13 +1303,17 @@ int dpgo_hip_problem_create_batch(int num_agents, const int* poses_per_agent, in
       h->state.ensure(num_agents) || h->coef_a.ensure(num_agents) || h->coef_b.ensure(num_agents) ||
       h->arrive.ensure(num_agents))
     return cleanup(fail(DPGO_HIP_ENOMEM, "device allocation failed"));
-  if (hipMemcpy(h->tile_agent.p, h->h_tile_agent.data(), sizeof(int) * T, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(h->tile_start.p, h->h_tile_start.data(), sizeof(int) * T, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(h->tile_count.p, h->h_tile_count.data(), sizeof(int) * T, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(h->agent_tile_off.p, h->h_agent_tile_off.data(), sizeof(int) * (num_agents + 1), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(h->agent_np.p, poses_per_agent, sizeof(int) * num_agents, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(h->state.p, 0, sizeof(AgentState) * num_agents) != hipSuccess ||
-      hipMemset(h->arrive.p, 0, sizeof(int) * num_agents) != hipSuccess)
+  // on the handle's (non-blocking) stream, then waited for: nothing the handle launches can overtake them
+  hipStream_t hs = h->stream;
+  if (hipMemcpyAsync(h->tile_agent.p, h->h_tile_agent.data(), sizeof(int) * T, hipMemcpyHostToDevice, hs) != hipSuccess ||
+      hipMemcpyAsync(h->tile_start.p, h->h_tile_start.data(), sizeof(int) * T, hipMemcpyHostToDevice, hs) != hipSuccess ||
+      hipMemcpyAsync(h->tile_count.p, h->h_tile_count.data(), sizeof(int) * T, hipMemcpyHostToDevice, hs) != hipSuccess ||
+      hipMemcpyAsync(h->agent_tile_off.p, h->h_agent_tile_off.data(), sizeof(int) * (num_agents + 1),
+                     hipMemcpyHostToDevice, hs) != hipSuccess ||
+      hipMemcpyAsync(h->agent_np.p, poses_per_agent, sizeof(int) * num_agents, hipMemcpyHostToDevice, hs) != hipSuccess ||
+      hipMemsetAsync(h->state.p, 0, sizeof(AgentState) * num_agents, hs) != hipSuccess ||
+      hipMemsetAsync(h->arrive.p, 0, sizeof(int) * num_agents, hs) != hipSuccess ||
+      hipStreamSynchronize(hs) != hipSuccess)
     return cleanup(fail(DPGO_HIP_EDEVICE, "device upload failed"));
   if (const char* ev = std::getenv("DPGO_FUSE_FINALIZE")) h->fuse_finalize = std::atoi(ev);
   if (hipHostMalloc(reinterpret_cast<void**>(&h->pub_host), sizeof(int) * num_agents,
@@ -1523,8 +1588,36 @@ int dpgo_hip_exact_factor_info(dpgo_hip_problem h, long long* nodes, int* levels
     for (int v : s) *max_s_tiles = std::max(*max_s_tiles, dpgo::sn_pad(v * h->b) / dpgo::kSnTile);
   }
   *panel_doubles = h->chol_doubles;
+  DPGO_TRY(resolve_factor_ms(h));
   *factor_ms = h->chol_factor_ms;
   *factor_count = h->chol_factor_count;
+  return DPGO_HIP_OK;
+}
+
+// Debug helper, not part of the ABI headers: the first 4 doubles of a fresh device allocation, so a test can confirm
+// that DPGO_POISON is in effect (NaN) before it trusts a poisoned run
+int dpgo_hip_debug_poison_probe(double* out4) {
+  if (!out4) return fail(DPGO_HIP_EINVAL, "null argument");
+  if (usable_devices() == 0) return fail(DPGO_HIP_ENODEV, "no gfx950 device available (no CPU fallback)");
+  dpgo::DevBuf<double> b;
+  HIP_TRY(b.ensure(4));
+  HIP_TRY(hipMemcpy(out4, b.p, sizeof(double) * 4, hipMemcpyDeviceToHost));
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_exact_fallback_agents(dpgo_hip_problem h, int* flags, int* count) {
+  DPGO_TRY(check_handle(h));
+  if (!count) return fail(DPGO_HIP_EINVAL, "null argument");
+  std::vector<int> f(h->K, 0);
+  if (h->chol_state == 1 && h->fac_not_pd.p && h->fac_not_pd.n >= static_cast<size_t>(h->K)) {
+    HIP_TRY(hipMemcpyAsync(f.data(), h->fac_not_pd.p, sizeof(int) * h->K, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+  } else if (h->chol_state == 2) {
+    std::fill(f.begin(), f.end(), 1);
+  }
+  *count = 0;
+  for (int a = 0; a < h->K; ++a) *count += f[a] != 0;
+  if (flags) std::copy(f.begin(), f.end(), flags);
   return DPGO_HIP_OK;
 }
 
@@ -2836,9 +2929,9 @@ int dpgo_hip_bench_hvp(dpgo_hip_problem h, const double* X_dev, double* V_dev, d
   if (reps <= 0 || !ms) return fail(DPGO_HIP_EINVAL, "reps must be > 0");
   // S and a tangent direction (the Riemannian gradient) at X
   DPGO_TRY(eval_at(h, X_dev, V_dev, h->S.p, h->pa.p, dpgo::FLAG_NONE));
-  hipEvent_t e0, e1;
-  HIP_TRY(hipEventCreate(&e0));
-  HIP_TRY(hipEventCreate(&e1));
+  ScopedEvents sev(2);  // destroyed on every return, the early HIP_TRY ones included
+  HIP_TRY(sev.create());
+  hipEvent_t e0 = sev.ev[0], e1 = sev.ev[1];
   auto c = make_ctx(h, dpgo::FLAG_NONE, h->pb.p);
   // untimed launches first: the kernel's code object is loaded on its first launch (each SpMM mode group is
   // its own translation unit), and that one-time cost must stay out of the per-launch average
@@ -2852,8 +2945,6 @@ int dpgo_hip_bench_hvp(dpgo_hip_problem h, const double* X_dev, double* V_dev, d
   float t = 0.f;
   HIP_TRY(hipEventElapsedTime(&t, e0, e1));
   *ms = static_cast<double>(t) / reps;
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   return DPGO_HIP_OK;
 }
 
@@ -2868,11 +2959,13 @@ int dpgo_hip_bench_precond(dpgo_hip_problem h, const double* V_dev, int reps, do
   if (h->chol_state != 1) return DPGO_HIP_OK;
   const dpgo::SnView v{h->sn_panel.p, h->sn_panel_off.p, h->sn_s.p,    h->sn_t.p,    h->sn_poses_off.p,
                        h->sn_poses.p, h->sn_f_off.p,     h->sn_u_off.p, h->sn_cpos_off.p, h->sn_cpos.p,
-                       h->sn_contrib.p, h->sn_F.p,       h->sn_U.p,    h->sn_node_agent.p, h->state.p, dpgo::FLAG_NONE};
+                       h->sn_contrib.p, h->sn_F.p,       h->sn_U.p,    h->sn_node_agent.p, h->state.p, dpgo::FLAG_NONE,
+                       h->fac_not_pd.p};
   const int2* it = h->sn_items.p;
   const int nl = static_cast<int>(h->sn_levels.size());
-  hipEvent_t ev[3];
-  for (auto& e : ev) HIP_TRY(hipEventCreate(&e));
+  ScopedEvents sev(3);  // destroyed on every return, the early HIP_TRY ones included
+  HIP_TRY(sev.create());
+  hipEvent_t* ev = sev.ev.data();
   double tf = 0.0, tb = 0.0;
   for (int i = 0; i < kBenchWarmup + reps; ++i) {  // untimed applications first (see dpgo_hip_bench_hvp)
     HIP_TRY(hipEventRecord(ev[0], h->stream));
@@ -2897,7 +2990,6 @@ int dpgo_hip_bench_precond(dpgo_hip_problem h, const double* V_dev, int reps, do
       tb += b;
     }
   }
-  for (auto& e : ev) (void)hipEventDestroy(e);
   *ms_fwd = tf / reps;
   *ms_bwd = tb / reps;
   return DPGO_HIP_OK;
@@ -2906,9 +2998,9 @@ int dpgo_hip_bench_precond(dpgo_hip_problem h, const double* V_dev, int reps, do
 int dpgo_hip_bench_spmm(dpgo_hip_problem h, const double* X_dev, double* Y_dev, int reps, double* ms) {
   DPGO_TRY(ready(h));
   if (reps <= 0 || !ms) return fail(DPGO_HIP_EINVAL, "reps must be > 0");
-  hipEvent_t e0, e1;
-  HIP_TRY(hipEventCreate(&e0));
-  HIP_TRY(hipEventCreate(&e1));
+  ScopedEvents sev(2);  // destroyed on every return, the early HIP_TRY ones included
+  HIP_TRY(sev.create());
+  hipEvent_t e0 = sev.ev[0], e1 = sev.ev[1];
   auto c = make_ctx(h, dpgo::FLAG_NONE, h->pa.p);
   for (int i = 0; i < kBenchWarmup + reps; ++i) {  // untimed launches first (see dpgo_hip_bench_hvp)
     if (i == kBenchWarmup) HIP_TRY(hipEventRecord(e0, h->stream));
@@ -2919,8 +3011,6 @@ int dpgo_hip_bench_spmm(dpgo_hip_problem h, const double* X_dev, double* Y_dev, 
   float t = 0.f;
   HIP_TRY(hipEventElapsedTime(&t, e0, e1));
   *ms = static_cast<double>(t) / reps;
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   return DPGO_HIP_OK;
 }
 

@@ -223,6 +223,9 @@ struct SnView {
   const int* node_agent = nullptr;  // [nodes] batch agent of the node
   const AgentState* state = nullptr;
   int flag_kind = 0;
+  // [agents] 1 where the agent's factorisation met a non-positive pivot: the reference's per-QuadraticProblem
+  // fallback (src/QuadraticProblem.cpp:81-86, out = in unprojected) -- that agent's supernodes are skipped
+  const int* ident = nullptr;
 };
 
 // Numeric supernodal factorisation of P = Q + shift I on the device (k_sn_factor), over the symbolic structure the
@@ -258,7 +261,8 @@ struct SnFactorView {
   double* F;              // this level's frontal buffer
   const double* Fchild;   // the level below
   double* panel;
-  int* not_pd;            // set to 1 when a pivot is not positive
+  const int* node_agent;  // [nodes] batch agent of the node
+  int* not_pd;            // [agents] set to 1 for the agent of a node that meets a non-positive pivot
 };
 // Loop closures one engine colour class reweights (PGOAgent::updateLoopClosuresWeights,
 // src/PGOAgent.cpp:1181-1244): pose sources >= 0 index the engine's X buffer, < 0 -> (-1 - s) the
@@ -393,10 +397,11 @@ hipError_t launch_sn_factor(int b, const SnFactorView& v, int count, hipStream_t
 // (node, row block / entry chunk / I / I << 16 | J)
 hipError_t launch_sn_factor_tiled(int b, const SnFactorView& v, int kind, int param, const int2* items, int count,
                                   hipStream_t stream);
-// z = P_X(zraw) (or z = zraw when project == 0); optional z_out / delta_out = -z; partials
-// <z, rref>, |rref|^2 per tile
+// z = P_X(zraw) (or z = zraw when project == 0; z = in, unprojected, for an agent with ident[agent] != 0 -- its
+// factorisation failed); optional z_out / delta_out = -z; partials <z, rref>, |rref|^2 per tile
 hipError_t launch_precond_finish(int r, int b, const LaunchCtx& c, const double* X, const double* zraw,
-                                 const double* rref, int project, double* z_out, double* delta_out);
+                                 const double* in, const int* ident, const double* rref, int project, double* z_out,
+                                 double* delta_out);
 hipError_t launch_bj_inverse(int b, int n, const QView& q, double shift, double* Minv, hipStream_t stream);
 // Rebuild the edge-stream Q on device from per-edge weights w[edge] (problem edge order): records
 // M = T diag(w kappa I, w tau) and packed diagonal blocks, the same arithmetic as the host build.

@@ -3245,7 +3245,8 @@ template <int R>
 __global__ __launch_bounds__(kThreads) void k_sn_assemble(SnView v, const int2* __restrict__ items, int b,
                                                           const double* __restrict__ rhs) {
   const int2 it = items[blockIdx.x];
-  if (v.node_agent && agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x])) return;
+  if (v.node_agent && (agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x]) ||
+                       (v.ident && v.ident[v.node_agent[it.x]]))) return;
   const int node = it.x, row = it.y * kThreads + static_cast<int>(threadIdx.x);
   const int s = v.s[node], t = v.t[node], sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), Rp = sn_pad_dev(tb);
   if (row >= Sp + Rp) return;
@@ -3289,7 +3290,8 @@ __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __res
   __shared__ double sfl[4 * kSnTileDev * R];  // triple-buffered frontal chunks, then the row tile's f rows (f_R)
   __shared__ int spz[kSnTileDev];                // the row tile's pose ids (S rows)
   const int2 it = items[blockIdx.x];
-  if (v.node_agent && agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x])) return;
+  if (v.node_agent && (agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x]) ||
+                       (v.ident && v.ident[v.node_agent[it.x]]))) return;
   constexpr int kTileD = kSnTileDev * kSnTileDev, kChunk = kSnTileDev * R;
   double (*sf)[kChunk] = reinterpret_cast<double (*)[kChunk]>(sfl);
   double* __restrict__ sfr = sfl + 3 * kChunk;
@@ -3419,7 +3421,8 @@ __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small
   __shared__ double sfr[kChunk];               // the row tile's f rows (f_R)
   __shared__ int spz[kSnTileDev];              // the row tile's pose ids (S rows)
   const int2 it = items[blockIdx.x];
-  if (v.node_agent && agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x])) return;
+  if (v.node_agent && (agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x]) ||
+                       (v.ident && v.ident[v.node_agent[it.x]]))) return;
   const int node = it.x, I = it.y;
   const int s = v.s[node], t = v.t[node], sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), ns = Sp / kSnTileDev;
   const double* __restrict__ f = v.F + v.f_off[node];
@@ -3503,7 +3506,8 @@ __global__ __launch_bounds__(kThreads) void k_sn_bwd(SnView v, const int2* __res
   __shared__ double sg[2][kSnTileDev * R];  // double-buffered [y_S ; -x_R] chunks
   __shared__ double red[kThreads / 64][16][4 * R];
   const int2 it = items[blockIdx.x];
-  if (v.node_agent && agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x])) return;
+  if (v.node_agent && (agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x]) ||
+                       (v.ident && v.ident[v.node_agent[it.x]]))) return;
   const int node = it.x, J = it.y;
   const int s = v.s[node], t = v.t[node], sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), Rp = sn_pad_dev(tb);
   const int ns = Sp / kSnTileDev, nI = (Sp + Rp) / kSnTileDev;
@@ -3827,7 +3831,7 @@ __global__ __launch_bounds__(kThreads) void k_sn_factor(SnFactorView v) {
       }
     }
   }
-  if (tid == 0 && s_bad) *v.not_pd = 1;
+  if (tid == 0 && s_bad) v.not_pd[v.node_agent[g]] = 1;
   // ---- panel: Z = [I ; L_RS] L_SS^-1, tile column J from the last: Z_IJ = (B_IJ - sum_{K > J} Z_IK L_KJ) L_JJ^-1,
   // B_IJ = 0 (S rows, I != J) or L_RS (R rows); Z_IK = 0 for S rows with K > I
   for (int J = ns - 1; J >= 0; --J) {
@@ -3995,7 +3999,7 @@ __global__ __launch_bounds__(kThreads) void k_snf_tile(SnFactorView v, const int
       const double li = j < i ? As[j * kFLD + i] : j == i ? s_dinv[i] : 0.0;
       panel[sn_tile_dev(ns, K, K) * kFT * kFT + x] = real ? li : 0.0;
     }
-    if (tid == 0 && s_bad) *v.not_pd = 1;
+    if (tid == 0 && s_bad) v.not_pd[v.node_agent[g]] = 1;
     return;
   }
   if constexpr (kind == 2) {
@@ -4090,6 +4094,8 @@ __global__ __launch_bounds__(kThreads) void k_snf_tile(SnFactorView v, const int
 template <int R, int B>
 __global__ __launch_bounds__(kThreads) void k_precond_finish(LaunchCtx c, const double* __restrict__ X,
                                                              const double* __restrict__ zraw,
+                                                             const double* __restrict__ in,
+                                                             const int* __restrict__ ident,
                                                              const double* __restrict__ rref, int project,
                                                              double* __restrict__ z_out,
                                                              double* __restrict__ delta_out) {
@@ -4098,8 +4104,11 @@ __global__ __launch_bounds__(kThreads) void k_precond_finish(LaunchCtx c, const 
   if (tile_skipped(c, p.agent)) return;
   const bool own = p.ok && p.k < B;
   const long off = p.j * (R * B) + p.k * R;
+  // an agent whose factorisation failed: out = in, unprojected (src/QuadraticProblem.cpp:81-86), per agent
+  const bool fallback = ident != nullptr && ident[p.agent] != 0;
+  if (fallback) project = 0;
   double zc[R], xc[R], rc[R];
-  load_col<R, B>(zraw, p.j, p.k, p.ok, zc);
+  load_col<R, B>(fallback ? in : zraw, p.j, p.k, p.ok, zc);
   load_col<R, B>(X, p.j, p.k, p.ok, xc);
   load_col<R, B>(rref, p.j, p.k, p.ok, rc);
   double z[R];
@@ -4607,10 +4616,11 @@ hipError_t launch_sn_factor_tiled(int b, const SnFactorView& v, int kind, int pa
 }
 
 hipError_t launch_precond_finish(int r, int b, const LaunchCtx& c, const double* X, const double* zraw,
-                                 const double* rref, int project, double* z_out, double* delta_out) {
+                                 const double* in, const int* ident, const double* rref, int project, double* z_out,
+                                 double* delta_out) {
   if (c.num_tiles == 0) return hipSuccess;
-  DPGO_DISPATCH(r, b, (k_precond_finish<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, zraw, rref, project, z_out,
-                                                                                      delta_out)));
+  DPGO_DISPATCH(r, b, (k_precond_finish<R, B><<<c.num_tiles, kThreads, 0, c.stream>>>(c, X, zraw, in, ident, rref,
+                                                                                      project, z_out, delta_out)));
   return hipGetLastError();
 }
 

@@ -15,6 +15,12 @@ namespace dpgo {
 int fail(int code, const std::string& msg);
 int usable_devices();
 
+// Debug runs (DPGO_POISON=1): every fresh device allocation, and the exact preconditioner's frontal / panel /
+// sweep buffers before each factorisation and application, are filled with 0xFF bytes -- a NaN in every double --
+// so a kernel that reads an entry nothing wrote yields NaN instead of a plausible stale value.
+bool poison_enabled();
+hipError_t poison_fill(void* p, size_t bytes, hipStream_t stream);
+
 #define HIP_TRY(expr)                                                                        \
   do {                                                                                       \
     hipError_t _e = (expr);                                                                  \
@@ -57,7 +63,10 @@ struct DevBuf {
     if (count <= n && p) return hipSuccess;
     release();
     n = std::max<size_t>(count, 1);
-    return hipMalloc(reinterpret_cast<void**>(&p), n * sizeof(T));
+    const hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), n * sizeof(T));
+    if (e != hipSuccess || !poison_enabled()) return e;
+    const hipError_t f = poison_fill(p, n * sizeof(T), nullptr);
+    return f != hipSuccess ? f : hipDeviceSynchronize();
   }
 };
 
@@ -136,7 +145,10 @@ struct dpgo_hip_problem_s {
   // pattern (sn_sym_ready); every refresh after a reweighting re-runs only k_sn_factor, level by level
   bool sn_sym_ready = false;
   std::vector<int> fac_level_off;  // [depth + 1] into fac_nodes
-  dpgo::DevBuf<int> fac_nodes, fac_ch_off, fac_ch, fac_tp_off, fac_tp, fac_ent_off, fac_src, fac_not_pd;
+  dpgo::DevBuf<int> fac_nodes, fac_ch_off, fac_ch, fac_tp_off, fac_tp, fac_ent_off, fac_src;
+  // [K] per agent: 1 = its factorisation met a non-positive pivot (identity preconditioner for that agent only,
+  // src/QuadraticProblem.cpp:81-86); written by the device factor, or uploaded by the host factorisation
+  dpgo::DevBuf<int> fac_not_pd;
   dpgo::DevBuf<long> fac_off;
   dpgo::DevBuf<dpgo::SnEntry> fac_ent;
   dpgo::DevBuf<double> fac_F[2];  // frontal matrices of the even / odd tree depths
@@ -148,6 +160,7 @@ struct dpgo_hip_problem_s {
   std::vector<std::vector<FacLaunch>> fac_seq;
   dpgo::DevBuf<int2> fac_titems;
   double chol_factor_ms = 0.0;    // the last device factorisation (hipEvent), for the benches
+  bool chol_factor_pending = false;  // fac_ev holds a factorisation whose time is not yet in chol_factor_ms
   int chol_factor_count = 0;
   // host copy of the edge-stream incidences (sync_q_edges), for the factor's assembly tables
   std::vector<int> h_inc_ptr;

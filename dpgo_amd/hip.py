@@ -91,6 +91,7 @@ _SIGS = [
     ("dpgo_hip_exact_factor_info", [C.c_void_p, C.POINTER(C.c_longlong), C.POINTER(C.c_int), C.POINTER(C.c_int),
                                     C.POINTER(C.c_longlong), C.POINTER(C.c_double), C.POINTER(C.c_int)], C.c_int),
     ("dpgo_hip_exact_factor_flops", [C.c_void_p, _dp, _dp], C.c_int),
+    ("dpgo_hip_exact_fallback_agents", [C.c_void_p, _ip, _ip], C.c_int),
     ("dpgo_hip_bench_precond", [C.c_void_p, C.c_void_p, C.c_int, _dp, _dp, _dp], C.c_int),
     ("dpgo_hip_problem_set_tuning", [C.c_void_p, C.c_int, C.c_int], C.c_int),
     ("dpgo_hip_spmm_bytes", [C.c_void_p], C.c_double),
@@ -419,6 +420,15 @@ class Problem:
         return {"nodes": n.value, "levels": lv.value, "max_s_tiles": mt.value, "panel_doubles": pd.value,
                 "factor_ms": ms.value, "factor_count": cnt.value, "cholesky_flops": fl.value,
                 "inverse_flops": ifl.value}
+
+    def exact_fallback_agents(self):
+        """Per agent 1 where the last exact factorisation met a non-positive pivot (that agent's preconditioner is
+        the identity, src/QuadraticProblem.cpp:81-86; the other agents keep their factors)."""
+        flags = np.zeros(self.K, np.int32)
+        cnt = C.c_int()
+        _check(lib().dpgo_hip_exact_fallback_agents(self.h, flags.ctypes.data_as(_ip), C.byref(cnt)))
+        assert int(flags.sum()) == cnt.value
+        return flags
 
     def set_tuning(self, key, value):
         """A tuning key on this handle only (dpgo_hip_problem_set_tuning)."""

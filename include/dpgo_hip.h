@@ -278,6 +278,11 @@ int dpgo_hip_exact_factor_info(dpgo_hip_problem h, long long* nodes, int* levels
  * work CHOLMOD does for src/QuadraticProblem.cpp:37-41), and the extra flops of the panels' inverse blocks
  * [L_SS^-1; L_RS L_SS^-1] (s^3/3 + s^2 t per node) that make the solves dense products.  Zeros before a factor. */
 int dpgo_hip_exact_factor_flops(dpgo_hip_problem h, double* cholesky_flops, double* inverse_flops);
+/* The agents of the handle whose last exact factorisation met a non-positive pivot: QuadraticProblem::PreConditioner's
+ * "Preconditioner failed" branch (src/QuadraticProblem.cpp:81-86) applies to them alone -- their output is their input,
+ * unprojected -- while the batch's other agents keep their factors.  flags (K ints, may be null) receives 1 per such
+ * agent, *count their number (0 before any factor).  Waits for the handle's stream. */
+int dpgo_hip_exact_fallback_agents(dpgo_hip_problem h, int* flags, int* count);
 /* The exact preconditioner's two sweeps over every agent of the handle (right-hand side V_dev, the handle's layout),
  * `reps` applications after 3 untimed ones, each timed with HIP events on the handle's stream: the forward sweep
  * (every level's k_sn_assemble + k_sn_fwd) and the backward sweep (every level's k_sn_bwd), ms per application, and

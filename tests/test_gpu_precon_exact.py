@@ -46,6 +46,97 @@ def test_exact_precondition(hip, name, r, fmt):
     assert rel(H.precondition(X, V2), P.precondition(X, V2, O.PRECON_EXACT)) <= 1e-10
 
 
+def _subset(meas, keep):
+    return O.Measurements(meas.d, meas.r1[keep], meas.r2[keep], meas.p1[keep], meas.p2[keep], meas.R[keep],
+                          meas.t[keep], meas.kappa[keep], meas.tau[keep], meas.weight[keep], meas.num_poses)
+
+
+@pytest.mark.parametrize("fmt", ["bsr", "edges"])
+def test_exact_precondition_dirty_reuse(hip, fmt):
+    """One handle, Q re-set to a smaller pattern (QuadraticProblem::setQ again, src/QuadraticProblem.cpp:31-42): the
+    factor, frontal, panel and sweep buffers of the larger first factor are reused (DevBuf::ensure keeps a larger
+    allocation), so they still hold the first factor's values -- a plausible, finite stale entry wherever the new
+    factorisation or sweeps read what they did not write.  Every application must still equal the oracle's sparse
+    LU of its own Q + 0.1 I at 1e-10 (the round-5 report: 0.235 off after recycled allocations), and the re-set
+    handle must agree bitwise with a fresh handle given the smaller Q directly."""
+    meas = load_meas("sphere2500")
+    d, n, r = meas.d, meas.num_poses, 3
+    m = len(meas.p1)
+    odo = np.abs(meas.p2 - meas.p1) == 1
+    graphs = [meas, _subset(meas, odo | (np.arange(m) % 7 == 0)), _subset(meas, odo)]
+    X = random_point(r, d, n, 91)
+    V = random_tangent(X, d, 92)
+
+    def set_q(H, g):
+        if fmt == "bsr":
+            H.set_Q_scipy(0, O.connection_laplacian(g, n))
+        else:
+            H.set_Q_edges(0, g.p1, g.p2, g.R, g.t, g.kappa, g.tau, g.weight)
+
+    H = hip.Problem(n, d, r)
+    H.set_precon(hip.PRECON_EXACT)
+    for g in graphs:
+        set_q(H, g)
+        P = O.QuadraticProblem(n, d, r)
+        P.set_Q(O.connection_laplacian(g, n))
+        got = H.precondition(X, V)
+        err = rel(got, P.precondition(X, V, O.PRECON_EXACT))
+        print(f"{fmt} edges={len(g.p1)}: vs LU {err:.2e}")
+        assert err <= 1e-10, (len(g.p1), err)
+    F = hip.Problem(n, d, r)
+    F.set_precon(hip.PRECON_EXACT)
+    set_q(F, graphs[-1])
+    assert np.array_equal(F.precondition(X, V), got)
+
+
+def _local_graph(meas, lo, hi):
+    keep = (meas.p1 >= lo) & (meas.p1 < hi) & (meas.p2 >= lo) & (meas.p2 < hi)
+    return O.Measurements(meas.d, meas.r1[keep], meas.r2[keep], meas.p1[keep] - lo, meas.p2[keep] - lo, meas.R[keep],
+                          meas.t[keep], meas.kappa[keep], meas.tau[keep], meas.weight[keep], hi - lo)
+
+
+@pytest.mark.parametrize("fmt", ["bsr", "edges"])
+def test_exact_fallback_per_agent(hip, fmt):
+    """QuadraticProblem::PreConditioner falls back per problem (src/QuadraticProblem.cpp:81-86: a failed solve prints
+    "Preconditioner failed" and returns its input, unprojected).  A batch of 5 agents in which agent 2's Q is negated
+    (Q + 0.1 I indefinite: a non-positive pivot in the host factorisation (bsr) or the device one (edges)): agent 2's
+    output is its input bitwise, the other four agents' outputs are bitwise those of the same batch with agent 2
+    healthy, and exact_fallback_agents names agent 2 alone.  The healthy batch matches the oracle per agent."""
+    meas = load_meas("smallGrid3D")
+    d, r, n, A, bad = 3, 5, meas.num_poses, 5, 2
+    b = d + 1
+    per = n // A
+    starts = [k * per for k in range(A)] + [n]
+    graphs = [_local_graph(meas, starts[k], starts[k + 1]) for k in range(A)]
+    X = random_point(r, d, n, 95)
+    V = random_tangent(X, d, 96)
+
+    def run(neg):
+        H = hip.Problem(None, d, r, poses_per_agent=[starts[k + 1] - starts[k] for k in range(A)])
+        H.set_precon(hip.PRECON_EXACT)
+        for k, g in enumerate(graphs):
+            s = -1.0 if k == neg else 1.0
+            if fmt == "bsr":
+                H.set_Q_scipy(k, s * O.connection_laplacian(g, g.num_poses))
+            else:
+                H.set_Q_edges(k, g.p1, g.p2, g.R, g.t, s * g.kappa, s * g.tau, g.weight)
+        return H.precondition(X, V), H.exact_fallback_agents()
+
+    z_ok, f_ok = run(-1)
+    z_bad, f_bad = run(bad)
+    assert f_ok.tolist() == [0] * A
+    assert f_bad.tolist() == [int(k == bad) for k in range(A)]
+    for k in range(A):
+        sl = slice(starts[k] * b, starts[k + 1] * b)
+        if k == bad:
+            assert np.array_equal(z_bad[:, sl], V[:, sl])
+        else:
+            assert np.array_equal(z_bad[:, sl], z_ok[:, sl]), k
+        P = O.QuadraticProblem(graphs[k].num_poses, d, r)
+        P.set_Q(O.connection_laplacian(graphs[k], graphs[k].num_poses))
+        assert rel(z_ok[:, sl], P.precondition(X[:, sl], V[:, sl], O.PRECON_EXACT)) <= 1e-10
+
+
 @pytest.mark.parametrize("name,r", [("smallGrid3D", 5), ("tinyGrid3D", 3), ("sphere2500", 3)])
 def test_rtr_exact_precon(hip, name, r):
     """PGOAgent::localPoseGraphOptimization settings with the reference's default (exact) preconditioner."""

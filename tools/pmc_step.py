@@ -85,8 +85,11 @@ def summarize(outdir):
         wr = write.get(name, (0.0, 0, 0.0))[0] * 1024.0
         others[name.split("(")[0]] = {"read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
                                       "launches_profiled": fetch[name][1]}
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from dpgo_amd import hip as H  # the library the profiled bench loaded (no GPU call: the id is a constant)
     out = {"workload": "bench.py defaults (1M-pose grid, 64 agents, distributed init + burn-in, CG regime), "
                        "--steps 3 --warmup 1; median over each kernel's last 200 launches",
+           "build_id": H.build_id(),
            "calibration_kernel": copy, "calibration_read_bytes": copy_bytes,
            "calibration_fetch_size_kb": fetch[copy][2], "read_factor": factor,
            "kernels": kernels, "other_kernels": others}
