@@ -647,6 +647,12 @@ int sync_chol(dpgo_hip_problem h) {
   std::vector<int2> contrib;
   int maxd = 0;
   long fo = 0, uo = 0, po = 0;
+  // DPGO_PANEL_GUARD=1 (debug runs): a one-tile gap of all-ones bytes (NaN) after EVERY supernode's panel and 1 Mi
+  // doubles after the last; exact_precond checks every gap after each application (a write past a node's panel into
+  // the next changes a gap), and a gap value read into a product turns the result NaN (a read past the panel)
+  static const bool guard = std::getenv("DPGO_PANEL_GUARD") != nullptr;
+  const long kGap = guard ? static_cast<long>(dpgo::kSnTile) * dpgo::kSnTile : 0;
+  std::vector<std::pair<long, long>> guards;
   double flops = 0.0, inv_flops = 0.0;
   for (int a = 0; a < K; ++a) {
     const auto& nodes = Fs[a].nodes;
@@ -664,6 +670,10 @@ int sync_chol(dpgo_hip_problem h) {
       }
       panel_off[g] = po;
       po += dpgo::sn_panel_tiles(s * b, t * b) * dpgo::kSnTile * dpgo::kSnTile;
+      if (guard) {
+        guards.emplace_back(po, kGap);
+        po += kGap;
+      }
       f_off[g] = fo;
       fo += static_cast<long>(dpgo::sn_pad(s * b) + dpgo::sn_pad(t * b)) * r;
       u_off[g] = uo;
@@ -748,14 +758,13 @@ int sync_chol(dpgo_hip_problem h) {
     return DPGO_HIP_OK;
   };
   HIP_TRY(hipStreamSynchronize(h->stream));
-  // DPGO_PANEL_GUARD=1 (debug runs, tools/panel_guard_probe.py): 1 Mi doubles of all-ones bytes (NaN) after the
-  // panels; exact_precond reports any guard value that changed (an out-of-bounds write), and a guard value read
-  // into a product makes the result NaN (an out-of-bounds read)
-  static const bool guard = std::getenv("DPGO_PANEL_GUARD") != nullptr;
   constexpr long kGuard = 1L << 20;
   HIP_TRY(h->sn_panel.ensure(std::max<long>(po, 1) + (guard ? kGuard : 0)));
-  if (guard) HIP_TRY(hipMemsetAsync(h->sn_panel.p + std::max<long>(po, 1), 0xFF, sizeof(double) * kGuard, h->stream));
-  h->sn_guard_at = guard ? std::max<long>(po, 1) : -1;
+  if (guard) {  // the whole buffer NaN first: the panels are written over it, the gaps keep it
+    HIP_TRY(hipMemsetAsync(h->sn_panel.p, 0xFF, sizeof(double) * (std::max<long>(po, 1) + kGuard), h->stream));
+    guards.emplace_back(std::max<long>(po, 1), kGuard);
+  }
+  h->sn_guards = guards;
   if (device && dpgo::poison_enabled()) HIP_TRY(dpgo::poison_fill(h->sn_panel.p, sizeof(double) * po, h->stream));
   if (!device)
     for (int a = 0; a < K; ++a) {
@@ -995,18 +1004,22 @@ int exact_precond(dpgo_hip_problem h, const double* in, double* z_out, double* d
       HIP_TRY(dpgo::launch_sn_bwd(h->r, h->b, v, it + L.bwd0, L.bwd_n, h->tA.p, h->tB.p, h->stream));
     }
     zraw = h->tB.p;
-    if (h->sn_guard_at >= 0) {  // DPGO_PANEL_GUARD: the guard after the panels untouched?
-      std::vector<unsigned long long> gbuf(1L << 20);
+    if (!h->sn_guards.empty()) {  // DPGO_PANEL_GUARD: every gap between the panels, and the one after them, untouched?
       HIP_TRY(hipStreamSynchronize(h->stream));
-      HIP_TRY(hipMemcpy(gbuf.data(), h->sn_panel.p + h->sn_guard_at, sizeof(double) * gbuf.size(), hipMemcpyDeviceToHost));
-      long bad = 0, first = -1;
-      for (size_t i = 0; i < gbuf.size(); ++i)
-        if (gbuf[i] != ~0ULL) {
-          ++bad;
-          if (first < 0) first = static_cast<long>(i);
-        }
-      std::fprintf(stderr, "[dpgo_hip] panel guard: %ld of %zu guard doubles changed (first at +%ld)\n", bad,
-                   gbuf.size(), first);
+      long bad = 0, total = 0, first = -1;
+      std::vector<unsigned long long> gbuf;
+      for (const auto& gr : h->sn_guards) {
+        gbuf.resize(gr.second);
+        HIP_TRY(hipMemcpy(gbuf.data(), h->sn_panel.p + gr.first, sizeof(double) * gr.second, hipMemcpyDeviceToHost));
+        for (long i = 0; i < gr.second; ++i)
+          if (gbuf[i] != ~0ULL) {
+            ++bad;
+            if (first < 0) first = gr.first + i;
+          }
+        total += gr.second;
+      }
+      std::fprintf(stderr, "[dpgo_hip] panel guard: %ld of %ld guard doubles in %zu gaps changed (first at %ld)\n", bad,
+                   total, h->sn_guards.size(), first);
     }
   }
   auto c = make_ctx(h, flag, partials);

@@ -138,7 +138,8 @@ struct dpgo_hip_problem_s {
   dpgo::DevBuf<double> rec_unit, diag_unit;
   bool central_unit = false;  // qview() serves rec_unit / diag_unit  // edge-stream Q: per tile stage ranges (LaunchCtx::tile_meta); empty otherwise
   long sn_nodes = 0;             // supernodes of the current symbolic structure (sn_s may be larger: capacity)
-  long sn_guard_at = -1;  // DPGO_PANEL_GUARD: offset of the guard after the panels (debug runs)
+  // DPGO_PANEL_GUARD (debug runs): (offset, doubles) of the NaN gap after every supernode's panel and after the last
+  std::vector<std::pair<long, long>> sn_guards;
   double chol_flops = 0.0;       // the factorisation's classic flop count: sum over supernodes s^3/3 + s^2 t + s t^2
   double chol_inv_flops = 0.0;   // the panels' extra: L_SS^-1 (s^3/3) and L_RS L_SS^-1 (s^2 t) per supernode
   // device numeric factorisation (TUNE_DEVICE_CHOL, edge-stream Q): the symbolic structure is built once per Q

@@ -653,6 +653,11 @@ struct CpuAgent {
   std::vector<long> poses;  // global ids, local order
   std::vector<int> edges;   // global edge ids touching the agent (private and shared)
   std::vector<double> w;    // this agent's weight per entry of edges (its own copy of a shared edge's)
+  // neighborPoseDict (src/PGOAgent.cpp:1201-1235): per entry of `edges` that is a shared loop closure, the neighbour's
+  // pose as this agent last received it (snapshot when the agent is selected, examples/MultiRobotExample.cpp:188-213),
+  // and whether it ever did; a reweighting reads only these
+  std::vector<double> dict;
+  std::vector<char> have;
   std::vector<SharedEdge> shared;
   OptStats st;
   double status_rel = 0.0;
@@ -834,11 +839,9 @@ double gnc_tls_weight(const CpuEngine& E, double rr) {
   return std::sqrt(bc * mu * (mu + 1) / rsq) - mu;
 }
 
-// computeMeasurementError (src/DPGO_utils.cpp:509-515) of edge e between global poses i and j of X
-double measurement_error(const CpuEngine& E, int e, long i, long j) {
+// computeMeasurementError (src/DPGO_utils.cpp:509-515) of edge e between the poses Xi (p1) and Xj (p2)
+double measurement_error(const CpuEngine& E, int e, const double* Xi, const double* Xj) {
   const int d = E.d, r = E.r;
-  const double* Xi = &E.X[static_cast<size_t>(i) * E.rb()];
-  const double* Xj = &E.X[static_cast<size_t>(j) * E.rb()];
   const double* Rm = &E.R[static_cast<size_t>(e) * d * d];
   const double* tv = &E.t[static_cast<size_t>(e) * d];
   double rot = 0.0, tr = 0.0;
@@ -855,23 +858,49 @@ double measurement_error(const CpuEngine& E, int e, long i, long j) {
   return E.kappa[e] * rot + E.tau[e] * tr;
 }
 
+// neighborPoseDict update of a selected agent (examples/MultiRobotExample.cpp:188-213: the driver hands the selected
+// robot its neighbours' public poses): every shared edge's other endpoint, as the neighbours hold it now
+void snapshot_neighbors(CpuEngine& E, int a) {
+  CpuAgent& c = E.ag[a];
+  const size_t rb = E.rb();
+  for (size_t q = 0; q < c.edges.size(); ++q) {
+    const int e = c.edges[q], i = E.p1[e], j = E.p2[e];
+    if (E.agent_of[i] == E.agent_of[j]) continue;
+    const long nb = E.agent_of[i] == a ? j : i;
+    std::memcpy(&c.dict[q * rb], &E.X[static_cast<size_t>(nb) * rb], sizeof(double) * rb);
+    c.have[q] = 1;
+  }
+}
+
 // PGOAgent::updateLoopClosuresWeights (src/PGOAgent.cpp:1181-1244) then constructQMatrix: private loop
-// closures (not odometry: consecutive local indices) and the shared ones this agent owns the update of
-// (the other agent has the larger ID), at the current global X; plus the converged ratio.
+// closures (not odometry: consecutive local indices) at the agent's own X, and the shared ones this agent owns the
+// update of (the other agent has the larger ID) against the neighbour's pose in the agent's own
+// dictionary -- an edge whose neighbour pose it never received keeps its weight ("cannot update edge"); plus the
+// converged ratio.
 void reweight_agent(CpuEngine& E, int a) {
   CpuAgent& c = E.ag[a];
+  const size_t rb = E.rb();
   long lc = 0, conv = 0;
   for (size_t q = 0; q < c.edges.size(); ++q) {
     const int e = c.edges[q], i = E.p1[e], j = E.p2[e];
     const int ai = E.agent_of[i], aj = E.agent_of[j];
+    const double* Xi = &E.X[static_cast<size_t>(i) * rb];
+    const double* Xj = &E.X[static_cast<size_t>(j) * rb];
     if (ai == aj) {
       if (E.local[j] == E.local[i] + 1) continue;  // odometry: never reweighted, not a loop closure
     } else if ((ai == a ? aj : ai) < a) {
       ++lc;  // the other agent updates it; this copy keeps its weight
       conv += (c.w[q] == 1.0 || c.w[q] == 0.0) ? 1 : 0;
       continue;
+    } else {
+      if (!c.have[q]) {  // not in neighborPoseDict: "cannot update edge", the weight stays
+        ++lc;
+        conv += (c.w[q] == 1.0 || c.w[q] == 0.0) ? 1 : 0;
+        continue;
+      }
+      (ai == a ? Xj : Xi) = &c.dict[q * rb];
     }
-    c.w[q] = gnc_tls_weight(E, std::sqrt(measurement_error(E, e, i, j)));
+    c.w[q] = gnc_tls_weight(E, std::sqrt(measurement_error(E, e, Xi, Xj)));
     ++lc;
     conv += (c.w[q] == 1.0 || c.w[q] == 0.0) ? 1 : 0;
   }
@@ -896,6 +925,7 @@ void ensure_factor(CpuAgent& c) {
 void iterate_agent(CpuEngine& E, int a, bool selected, bool restart, Work& w, bool reweight = false) {
   CpuAgent& c = E.ag[a];
   const size_t rb = E.rb();
+  if (selected && E.robust) snapshot_neighbors(E, a);  // this iteration's neighbour poses, before any reweighting
   if (reweight) {  // shouldUpdateLoopClosureWeights: reweight, then initializeAcceleration (XPrev = V = Y = X)
     reweight_agent(E, a);
     if (E.accel)
@@ -1010,6 +1040,8 @@ void* dpgo_cpu_rbcd_create(int d, int r, int m, const int* p1, const int* p2, co
   for (int a = 0; a < num_agents; ++a) {
     E->ag[a].edges = edges[a];
     E->ag[a].w.assign(edges[a].size(), 1.0);
+    E->ag[a].dict.assign(robust ? edges[a].size() * static_cast<size_t>(r) * (d + 1) : 0, 0.0);
+    E->ag[a].have.assign(edges[a].size(), 0);
     build_agent(d, r, m, p1, p2, R, t, kappa, tau, agent_of_pose, local, a, edges[a], E->ag[a]);
     E->ag[a].A.exact = precon_exact != 0;
   }

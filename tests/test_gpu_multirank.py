@@ -227,3 +227,124 @@ def test_robust_cost_any_colour_order_across_ranks(accel, halo):
     for a in range(A ** 3):
         assert outs[ranks[a]][2][a] == rc1[a] and outs[ranks[a]][3][a] == rd1[a]
     assert not np.array_equal(X1, X0)
+
+
+# a partition with three or more colours: 8 agents over the poses at random (seeded), so the agent adjacency graph is
+# far from the cube partition's bipartite one
+def _aop_many(g):
+    return np.random.default_rng(21).integers(0, A ** 3, g.n).astype(np.int32)
+
+
+def _order_many(e):
+    """12 iterations over the colours out of cyclic order; every third one the example's single-robot round (the
+    lowest-id agent of that colour)."""
+    C = e.num_colors
+    cols = [(2 * it + it // 3) % C for it in range(12)]
+    out = []
+    for it, c in enumerate(cols):
+        sel = None
+        if it % 3 == 2:
+            sel = int(np.nonzero(e.color_of_agent == c)[0][0])
+        out.append((c, sel))
+    return out
+
+
+def _run_many(H, e, world):
+    s = torch.cuda.Stream()
+    e.set_stream(s.cuda_stream)
+    send = recv = None
+    with torch.cuda.stream(s):
+        send = torch.zeros(max(int(e.send_counts.sum()), 1), dtype=torch.float64, device="cuda")
+        recv = torch.zeros(max(int(e.recv_counts.sum()), 1), dtype=torch.float64, device="cuda")
+        for c, sel in _order_many(e):
+            mask = None
+            if sel is not None:
+                mask = np.zeros(A ** 3, np.int32)
+                mask[sel] = 1
+            e.set_selected(mask)
+            e.pre_exchange(c)
+            if world == 1:
+                e.update(c, None)
+                continue
+            rs_c = [int(x) for x in e.recv_counts_color[c]]
+            ss_c = [int(x) for x in e.send_counts_color[c]]
+            e.pack_color(c, send.data_ptr())
+            hr = torch.empty(sum(rs_c), dtype=torch.float64)
+            dist.all_to_all_single(hr, send[:sum(ss_c)].cpu(), rs_c, ss_c)
+            recv[:sum(rs_c)].copy_(hr)
+            e.update_color(c, recv.data_ptr())
+        e.set_selected(None)
+    torch.cuda.synchronize()
+
+
+def _many_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dpgo_amd import hip as H
+        g = H.Graph.grid3d(K, seed=5)
+        ranks = (np.arange(A ** 3) * world // A ** 3).astype(np.int32)
+        e = H.Rbcd(g, _aop_many(g), ranks, rank, world, _params(H, True, "GNC_TLS"))
+        X0 = g.chain_init(R, O.lifting_matrix(3, R))
+        e.set_X(X0)
+        _run_many(H, e, world)
+        out = np.zeros(X0.size)
+        e.get_X_into(out)
+        q.put((rank, out, int(e.num_colors)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_robust_cost_many_colours_non_cyclic_across_ranks():
+    """GNC_TLS on a partition with >= 3 colours (the per-colour halo once had a full-halo fallback for
+    this case), per-colour halos, colours out of cyclic order mixed with single-robot rounds, two ranks: bitwise the
+    one-rank engine (every reweighting reads the agent's own X and its neighbour-pose dictionary)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_many_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=240) for _ in range(2)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+    from dpgo_amd import hip as H
+    g = H.Graph.grid3d(K, seed=5)
+    X0 = g.chain_init(R, O.lifting_matrix(3, R))
+    e1 = H.Rbcd(g, _aop_many(g), np.zeros(A ** 3, np.int32), 0, 1, _params(H, True, "GNC_TLS"))
+    assert e1.num_colors >= 3 and outs[0][2] == e1.num_colors
+    e1.set_X(X0)
+    _run_many(H, e1, 1)
+    X1 = np.zeros(X0.size)
+    e1.get_X_into(X1)
+    assert np.array_equal(outs[0][1] + outs[1][1], X1)
+    assert not np.array_equal(X1, X0)
+
+
+def test_gnc_many_colours_cyclic_matches_oracle():
+    """The same >= 3-colour random partition under the cyclic colour schedule, GNC_TLS reweighting every 3 iterations
+    (the first before the last colour was ever selected: its dictionaries are empty, its shared edges keep their
+    weights): the one-rank engine against the numpy PGOAgent restatement at 1e-9."""
+    from dpgo_amd import hip as H
+    g = H.Graph.grid3d(K, seed=5)
+    aop = _aop_many(g)
+    X0 = g.chain_init(R, O.lifting_matrix(3, R))
+    e = H.Rbcd(g, aop, np.zeros(A ** 3, np.int32), 0, 1, _params(H, True, "GNC_TLS"))
+    assert e.num_colors >= 3
+    e.set_X(X0)
+    iters = 9
+    for it in range(iters):
+        e.pre_exchange(it % e.num_colors)
+        e.update(it % e.num_colors, None)
+    X1 = np.zeros(X0.size)
+    e.get_X_into(X1)
+    a = g.arrays()
+    meas = O.Measurements(3, np.zeros(g.m, np.int64), np.zeros(g.m, np.int64), a["p1"].astype(np.int64),
+                          a["p2"].astype(np.int64), a["R"], a["t"], a["kappa"], a["tau"], np.ones(g.m), g.n)
+    Xo, colors = O.colour_rbcd(meas, aop, A ** 3, X0, iters, R, acceleration=True, robust="GNC_TLS",
+                               robust_opt_inner_iters=3)
+    assert max(colors) + 1 == e.num_colors
+    assert rel(H.from_dev_layout(X1, R), Xo) <= 1e-9

@@ -30,3 +30,21 @@ def test_poison_fills_fresh_allocations():
         f.argtypes = [C.c_void_p]
         f.restype = C.c_int
         assert f(o.ctypes.data) == 0 and np.isnan(o).all()
+
+
+def test_panel_guard_gaps_untouched():
+    """DPGO_PANEL_GUARD=1: a NaN gap after every supernode's panel (and after the last).  The exact preconditioner's
+    single-application, dirty-reuse and per-agent-fallback tests run in a child process with it set: every
+    application reports its gaps, none may change (no factor or sweep kernel writes past a node's panel), and the
+    tests themselves pass (a gap read into a product would turn the compared output NaN)."""
+    import re
+    env = dict(os.environ, DPGO_PANEL_GUARD="1")
+    out = subprocess.run([sys.executable, "-m", "pytest", "-q", "-s", "-p", "no:cacheprovider", "-m", "gpu",
+                          os.path.join(ROOT, "tests", "test_gpu_precon_exact.py"), "-k",
+                          "test_exact_precondition or dirty_reuse or fallback_per_agent"],
+                         env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    rows = re.findall(r"panel guard: (\d+) of (\d+) guard doubles in (\d+) gaps changed", out.stderr)
+    assert len(rows) >= 12, out.stderr[-2000:]
+    assert all(int(bad) == 0 and int(gaps) >= 2 for bad, _, gaps in rows), rows[:5]
+    print(f"{len(rows)} applications checked, {max(int(g) for _, _, g in rows)} gaps at most, none changed")

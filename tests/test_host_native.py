@@ -251,6 +251,36 @@ def test_cpu_engine_gnc_tls_matches_oracle(accel):
     assert min(ag.converged_loop_closure_ratio() for ag in agents) < 1.0  # the reweighting decided some
 
 
+def test_cpu_engine_gnc_dictionary_many_colours():
+    """oracle/cpu's GNC_TLS reads a shared loop closure's other endpoint from the agent's own neighbour-pose dictionary
+    (PGOAgent::neighborPoseDict, src/PGOAgent.cpp:1201-1235), filled only when the agent is selected
+    (examples/MultiRobotExample.cpp:188-213), and keeps the weight of an edge whose neighbour pose it never received.
+    A random 6-agent partition (>= 3 colours) reweighted every 2 iterations -- the first reweighting comes before
+    some colours were ever selected, later ones read dictionaries older than the neighbours' current X -- against the
+    numpy PGOAgent restatement at 1e-9."""
+    from oracle import cpu_port
+    k, K, r, inner, iters = 5, 6, 5, 2, 9
+    g = O.grid3d(k, seed=4)
+    aop = np.random.default_rng(11).integers(0, K, g.num_poses).astype(np.int32)
+    assert max(O.greedy_colors(g, aop, K)) + 1 >= 3
+    rng = np.random.default_rng(8)
+    lc = np.nonzero(np.abs(g.p2 - g.p1) != 1)[0]
+    bad = rng.choice(lc, size=max(1, len(lc) // 8), replace=False)
+    g.t = g.t.copy()
+    g.t[bad] += rng.normal(0.0, 5.0, size=(len(bad), 3))
+    X0 = O.lifting_matrix(3, r) @ O.chain_initialization(3, g.num_poses, g)
+    arrays = dict(p1=g.p1, p2=g.p2, R=g.R, t=g.t, kappa=g.kappa, tau=g.tau)
+    E = cpu_port.CpuRbcd(3, r, arrays, g.num_poses, aop, K, True, robust="GNC_TLS", robust_opt_inner_iters=inner)
+    E.set_X(O.to_dev(X0))
+    for _ in range(iters):
+        E.iterate(threads=4)
+    agents = []
+    Xo, _ = O.colour_rbcd(g, aop, K, X0, iters, r, acceleration=True, robust="GNC_TLS",
+                          robust_opt_inner_iters=inner, agents_out=agents)
+    assert rel(O.from_dev(E.get_X(), r), Xo) <= 1e-9
+    assert min(ag.converged_loop_closure_ratio() for ag in agents) < 1.0
+
+
 @pytest.mark.parametrize("accel,robust", [(False, "L2"), (True, "L2"), (True, "GNC_TLS")])
 def test_cpu_engine_exact_precon_matches_oracle(accel, robust):
     """oracle/cpu's exact preconditioner (P = Q + 0.1 I factorised per Q, src/QuadraticProblem.cpp:31-42, 75-87;
