@@ -30,7 +30,8 @@ def run(outdir, groups):
         d = os.path.join(outdir, f"g{i}")
         cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--kernel-trace", "--pmc"] + grp.split() + [
             "-d", d, "-o", "run", "--", sys.executable, "bench.py", "--steps", "2", "--warmup", "0",
-            "--cpu-baseline", "0", "--boundary-leg", "0", "--kernel-timing", "0", "--spmm-reps", "2"]
+            "--cpu-baseline", "0", "--boundary-leg", "0", "--exact-leg", "0", "--kernel-timing", "0", "--spmm-reps",
+            "2"]
         with open(d + ".log", "w") as f:
             rc = subprocess.call(cmd, stdout=f, stderr=subprocess.STDOUT, env=env)
         if rc != 0:
@@ -69,6 +70,9 @@ def summarize(outdir, last=40):
         if "TCC_HIT_sum" in row and "TCC_MISS_sum" in row:
             row["l2_hit_rate"] = row["TCC_HIT_sum"] / max(row["TCC_HIT_sum"] + row["TCC_MISS_sum"], 1.0)
         out[k] = row
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from dpgo_amd import hip as H  # the profiled library's build (a constant: no GPU call)
+    out["build_id"] = H.build_id()
     print(json.dumps(out, indent=1, sort_keys=True))
 
 

@@ -29,7 +29,7 @@ def run(outdir):
         cmd = ["timeout", "-s", "KILL", "300", "rocprofv3", "--kernel-trace", "--pmc", ctr, "-d",
                os.path.join(outdir, ctr), "-o", "run", "--", sys.executable, "bench.py", "--steps", "3", "--warmup",
                "1", "--cpu-baseline", "0", "--kernel-timing", "0", "--spmm-reps", "3",
-               "--pmc-calib-mb", str(CALIB_MB)]
+               "--pmc-calib-mb", str(CALIB_MB), "--exact-leg", "0", "--boundary-leg", "0"]
         with open(os.path.join(outdir, ctr + ".log"), "w") as f:
             rc = subprocess.call(cmd, stdout=f, stderr=subprocess.STDOUT, env=env)
         if rc != 0:
