@@ -1066,6 +1066,24 @@ void dpgo_cpu_rbcd_set_X(void* h, const double* Xg) {
   E->iteration = 0;
 }
 
+// Rounding-noise model for parity bars (test infrastructure): every entry of X, Y and V multiplied by (1 + eps u),
+// u uniform in [-1, 1) from SplitMix64(seed), WITHOUT touching the Nesterov state (set_X would restart it).  Applied
+// after every iteration at eps ~ 1e-16 it stands for an implementation whose rounding differs from this one's in
+// every step -- the GPU's -- so "port vs port-with-noise" measures how far the trajectory itself carries such
+// differences.
+void dpgo_cpu_rbcd_perturb(void* h, double eps, unsigned long long seed) {
+  auto* E = static_cast<CpuEngine*>(h);
+  unsigned long long z = seed;
+  auto next = [&z]() {
+    unsigned long long x = (z += 0x9E3779B97F4A7C15ULL);
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+  };
+  for (auto* v : {&E->X, &E->Y, &E->V})
+    for (double& x : *v) x *= 1.0 + eps * (static_cast<double>(next() >> 11) * 0x1.0p-52 - 1.0);
+}
+
 void dpgo_cpu_rbcd_get_X(void* h, double* Xg) {
   auto* E = static_cast<CpuEngine*>(h);
   std::memcpy(Xg, E->X.data(), sizeof(double) * E->X.size());

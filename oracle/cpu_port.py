@@ -117,6 +117,7 @@ class CpuRbcd:
             L.dpgo_cpu_rbcd_time_sample.argtypes = [vp, ip, C.c_int, C.c_int, C.c_int, dp, dp]
             L.dpgo_cpu_rbcd_time_sample.restype = C.c_double
             L.dpgo_cpu_rbcd_factor_info.argtypes = [vp, ip, dp]
+            L.dpgo_cpu_rbcd_perturb.argtypes = [vp, C.c_double, C.c_ulonglong]
             L._rbcd_bound = True
         self._keep = [np.ascontiguousarray(arrays["p1"], np.int32), np.ascontiguousarray(arrays["p2"], np.int32),
                       np.ascontiguousarray(arrays["R"], np.float64).ravel(),
@@ -143,6 +144,12 @@ class CpuRbcd:
     def set_X(self, X_dev_layout):
         x = np.ascontiguousarray(X_dev_layout, np.float64)
         lib().dpgo_cpu_rbcd_set_X(self.h, x.ctypes.data_as(C.POINTER(C.c_double)))
+
+    def perturb(self, eps, seed):
+        """X, Y, V entries times (1 + eps u), u uniform in [-1, 1), Nesterov state kept (a rounding-noise model for
+        parity bars: the port with this after every iteration differs from itself as another implementation's
+        rounding would)."""
+        lib().dpgo_cpu_rbcd_perturb(self.h, float(eps), int(seed))
 
     def get_X(self):
         x = np.empty(self.n * (self.d + 1) * self.r)
