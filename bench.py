@@ -593,7 +593,7 @@ def main():
                          "frac": pb / (mb * 1e-3) / 1e9 / HBM_PEAK_GBS if mb > 0 else 0.0,
                          "kernels": "every level's k_sn_bwd"},
             "what": "one full application over every agent of colour 0 (no tCG skip), mean of 5 after 3 untimed; "
-                    "bytes = the stored panels (64 x 64 tiles, padding included), read once per sweep"}
+                    "bytes = the panels each sweep reads once: wide supernodes' 64 x 64 tiles (padding included), narrow ones' compact copies"}
     out["halo"] = {"kind": args.halo if world > 1 else "none (one rank)",
                    "bytes_sent_per_step_this_rank": 8.0 * (sum(sum(v) for v in c_in) if args.halo == "color"
                                                            else eng.num_colors * int(eng.send_counts.sum())),
@@ -761,8 +761,9 @@ def exact_leg(args, H, torch, dev):
                     "frac": pb / (mf * 1e-3) / 1e9 / HBM_PEAK_GBS if mf > 0 else 0.0},
         "backward": {"ms": mb, "GBps": pb / (mb * 1e-3) / 1e9 if mb > 0 else 0.0,
                      "frac": pb / (mb * 1e-3) / 1e9 / HBM_PEAK_GBS if mb > 0 else 0.0},
-        "what": "one full application over every agent of colour 0, mean of 5 after 3 untimed; bytes = the stored "
-                "panels (64 x 64 tiles, padding included), read once per sweep"}
+        "what": "one full application over every agent of colour 0, mean of 5 after 3 untimed; bytes = the panels "
+                "each sweep reads once: wide supernodes' 64 x 64 tiles (padding included), narrow ones' compact "
+                "copies"}
     if args.cpu_baseline:
         try:
             from oracle import cpu_port

@@ -493,6 +493,20 @@ int resolve_factor_ms(dpgo_hip_problem h) {
   return DPGO_HIP_OK;
 }
 
+// DPGO_SN_COMPACT=0: the sweeps read every supernode's 64 x 64 tiles (no compact copy of the narrow ones), for A/B
+bool sn_compact_on() {
+  const char* e = std::getenv("DPGO_SN_COMPACT");
+  return !(e && e[0] == '0');
+}
+
+// The narrow supernodes' compact panels from the freshly factorised tiles (stream-ordered after the factor)
+int compact_panels(dpgo_hip_problem h) {
+  if (!h->sn_compact || h->sn_citems_n == 0) return DPGO_HIP_OK;
+  HIP_TRY(dpgo::launch_sn_compact(h->b, h->sn_panel.p, h->sn_panel_off.p, h->sn_s.p, h->sn_t.p, h->sn_cpanel_off.p,
+                                  h->sn_cpanel.p, h->sn_citems.p, h->sn_citems_n, h->stream));
+  return DPGO_HIP_OK;
+}
+
 // The device numeric factorisation: k_sn_factor level by level (deepest first) over the symbolic structure and
 // the current edge-stream Q.  A non-positive pivot marks its agent in fac_not_pd ([K], reset here); that agent's
 // sweeps are skipped and its preconditioner output is its input, unprojected -- the reference's fallback per
@@ -530,6 +544,7 @@ int device_factor(dpgo_hip_problem h) {
   }
   if (verbose) HIP_TRY(hipEventRecord(lev.ev[0], h->stream));
   HIP_TRY(hipEventRecord(e1, h->stream));
+  DPGO_TRY(compact_panels(h));  // after the factor's timing window: part of the sweeps' data, not the factorisation
   h->chol_factor_count += 1;
   h->chol_factor_pending = true;
   h->chol_state = 1;
@@ -793,6 +808,31 @@ int sync_chol(dpgo_hip_problem h) {
     for (int g = base[a]; g < base[a + 1]; ++g) node_agent[g] = a;
   DPGO_TRY(up(h->sn_node_agent, node_agent));
   if (!device) DPGO_TRY(up(h->fac_not_pd, host_ident));
+  {  // narrow supernodes (<= kSnSmallNs S column tiles): a compact (s b + t b) x ld copy the sweeps read instead
+    h->sn_compact = sn_compact_on();
+    std::vector<long> coff(nn, -1);
+    std::vector<int2> citems;
+    long co = 0;
+    double bytes = 0.0;
+    for (int g = 0; g < nn; ++g) {
+      const int sb = s_[g] * b, tb = t_[g] * b;
+      const long tiles = dpgo::sn_panel_tiles(sb, tb) * dpgo::kSnTile * dpgo::kSnTile;
+      if (h->sn_compact && dpgo::sn_pad(sb) / dpgo::kSnTile <= dpgo::kSnSmallNs) {
+        coff[g] = co;
+        const long dbl = static_cast<long>(sb + tb) * dpgo::sn_compact_ld(sb);
+        co += (dbl + 15) / 16 * 16;  // 128-byte aligned nodes
+        bytes += 8.0 * static_cast<double>(dbl);
+        for (int r0 = 0; r0 < sb + tb; r0 += dpgo::kSnTile) citems.push_back(make_int2(g, r0 / dpgo::kSnTile));
+      } else {
+        bytes += 8.0 * static_cast<double>(tiles);
+      }
+    }
+    h->sn_sweep_bytes = bytes;
+    h->sn_citems_n = static_cast<int>(citems.size());
+    DPGO_TRY(up(h->sn_cpanel_off, coff));
+    DPGO_TRY(up(h->sn_citems, citems));
+    HIP_TRY(h->sn_cpanel.ensure(std::max<long>(co, 1)));
+  }
   HIP_TRY(h->sn_F.ensure(std::max<long>(fo, 1)));
   HIP_TRY(h->sn_U.ensure(std::max<long>(uo, 1)));
   h->chol_doubles = po;
@@ -800,6 +840,7 @@ int sync_chol(dpgo_hip_problem h) {
   h->chol_flops = flops;
   h->chol_inv_flops = inv_flops;
   if (!device) {
+    DPGO_TRY(compact_panels(h));
     HIP_TRY(hipStreamSynchronize(h->stream));  // the uploaded host tables die with this frame
     h->chol_state = 1;
     return DPGO_HIP_OK;
@@ -988,7 +1029,7 @@ int exact_precond(dpgo_hip_problem h, const double* in, double* z_out, double* d
     const dpgo::SnView v{h->sn_panel.p, h->sn_panel_off.p, h->sn_s.p,    h->sn_t.p,    h->sn_poses_off.p,
                          h->sn_poses.p, h->sn_f_off.p,     h->sn_u_off.p, h->sn_cpos_off.p, h->sn_cpos.p,
                          h->sn_contrib.p, h->sn_F.p,       h->sn_U.p,    h->sn_node_agent.p, h->state.p, flag,
-                         h->fac_not_pd.p};
+                         h->fac_not_pd.p, h->sn_cpanel.p, h->sn_compact ? h->sn_cpanel_off.p : nullptr};
     const int2* it = h->sn_items.p;
     const int nl = static_cast<int>(h->sn_levels.size());
     if (dpgo::poison_enabled())  // debug: frontal / update / sweep vectors as nothing-written NaN
@@ -2968,12 +3009,12 @@ int dpgo_hip_bench_precond(dpgo_hip_problem h, const double* V_dev, int reps, do
   if (reps <= 0 || !ms_fwd || !ms_bwd || !panel_bytes) return fail(DPGO_HIP_EINVAL, "bad argument");
   DPGO_TRY(sync_chol(h));
   *ms_fwd = *ms_bwd = 0.0;
-  *panel_bytes = 8.0 * static_cast<double>(h->chol_doubles);
+  *panel_bytes = h->sn_sweep_bytes;  // what one sweep streams: wide supernodes' tiles, narrow ones' compact copies
   if (h->chol_state != 1) return DPGO_HIP_OK;
   const dpgo::SnView v{h->sn_panel.p, h->sn_panel_off.p, h->sn_s.p,    h->sn_t.p,    h->sn_poses_off.p,
                        h->sn_poses.p, h->sn_f_off.p,     h->sn_u_off.p, h->sn_cpos_off.p, h->sn_cpos.p,
                        h->sn_contrib.p, h->sn_F.p,       h->sn_U.p,    h->sn_node_agent.p, h->state.p, dpgo::FLAG_NONE,
-                       h->fac_not_pd.p};
+                       h->fac_not_pd.p, h->sn_cpanel.p, h->sn_compact ? h->sn_cpanel_off.p : nullptr};
   const int2* it = h->sn_items.p;
   const int nl = static_cast<int>(h->sn_levels.size());
   ScopedEvents sev(3);  // destroyed on every return, the early HIP_TRY ones included

@@ -226,7 +226,19 @@ struct SnView {
   // [agents] 1 where the agent's factorisation met a non-positive pivot: the reference's per-QuadraticProblem
   // fallback (src/QuadraticProblem.cpp:81-86, out = in unprojected) -- that agent's supernodes are skipped
   const int* ident = nullptr;
+  // Narrow supernodes (at most kSnSmallNs S column tiles) are also kept compact: [L_SS^-1 ; L_RS L_SS^-1] as one
+  // (s b + t b) x ld row-major matrix (ld = s b rounded up to 4) with none of the 64-row / 64-column tile padding
+  // (deep nested-dissection levels: 2-2.4x padding).  cpanel_off[node] >= 0: the sweeps read it there instead of the
+  // tiles (the same products in the same order, padding entries read as exact zeros); -1: tiles only.
+  const double* cpanel = nullptr;
+  const long* cpanel_off = nullptr;
 };
+
+// The compact copy of the narrow supernodes' panels (SnView::cpanel) from their tiles: items (node, 64-row block of
+// the compact matrix); launched after every factorisation
+hipError_t launch_sn_compact(int b, const double* panel, const long* panel_off, const int* s, const int* t,
+                             const long* cpanel_off, double* cpanel, const int2* items, int count, hipStream_t stream);
+__host__ __device__ constexpr int sn_compact_ld(int sb) { return (sb + 3) / 4 * 4; }
 
 // Numeric supernodal factorisation of P = Q + shift I on the device (k_sn_factor), over the symbolic structure the
 // host built once (chol_internal.h supernodal_symbolic): one workgroup per supernode, one launch per tree level

@@ -3241,6 +3241,63 @@ __device__ __forceinline__ void sn_load_tile_buf(__amdgpu_buffer_rsrc_t r, unsig
   }
 }
 
+// A narrow supernode's compact panel (SnView::cpanel): buffer resource bounded by the node's bytes, so an offset of
+// 0x80000000 (a padding row or column) loads exact zeros -- the tile path's stored padding -- with no branch
+struct SnCompact {
+  __amdgpu_buffer_rsrc_t r;
+  int sb, tb, ld;
+};
+__device__ __forceinline__ SnCompact sn_compact_view(const SnView& v, long coff, int sb, int tb) {
+  const int ld = sn_compact_ld(sb);
+  return SnCompact{__builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(v.cpanel + coff), static_cast<short>(0),
+                                                     8 * (sb + tb) * ld, 0x00020000),
+                   sb, tb, ld};
+}
+// Rows 4 rq .. 4 rq + 3, columns 4 cq .. 4 cq + 3 of logical tile (I, J) (the tile path's numbering: row tiles I < ns
+// of the S part, then the R part's) from the compact matrix
+__device__ __forceinline__ void sn_load_tile_cmp(const SnCompact& cm, int ns, int I, int J, int rq, int cq,
+                                                 double (&p)[4][4]) {
+  const int col = J * kSnTileDev + cq * 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int prow = (I < ns ? I : I - ns) * kSnTileDev + rq * 4 + i;  // row inside the S or the R part
+    const bool ok = (I < ns ? prow < cm.sb : prow < cm.tb) && col < cm.ld;
+    const int cr = I < ns ? prow : cm.sb + prow;
+    const unsigned o = ok ? 8u * static_cast<unsigned>(cr * cm.ld + col) : 0x80000000u;
+    const f64x2 a = __builtin_bit_cast(f64x2, __builtin_amdgcn_raw_buffer_load_b128(cm.r, o, 0, 0));
+    const f64x2 c = __builtin_bit_cast(f64x2, __builtin_amdgcn_raw_buffer_load_b128(cm.r, o + 16u, 0, 0));
+    p[i][0] = a.x;
+    p[i][1] = a.y;
+    p[i][2] = c.x;
+    p[i][3] = c.y;
+  }
+}
+
+// The compact copy of narrow supernodes' panels: item (node, block of 64 compact rows); compact row cr < sb is S row
+// cr, row sb + q is R row q; column c < sb (columns sb .. ld - 1 are zero)
+__global__ __launch_bounds__(kThreads) void k_sn_compact(int b, const double* __restrict__ panel,
+                                                         const long* __restrict__ panel_off, const int* __restrict__ sv,
+                                                         const int* __restrict__ tv, const long* __restrict__ cpanel_off,
+                                                         double* __restrict__ cpanel, const int2* __restrict__ items) {
+  const int2 it = items[blockIdx.x];
+  const int node = it.x;
+  const int sb = sv[node] * b, tb = tv[node] * b, ld = sn_compact_ld(sb), Sp = sn_pad_dev(sb), ns = Sp / kSnTileDev;
+  const double* __restrict__ src = panel + panel_off[node];
+  double* __restrict__ dst = cpanel + cpanel_off[node];
+  const int r0 = it.y * kSnTileDev, r1 = min(sb + tb, r0 + kSnTileDev);
+  for (int x = threadIdx.x; x < (r1 - r0) * ld; x += kThreads) {
+    const int cr = r0 + x / ld, c = x - (x / ld) * ld;
+    double val = 0.0;
+    if (c < sb) {
+      const int pr = cr < sb ? cr : Sp + (cr - sb);  // padded row
+      const int I = pr / kSnTileDev, J = c / kSnTileDev;
+      val = src[sn_tile_dev(ns, I, J) * (kSnTileDev * kSnTileDev) + (pr - I * kSnTileDev) * kSnTileDev +
+                (c - J * kSnTileDev)];
+    }
+    dst[static_cast<long>(cr) * ld + c] = val;
+  }
+}
+
 template <int R>
 __global__ __launch_bounds__(kThreads) void k_sn_assemble(SnView v, const int2* __restrict__ items, int b,
                                                           const double* __restrict__ rhs) {
@@ -3347,24 +3404,32 @@ __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __res
   };
   const __amdgpu_buffer_rsrc_t rp = buf_rsrc(panel);
   auto tile = [&](int J) { return 8u * static_cast<unsigned>(sn_tile_dev(ns, I, J) * kTileD); };
+  const long coff = v.cpanel_off ? v.cpanel_off[node] : -1;  // a narrow node's compact panel (workgroup-uniform)
+  const SnCompact cm = coff >= 0 ? sn_compact_view(v, coff, sb, t * b) : SnCompact{rp, 0, 0, 0};
+  auto load_tile = [&](int J, double (&pt)[4][4]) {
+    if (coff >= 0)
+      sn_load_tile_cmp(cm, ns, I, J, rq, cq, pt);
+    else
+      sn_load_tile_buf(rp, tile(J), rq, cq, pt);
+  };
   // Sub-step J: store chunk J + 1 (loaded one sub-step earlier; its wait is for loads issued before tile J + 1's),
   // issue chunk J + 2 and tile J + 2, consume tile J: tiles J + 1 and J + 2 stay in flight while tile J is
   // consumed.  Three register sets (tile J in set J % 3), chunk J in LDS buffer J % 3, one barrier per tile.
   if (nJ > 0) {
     load_chunk(0);
-    sn_load_tile_buf(rp, tile(0), rq, cq, p);
+    load_tile(0, p);
     store_chunk(0);
   }
   if (nJ > 1) {
     load_chunk(1);
-    sn_load_tile_buf(rp, tile(1), rq, cq, pn);
+    load_tile(1, pn);
   }
   __syncthreads();
   auto sub_step = [&](int J, const double (&pc)[4][4], double (&pnext)[4][4], int bc, int b1) {
     if (J + 1 < nJ) store_chunk(b1);
     if (J + 2 < nJ) {
       load_chunk(J + 2);
-      sn_load_tile_buf(rp, tile(J + 2), rq, cq, pnext);
+      load_tile(J + 2, pnext);
     }
     consume(pc, bc);
     __syncthreads();  // chunk J + 1 visible; every read of buffer bc done before chunk J + 3 lands there
@@ -3444,9 +3509,17 @@ __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small
   }
   const __amdgpu_buffer_rsrc_t rp = buf_rsrc(panel);
   double p[kSnSmallNs][4][4];
+  const long coff = v.cpanel_off ? v.cpanel_off[node] : -1;  // a narrow node's compact panel (workgroup-uniform)
+  if (coff >= 0) {
+    const SnCompact cm = sn_compact_view(v, coff, sb, tb);
 #pragma unroll
-  for (int J = 0; J < kSnSmallNs; ++J)
-    if (J < nJ) sn_load_tile_buf(rp, 8u * static_cast<unsigned>(sn_tile_dev(ns, I, J) * kTileD), rq, cq, p[J]);
+    for (int J = 0; J < kSnSmallNs; ++J)
+      if (J < nJ) sn_load_tile_cmp(cm, ns, I, J, rq, cq, p[J]);
+  } else {
+#pragma unroll
+    for (int J = 0; J < kSnSmallNs; ++J)
+      if (J < nJ) sn_load_tile_buf(rp, 8u * static_cast<unsigned>(sn_tile_dev(ns, I, J) * kTileD), rq, cq, p[J]);
+  }
 #pragma unroll
   for (int i = 0; i < KV; ++i) {
     const int e = tid + i * kThreads;
@@ -3546,8 +3619,16 @@ __global__ __launch_bounds__(kThreads) void k_sn_bwd(SnView v, const int2* __res
       if (e < kChunk) sg[buf][e] = gv[i];
     }
   };
+  const long coff = v.cpanel_off ? v.cpanel_off[node] : -1;  // a narrow node's compact panel (workgroup-uniform)
+  const SnCompact cm = coff >= 0 ? sn_compact_view(v, coff, sb, tb) : SnCompact{buf_rsrc(panel), 0, 0, 0};
+  auto load_tile = [&](int I, double (&pt)[4][4]) {
+    if (coff >= 0)
+      sn_load_tile_cmp(cm, ns, I, J, rq, cq, pt);
+    else
+      sn_load_tile(panel + sn_tile_dev(ns, I, J) * kTileD, rq, cq, pt);
+  };
   if (J < nI) {
-    sn_load_tile(panel + sn_tile_dev(ns, J, J) * kTileD, rq, cq, p);
+    load_tile(J, p);
     load_chunk(J);
     store_chunk(0);
   }
@@ -3555,7 +3636,7 @@ __global__ __launch_bounds__(kThreads) void k_sn_bwd(SnView v, const int2* __res
   for (int I = J; I < nI; ++I) {
     const bool more = I + 1 < nI;
     if (more) {
-      sn_load_tile(panel + sn_tile_dev(ns, I + 1, J) * kTileD, rq, cq, pn);
+      load_tile(I + 1, pn);
       load_chunk(I + 1);
     }
     const double* cg = sg[(I - J) & 1];
@@ -4573,6 +4654,13 @@ hipError_t launch_sn_bwd(int r, int b, const SnView& v, const int2* items, int c
                          hipStream_t stream) {
   if (count == 0) return hipSuccess;
   DPGO_DISPATCH_R(r, (k_sn_bwd<R><<<count, kThreads, 0, stream>>>(v, items, b, y, x)));
+  return hipGetLastError();
+}
+
+hipError_t launch_sn_compact(int b, const double* panel, const long* panel_off, const int* s, const int* t,
+                             const long* cpanel_off, double* cpanel, const int2* items, int count, hipStream_t stream) {
+  if (count == 0) return hipSuccess;
+  k_sn_compact<<<count, kThreads, 0, stream>>>(b, panel, panel_off, s, t, cpanel_off, cpanel, items);
   return hipGetLastError();
 }
 

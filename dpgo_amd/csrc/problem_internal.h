@@ -131,6 +131,14 @@ struct dpgo_hip_problem_s {
     int asm0 = 0, asm_n = 0, fws0 = 0, fws_n = 0, fwd0 = 0, fwd_n = 0, bwd0 = 0, bwd_n = 0;  // fws: k_sn_fwd_small's
   };
   std::vector<SnLevel> sn_levels;  // index = depth (0 = the roots)
+  // narrow supernodes' compact panels (SnView::cpanel): per node its offset (-1: tiles only), the copy's items
+  // (node, 64-row block) for launch_sn_compact after every factorisation, and the bytes a sweep then reads
+  dpgo::DevBuf<double> sn_cpanel;
+  dpgo::DevBuf<long> sn_cpanel_off;
+  dpgo::DevBuf<int2> sn_citems;
+  int sn_citems_n = 0;
+  bool sn_compact = false;
+  double sn_sweep_bytes = 0.0;
   long chol_doubles = 0;
   dpgo::DevBuf<int4> tile_meta;
   // edge-stream records and diagonal blocks at unit weights (kept by the engine under a robust cost): the central

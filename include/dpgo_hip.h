@@ -286,7 +286,8 @@ int dpgo_hip_exact_fallback_agents(dpgo_hip_problem h, int* flags, int* count);
 /* The exact preconditioner's two sweeps over every agent of the handle (right-hand side V_dev, the handle's layout),
  * `reps` applications after 3 untimed ones, each timed with HIP events on the handle's stream: the forward sweep
  * (every level's k_sn_assemble + k_sn_fwd) and the backward sweep (every level's k_sn_bwd), ms per application, and
- * the bytes of the stored panels, which each sweep streams once (64 x 64 tiles, padding included). */
+ * the panel bytes each sweep streams once: the 64 x 64 tiles of wide supernodes (padding included) and the compact
+ * copies of narrow ones (at most 2 S column tiles; no tile padding). */
 int dpgo_hip_bench_precond(dpgo_hip_problem h, const double* V_dev, int reps, double* ms_fwd, double* ms_bwd,
                            double* panel_bytes);
 /* The process default of a tuning key. */

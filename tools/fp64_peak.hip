@@ -5,7 +5,11 @@
 // the run reports the clock the chip held under each load and the SIMD cycles per instruction -- which tells an
 // under-issued MFMA stream (cycles per MFMA above its issue rate) from a lower clock under MFMA load (same cycles per
 // instruction, fewer cycles per second).  Measurement tool only; prints one JSON line.
-//   hipcc --offload-arch=gfx950 -O3 -o tools/fp64_peak tools/fp64_peak.hip && ./tools/fp64_peak
+// Build with the MFMA accumulators in VGPRs (-amdgpu-mfma-vgpr-form): by default the compiler keeps the loop-carried
+// accumulators in VGPRs and copies all of them through AGPRs around every iteration's MFMAs (128 v_accvgpr moves per
+// 8 MFMAs), which is what round 5's 49 TFLOP/s "ceiling" measured.
+//   hipcc --offload-arch=gfx950 -O3 -mllvm -amdgpu-mfma-vgpr-form=1 -o tools/fp64_peak tools/fp64_peak.hip
+//   ./tools/fp64_peak
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
