@@ -583,17 +583,7 @@ def main():
         # the solves' roofline: each sweep streams every stored panel once (HBM-bound; HIP events around the sweeps of
         # standalone applications over colour 0, outside the timed steps)
         with torch.cuda.stream(stream):
-            mf, mb, pb = eng.bench_precond(0, 5)
-        out["exact_roofline"] = {
-            "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "panel_bytes_per_sweep": pb,
-            "forward": {"ms": mf, "GBps": pb / (mf * 1e-3) / 1e9 if mf > 0 else 0.0,
-                        "frac": pb / (mf * 1e-3) / 1e9 / HBM_PEAK_GBS if mf > 0 else 0.0,
-                        "kernels": "every level's k_sn_assemble + k_sn_fwd"},
-            "backward": {"ms": mb, "GBps": pb / (mb * 1e-3) / 1e9 if mb > 0 else 0.0,
-                         "frac": pb / (mb * 1e-3) / 1e9 / HBM_PEAK_GBS if mb > 0 else 0.0,
-                         "kernels": "every level's k_sn_bwd"},
-            "what": "one full application over every agent of colour 0 (no tCG skip), mean of 5 after 3 untimed; "
-                    "bytes = the panels each sweep reads once: wide supernodes' 64 x 64 tiles (padding included), narrow ones' compact copies"}
+            out["exact_roofline"] = sweep_roofline(eng)
     out["halo"] = {"kind": args.halo if world > 1 else "none (one rank)",
                    "bytes_sent_per_step_this_rank": 8.0 * (sum(sum(v) for v in c_in) if args.halo == "color"
                                                            else eng.num_colors * int(eng.send_counts.sum())),
@@ -690,6 +680,24 @@ def main():
         dist.destroy_process_group()
 
 
+def sweep_roofline(eng):
+    """The exact preconditioner's solves as an HBM roofline: one full application over every agent of colour 0 timed
+    sweep by sweep (dpgo_rbcd_bench_precond, HIP events, mean of 5 after 3 untimed), against the panel bytes each
+    sweep reads once (dpgo_rbcd_exact_sweep_bytes: wide supernodes' 64 x 64 tiles, narrow ones' compact copies)."""
+    mf, mb, stored = eng.bench_precond(0, 5)
+    bf, bb = eng.exact_sweep_bytes(0)
+
+    def leg(ms, byt, kernels):
+        gbps = byt / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        return {"ms": ms, "bytes": byt, "GBps": gbps, "frac": gbps / HBM_PEAK_GBS, "kernels": kernels}
+    return {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "stored_panel_bytes": stored,
+            "forward": leg(mf, bf, "every level's k_sn_assemble + k_sn_fwd_small / k_sn_fwd"),
+            "backward": leg(mb, bb, "every level's k_sn_bwd"),
+            "what": "one full application over every agent of colour 0 (no tCG skip), mean of 5 after 3 untimed; "
+                    "bytes = the panels each sweep reads once: wide supernodes' 64 x 64 tiles (padding included), "
+                    "narrow ones' compact copies (k_sn_fwd on mixed levels reads their tiles)"}
+
+
 def exact_leg(args, H, torch, dev):
     """The reference's default configuration -- GNC_TLS robust cost and the exact preconditioner (the factor of
     Q + 0.1 I, src/QuadraticProblem.cpp:37-41, refactorised after every GNC reweighting, src/PGOAgent.cpp:1110-1112) --
@@ -735,7 +743,7 @@ def exact_leg(args, H, torch, dev):
         el = time.perf_counter() - t0
         refac = factors() - fc0
         st = (eng.stats() - st0).astype(np.int64).sum(axis=0)
-        mf, mb, pb = eng.bench_precond(0, 5)
+        roof = sweep_roofline(eng)
     updates = num_agents * args.steps
     tot = dict(zip(STATS, (int(v) for v in st)))
     leg = {"workload": f"grid3d k={k} ({g.n} poses), r={args.r}, {num_agents} agents, Nesterov={bool(args.accel)}, "
@@ -755,15 +763,7 @@ def exact_leg(args, H, torch, dev):
                 fi["factor_frac_of_mfma_f64"] = fi["factor_tflops"] / peak["mfma_f64_16x16x4_tflops"]
                 fi["factor_frac_of_valu_f64"] = fi["factor_tflops"] / peak.get("valu_fma_f64_tflops", float("nan"))
     leg["exact_factor"] = fac
-    leg["exact_roofline"] = {
-        "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "panel_bytes_per_sweep": pb,
-        "forward": {"ms": mf, "GBps": pb / (mf * 1e-3) / 1e9 if mf > 0 else 0.0,
-                    "frac": pb / (mf * 1e-3) / 1e9 / HBM_PEAK_GBS if mf > 0 else 0.0},
-        "backward": {"ms": mb, "GBps": pb / (mb * 1e-3) / 1e9 if mb > 0 else 0.0,
-                     "frac": pb / (mb * 1e-3) / 1e9 / HBM_PEAK_GBS if mb > 0 else 0.0},
-        "what": "one full application over every agent of colour 0, mean of 5 after 3 untimed; bytes = the panels "
-                "each sweep reads once: wide supernodes' 64 x 64 tiles (padding included), narrow ones' compact "
-                "copies"}
+    leg["exact_roofline"] = roof
     if args.cpu_baseline:
         try:
             from oracle import cpu_port

@@ -718,6 +718,7 @@ int sync_chol(dpgo_hip_problem h) {
     }
   }
   std::vector<int2> items;
+  std::vector<char> level_small;  // per depth: every node narrow (its forward items through k_sn_fwd_small)
   h->sn_levels.assign(maxd + 1, {});
   for (int dep = 0; dep <= maxd; ++dep) {
     auto& L = h->sn_levels[dep];
@@ -738,6 +739,7 @@ int sync_chol(dpgo_hip_problem h) {
     // nodes' items gained, profiles/r05k_levels.txt)
     bool small = sn_fwd_small_on();
     const bool pair_rows = sn_pair_on();
+    level_small.resize(maxd + 1, 0);
     for (int a = 0; a < K && small; ++a)
       for (size_t x = 0; x < Fs[a].nodes.size(); ++x)
         if (Fs[a].nodes[x].depth == dep && dpgo::sn_pad(s_[base[a] + static_cast<int>(x)] * b) / dpgo::kSnTile > dpgo::kSnSmallNs) {
@@ -762,6 +764,7 @@ int sync_chol(dpgo_hip_problem h) {
           }
       if (pass == 0) L.fws_n = static_cast<int>(items.size()) - L.fws0;
     }
+    level_small[dep] = small ? 1 : 0;
     L.fwd_n = static_cast<int>(items.size()) - L.fwd0;
     L.bwd0 = static_cast<int>(items.size());
     for (int a = 0; a < K; ++a)
@@ -821,24 +824,31 @@ int sync_chol(dpgo_hip_problem h) {
   if (!device) DPGO_TRY(up(h->fac_not_pd, host_ident));
   {  // narrow supernodes (<= kSnSmallNs S column tiles): a compact (s b + t b) x ld copy the sweeps read instead
     h->sn_compact = sn_compact_on();
+    // (k_sn_bwd reads every narrow node compact; the forward sweep only through k_sn_fwd_small, i.e. on levels of
+    // narrow nodes only -- k_sn_fwd keeps to the tiles)
     std::vector<long> coff(nn, -1);
     std::vector<int2> citems;
     long co = 0;
-    double bytes = 0.0;
-    for (int g = 0; g < nn; ++g) {
-      const int sb = s_[g] * b, tb = t_[g] * b;
-      const long tiles = dpgo::sn_panel_tiles(sb, tb) * dpgo::kSnTile * dpgo::kSnTile;
-      if (h->sn_compact && dpgo::sn_pad(sb) / dpgo::kSnTile <= dpgo::kSnSmallNs) {
-        coff[g] = co;
-        const long dbl = static_cast<long>(sb + tb) * dpgo::sn_compact_ld(sb);
-        co += (dbl + 15) / 16 * 16;  // 128-byte aligned nodes
-        bytes += 8.0 * static_cast<double>(dbl);
-        for (int r0 = 0; r0 < sb + tb; r0 += dpgo::kSnTile) citems.push_back(make_int2(g, r0 / dpgo::kSnTile));
-      } else {
-        bytes += 8.0 * static_cast<double>(tiles);
+    double fwd_bytes = 0.0, bwd_bytes = 0.0;
+    for (int a = 0; a < K; ++a)
+      for (size_t x = 0; x < Fs[a].nodes.size(); ++x) {
+        const int g = base[a] + static_cast<int>(x);
+        const int sb = s_[g] * b, tb = t_[g] * b;
+        const double tiles = 8.0 * static_cast<double>(dpgo::sn_panel_tiles(sb, tb) * dpgo::kSnTile * dpgo::kSnTile);
+        if (h->sn_compact && dpgo::sn_pad(sb) / dpgo::kSnTile <= dpgo::kSnSmallNs) {
+          coff[g] = co;
+          const long dbl = static_cast<long>(sb + tb) * dpgo::sn_compact_ld(sb);
+          co += (dbl + 15) / 16 * 16;  // 128-byte aligned nodes
+          bwd_bytes += 8.0 * static_cast<double>(dbl);
+          fwd_bytes += level_small[Fs[a].nodes[x].depth] ? 8.0 * static_cast<double>(dbl) : tiles;
+          for (int r0 = 0; r0 < sb + tb; r0 += dpgo::kSnTile) citems.push_back(make_int2(g, r0 / dpgo::kSnTile));
+        } else {
+          fwd_bytes += tiles;
+          bwd_bytes += tiles;
+        }
       }
-    }
-    h->sn_sweep_bytes = bytes;
+    h->sn_sweep_bytes_fwd = fwd_bytes;
+    h->sn_sweep_bytes_bwd = bwd_bytes;
     h->sn_citems_n = static_cast<int>(citems.size());
     DPGO_TRY(up(h->sn_cpanel_off, coff));
     DPGO_TRY(up(h->sn_citems, citems));
@@ -1683,6 +1693,14 @@ int dpgo_hip_exact_fallback_agents(dpgo_hip_problem h, int* flags, int* count) {
   *count = 0;
   for (int a = 0; a < h->K; ++a) *count += f[a] != 0;
   if (flags) std::copy(f.begin(), f.end(), flags);
+  return DPGO_HIP_OK;
+}
+
+int dpgo_hip_exact_sweep_bytes(dpgo_hip_problem h, double* fwd_bytes, double* bwd_bytes) {
+  DPGO_TRY(check_handle(h));
+  if (!fwd_bytes || !bwd_bytes) return fail(DPGO_HIP_EINVAL, "null argument");
+  *fwd_bytes = h->chol_doubles > 0 ? h->sn_sweep_bytes_fwd : 0.0;
+  *bwd_bytes = h->chol_doubles > 0 ? h->sn_sweep_bytes_bwd : 0.0;
   return DPGO_HIP_OK;
 }
 
@@ -3020,7 +3038,7 @@ int dpgo_hip_bench_precond(dpgo_hip_problem h, const double* V_dev, int reps, do
   if (reps <= 0 || !ms_fwd || !ms_bwd || !panel_bytes) return fail(DPGO_HIP_EINVAL, "bad argument");
   DPGO_TRY(sync_chol(h));
   *ms_fwd = *ms_bwd = 0.0;
-  *panel_bytes = h->sn_sweep_bytes;  // what one sweep streams: wide supernodes' tiles, narrow ones' compact copies
+  *panel_bytes = 8.0 * static_cast<double>(h->chol_doubles);  // the stored tiles (dpgo_hip_exact_sweep_bytes: read)
   if (h->chol_state != 1) return DPGO_HIP_OK;
   const dpgo::SnView v{h->sn_panel.p, h->sn_panel_off.p, h->sn_s.p,    h->sn_t.p,    h->sn_poses_off.p,
                        h->sn_poses.p, h->sn_f_off.p,     h->sn_u_off.p, h->sn_cpos_off.p, h->sn_cpos.p,

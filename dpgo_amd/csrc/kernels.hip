@@ -3341,8 +3341,11 @@ __global__ __launch_bounds__(kThreads) void k_sn_assemble(SnView v, const int2* 
 // a tile's 64 vector elements (64 R doubles) through registers: element e = tid + 256 i, i < kSnVecRegs
 constexpr int kSnVecRegs = (kSnTileDev * 8 + kThreads - 1) / kThreads;  // enough for R <= 8
 
+#ifndef DPGO_SNF_WAVES
+#define DPGO_SNF_WAVES 3  // k_sn_fwd's occupancy (waves per SIMD): its three-deep tile pipeline fits 168 VGPRs
+#endif
 template <int R>
-__global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __restrict__ items, int b,
+__global__ __launch_bounds__(kThreads, DPGO_SNF_WAVES) void k_sn_fwd(SnView v, const int2* __restrict__ items, int b,
                                                      double* __restrict__ y) {
   __shared__ double sfl[4 * kSnTileDev * R];  // triple-buffered frontal chunks, then the row tile's f rows (f_R)
   __shared__ int spz[kSnTileDev];                // the row tile's pose ids (S rows)
@@ -3404,14 +3407,9 @@ __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __res
   };
   const __amdgpu_buffer_rsrc_t rp = buf_rsrc(panel);
   auto tile = [&](int J) { return 8u * static_cast<unsigned>(sn_tile_dev(ns, I, J) * kTileD); };
-  const long coff = v.cpanel_off ? v.cpanel_off[node] : -1;  // a narrow node's compact panel (workgroup-uniform)
-  const SnCompact cm = coff >= 0 ? sn_compact_view(v, coff, sb, t * b) : SnCompact{rp, 0, 0, 0};
-  auto load_tile = [&](int J, double (&pt)[4][4]) {
-    if (coff >= 0)
-      sn_load_tile_cmp(cm, ns, I, J, rq, cq, pt);
-    else
-      sn_load_tile_buf(rp, tile(J), rq, cq, pt);
-  };
+  // (the tiles even for a narrow node of a mixed level: the compact path's offsets cost this three-deep pipeline its
+  // third wave -- 172 VGPRs; k_sn_fwd_small and k_sn_bwd read narrow nodes compact)
+  auto load_tile = [&](int J, double (&pt)[4][4]) { sn_load_tile_buf(rp, tile(J), rq, cq, pt); };
   // Sub-step J: store chunk J + 1 (loaded one sub-step earlier; its wait is for loads issued before tile J + 1's),
   // issue chunk J + 2 and tile J + 2, consume tile J: tiles J + 1 and J + 2 stay in flight while tile J is
   // consumed.  Three register sets (tile J in set J % 3), chunk J in LDS buffer J % 3, one barrier per tile.
@@ -3475,7 +3473,7 @@ __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __res
 // tiles) is issued at once and waited for once -- in about half k_sn_fwd's registers, so more workgroups (and bytes)
 // are in flight per CU on the levels where each streams only 32-64 KB.
 #ifndef DPGO_SNF_SMALL_WAVES
-#define DPGO_SNF_SMALL_WAVES 1  // k_sn_fwd_small's occupancy hint (waves per SIMD; 1 = none)
+#define DPGO_SNF_SMALL_WAVES 4  // k_sn_fwd_small's occupancy (waves per SIMD): <= 128 VGPRs
 #endif
 template <int R>
 __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small(SnView v, const int2* __restrict__ items, int b,
@@ -3540,9 +3538,11 @@ __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small
     if (e < nJ * kChunk) sf[e] = fv[i];
   }
   __syncthreads();
-#pragma unroll
-  for (int u = 0; u < kSnSmallNs; ++u) {
-    if (u >= nrt) break;
+  // row tile Iu: products with tiles p[0 .. nj - 1], the 16 column groups' sums in a fixed order, then y_S or the
+  // update u = f_R - M f_S.  A pair runs it twice with nj = 1, row tile I + 1's tile moved into p[0] in between.
+  const int nj = pair ? 1 : nJ;
+#pragma unroll 1
+  for (int u = 0; u < nrt; ++u) {
     const int Iu = I + u;
     double acc[4][R];
 #pragma unroll
@@ -3551,9 +3551,8 @@ __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small
       for (int a = 0; a < R; ++a) acc[i][a] = 0.0;
 #pragma unroll
     for (int J = 0; J < kSnSmallNs; ++J) {
-      if (J >= nJ) break;
+      if (J >= nj) break;
       const double* cf = sf + J * kChunk;
-      const int pj = pair ? u : J;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         double fc[R];
@@ -3562,7 +3561,7 @@ __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int a = 0; a < R; ++a) acc[i][a] = fma(p[pj][i][c], fc[a], acc[i][a]);
+          for (int a = 0; a < R; ++a) acc[i][a] = fma(p[J][i][c], fc[a], acc[i][a]);
       }
     }
 #pragma unroll
@@ -3591,6 +3590,10 @@ __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small
         }
       }
     }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) p[0][i][c] = p[1][i][c];
   }
 }
 

@@ -138,7 +138,7 @@ struct dpgo_hip_problem_s {
   dpgo::DevBuf<int2> sn_citems;
   int sn_citems_n = 0;
   bool sn_compact = false;
-  double sn_sweep_bytes = 0.0;
+  double sn_sweep_bytes_fwd = 0.0, sn_sweep_bytes_bwd = 0.0;
   long chol_doubles = 0;
   dpgo::DevBuf<int4> tile_meta;
   // edge-stream records and diagonal blocks at unit weights (kept by the engine under a robust cost): the central

@@ -1401,6 +1401,15 @@ int dpgo_rbcd_bench_precond(dpgo_rbcd e, int color, int reps, double* ms_fwd, do
   return dpgo_hip_bench_precond(e->prob[color], color_ptr(e, e->X, color), reps, ms_fwd, ms_bwd, panel_bytes);
 }
 
+int dpgo_rbcd_exact_sweep_bytes(dpgo_rbcd e, int color, double* fwd_bytes, double* bwd_bytes) {
+  if (!e || color < 0 || color >= e->ncolors || !fwd_bytes || !bwd_bytes) return fail(DPGO_HIP_EINVAL, "bad argument");
+  if (!e->prob[color]) {
+    *fwd_bytes = *bwd_bytes = 0.0;
+    return DPGO_HIP_OK;
+  }
+  return dpgo_hip_exact_sweep_bytes(e->prob[color], fwd_bytes, bwd_bytes);
+}
+
 int dpgo_rbcd_exact_factor_flops(dpgo_rbcd e, int color, double* cholesky_flops, double* inverse_flops) {
   if (!e || color < 0 || color >= e->ncolors || !cholesky_flops || !inverse_flops) return fail(DPGO_HIP_EINVAL, "bad argument");
   if (!e->prob[color]) {

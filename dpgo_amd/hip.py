@@ -92,6 +92,7 @@ _SIGS = [
                                     C.POINTER(C.c_longlong), C.POINTER(C.c_double), C.POINTER(C.c_int)], C.c_int),
     ("dpgo_hip_exact_factor_flops", [C.c_void_p, _dp, _dp], C.c_int),
     ("dpgo_hip_exact_fallback_agents", [C.c_void_p, _ip, _ip], C.c_int),
+    ("dpgo_hip_exact_sweep_bytes", [C.c_void_p, _dp, _dp], C.c_int),
     ("dpgo_hip_bench_precond", [C.c_void_p, C.c_void_p, C.c_int, _dp, _dp, _dp], C.c_int),
     ("dpgo_hip_problem_set_tuning", [C.c_void_p, C.c_int, C.c_int], C.c_int),
     ("dpgo_hip_spmm_bytes", [C.c_void_p], C.c_double),
@@ -555,6 +556,7 @@ _SIGS2 = [
                                      C.POINTER(C.c_int)], C.c_int),
     ("dpgo_rbcd_exact_factor_flops", [C.c_void_p, C.c_int, _dp, _dp], C.c_int),
     ("dpgo_rbcd_bench_precond", [C.c_void_p, C.c_int, C.c_int, _dp, _dp, _dp], C.c_int),
+    ("dpgo_rbcd_exact_sweep_bytes", [C.c_void_p, C.c_int, _dp, _dp], C.c_int),
     ("dpgo_rbcd_exchange", [C.c_void_p, C.POINTER(C.c_void_p)], C.c_int),
     ("dpgo_rbcd_set_kernel_timing", [C.c_void_p, C.c_int], C.c_int),
     ("dpgo_rbcd_set_tuning", [C.c_void_p, C.c_int, C.c_int], C.c_int),
@@ -899,10 +901,18 @@ class Rbcd:
         return out
 
     def bench_precond(self, color, reps):
-        """The exact preconditioner's forward / backward sweeps over colour class c: (ms_fwd, ms_bwd, panel bytes)."""
+        """The exact preconditioner's forward / backward sweeps over colour class c: (ms_fwd, ms_bwd, stored panel
+        bytes)."""
         f, b, p = C.c_double(), C.c_double(), C.c_double()
         _check(lib().dpgo_rbcd_bench_precond(self.h, int(color), int(reps), C.byref(f), C.byref(b), C.byref(p)))
         return f.value, b.value, p.value
+
+    def exact_sweep_bytes(self, color):
+        """(forward, backward) panel bytes one application over colour class c reads (wide nodes' tiles, narrow nodes'
+        compact copies)."""
+        f, b = C.c_double(), C.c_double()
+        _check(lib().dpgo_rbcd_exact_sweep_bytes(self.h, int(color), C.byref(f), C.byref(b)))
+        return f.value, b.value
 
     def comm_info(self):
         """(ncclCommCount, ncclCommUserRank) of the engine's own RCCL communicator, (-1, -1) without one."""

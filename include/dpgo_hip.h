@@ -286,10 +286,13 @@ int dpgo_hip_exact_fallback_agents(dpgo_hip_problem h, int* flags, int* count);
 /* The exact preconditioner's two sweeps over every agent of the handle (right-hand side V_dev, the handle's layout),
  * `reps` applications after 3 untimed ones, each timed with HIP events on the handle's stream: the forward sweep
  * (every level's k_sn_assemble + k_sn_fwd) and the backward sweep (every level's k_sn_bwd), ms per application, and
- * the panel bytes each sweep streams once: the 64 x 64 tiles of wide supernodes (padding included) and the compact
- * copies of narrow ones (at most 2 S column tiles; no tile padding). */
+ * the bytes of the stored panel tiles (64 x 64, padding included). */
 int dpgo_hip_bench_precond(dpgo_hip_problem h, const double* V_dev, int reps, double* ms_fwd, double* ms_bwd,
                            double* panel_bytes);
+/* The panel bytes one application's sweeps read: every wide supernode's 64 x 64 tiles (padding included) and the
+ * compact copy of every narrow one (at most 2 S column tiles: the backward sweep always, the forward sweep on levels
+ * of narrow nodes only).  Zeros before a factor. */
+int dpgo_hip_exact_sweep_bytes(dpgo_hip_problem h, double* fwd_bytes, double* bwd_bytes);
 /* The process default of a tuning key. */
 int dpgo_hip_get_tuning(int key, int* value);
 /* The same keys on one existing handle (A/B timing of variants on one problem without rebuilding it). */

@@ -230,6 +230,8 @@ int dpgo_rbcd_exact_factor_info(dpgo_rbcd e, int color, long long* nodes, int* l
                                 long long* panel_doubles, double* factor_ms, int* factor_count);
 /* dpgo_hip_exact_factor_flops of the colour's batched problem (zeros when this rank owns none of its agents) */
 int dpgo_rbcd_exact_factor_flops(dpgo_rbcd e, int color, double* cholesky_flops, double* inverse_flops);
+/* dpgo_hip_exact_sweep_bytes of the colour's batched problem (zeros when this rank owns none of its agents) */
+int dpgo_rbcd_exact_sweep_bytes(dpgo_rbcd e, int color, double* fwd_bytes, double* bwd_bytes);
 /* dpgo_hip_bench_precond over colour class c's batched problem, right-hand side the colour's current X */
 int dpgo_rbcd_bench_precond(dpgo_rbcd e, int color, int reps, double* ms_fwd, double* ms_bwd, double* panel_bytes);
 /* The engine's RCCL communicator as RCCL sees it (ncclCommCount, ncclCommUserRank); -1, -1 without one. */
