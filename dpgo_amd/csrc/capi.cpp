@@ -568,11 +568,6 @@ bool sn_fwd_small_on() {
   return !(e && e[0] == '0');
 }
 
-// DPGO_SN_PAIR=0: one row tile per k_sn_fwd_small workgroup for one-column-tile nodes too (A/B and bitwise tests)
-bool sn_pair_on() {
-  const char* e = std::getenv("DPGO_SN_PAIR");
-  return !(e && e[0] == '0');
-}
 
 int sync_chol(dpgo_hip_problem h) {
   if (h->chol_state != 0) return DPGO_HIP_OK;
@@ -738,7 +733,6 @@ int sync_chol(dpgo_hip_problem h) {
     // (a level with both kinds runs every item through k_sn_fwd: a second launch there cost more than the narrow
     // nodes' items gained, profiles/r05k_levels.txt)
     bool small = sn_fwd_small_on();
-    const bool pair_rows = sn_pair_on();
     level_small.resize(maxd + 1, 0);
     for (int a = 0; a < K && small; ++a)
       for (size_t x = 0; x < Fs[a].nodes.size(); ++x)
@@ -756,11 +750,7 @@ int sync_chol(dpgo_hip_problem h) {
             const bool narrow = small && ns <= dpgo::kSnSmallNs;
             if (narrow != (pass == 0)) continue;
             const int nI = (dpgo::sn_pad(s_[g] * b) + dpgo::sn_pad(t_[g] * b)) / dpgo::kSnTile;
-            if (narrow && ns == 1 && pair_rows) {  // k_sn_fwd_small: row tiles I, I + 1 in one workgroup
-              for (int I = 0; I < nI; I += 2) items.push_back(make_int2(g, I | (I + 1 < nI ? dpgo::kSnPairBit : 0)));
-            } else {
-              for (int I = 0; I < nI; ++I) items.push_back(make_int2(g, I));
-            }
+            for (int I = 0; I < nI; ++I) items.push_back(make_int2(g, I));
           }
       if (pass == 0) L.fws_n = static_cast<int>(items.size()) - L.fws0;
     }

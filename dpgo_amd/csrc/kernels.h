@@ -204,7 +204,6 @@ struct GEdges {
 // ((S_pad + R_pad) scalar rows x r) and update vectors U (t b rows x r) are work space.
 constexpr int kSnTileDev = 64;
 constexpr int kSnSmallNs = 2;  // k_sn_fwd_small: nodes of at most this many S column tiles
-constexpr int kSnPairBit = 1 << 30;  // k_sn_fwd_small item flag: row tiles I and I + 1 of a one-column-tile node
 struct SnView {
   const double* panel;
   const long* panel_off;  // [nodes] first double of the node's panel

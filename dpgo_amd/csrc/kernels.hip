@@ -3341,11 +3341,8 @@ __global__ __launch_bounds__(kThreads) void k_sn_assemble(SnView v, const int2* 
 // a tile's 64 vector elements (64 R doubles) through registers: element e = tid + 256 i, i < kSnVecRegs
 constexpr int kSnVecRegs = (kSnTileDev * 8 + kThreads - 1) / kThreads;  // enough for R <= 8
 
-#ifndef DPGO_SNF_WAVES
-#define DPGO_SNF_WAVES 3  // k_sn_fwd's occupancy (waves per SIMD): its three-deep tile pipeline fits 168 VGPRs
-#endif
 template <int R>
-__global__ __launch_bounds__(kThreads, DPGO_SNF_WAVES) void k_sn_fwd(SnView v, const int2* __restrict__ items, int b,
+__global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __restrict__ items, int b,
                                                      double* __restrict__ y) {
   __shared__ double sfl[4 * kSnTileDev * R];  // triple-buffered frontal chunks, then the row tile's f rows (f_R)
   __shared__ int spz[kSnTileDev];                // the row tile's pose ids (S rows)
@@ -3473,7 +3470,7 @@ __global__ __launch_bounds__(kThreads, DPGO_SNF_WAVES) void k_sn_fwd(SnView v, c
 // tiles) is issued at once and waited for once -- in about half k_sn_fwd's registers, so more workgroups (and bytes)
 // are in flight per CU on the levels where each streams only 32-64 KB.
 #ifndef DPGO_SNF_SMALL_WAVES
-#define DPGO_SNF_SMALL_WAVES 4  // k_sn_fwd_small's occupancy (waves per SIMD): <= 128 VGPRs
+#define DPGO_SNF_SMALL_WAVES 1  // k_sn_fwd_small's occupancy hint (waves per SIMD; 1 = none)
 #endif
 template <int R>
 __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small(SnView v, const int2* __restrict__ items, int b,
@@ -3481,29 +3478,23 @@ __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small
   constexpr int kTileD = kSnTileDev * kSnTileDev, kChunk = kSnTileDev * R;
   constexpr int KV = (kSnSmallNs * kChunk + kThreads - 1) / kThreads;
   __shared__ double sf[kSnSmallNs * kChunk];  // frontal chunks 0 .. nJ - 1
-  __shared__ double sfr[kSnSmallNs][kChunk];   // the row tiles' f rows (f_R)
+  __shared__ double sfr[kChunk];               // the row tile's f rows (f_R)
   __shared__ int spz[kSnTileDev];              // the row tile's pose ids (S rows)
   const int2 it = items[blockIdx.x];
   if (v.node_agent && (agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x]) ||
                        (v.ident && v.ident[v.node_agent[it.x]]))) return;
-  // kSnPairBit: a node with one S column tile (ns = 1) hands one workgroup two consecutive row tiles I, I + 1 -- both
-  // read tile column 0 and frontal chunk 0 only, so their two tiles load together and the workgroup count halves
-  const bool pair = (it.y & kSnPairBit) != 0;
-  const int node = it.x, I = it.y & ~kSnPairBit, nrt = pair ? 2 : 1;
+  const int node = it.x, I = it.y;
   const int s = v.s[node], t = v.t[node], sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), ns = Sp / kSnTileDev;
   const double* __restrict__ f = v.F + v.f_off[node];
   const double* __restrict__ panel = v.panel + v.panel_off[node];
   const int* __restrict__ pz = v.poses + v.poses_off[node];
   const int tid = static_cast<int>(threadIdx.x), rq = tid >> 4, cq = tid & 15;
-  const int nJ = I < ns ? I + 1 : ns;  // <= kSnSmallNs (host: ns <= kSnSmallNs); 1 for a pair (ns = 1)
-  for (int u = 0; u < nrt; ++u) {
-    const int Iu = I + u;
-    if (Iu < ns) {
-      const int row = Iu * kSnTileDev + tid;
-      if (tid < kSnTileDev && row < sb) spz[tid] = pz[row / b];
-    } else {
-      for (int e = tid; e < kChunk; e += kThreads) sfr[u][e] = f[static_cast<long>(Iu) * kChunk + e];
-    }
+  const int nJ = I < ns ? I + 1 : ns;  // <= kSnSmallNs (host: ns <= kSnSmallNs)
+  if (I < ns) {
+    const int row = I * kSnTileDev + tid;
+    if (tid < kSnTileDev && row < sb) spz[tid] = pz[row / b];
+  } else {
+    for (int e = tid; e < kChunk; e += kThreads) sfr[e] = f[static_cast<long>(I) * kChunk + e];
   }
   double fv[KV];
 #pragma unroll
@@ -3512,25 +3503,17 @@ __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small
     if (e < nJ * kChunk) fv[i] = f[e];
   }
   const __amdgpu_buffer_rsrc_t rp = buf_rsrc(panel);
-  double p[kSnSmallNs][4][4];  // tiles (I, J), J < nJ; for a pair tiles (I, 0) and (I + 1, 0)
+  double p[kSnSmallNs][4][4];
   const long coff = v.cpanel_off ? v.cpanel_off[node] : -1;  // a narrow node's compact panel (workgroup-uniform)
   if (coff >= 0) {
     const SnCompact cm = sn_compact_view(v, coff, sb, tb);
 #pragma unroll
-    for (int J = 0; J < kSnSmallNs; ++J) {
-      if (pair)
-        sn_load_tile_cmp(cm, ns, I + J, 0, rq, cq, p[J]);
-      else if (J < nJ)
-        sn_load_tile_cmp(cm, ns, I, J, rq, cq, p[J]);
-    }
+    for (int J = 0; J < kSnSmallNs; ++J)
+      if (J < nJ) sn_load_tile_cmp(cm, ns, I, J, rq, cq, p[J]);
   } else {
 #pragma unroll
-    for (int J = 0; J < kSnSmallNs; ++J) {
-      if (pair)
-        sn_load_tile_buf(rp, 8u * static_cast<unsigned>(sn_tile_dev(ns, I + J, 0) * kTileD), rq, cq, p[J]);
-      else if (J < nJ)
-        sn_load_tile_buf(rp, 8u * static_cast<unsigned>(sn_tile_dev(ns, I, J) * kTileD), rq, cq, p[J]);
-    }
+    for (int J = 0; J < kSnSmallNs; ++J)
+      if (J < nJ) sn_load_tile_buf(rp, 8u * static_cast<unsigned>(sn_tile_dev(ns, I, J) * kTileD), rq, cq, p[J]);
   }
 #pragma unroll
   for (int i = 0; i < KV; ++i) {
@@ -3538,62 +3521,50 @@ __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small
     if (e < nJ * kChunk) sf[e] = fv[i];
   }
   __syncthreads();
-  // row tile Iu: products with tiles p[0 .. nj - 1], the 16 column groups' sums in a fixed order, then y_S or the
-  // update u = f_R - M f_S.  A pair runs it twice with nj = 1, row tile I + 1's tile moved into p[0] in between.
-  const int nj = pair ? 1 : nJ;
-#pragma unroll 1
-  for (int u = 0; u < nrt; ++u) {
-    const int Iu = I + u;
-    double acc[4][R];
+  double acc[4][R];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int a = 0; a < R; ++a) acc[i][a] = 0.0;
+    for (int a = 0; a < R; ++a) acc[i][a] = 0.0;
 #pragma unroll
-    for (int J = 0; J < kSnSmallNs; ++J) {
-      if (J >= nj) break;
-      const double* cf = sf + J * kChunk;
+  for (int J = 0; J < kSnSmallNs; ++J) {
+    if (J >= nJ) break;
+    const double* cf = sf + J * kChunk;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        double fc[R];
+    for (int c = 0; c < 4; ++c) {
+      double fc[R];
 #pragma unroll
-        for (int a = 0; a < R; ++a) fc[a] = cf[(cq * 4 + c) * R + a];
+      for (int a = 0; a < R; ++a) fc[a] = cf[(cq * 4 + c) * R + a];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int a = 0; a < R; ++a) acc[i][a] = fma(p[J][i][c], fc[a], acc[i][a]);
-      }
+        for (int a = 0; a < R; ++a) acc[i][a] = fma(p[J][i][c], fc[a], acc[i][a]);
     }
+  }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int a = 0; a < R; ++a) {
-        double x = acc[i][a];
+    for (int a = 0; a < R; ++a) {
+      double x = acc[i][a];
 #pragma unroll
-        for (int off = 1; off < 16; off <<= 1) x += __shfl_xor(x, off, 64);
-        acc[i][a] = x;
-      }
-    if (cq == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = Iu * kSnTileDev + rq * 4 + i;
-        if (row < sb) {
-          const int pos = row / b, k = row - pos * b;
-          double* dst = y + (static_cast<long>(spz[rq * 4 + i]) * b + k) * R;
-#pragma unroll
-          for (int a = 0; a < R; ++a) dst[a] = acc[i][a];
-        } else if (row >= Sp && row - Sp < tb) {
-          const double* fr = sfr[u] + (rq * 4 + i) * R;
-          double* dst = v.U + v.u_off[node] + static_cast<long>(row - Sp) * R;
-#pragma unroll
-          for (int a = 0; a < R; ++a) dst[a] = fr[a] - acc[i][a];
-        }
-      }
+      for (int off = 1; off < 16; off <<= 1) x += __shfl_xor(x, off, 64);
+      acc[i][a] = x;
     }
+  if (cq != 0) return;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i) {
+    const int row = I * kSnTileDev + rq * 4 + i;
+    if (row < sb) {
+      const int pos = row / b, k = row - pos * b;
+      double* dst = y + (static_cast<long>(spz[rq * 4 + i]) * b + k) * R;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) p[0][i][c] = p[1][i][c];
+      for (int a = 0; a < R; ++a) dst[a] = acc[i][a];
+    } else if (row >= Sp && row - Sp < tb) {
+      const double* fr = sfr + (rq * 4 + i) * R;
+      double* dst = v.U + v.u_off[node] + static_cast<long>(row - Sp) * R;
+#pragma unroll
+      for (int a = 0; a < R; ++a) dst[a] = fr[a] - acc[i][a];
+    }
   }
 }
 
