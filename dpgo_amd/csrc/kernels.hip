@@ -409,6 +409,14 @@ constexpr int kIncStage = 512;
 #define DPGO_STAGE_V5 1
 #endif
 constexpr bool kStageV5 = DPGO_STAGE_V5 != 0;
+// A/B builds only (-DDPGO_STAGE_DMA=1 -DDPGO_LDS_REC_PAD=0): the standalone X.Q's stage by LDS-DMA (global_load_lds:
+// no VGPR destination, no ds_write pass).  Its LDS image is lane-linear, so the records lose their padding double
+// (the 4-way bank conflicts the pad removed come back) -- DESIGN.md section 3.5 has the measurement.
+#ifndef DPGO_STAGE_DMA
+#define DPGO_STAGE_DMA 0
+#endif
+constexpr bool kStageDma = DPGO_STAGE_DMA != 0;
+typedef __attribute__((address_space(3))) void lds_void_t;
 #ifndef DPGO_BUFFER_GATHER
 #define DPGO_BUFFER_GATHER 1
 #endif
@@ -1581,6 +1589,18 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
           s_recd[(ns + rr) * RS + 2 * w] = v.x;
           s_recd[(ns + rr) * RS + 2 * w + 1] = v.y;
         }
+      } else if constexpr (kStageDma && (MODE == MODE_XQ || MODE == MODE_XQ_G)) {
+        static_assert(RS == RW, "LDS-DMA staging writes the records lane-linearly: build with DPGO_LDS_REC_PAD=0");
+        const int lane = static_cast<int>(threadIdx.x) & 63, wave = static_cast<int>(threadIdx.x) >> 6;
+        const int nw = 2 * ni;  // incidences as 4-byte words (int2 entries need only 4-byte alignment)
+        const int* isrc = reinterpret_cast<const int*>(q.inc + i0);
+        for (int w0 = wave * 64; w0 < nw; w0 += kThreads)
+          __builtin_amdgcn_global_load_lds(isrc + min(w0 + lane, nw - 1),
+                                           (lds_void_t*)(reinterpret_cast<int*>(s_inc) + w0), 4, 0, 0);
+        const int nc = ne * (RW / 2);  // records as 16-byte chunks
+        const f64x2* rsrc = reinterpret_cast<const f64x2*>(q.rec) + static_cast<long>(e0) * (RW / 2);
+        for (int c0 = wave * 64; c0 < nc; c0 += kThreads)
+          __builtin_amdgcn_global_load_lds(rsrc + min(c0 + lane, nc - 1), (lds_void_t*)(s_recd + 2 * c0), 16, 0, 0);
       } else if constexpr (!kStageV5) {  // round 4's stage loop (A/B builds only, -DDPGO_STAGE_V5=0)
         for (int x = threadIdx.x; x < ni; x += kThreads) s_inc[x] = q.inc[i0 + x];
         const f64x2* src = reinterpret_cast<const f64x2*>(q.rec) + static_cast<long>(e0) * (RW / 2);
@@ -1625,6 +1645,7 @@ __global__ __launch_bounds__(kThreads, FMT == QFMT_EDGES ? evar_waves(VAR) : 1) 
       }
     }
     if (late_skip && skip) {  // uniform over the block: every thread leaves here
+      if constexpr (kStageDma) __builtin_amdgcn_s_waitcnt(0);  // no LDS-DMA write may outlive the workgroup
       if constexpr (spmm_fusable(MODE)) spmm_arrive(args, p.agent);
       return;
     }
