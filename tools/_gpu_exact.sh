@@ -11,3 +11,5 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_exa
   --robust GNC_TLS --burnin 60 --cpu-baseline 0 --boundary-leg 0 --exact-leg 0 > gpurun_out/${TAG}_exact_kt.log 2>&1 || exit 1
 python3 tools/rocpd_stats.py gpurun_out/prof_${TAG}_exact > gpurun_out/${TAG}_exact_kernel_stats.csv 2>&1 || exit 1
 head -12 gpurun_out/${TAG}_exact_kernel_stats.csv
+python3 tools/sweep_levels.py gpurun_out/prof_${TAG}_exact > gpurun_out/${TAG}_sweep_levels.txt 2>&1
+rm -rf gpurun_out/prof_${TAG}_exact  # the database exceeds what gpurun copies back
