@@ -1368,17 +1368,19 @@ int dpgo_hip_problem_create_batch(int num_agents, const int* poses_per_agent, in
       h->state.ensure(num_agents) || h->coef_a.ensure(num_agents) || h->coef_b.ensure(num_agents) ||
       h->arrive.ensure(num_agents))
     return cleanup(fail(DPGO_HIP_ENOMEM, "device allocation failed"));
-  // on the handle's (non-blocking) stream, then waited for: nothing the handle launches can overtake them
-  hipStream_t hs = h->stream;
-  if (hipMemcpyAsync(h->tile_agent.p, h->h_tile_agent.data(), sizeof(int) * T, hipMemcpyHostToDevice, hs) != hipSuccess ||
-      hipMemcpyAsync(h->tile_start.p, h->h_tile_start.data(), sizeof(int) * T, hipMemcpyHostToDevice, hs) != hipSuccess ||
-      hipMemcpyAsync(h->tile_count.p, h->h_tile_count.data(), sizeof(int) * T, hipMemcpyHostToDevice, hs) != hipSuccess ||
+  // on the null stream, then waited for, so nothing the handle later launches on its non-blocking stream can overtake
+  // them.  (Not on the handle's own stream: a stream's first command fixes which hardware queue it lands on, and
+  // giving the handle's stream its first work here, before the engine's other streams exist, put the two-stream split
+  // of small batches (TUNE_SPLIT_STREAMS) on a shared queue -- 1.41 against 1.11 ms/step at the 8-GPU share.)
+  if (hipMemcpyAsync(h->tile_agent.p, h->h_tile_agent.data(), sizeof(int) * T, hipMemcpyHostToDevice, nullptr) != hipSuccess ||
+      hipMemcpyAsync(h->tile_start.p, h->h_tile_start.data(), sizeof(int) * T, hipMemcpyHostToDevice, nullptr) != hipSuccess ||
+      hipMemcpyAsync(h->tile_count.p, h->h_tile_count.data(), sizeof(int) * T, hipMemcpyHostToDevice, nullptr) != hipSuccess ||
       hipMemcpyAsync(h->agent_tile_off.p, h->h_agent_tile_off.data(), sizeof(int) * (num_agents + 1),
-                     hipMemcpyHostToDevice, hs) != hipSuccess ||
-      hipMemcpyAsync(h->agent_np.p, poses_per_agent, sizeof(int) * num_agents, hipMemcpyHostToDevice, hs) != hipSuccess ||
-      hipMemsetAsync(h->state.p, 0, sizeof(AgentState) * num_agents, hs) != hipSuccess ||
-      hipMemsetAsync(h->arrive.p, 0, sizeof(int) * num_agents, hs) != hipSuccess ||
-      hipStreamSynchronize(hs) != hipSuccess)
+                     hipMemcpyHostToDevice, nullptr) != hipSuccess ||
+      hipMemcpyAsync(h->agent_np.p, poses_per_agent, sizeof(int) * num_agents, hipMemcpyHostToDevice, nullptr) != hipSuccess ||
+      hipMemsetAsync(h->state.p, 0, sizeof(AgentState) * num_agents, nullptr) != hipSuccess ||
+      hipMemsetAsync(h->arrive.p, 0, sizeof(int) * num_agents, nullptr) != hipSuccess ||
+      hipStreamSynchronize(nullptr) != hipSuccess)
     return cleanup(fail(DPGO_HIP_EDEVICE, "device upload failed"));
   if (const char* ev = std::getenv("DPGO_FUSE_FINALIZE")) h->fuse_finalize = std::atoi(ev);
   if (hipHostMalloc(reinterpret_cast<void**>(&h->pub_host), sizeof(int) * num_agents,
