@@ -1404,12 +1404,14 @@ int dpgo_hip_problem_destroy(dpgo_hip_problem h) {
     (void)hipStreamSynchronize(h->own_stream);
     (void)hipStreamDestroy(h->own_stream);
   }
-  if (h->split_stream) {
-    (void)hipStreamSynchronize(h->split_stream);
-    (void)hipStreamDestroy(h->split_stream);
-    (void)hipEventDestroy(h->split_fork);
-    (void)hipEventDestroy(h->split_join);
+  for (int g = 0; g < dpgo_hip_problem_s::kMaxSplit - 1; ++g) {
+    if (h->split_stream[g]) {
+      (void)hipStreamSynchronize(h->split_stream[g]);
+      (void)hipStreamDestroy(h->split_stream[g]);
+    }
+    if (h->split_join[g]) (void)hipEventDestroy(h->split_join[g]);
   }
+  if (h->split_fork) (void)hipEventDestroy(h->split_fork);
   (void)hipDeviceSynchronize();
   if (h->pub_host) (void)hipHostFree(h->pub_host);
   delete h;
@@ -2097,30 +2099,38 @@ int dpgo::optimize_dev_status(dpgo_hip_problem h, const dpgo_opt_params* params,
     // 100.8, profiles/r03ze_*).
     const bool classic_ahead = !merged && single && !qf0 && P.tr_max_inner > 0 && la == 2;
     if (split) {
-      if (!h->split_stream) {
-        HIP_TRY(hipStreamCreateWithFlags(&h->split_stream, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&h->split_fork, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&h->split_join, hipEventDisableTiming));
+      // groups of agents [a_g, a_g+1): two halves (values 1, 2), four groups (3) or one group per agent up to
+      // eight (4); group 0 on the launch stream, group g on split_stream[g - 1]
+      const int sv = h->tuning[dpgo::TUNE_SPLIT_STREAMS];
+      const int G = std::min(K, sv == 3 ? 4 : sv >= 4 ? dpgo_hip_problem_s::kMaxSplit : 2);
+      if (!h->split_fork) HIP_TRY(hipEventCreateWithFlags(&h->split_fork, hipEventDisableTiming));
+      for (int g = 0; g + 1 < G; ++g) {
+        if (!h->split_stream[g]) HIP_TRY(hipStreamCreateWithFlags(&h->split_stream[g], hipStreamNonBlocking));
+        if (!h->split_join[g]) HIP_TRY(hipEventCreateWithFlags(&h->split_join[g], hipEventDisableTiming));
       }
+      auto on = [&](int g) { return g == 0 ? h->stream : h->split_stream[g - 1]; };
+      auto first = [&](int g) { return static_cast<int>(static_cast<long>(K) * g / G); };
       // value 2: the second half starts once the first half's first iteration is done, so the two halves run
       // out of phase (one half's HESS_M beside the other's k_tcg_updir) rather than side by side
-      const bool offset = h->tuning[dpgo::TUNE_SPLIT_STREAMS] == 2;
-      const int am = K / 2;
+      const bool offset = sv == 2 && G == 2;
       if (!offset) {
         HIP_TRY(hipEventRecord(h->split_fork, h->stream));
-        HIP_TRY(hipStreamWaitEvent(h->split_stream, h->split_fork, 0));
+        for (int g = 1; g < G; ++g) HIP_TRY(hipStreamWaitEvent(on(g), h->split_fork, 0));
       }
       for (int j = 0; j < P.tr_max_inner; ++j) {
         const int mode = j == 0 ? dpgo::MODE_HESS_QF_M : dpgo::MODE_HESS_M;
-        DPGO_TRY(launch_merged_range(j, mode, dpgo::FLAG_TCG, dpgo::OP_TCG_STEP_CHECK, 0, am, h->stream));
+        DPGO_TRY(launch_merged_range(j, mode, dpgo::FLAG_TCG, dpgo::OP_TCG_STEP_CHECK, first(0), first(1), on(0)));
         if (offset && j == 0) {
           HIP_TRY(hipEventRecord(h->split_fork, h->stream));
-          HIP_TRY(hipStreamWaitEvent(h->split_stream, h->split_fork, 0));
+          HIP_TRY(hipStreamWaitEvent(on(1), h->split_fork, 0));
         }
-        DPGO_TRY(launch_merged_range(j, mode, dpgo::FLAG_TCG, dpgo::OP_TCG_STEP_CHECK, am, K, h->split_stream));
+        for (int g = 1; g < G; ++g)
+          DPGO_TRY(launch_merged_range(j, mode, dpgo::FLAG_TCG, dpgo::OP_TCG_STEP_CHECK, first(g), first(g + 1), on(g)));
       }
-      HIP_TRY(hipEventRecord(h->split_join, h->split_stream));
-      HIP_TRY(hipStreamWaitEvent(h->stream, h->split_join, 0));
+      for (int g = 1; g < G; ++g) {
+        HIP_TRY(hipEventRecord(h->split_join[g - 1], on(g)));
+        HIP_TRY(hipStreamWaitEvent(h->stream, h->split_join[g - 1], 0));
+      }
       cg_agents = true;
     } else if (all_ahead) {
       for (int j = 0; j < P.tr_max_inner; ++j)

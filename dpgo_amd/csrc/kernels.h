@@ -319,7 +319,8 @@ enum TuneKey { TUNE_SPMM_VARIANT = 0, TUNE_EDGE_VARIANT = 1, TUNE_EPI_PREFETCH =
                TUNE_SPLIT_STREAMS = 10,  // merged tCG queued at once: the batch's agents in two halves on two
                                          // streams (one half's VALU-bound HESS_M beside the other's HBM-bound
                                          // k_tcg_updir); 0 off, 1 on (default: 1M -0.7 %, the 125 k
-                                         // share -4.6 % ms/step), 2 the halves out of phase (no gain)
+                                         // share -4.6 % ms/step), 2 the halves out of phase (no gain),
+                                         // 3 four agent groups on four streams, 4 one group per agent (<= 8)
                TUNE_DEVICE_CHOL = 12,  // exact preconditioner over an edge-stream Q: 1 numeric factorisation on the
                                        // device (k_sn_factor), 0 on the host (chol.cpp, panels uploaded)
                TUNE_SPMM_V2 = 11,  // > 0: the merged partials at kMergedDdSlots (edge variant bit 6) and the rotated

@@ -182,10 +182,11 @@ struct dpgo_hip_problem_s {
   // its agent's outcome was decided (an in-place X_in is overwritten by then)
   dpgo::DevBuf<double> pc;
   dpgo::DevBuf<double> peh;  // merged tCG: k_tcg_updir's <eta_old, Hdelta> partials (FinalizeArgs::pc)
-  // TUNE_SPLIT_STREAMS: the second half of the agents' merged tCG iterations run on split_stream, forked
+  // TUNE_SPLIT_STREAMS: agent groups 1.. of the merged tCG iterations run on split_stream[g - 1], forked
   // from / joined into the launch stream by events
-  hipStream_t split_stream = nullptr;
-  hipEvent_t split_fork = nullptr, split_join = nullptr;
+  static constexpr int kMaxSplit = 8;
+  hipStream_t split_stream[kMaxSplit - 1] = {};
+  hipEvent_t split_fork = nullptr, split_join[kMaxSplit - 1] = {};
   dpgo::DevBuf<dpgo::AgentState> state;
   std::vector<dpgo::AgentState> h_state;
   // per-agent arrival counts of a k_spmm with a fused finalize (0 between launches)

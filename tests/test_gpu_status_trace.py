@@ -723,13 +723,13 @@ def test_status_fold_bitwise(hip, accel):
 
 def test_split_streams_bitwise(hip):
     """The merged tCG iterations queued at once with the batch's agents in two halves on two streams (tuning
-    key TUNE_SPLIT_STREAMS) give bitwise the one-stream iterates, traces and counters: the halves touch
+    key TUNE_SPLIT_STREAMS; also four groups and one group per agent) give bitwise the one-stream iterates, traces and counters: the halves touch
     disjoint agents' poses, tiles, partial slots and finalize rows."""
     g = hip.Graph.grid3d(12, seed=5)
     aop = g.grid_partition(2)
     X0, _, _ = g.distributed_init(aop, 5, hip.lifting_matrix(3, 5), gpu=True, rtol=1e-12, dev_layout=True)
     out = []
-    for split in (0, 1, 2):
+    for split in (0, 1, 2, 3, 4):
         hip.set_tuning(10, split)
         hip.set_tuning(7, 2)  # every tCG iteration queued at once (the path the split applies to)
         try:
