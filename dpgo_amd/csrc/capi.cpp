@@ -785,17 +785,44 @@ int sync_chol(dpgo_hip_problem h) {
   }
   h->sn_guards = guards;
   if (device && dpgo::poison_enabled()) HIP_TRY(dpgo::poison_fill(h->sn_panel.p, sizeof(double) * po, h->stream));
-  if (!device)
+  if (!device) {
+    // The host factor's panels go up through a pinned staging buffer, one agent at a time: one DMA per node from
+    // pinned memory instead of the runtime's pageable-copy path (DPGO_PANEL_UPLOAD_DIRECT=1: the pageable copies).
+    const char* dv = std::getenv("DPGO_PANEL_UPLOAD_DIRECT");
+    const bool direct = dv != nullptr && std::atoi(dv) != 0;
+    size_t stage_n = 0;
+    for (int a = 0; a < K && !direct; ++a) {
+      size_t na = 0;
+      for (const auto& nd : Fs[a].nodes) na += nd.panel.size();
+      stage_n = std::max(stage_n, na);
+    }
+    double* stage = nullptr;
+    if (stage_n > 0 && hipHostMalloc(reinterpret_cast<void**>(&stage), sizeof(double) * stage_n) != hipSuccess)
+      return fail(DPGO_HIP_ENOMEM, "pinned staging buffer for the panels");
+    struct StageFree {
+      double* p;
+      ~StageFree() {
+        if (p) (void)hipHostFree(p);
+      }
+    } stage_free{stage};
     for (int a = 0; a < K; ++a) {
+      size_t so = 0;
       for (size_t x = 0; x < Fs[a].nodes.size(); ++x) {
         const auto& P = Fs[a].nodes[x].panel;
-        if (!P.empty())
-          HIP_TRY(hipMemcpyAsync(h->sn_panel.p + panel_off[base[a] + x], P.data(), sizeof(double) * P.size(),
-                                 hipMemcpyHostToDevice, h->stream));
+        if (P.empty()) continue;
+        const double* src = P.data();
+        if (!direct) {
+          std::memcpy(stage + so, P.data(), sizeof(double) * P.size());
+          src = stage + so;
+          so += P.size();
+        }
+        HIP_TRY(hipMemcpyAsync(h->sn_panel.p + panel_off[base[a] + x], src, sizeof(double) * P.size(),
+                               hipMemcpyHostToDevice, h->stream));
       }
-      HIP_TRY(hipStreamSynchronize(h->stream));  // then release the agent's host panels
+      HIP_TRY(hipStreamSynchronize(h->stream));  // then release the agent's host panels (and reuse the stage)
       for (auto& nd : Fs[a].nodes) std::vector<double>().swap(nd.panel);
     }
+  }
   DPGO_TRY(up(h->sn_panel_off, panel_off));
   DPGO_TRY(up(h->sn_f_off, f_off));
   DPGO_TRY(up(h->sn_u_off, u_off));
@@ -1358,6 +1385,15 @@ int dpgo_hip_problem_create_batch(int num_agents, const int* poses_per_agent, in
   if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess)
     return cleanup(fail(DPGO_HIP_EDEVICE, "hipStreamCreate failed"));
   h->stream = h->own_stream;
+  // A/B only: the exact preconditioner's panels in physically contiguous memory (DPGO_PANEL_CONTIG bit 0: the tile
+  // panels, bit 1: the compact copies; DevBuf falls back to hipMalloc when it cannot be had).  Not the default: the
+  // exact tests then read wrong panel values after earlier problems of the process freed theirs.
+  {
+    const char* ev = std::getenv("DPGO_PANEL_CONTIG");
+    const int cm = ev == nullptr ? 0 : std::atoi(ev);
+    if (cm & 1) h->sn_panel.alloc_flags = hipDeviceMallocContiguous;
+    if (cm & 2) h->sn_cpanel.alloc_flags = hipDeviceMallocContiguous;
+  }
   const int T = h->num_tiles;
   if (h->tile_agent.ensure(T) || h->tile_start.ensure(T) || h->tile_count.ensure(T) ||
       h->agent_tile_off.ensure(num_agents + 1) || h->agent_np.ensure(num_agents) ||

@@ -3294,12 +3294,23 @@ __device__ __forceinline__ void sn_load_tile_cmp(const SnCompact& cm, int ns, in
   }
 }
 
+// A/B probe only (-DDPGO_SN_ACQUIRE_TEST): an agent-scope acquire (L2 invalidate) at the start of every supernodal
+// kernel, to test whether a wrong exact-preconditioner result with contiguous panel memory is a stale L2 line
+#ifdef DPGO_SN_ACQUIRE_TEST
+#define DPGO_SN_ACQUIRE() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent")
+#else
+#define DPGO_SN_ACQUIRE() \
+  do {                    \
+  } while (0)
+#endif
+
 // The compact copy of narrow supernodes' panels: item (node, block of 64 compact rows); compact row cr < sb is S row
 // cr, row sb + q is R row q; column c < sb (columns sb .. ld - 1 are zero)
 __global__ __launch_bounds__(kThreads) void k_sn_compact(int b, const double* __restrict__ panel,
                                                          const long* __restrict__ panel_off, const int* __restrict__ sv,
                                                          const int* __restrict__ tv, const long* __restrict__ cpanel_off,
                                                          double* __restrict__ cpanel, const int2* __restrict__ items) {
+  DPGO_SN_ACQUIRE();
   const int2 it = items[blockIdx.x];
   const int node = it.x;
   const int sb = sv[node] * b, tb = tv[node] * b, ld = sn_compact_ld(sb), Sp = sn_pad_dev(sb), ns = Sp / kSnTileDev;
@@ -3322,6 +3333,7 @@ __global__ __launch_bounds__(kThreads) void k_sn_compact(int b, const double* __
 template <int R>
 __global__ __launch_bounds__(kThreads) void k_sn_assemble(SnView v, const int2* __restrict__ items, int b,
                                                           const double* __restrict__ rhs) {
+  DPGO_SN_ACQUIRE();
   const int2 it = items[blockIdx.x];
   if (v.node_agent && (agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x]) ||
                        (v.ident && v.ident[v.node_agent[it.x]]))) return;
@@ -3365,6 +3377,7 @@ constexpr int kSnVecRegs = (kSnTileDev * 8 + kThreads - 1) / kThreads;  // enoug
 template <int R>
 __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __restrict__ items, int b,
                                                      double* __restrict__ y) {
+  DPGO_SN_ACQUIRE();
   __shared__ double sfl[4 * kSnTileDev * R];  // triple-buffered frontal chunks, then the row tile's f rows (f_R)
   __shared__ int spz[kSnTileDev];                // the row tile's pose ids (S rows)
   const int2 it = items[blockIdx.x];
@@ -3496,6 +3509,7 @@ __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __res
 template <int R>
 __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small(SnView v, const int2* __restrict__ items, int b,
                                                            double* __restrict__ y) {
+  DPGO_SN_ACQUIRE();
   constexpr int kTileD = kSnTileDev * kSnTileDev, kChunk = kSnTileDev * R;
   constexpr int KV = (kSnSmallNs * kChunk + kThreads - 1) / kThreads;
   __shared__ double sf[kSnSmallNs * kChunk];  // frontal chunks 0 .. nJ - 1
@@ -3592,6 +3606,7 @@ __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small
 template <int R>
 __global__ __launch_bounds__(kThreads) void k_sn_bwd(SnView v, const int2* __restrict__ items, int b,
                                                      const double* __restrict__ y, double* __restrict__ x) {
+  DPGO_SN_ACQUIRE();
   __shared__ double sg[2][kSnTileDev * R];  // double-buffered [y_S ; -x_R] chunks
   __shared__ double red[kThreads / 64][16][4 * R];
   const int2 it = items[blockIdx.x];
@@ -3821,6 +3836,7 @@ __device__ __forceinline__ int sn_frow(int pos, int k, int s, int b, int Sp) {
 
 template <int B>
 __global__ __launch_bounds__(kThreads) void k_sn_factor(SnFactorView v) {
+  DPGO_SN_ACQUIRE();
   constexpr int D = B - 1, RW = edge_rec_width(D), DW = diag_width(D);
   __shared__ double As[kFT * kFLD], Bs[kFT * kFLD];
   __shared__ int s_bad;
@@ -3983,6 +3999,7 @@ __global__ __launch_bounds__(kThreads) void k_sn_factor(SnFactorView v) {
 // ------------------------------------------------------------------------------------------
 template <int B>
 __global__ __launch_bounds__(kThreads) void k_snf_asm(SnFactorView v, const int2* __restrict__ items, int phase) {
+  DPGO_SN_ACQUIRE();
   constexpr int D = B - 1, RW = edge_rec_width(D), DW = diag_width(D);
   const int2 it = items[blockIdx.x];
   const int g = it.x;
@@ -4058,6 +4075,7 @@ constexpr int kSnfBlockK = 4;
 // (node, I); 3: F_IJ -= L_IK L_JK^T, item (node, I << 16 | J); 4: the panel's tile (I, J = param), item (node, I)
 template <int B, int KIND>
 __global__ __launch_bounds__(kThreads) void k_snf_tile(SnFactorView v, const int2* __restrict__ items, int P) {
+  DPGO_SN_ACQUIRE();
   constexpr int kind = KIND;
   __shared__ double As[kFT * kFLD], Bs[kFT * kFLD];
   __shared__ int s_bad;

@@ -50,6 +50,7 @@ template <typename T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;
+  unsigned alloc_flags = 0;  // hipExtMallocWithFlags flags (e.g. hipDeviceMallocContiguous); hipMalloc if it fails
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
@@ -63,7 +64,15 @@ struct DevBuf {
     if (count <= n && p) return hipSuccess;
     release();
     n = std::max<size_t>(count, 1);
-    const hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), n * sizeof(T));
+    hipError_t e = hipErrorMemoryAllocation;
+    if (alloc_flags != 0) {
+      e = hipExtMallocWithFlags(reinterpret_cast<void**>(&p), n * sizeof(T), alloc_flags);
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        p = nullptr;
+      }
+    }
+    if (e != hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&p), n * sizeof(T));
     if (e != hipSuccess || !poison_enabled()) return e;
     const hipError_t f = poison_fill(p, n * sizeof(T), nullptr);
     return f != hipSuccess ? f : hipDeviceSynchronize();
