@@ -27,6 +27,17 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# HIP hardware queues per process (HIP's default: 4), read when the runtime initialises: a stream takes its queue at
+# its first command, and a run with N > 1 has more live streams than 4 -- the launch stream, one second-half stream per
+# colour problem (TUNE_SPLIT_STREAMS), the halo side stream, the collective's stream.  Two of them sharing a queue
+# serialise (the 8-GPU share measured 1.38 instead of 1.10 ms/step with its two halves on one queue).
+# Spawned ranks inherit the value.
+try:
+    _hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+except ValueError:
+    _hwq = 4
+if _hwq < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 METRIC = "RBCD iters/sec + X·Q SpMM HBM GB/s, 1M-pose synth grid r=5, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -446,6 +457,7 @@ def main():
     # the communicator reports it, ranks sharing a device, and per colour this rank's halo bytes and exchange time
     comm = {"world_size": world, "gpus_arg": args.gpus, "backend": dist.get_backend() if world > 1 else None,
             "torch_world": dist.get_world_size() if world > 1 else 1,
+            "hip_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")),
             "launcher": ("bench.py spawn (one child process per rank)" if os.environ.get("DPGO_BENCH_SPAWNED")
                          else "external (torchrun or equivalent)" if world > 1 else None)}
     if native:
