@@ -31,12 +31,14 @@ sys.path.insert(0, ROOT)
 # its first command, and a run with N > 1 has more live streams than 4 -- the launch stream, one second-half stream per
 # colour problem (TUNE_SPLIT_STREAMS), the halo side stream, the collective's stream.  Two of them sharing a queue
 # serialise (the 8-GPU share measured 1.38 instead of 1.10 ms/step with its two halves on one queue).
-# Spawned ranks inherit the value.
+# Spawned ranks inherit the value.  Not for the one-device rehearsal (DPGO_BENCH_ONE_DEVICE=1): N processes x 8
+# queues on one device oversubscribe its hardware queue slots (k = 48 rehearsal: N = 4 4.5 -> 43 ms/step, N = 8 23.6 ->
+# 79, profiles/r06fin_spawn_rehearsal_q8_*); one process per device, as the driver's runs are, holds 8 on its own device.
 try:
     _hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
 except ValueError:
     _hwq = 4
-if _hwq < 8:
+if _hwq < 8 and os.environ.get("DPGO_BENCH_ONE_DEVICE") != "1":
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 METRIC = "RBCD iters/sec + X·Q SpMM HBM GB/s, 1M-pose synth grid r=5, 1/2/4/8 GPUs"
