@@ -499,6 +499,12 @@ bool sn_compact_on() {
   return !(e && e[0] == '0');
 }
 
+// the sweeps read their items' records (SnView::desc); DPGO_SN_DESC=0: the per-node arrays (A/B)
+bool sn_desc_on() {
+  const char* e = std::getenv("DPGO_SN_DESC");
+  return !(e && e[0] == '0');
+}
+
 // The narrow supernodes' compact panels from the freshly factorised tiles (stream-ordered after the factor)
 int compact_panels(dpgo_hip_problem h) {
   if (!h->sn_compact || h->sn_citems_n == 0) return DPGO_HIP_OK;
@@ -870,6 +876,24 @@ int sync_chol(dpgo_hip_problem h) {
     DPGO_TRY(up(h->sn_cpanel_off, coff));
     DPGO_TRY(up(h->sn_citems, citems));
     HIP_TRY(h->sn_cpanel.ensure(std::max<long>(co, 1)));
+    // every sweep item's record (k_sn_fwd, k_sn_fwd_small, k_sn_bwd read it in one load)
+    std::vector<dpgo::SnItem> desc(items.size());
+    for (size_t i = 0; i < items.size(); ++i) {
+      const int g = items[i].x;
+      dpgo::SnItem& d = desc[i];
+      d.node = g;
+      d.tile = items[i].y;
+      d.agent = node_agent[g];
+      d.s = s_[g];
+      d.t = t_[g];
+      d.pad = 0;
+      d.f_off = f_off[g];
+      d.u_off = u_off[g];
+      d.panel_off = panel_off[g];
+      d.cpanel_off = h->sn_compact ? coff[g] : -1;
+      d.poses_off = poses_off[g];
+    }
+    DPGO_TRY(up(h->sn_desc, desc));
   }
   HIP_TRY(h->sn_F.ensure(std::max<long>(fo, 1)));
   HIP_TRY(h->sn_U.ensure(std::max<long>(uo, 1)));
@@ -1064,11 +1088,13 @@ int exact_precond(dpgo_hip_problem h, const double* in, double* z_out, double* d
   DPGO_TRY(sync_chol(h));
   const double* zraw = in;
   if (h->chol_state == 1) {
-    const dpgo::SnView v{h->sn_panel.p, h->sn_panel_off.p, h->sn_s.p,    h->sn_t.p,    h->sn_poses_off.p,
-                         h->sn_poses.p, h->sn_f_off.p,     h->sn_u_off.p, h->sn_cpos_off.p, h->sn_cpos.p,
-                         h->sn_contrib.p, h->sn_F.p,       h->sn_U.p,    h->sn_node_agent.p, h->state.p, flag,
-                         h->fac_not_pd.p, h->sn_cpanel.p, h->sn_compact ? h->sn_cpanel_off.p : nullptr};
+    dpgo::SnView v{h->sn_panel.p, h->sn_panel_off.p, h->sn_s.p,    h->sn_t.p,    h->sn_poses_off.p,
+                   h->sn_poses.p, h->sn_f_off.p,     h->sn_u_off.p, h->sn_cpos_off.p, h->sn_cpos.p,
+                   h->sn_contrib.p, h->sn_F.p,       h->sn_U.p,    h->sn_node_agent.p, h->state.p, flag,
+                   h->fac_not_pd.p, h->sn_cpanel.p, h->sn_compact ? h->sn_cpanel_off.p : nullptr};
     const int2* it = h->sn_items.p;
+    v.desc = sn_desc_on() ? h->sn_desc.p : nullptr;
+    v.items_base = it;
     const int nl = static_cast<int>(h->sn_levels.size());
     if (dpgo::poison_enabled())  // debug: frontal / update / sweep vectors as nothing-written NaN
       for (auto* B : {&h->sn_F, &h->sn_U, &h->tA, &h->tB}) HIP_TRY(dpgo::poison_fill(B->p, sizeof(double) * B->n, h->stream));
@@ -3078,11 +3104,13 @@ int dpgo_hip_bench_precond(dpgo_hip_problem h, const double* V_dev, int reps, do
   *ms_fwd = *ms_bwd = 0.0;
   *panel_bytes = 8.0 * static_cast<double>(h->chol_doubles);  // the stored tiles (dpgo_hip_exact_sweep_bytes: read)
   if (h->chol_state != 1) return DPGO_HIP_OK;
-  const dpgo::SnView v{h->sn_panel.p, h->sn_panel_off.p, h->sn_s.p,    h->sn_t.p,    h->sn_poses_off.p,
-                       h->sn_poses.p, h->sn_f_off.p,     h->sn_u_off.p, h->sn_cpos_off.p, h->sn_cpos.p,
-                       h->sn_contrib.p, h->sn_F.p,       h->sn_U.p,    h->sn_node_agent.p, h->state.p, dpgo::FLAG_NONE,
-                       h->fac_not_pd.p, h->sn_cpanel.p, h->sn_compact ? h->sn_cpanel_off.p : nullptr};
+  dpgo::SnView v{h->sn_panel.p, h->sn_panel_off.p, h->sn_s.p,    h->sn_t.p,    h->sn_poses_off.p,
+                 h->sn_poses.p, h->sn_f_off.p,     h->sn_u_off.p, h->sn_cpos_off.p, h->sn_cpos.p,
+                 h->sn_contrib.p, h->sn_F.p,       h->sn_U.p,    h->sn_node_agent.p, h->state.p, dpgo::FLAG_NONE,
+                 h->fac_not_pd.p, h->sn_cpanel.p, h->sn_compact ? h->sn_cpanel_off.p : nullptr};
   const int2* it = h->sn_items.p;
+  v.desc = sn_desc_on() ? h->sn_desc.p : nullptr;
+  v.items_base = it;
   const int nl = static_cast<int>(h->sn_levels.size());
   ScopedEvents sev(3);  // destroyed on every return, the early HIP_TRY ones included
   HIP_TRY(sev.create());

@@ -204,6 +204,16 @@ struct GEdges {
 // ((S_pad + R_pad) scalar rows x r) and update vectors U (t b rows x r) are work space.
 constexpr int kSnTileDev = 64;
 constexpr int kSnSmallNs = 2;  // k_sn_fwd_small: nodes of at most this many S column tiles
+// One sweep item (supernode, tile) with everything its workgroup needs before its first data load: one 64-byte
+// record instead of the item, then the node's agent, then the agent's flags, then the node's sizes and offsets --
+// three dependent round trips ahead of the panel loads, which on the deep levels (tens of thousands of workgroups
+// streaming 16-64 KB each) are most of a workgroup's life.
+struct alignas(64) SnItem {
+  int node, tile, agent, s, t, pad;
+  long f_off, u_off, panel_off, cpanel_off, poses_off;  // cpanel_off -1: tiles only
+};
+static_assert(sizeof(SnItem) == 64, "one cache line per sweep item");
+
 struct SnView {
   const double* panel;
   const long* panel_off;  // [nodes] first double of the node's panel
@@ -232,6 +242,10 @@ struct SnView {
   // tiles (the same products in the same order, padding entries read as exact zeros); -1: tiles only.
   const double* cpanel = nullptr;
   const long* cpanel_off = nullptr;
+  // per item of items_base (SnItem): k_sn_fwd, k_sn_fwd_small and k_sn_bwd read their item's record there (null:
+  // from the arrays above)
+  const SnItem* desc = nullptr;
+  const int2* items_base = nullptr;
 };
 
 // The compact copy of the narrow supernodes' panels (SnView::cpanel) from their tiles: items (node, 64-row block of

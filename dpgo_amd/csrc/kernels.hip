@@ -3268,6 +3268,29 @@ struct SnCompact {
   __amdgpu_buffer_rsrc_t r;
   int sb, tb, ld;
 };
+// The item's record: from SnView::desc (one load), or assembled from the per-node arrays
+__device__ __forceinline__ SnItem sn_item(const SnView& v, const int2* items) {
+  const long idx = static_cast<long>(blockIdx.x);
+  if (v.desc != nullptr) return v.desc[(items - v.items_base) + idx];
+  const int2 it = items[idx];
+  SnItem d;
+  d.node = it.x;
+  d.tile = it.y;
+  d.agent = v.node_agent ? v.node_agent[it.x] : 0;
+  d.s = v.s[it.x];
+  d.t = v.t[it.x];
+  d.pad = 0;
+  d.f_off = v.f_off[it.x];
+  d.u_off = v.u_off[it.x];
+  d.panel_off = v.panel_off[it.x];
+  d.cpanel_off = v.cpanel_off ? v.cpanel_off[it.x] : -1;
+  d.poses_off = v.poses_off[it.x];
+  return d;
+}
+__device__ __forceinline__ bool sn_item_skipped(const SnView& v, const SnItem& d) {
+  return v.node_agent && (agent_skipped(v.state, v.flag_kind, 0, d.agent) || (v.ident && v.ident[d.agent]));
+}
+
 __device__ __forceinline__ SnCompact sn_compact_view(const SnView& v, long coff, int sb, int tb) {
   const int ld = sn_compact_ld(sb);
   return SnCompact{__builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(v.cpanel + coff), static_cast<short>(0),
@@ -3380,17 +3403,16 @@ __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __res
   DPGO_SN_ACQUIRE();
   __shared__ double sfl[4 * kSnTileDev * R];  // triple-buffered frontal chunks, then the row tile's f rows (f_R)
   __shared__ int spz[kSnTileDev];                // the row tile's pose ids (S rows)
-  const int2 it = items[blockIdx.x];
-  if (v.node_agent && (agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x]) ||
-                       (v.ident && v.ident[v.node_agent[it.x]]))) return;
+  const SnItem d = sn_item(v, items);
+  if (sn_item_skipped(v, d)) return;
   constexpr int kTileD = kSnTileDev * kSnTileDev, kChunk = kSnTileDev * R;
   double (*sf)[kChunk] = reinterpret_cast<double (*)[kChunk]>(sfl);
   double* __restrict__ sfr = sfl + 3 * kChunk;
-  const int node = it.x, I = it.y;
-  const int s = v.s[node], t = v.t[node], sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), ns = Sp / kSnTileDev;
-  const double* __restrict__ f = v.F + v.f_off[node];
-  const double* __restrict__ panel = v.panel + v.panel_off[node];
-  const int* __restrict__ pz = v.poses + v.poses_off[node];
+  const int I = d.tile;
+  const int s = d.s, t = d.t, sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), ns = Sp / kSnTileDev;
+  const double* __restrict__ f = v.F + d.f_off;
+  const double* __restrict__ panel = v.panel + d.panel_off;
+  const int* __restrict__ pz = v.poses + d.poses_off;
   const int tid = static_cast<int>(threadIdx.x), rq = tid >> 4, cq = tid & 15;
   // the epilogue's operands (the S rows' pose ids, or the R rows' f values) staged into LDS with chunk 0: the
   // workgroup's outputs then wait on no load after the sweep
@@ -3491,7 +3513,7 @@ __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __res
       for (int a = 0; a < R; ++a) dst[a] = acc[i][a];
     } else if (row >= Sp && row - Sp < tb) {  // update u = f_R - M f_S
       const double* fr = sfr + (rq * 4 + i) * R;
-      double* dst = v.U + v.u_off[node] + static_cast<long>(row - Sp) * R;
+      double* dst = v.U + d.u_off + static_cast<long>(row - Sp) * R;
 #pragma unroll
       for (int a = 0; a < R; ++a) dst[a] = fr[a] - acc[i][a];
     }
@@ -3515,14 +3537,13 @@ __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small
   __shared__ double sf[kSnSmallNs * kChunk];  // frontal chunks 0 .. nJ - 1
   __shared__ double sfr[kChunk];               // the row tile's f rows (f_R)
   __shared__ int spz[kSnTileDev];              // the row tile's pose ids (S rows)
-  const int2 it = items[blockIdx.x];
-  if (v.node_agent && (agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x]) ||
-                       (v.ident && v.ident[v.node_agent[it.x]]))) return;
-  const int node = it.x, I = it.y;
-  const int s = v.s[node], t = v.t[node], sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), ns = Sp / kSnTileDev;
-  const double* __restrict__ f = v.F + v.f_off[node];
-  const double* __restrict__ panel = v.panel + v.panel_off[node];
-  const int* __restrict__ pz = v.poses + v.poses_off[node];
+  const SnItem d = sn_item(v, items);
+  if (sn_item_skipped(v, d)) return;
+  const int I = d.tile;
+  const int s = d.s, t = d.t, sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), ns = Sp / kSnTileDev;
+  const double* __restrict__ f = v.F + d.f_off;
+  const double* __restrict__ panel = v.panel + d.panel_off;
+  const int* __restrict__ pz = v.poses + d.poses_off;
   const int tid = static_cast<int>(threadIdx.x), rq = tid >> 4, cq = tid & 15;
   const int nJ = I < ns ? I + 1 : ns;  // <= kSnSmallNs (host: ns <= kSnSmallNs)
   if (I < ns) {
@@ -3539,7 +3560,7 @@ __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small
   }
   const __amdgpu_buffer_rsrc_t rp = buf_rsrc(panel);
   double p[kSnSmallNs][4][4];
-  const long coff = v.cpanel_off ? v.cpanel_off[node] : -1;  // a narrow node's compact panel (workgroup-uniform)
+  const long coff = d.cpanel_off;  // a narrow node's compact panel (workgroup-uniform)
   if (coff >= 0) {
     const SnCompact cm = sn_compact_view(v, coff, sb, tb);
 #pragma unroll
@@ -3596,7 +3617,7 @@ __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small
       for (int a = 0; a < R; ++a) dst[a] = acc[i][a];
     } else if (row >= Sp && row - Sp < tb) {
       const double* fr = sfr + (rq * 4 + i) * R;
-      double* dst = v.U + v.u_off[node] + static_cast<long>(row - Sp) * R;
+      double* dst = v.U + d.u_off + static_cast<long>(row - Sp) * R;
 #pragma unroll
       for (int a = 0; a < R; ++a) dst[a] = fr[a] - acc[i][a];
     }
@@ -3609,14 +3630,13 @@ __global__ __launch_bounds__(kThreads) void k_sn_bwd(SnView v, const int2* __res
   DPGO_SN_ACQUIRE();
   __shared__ double sg[2][kSnTileDev * R];  // double-buffered [y_S ; -x_R] chunks
   __shared__ double red[kThreads / 64][16][4 * R];
-  const int2 it = items[blockIdx.x];
-  if (v.node_agent && (agent_skipped(v.state, v.flag_kind, 0, v.node_agent[it.x]) ||
-                       (v.ident && v.ident[v.node_agent[it.x]]))) return;
-  const int node = it.x, J = it.y;
-  const int s = v.s[node], t = v.t[node], sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), Rp = sn_pad_dev(tb);
+  const SnItem d = sn_item(v, items);
+  if (sn_item_skipped(v, d)) return;
+  const int J = d.tile;
+  const int s = d.s, t = d.t, sb = s * b, tb = t * b, Sp = sn_pad_dev(sb), Rp = sn_pad_dev(tb);
   const int ns = Sp / kSnTileDev, nI = (Sp + Rp) / kSnTileDev;
-  const double* __restrict__ panel = v.panel + v.panel_off[node];
-  const int* __restrict__ poses = v.poses + v.poses_off[node];
+  const double* __restrict__ panel = v.panel + d.panel_off;
+  const int* __restrict__ poses = v.poses + d.poses_off;
   const int tid = static_cast<int>(threadIdx.x), rq = tid >> 4, cq = tid & 15;
   double acc[4][R];  // columns 4 cq + c
 #pragma unroll
@@ -3650,7 +3670,7 @@ __global__ __launch_bounds__(kThreads) void k_sn_bwd(SnView v, const int2* __res
       if (e < kChunk) sg[buf][e] = gv[i];
     }
   };
-  const long coff = v.cpanel_off ? v.cpanel_off[node] : -1;  // a narrow node's compact panel (workgroup-uniform)
+  const long coff = d.cpanel_off;  // a narrow node's compact panel (workgroup-uniform)
   const SnCompact cm = coff >= 0 ? sn_compact_view(v, coff, sb, tb) : SnCompact{buf_rsrc(panel), 0, 0, 0};
   auto load_tile = [&](int I, double (&pt)[4][4]) {
     if (coff >= 0)

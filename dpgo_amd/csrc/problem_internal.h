@@ -145,6 +145,7 @@ struct dpgo_hip_problem_s {
   dpgo::DevBuf<double> sn_cpanel;
   dpgo::DevBuf<long> sn_cpanel_off;
   dpgo::DevBuf<int2> sn_citems;
+  dpgo::DevBuf<dpgo::SnItem> sn_desc;  // [items] per sweep item its node's record (SnView::desc)
   int sn_citems_n = 0;
   bool sn_compact = false;
   double sn_sweep_bytes_fwd = 0.0, sn_sweep_bytes_bwd = 0.0;
