@@ -102,6 +102,37 @@ __device__ __forceinline__ double lane_plus16(double v) {
   return __longlong_as_double((static_cast<long long>(b[1]) << 32) | static_cast<unsigned int>(a[1]));
 }
 
+// Sum over each row of 16 lanes, every lane of the row getting it: __shfl_xor's butterfly (partners l ^ 1, ^ 2, ^ 4,
+// ^ 8) bitwise, from DPP moves instead of eight ds_bpermute per double.  After each step both lanes of a pair hold
+// the same value, so the row_half_mirror partner (7 - l, the other quad of the 8) and the row_mirror partner (15 - l,
+// the other 8 of the row) add the same two numbers as the xor partners (IEEE addition commutes).
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]: l ^ 1
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]: l ^ 2
+  v += dpp_f64<0x141>(v);  // row_half_mirror
+  v += dpp_f64<0x140>(v);  // row_mirror
+  return v;
+}
+// value of lane l ^ 16 / l ^ 32 (__shfl_xor(v, 16 / 32)) from one v_permlane16_swap / v_permlane32_swap per half
+__device__ __forceinline__ double lane_xor16(double v) {
+  const long long l = __double_as_longlong(v);
+  const int lo = static_cast<int>(l), hi = static_cast<int>(l >> 32);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);  // [0]: rows (0,0,2,2), [1]: rows (1,1,3,3)
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const bool odd = (__lane_id() >> 4) & 1;
+  const int rl = odd ? a[0] : a[1], rh = odd ? b[0] : b[1];
+  return __longlong_as_double((static_cast<long long>(rh) << 32) | static_cast<unsigned int>(rl));
+}
+__device__ __forceinline__ double lane_xor32(double v) {
+  const long long l = __double_as_longlong(v);
+  const int lo = static_cast<int>(l), hi = static_cast<int>(l >> 32);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);  // [0]: halves (0,0), [1]: halves (1,1)
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const bool up = __lane_id() >= 32;
+  const int rl = up ? a[0] : a[1], rh = up ? b[0] : b[1];
+  return __longlong_as_double((static_cast<long long>(rh) << 32) | static_cast<unsigned int>(rl));
+}
+
 // Sum over the 64 lanes, valid in LANE 0 ONLY: the halving tree lane 0 sees with __shfl_down or
 // __shfl_xor (v_l + v_{l+32}, then + 16, 8, 4, 2, 1) -- the same additions in the same order, so bitwise
 // the same -- from two permlane swaps and four DPP row shifts (row_shl:n, lane l reads l + n) instead of

@@ -3317,6 +3317,13 @@ __device__ __forceinline__ void sn_load_tile_cmp(const SnCompact& cm, int ns, in
   }
 }
 
+// The sweeps' cross-lane sums by DPP / permlane swaps (row16_sum, lane_xor16 / 32: bitwise __shfl_xor's) instead of
+// ds_bpermute; -DDPGO_SN_DPP_SUMS=0 restores the shuffles (A/B)
+#ifndef DPGO_SN_DPP_SUMS
+#define DPGO_SN_DPP_SUMS 1
+#endif
+constexpr bool kSnDppSums = DPGO_SN_DPP_SUMS != 0;
+
 // A/B probe only (-DDPGO_SN_ACQUIRE_TEST): an agent-scope acquire (L2 invalidate) at the start of every supernodal
 // kernel, to test whether a wrong exact-preconditioner result with contiguous panel memory is a stale L2 line
 #ifdef DPGO_SN_ACQUIRE_TEST
@@ -3498,8 +3505,12 @@ __global__ __launch_bounds__(kThreads) void k_sn_fwd(SnView v, const int2* __res
 #pragma unroll
     for (int a = 0; a < R; ++a) {
       double x = acc[i][a];
+      if constexpr (kSnDppSums) {
+        x = row16_sum(x);
+      } else {
 #pragma unroll
-      for (int off = 1; off < 16; off <<= 1) x += __shfl_xor(x, off, 64);
+        for (int off = 1; off < 16; off <<= 1) x += __shfl_xor(x, off, 64);
+      }
       acc[i][a] = x;
     }
   if (cq != 0) return;
@@ -3602,8 +3613,12 @@ __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small
 #pragma unroll
     for (int a = 0; a < R; ++a) {
       double x = acc[i][a];
+      if constexpr (kSnDppSums) {
+        x = row16_sum(x);
+      } else {
 #pragma unroll
-      for (int off = 1; off < 16; off <<= 1) x += __shfl_xor(x, off, 64);
+        for (int off = 1; off < 16; off <<= 1) x += __shfl_xor(x, off, 64);
+      }
       acc[i][a] = x;
     }
   if (cq != 0) return;
@@ -3715,8 +3730,8 @@ __global__ __launch_bounds__(kThreads) void k_sn_bwd(SnView v, const int2* __res
 #pragma unroll
     for (int a = 0; a < R; ++a) {
       double z = acc[c][a];
-      z += __shfl_xor(z, 16, 64);
-      z += __shfl_xor(z, 32, 64);
+      z += kSnDppSums ? lane_xor16(z) : __shfl_xor(z, 16, 64);
+      z += kSnDppSums ? lane_xor32(z) : __shfl_xor(z, 32, 64);
       acc[c][a] = z;
     }
   if (lane < 16) {
