@@ -3639,8 +3639,11 @@ __global__ __launch_bounds__(kThreads, DPGO_SNF_SMALL_WAVES) void k_sn_fwd_small
   }
 }
 
+#ifndef DPGO_SNB_WAVES
+#define DPGO_SNB_WAVES 1  // k_sn_bwd's occupancy hint (waves per SIMD; 1 = none)
+#endif
 template <int R>
-__global__ __launch_bounds__(kThreads) void k_sn_bwd(SnView v, const int2* __restrict__ items, int b,
+__global__ __launch_bounds__(kThreads, DPGO_SNB_WAVES) void k_sn_bwd(SnView v, const int2* __restrict__ items, int b,
                                                      const double* __restrict__ y, double* __restrict__ x) {
   DPGO_SN_ACQUIRE();
   __shared__ double sg[2][kSnTileDev * R];  // double-buffered [y_S ; -x_R] chunks
