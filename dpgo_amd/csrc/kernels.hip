@@ -4108,11 +4108,20 @@ __global__ __launch_bounds__(kThreads) void k_snf_asm(SnFactorView v, const int2
 
 // kind 5 (the blocked trailing update): the tiles right of the current block of kSnfBlockK columns
 constexpr int kSnfBlockK = 4;
+// kind 5 with the next K's operands loaded during the current K's MFMAs (-DDPGO_SNF5_PIPE=0: load, then multiply)
+#ifndef DPGO_SNF5_PIPE
+#define DPGO_SNF5_PIPE 1
+#endif
+constexpr bool kSnf5Pipe = DPGO_SNF5_PIPE != 0;
+#ifndef DPGO_SNF5_WAVES
+#define DPGO_SNF5_WAVES 1  // the pipelined kind 5's occupancy hint (waves per SIMD; 1 = none)
+#endif
 
 // kind 1: the diagonal tile K of every node (POTRF, its inverse into the panel); 2: L_IK = F_IK L_KK^-T, item
 // (node, I); 3: F_IJ -= L_IK L_JK^T, item (node, I << 16 | J); 4: the panel's tile (I, J = param), item (node, I)
 template <int B, int KIND>
-__global__ __launch_bounds__(kThreads) void k_snf_tile(SnFactorView v, const int2* __restrict__ items, int P) {
+__global__ __launch_bounds__(kThreads, KIND == 5 && kSnf5Pipe ? DPGO_SNF5_WAVES : 1) void k_snf_tile(SnFactorView v,
+                                                                                    const int2* __restrict__ items, int P) {
   DPGO_SN_ACQUIRE();
   constexpr int kind = KIND;
   __shared__ double As[kFT * kFLD], Bs[kFT * kFLD];
@@ -4178,6 +4187,44 @@ __global__ __launch_bounds__(kThreads) void k_snf_tile(SnFactorView v, const int
     double* gt = F + static_cast<long>(I) * kFT * ld + J * kFT;
     f64x4 acc[4];
     sn_strip_load(acc, gt, ld, wave * 16);
+    if constexpr (kSnf5Pipe) {
+      // K + 1's B tile loaded into registers while K's MFMAs run (its A strip right after them, in flight across the
+      // barrier and the tile's LDS store): the same MFMA sequence, one LDS tile
+      constexpr int kTV = kFT * kFT / kThreads;
+      double a[kFT / 4], bn[kTV];
+      auto load_b = [&](int K) {
+        const double* g = F + static_cast<long>(J) * kFT * ld + K * kFT;
+#pragma unroll
+        for (int u = 0; u < kTV; ++u) {
+          const int x = tid + u * kThreads, i = x / kFT, j = x % kFT;
+          bn[u] = g[i * ld + j];
+        }
+      };
+      auto store_b = [&]() {
+#pragma unroll
+        for (int u = 0; u < kTV; ++u) {
+          const int x = tid + u * kThreads, i = x / kFT, j = x % kFT;
+          Bs[i * kFLD + j] = bn[u];
+        }
+      };
+      sn_strip_a(a, F + static_cast<long>(I) * kFT * ld + P * kFT, ld, wave * 16);
+      load_b(P);
+      store_b();
+      __syncthreads();
+      for (int K = P; K < K1; ++K) {
+        const bool more = K + 1 < K1;
+        if (more) load_b(K + 1);
+        mfma_strip_ra(acc, a, Bs, -1.0);
+        if (more) {
+          sn_strip_a(a, F + static_cast<long>(I) * kFT * ld + (K + 1) * kFT, ld, wave * 16);
+          __syncthreads();
+          store_b();
+          __syncthreads();
+        }
+      }
+      sn_strip_store(acc, gt, ld, wave * 16);
+      return;
+    }
     for (int K = P; K < K1; ++K) {
       double a[kFT / 4];
       sn_strip_a(a, F + static_cast<long>(I) * kFT * ld + K * kFT, ld, wave * 16);
