@@ -4113,6 +4113,11 @@ constexpr int kSnfBlockK = 4;
 #define DPGO_SNF5_PIPE 1
 #endif
 constexpr bool kSnf5Pipe = DPGO_SNF5_PIPE != 0;
+// kind 4 (the panel tiles) pipelined the same way (-DDPGO_SNF4_PIPE=0: load, then multiply)
+#ifndef DPGO_SNF4_PIPE
+#define DPGO_SNF4_PIPE 1
+#endif
+constexpr bool kSnf4Pipe = DPGO_SNF4_PIPE != 0;
 #ifndef DPGO_SNF5_WAVES
 #define DPGO_SNF5_WAVES 1  // the pipelined kind 5's occupancy hint (waves per SIMD; 1 = none)
 #endif
@@ -4254,13 +4259,49 @@ __global__ __launch_bounds__(kThreads, KIND == 5 && kSnf5Pipe ? DPGO_SNF5_WAVES 
   f64x4 acc[4] = {};
   if (I >= ns) sn_strip_load(acc, F + static_cast<long>(I) * kFT * ld + J * kFT, ld, wave * 16);
   const int Kmax = I < ns ? I : ns - 1;
-  for (int K = J + 1; K <= Kmax; ++K) {
-    double a[kFT / 4];
-    sn_strip_a(a, panel + sn_tile_dev(ns, I, K) * kFT * kFT, kFT, wave * 16);
-    sn_tile_to_lds(Bs, F + static_cast<long>(K) * kFT * ld + J * kFT, ld);
+  if (kSnf4Pipe && J + 1 <= Kmax) {
+    // as kind 5: K + 1's B tile in registers while K's MFMAs run, its A strip right after them (same MFMA sequence)
+    constexpr int kTV = kFT * kFT / kThreads;
+    double a[kFT / 4], bn[kTV];
+    auto load_b = [&](int K) {
+      const double* g = F + static_cast<long>(K) * kFT * ld + J * kFT;
+#pragma unroll
+      for (int u = 0; u < kTV; ++u) {
+        const int x = tid + u * kThreads, i = x / kFT, j = x % kFT;
+        bn[u] = g[i * ld + j];
+      }
+    };
+    auto store_b = [&]() {
+#pragma unroll
+      for (int u = 0; u < kTV; ++u) {
+        const int x = tid + u * kThreads, i = x / kFT, j = x % kFT;
+        Bs[i * kFLD + j] = bn[u];
+      }
+    };
+    sn_strip_a(a, panel + sn_tile_dev(ns, I, J + 1) * kFT * kFT, kFT, wave * 16);
+    load_b(J + 1);
+    store_b();
     __syncthreads();
-    mfma_strip_ra<false>(acc, a, Bs, -1.0);
-    __syncthreads();
+    for (int K = J + 1; K <= Kmax; ++K) {
+      const bool more = K + 1 <= Kmax;
+      if (more) load_b(K + 1);
+      mfma_strip_ra<false>(acc, a, Bs, -1.0);
+      if (more) sn_strip_a(a, panel + sn_tile_dev(ns, I, K + 1) * kFT * kFT, kFT, wave * 16);
+      __syncthreads();
+      if (more) {
+        store_b();
+        __syncthreads();
+      }
+    }
+  } else {
+    for (int K = J + 1; K <= Kmax; ++K) {
+      double a[kFT / 4];
+      sn_strip_a(a, panel + sn_tile_dev(ns, I, K) * kFT * kFT, kFT, wave * 16);
+      sn_tile_to_lds(Bs, F + static_cast<long>(K) * kFT * ld + J * kFT, ld);
+      __syncthreads();
+      mfma_strip_ra<false>(acc, a, Bs, -1.0);
+      __syncthreads();
+    }
   }
   const int l = tid & 63;
   double a[kFT / 4];
