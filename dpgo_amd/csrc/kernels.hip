@@ -4035,6 +4035,12 @@ __global__ __launch_bounds__(kThreads) void k_sn_factor(SnFactorView v) {
 // right-looking K loop and the panel's J loop as launch sequences on the stream (FacLaunchKind).  Each tile sees
 // the same operations in the same order as in k_sn_factor, so the factors agree bitwise.
 // ------------------------------------------------------------------------------------------
+// k_snf_asm's extend-add in batches of four positions per lane (-DDPGO_SNF_ASM_BATCH=0: one at a time)
+#ifndef DPGO_SNF_ASM_BATCH
+#define DPGO_SNF_ASM_BATCH 1
+#endif
+constexpr bool kSnfAsmBatch = DPGO_SNF_ASM_BATCH != 0;
+
 template <int B>
 __global__ __launch_bounds__(kThreads) void k_snf_asm(SnFactorView v, const int2* __restrict__ items, int phase) {
   DPGO_SN_ACQUIRE();
@@ -4099,9 +4105,35 @@ __global__ __launch_bounds__(kThreads) void k_snf_asm(SnFactorView v, const int2
   const int r1 = min(tcb, it.y * kFT + kFT);
   for (int ri = it.y * kFT + wave; ri < r1; ri += 4) {
     const long pr = sn_frow(tp[ri / B], ri % B, s, B, Sp);
-    for (int rj = lane; rj <= ri; rj += 64) {
-      const long pc = sn_frow(tp[rj / B], rj % B, s, B, Sp);
-      F[pr * ld + pc] += U[static_cast<long>(ri) * ldc + rj];
+    if constexpr (kSnfAsmBatch) {
+      // four of the lane's positions per pass: every position and load issued before any add and store (the
+      // positions of one row are distinct, so the batch reorders no dependent access; each entry gets the same add)
+      constexpr int NB = 4;
+      for (int rj0 = lane; rj0 <= ri; rj0 += NB * 64) {
+        long pc[NB];
+        double fu[NB], uu[NB];
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+          const int rj = rj0 + u * 64;
+          pc[u] = rj <= ri ? sn_frow(tp[rj / B], rj % B, s, B, Sp) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+          const int rj = rj0 + u * 64;
+          if (rj <= ri) {
+            uu[u] = U[static_cast<long>(ri) * ldc + rj];
+            fu[u] = F[pr * ld + pc[u]];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < NB; ++u)
+          if (rj0 + u * 64 <= ri) F[pr * ld + pc[u]] = fu[u] + uu[u];
+      }
+    } else {
+      for (int rj = lane; rj <= ri; rj += 64) {
+        const long pc = sn_frow(tp[rj / B], rj % B, s, B, Sp);
+        F[pr * ld + pc] += U[static_cast<long>(ri) * ldc + rj];
+      }
     }
   }
 }

@@ -1,0 +1,19 @@
+# k_snf_asm extend-add batched four positions per lane (tree) against one at a time (ab/noasmb, -DDPGO_SNF_ASM_BATCH=0):
+# sweep outputs (device factor) bitwise, then the C5 GNC_TLS + exact bench's factor time and ms/step, alternated twice.
+set -o pipefail
+mkdir -p gpurun_out
+T=${1:-r06zh}
+lib() { [ $1 = tree ] && echo "" || echo "DPGO_HIP_LIB=$PWD/dpgo_amd/ab/$1/libdpgo_hip.so"; }
+for v in tree noasmb; do
+  env $(lib $v) timeout -k 10 300 python3 -u tools/precond_dump.py gpurun_out/${T}_$v.npz > /dev/null 2>&1 || exit 1
+done
+python3 tools/precond_dump.py --compare gpurun_out/${T}_tree.npz gpurun_out/${T}_noasmb.npz || exit 1
+for i in 1 2; do
+  for v in tree noasmb; do
+    env $(lib $v) timeout -k 10 400 python3 -u bench.py --precon exact --robust GNC_TLS --burnin 60 --boundary-leg 0 \
+      --exact-leg 0 --cpu-baseline 0 > gpurun_out/${T}_${v}_$i.log 2>&1 || exit 1
+    grep '^{' gpurun_out/${T}_${v}_$i.log | python3 -c "
+import json,sys; d=json.loads(sys.stdin.read()); f=d['exact_factor']
+print('$v', round(d['ms_per_step'],2), round(f['color0']['factor_ms'],1), round(f['color1']['factor_ms'],1))"
+  done
+done
