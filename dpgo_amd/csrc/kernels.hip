@@ -4145,6 +4145,11 @@ constexpr int kSnfBlockK = 4;
 #define DPGO_SNF5_PIPE 1
 #endif
 constexpr bool kSnf5Pipe = DPGO_SNF5_PIPE != 0;
+// kind 1's triangular inverse right-looking over all threads (-DDPGO_SNF1_RIGHT=0: one thread per column)
+#ifndef DPGO_SNF1_RIGHT
+#define DPGO_SNF1_RIGHT 1
+#endif
+constexpr bool kSnf1Right = DPGO_SNF1_RIGHT != 0;
 // kind 4 (the panel tiles) pipelined the same way (-DDPGO_SNF4_PIPE=0: load, then multiply)
 #ifndef DPGO_SNF4_PIPE
 #define DPGO_SNF4_PIPE 1
@@ -4180,17 +4185,36 @@ __global__ __launch_bounds__(kThreads, KIND == 5 && kSnf5Pipe ? DPGO_SNF5_WAVES 
     // L^-1 by sn_trtri_lds's recurrence, kept in the same tile: its strict lower part transposed into the (unused)
     // strict upper triangle, its diagonal in s_dinv -- one LDS tile instead of two
     __shared__ double s_dinv[kFT];
-    if (tid < kFT) {
-      const int c = tid;
-      const double dc = 1.0 / As[c * kFLD + c];
-      s_dinv[c] = dc;
-      for (int i = c + 1; i < kFT; ++i) {
-        double acc = 0.0;
-        for (int k = c; k < i; ++k) acc = fma(As[i * kFLD + k], k == c ? dc : As[c * kFLD + k], acc);
-        As[c * kFLD + i] = -acc / As[i * kFLD + i];
+    if constexpr (kSnf1Right) {
+      // Right-looking: the partial sum of X[i][c] (i > c, held in Bs) takes L[i][k] X[k][c] as soon as X[k][c] is
+      // final, for k = c, c + 1, ... -- the column recurrence's fma chain in its order, from 0.0, so X is bitwise the
+      // same; every thread works on every step instead of thread c walking column c alone
+      if (tid < kFT) s_dinv[tid] = 1.0 / As[tid * kFLD + tid];
+      __syncthreads();
+      for (int k = 0; k < kFT; ++k) {
+        if (tid < k) As[tid * kFLD + k] = -Bs[k * kFLD + tid] / As[k * kFLD + k];  // X[k][c], c = tid
+        __syncthreads();
+        const int w = k + 1, n = (kFT - 1 - k) * w;  // rows k + 1 .. 63, columns 0 .. k
+        for (int x = tid; x < n; x += kThreads) {
+          const int i = k + 1 + x / w, c = x - (x / w) * w;
+          const double xk = c == k ? s_dinv[k] : As[c * kFLD + k];
+          Bs[i * kFLD + c] = fma(As[i * kFLD + k], xk, c == k ? 0.0 : Bs[i * kFLD + c]);
+        }
+        __syncthreads();
       }
+    } else {
+      if (tid < kFT) {
+        const int c = tid;
+        const double dc = 1.0 / As[c * kFLD + c];
+        s_dinv[c] = dc;
+        for (int i = c + 1; i < kFT; ++i) {
+          double acc = 0.0;
+          for (int k = c; k < i; ++k) acc = fma(As[i * kFLD + k], k == c ? dc : As[c * kFLD + k], acc);
+          As[c * kFLD + i] = -acc / As[i * kFLD + i];
+        }
+      }
+      __syncthreads();
     }
-    __syncthreads();
     for (int x = tid; x < kFT * kFT; x += kThreads) {
       const int i = x / kFT, j = x % kFT;
       if (j <= i) F[(static_cast<long>(K) * kFT + i) * ld + K * kFT + j] = As[i * kFLD + j];  // L (upper unchanged)
